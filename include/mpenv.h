@@ -1,0 +1,287 @@
+/*
+ * mpenv.h — C ABI of the MI355X-native madrona-mp-env engine.
+ *
+ * Drop-in boundary for the world-batched Zone step.  Every entry point maps
+ * to a method of the reference's Manager class (src/mgr.hpp:31-161) or its
+ * Python binding (src/bindings.cpp:11-160); the cited lines are what each
+ * function replaces.  Plain pointers and sizes only — no torch/HIP types in
+ * the signatures (the stream is passed as an opaque hipStream_t pointer).
+ *
+ * Errors: every int-returning function returns 0 on success and a negative
+ * MPENV_ERR_* code on failure; mpenv_last_error() gives the message.  The
+ * reference FATALs on I/O failure (mgr.cpp:205,214) and asserts otherwise.
+ */
+#ifndef MPENV_H
+#define MPENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPENV_ABI_VERSION 1
+
+/* Error codes */
+#define MPENV_OK 0
+#define MPENV_ERR_INVALID -1
+#define MPENV_ERR_IO -2
+#define MPENV_ERR_HIP -3
+#define MPENV_ERR_UNSUPPORTED -4
+
+/* ExecMode (madrona::ExecMode, used at scripts/jax_train.py:111).  This build
+ * is HIP-only: MPENV_EXEC_CPU is rejected with MPENV_ERR_UNSUPPORTED (no
+ * silent CPU fallback). */
+#define MPENV_EXEC_CPU 0
+#define MPENV_EXEC_CUDA 1 /* = HIP on gfx950 */
+
+/* Task (types.hpp:45-51) */
+#define MPENV_TASK_EXPLORE 0
+#define MPENV_TASK_TDM 1
+#define MPENV_TASK_ZONE 2
+#define MPENV_TASK_TURRET 3
+#define MPENV_TASK_ZONE_CAPTURE_DEFEND 4
+
+/* SimFlags (sim_flags.hpp:7-20) */
+#define MPENV_SIMFLAG_DEFAULT 0u
+#define MPENV_SIMFLAG_SPAWN_IN_MIDDLE (1u << 0)
+#define MPENV_SIMFLAG_RANDOMIZE_HP_MAGAZINE (1u << 1)
+#define MPENV_SIMFLAG_NAVMESH_SPAWN (1u << 2)
+#define MPENV_SIMFLAG_NO_RESPAWN (1u << 3)
+#define MPENV_SIMFLAG_STAGGER_STARTS (1u << 4)
+#define MPENV_SIMFLAG_ENABLE_CURRICULUM (1u << 5)
+#define MPENV_SIMFLAG_HARDCODED_SPAWNS (1u << 6)
+#define MPENV_SIMFLAG_RANDOM_FLIP_TEAMS (1u << 7)
+#define MPENV_SIMFLAG_STATIC_FLIP_TEAMS (1u << 8)
+#define MPENV_SIMFLAG_FULL_TEAM_POLICY (1u << 9)
+#define MPENV_SIMFLAG_SIM_EVAL_MODE (1u << 10)
+#define MPENV_SIMFLAG_SUB_ZONES (1u << 11)
+
+/* ExportID (sim.hpp:15-66), same numbering. */
+enum mpenv_export_id {
+    MPENV_EXPORT_RESET = 0,
+    MPENV_EXPORT_WORLD_CURRICULUM = 1,
+    MPENV_EXPORT_EXPLORE_ACTION = 2,
+    MPENV_EXPORT_PVP_DISCRETE_ACTION = 3,
+    MPENV_EXPORT_PVP_AIM_ACTION = 4,
+    MPENV_EXPORT_PVP_DISCRETE_AIM_ACTION = 5,
+    MPENV_EXPORT_REWARD = 6,
+    MPENV_EXPORT_DONE = 7,
+    MPENV_EXPORT_MATCH_RESULT = 8,
+    MPENV_EXPORT_AGENT_POLICY = 9,
+    MPENV_EXPORT_SELF_OBSERVATION = 10,
+    MPENV_EXPORT_TEAMMATE_OBSERVATIONS = 11,
+    MPENV_EXPORT_OPPONENT_OBSERVATIONS = 12,
+    MPENV_EXPORT_OPPONENT_LAST_KNOWN_OBSERVATIONS = 13,
+    MPENV_EXPORT_SELF_POSITION = 14,
+    MPENV_EXPORT_TEAMMATE_POSITIONS = 15,
+    MPENV_EXPORT_OPPONENT_POSITIONS = 16,
+    MPENV_EXPORT_OPPONENT_LAST_KNOWN_POSITIONS = 17,
+    MPENV_EXPORT_OPPONENT_MASKS = 18,
+    MPENV_EXPORT_FWD_LIDAR = 19,
+    MPENV_EXPORT_REAR_LIDAR = 20,
+    MPENV_EXPORT_AGENT_MAP = 21,
+    MPENV_EXPORT_UNMASKED_AGENT_MAP = 22,
+    MPENV_EXPORT_HP = 23,
+    MPENV_EXPORT_ALIVE = 24,
+    MPENV_EXPORT_MAGAZINE = 25,
+    MPENV_EXPORT_FULL_TEAM_ACTIONS = 26,
+    MPENV_EXPORT_FULL_TEAM_GLOBAL = 27,
+    MPENV_EXPORT_FULL_TEAM_PLAYERS = 28,
+    MPENV_EXPORT_FULL_TEAM_ENEMIES = 29,
+    MPENV_EXPORT_FULL_TEAM_LAST_KNOWN_ENEMIES = 30,
+    MPENV_EXPORT_FULL_TEAM_FWD_LIDAR = 31,
+    MPENV_EXPORT_FULL_TEAM_REAR_LIDAR = 32,
+    MPENV_EXPORT_FULL_TEAM_REWARD = 33,
+    MPENV_EXPORT_FULL_TEAM_DONE = 34,
+    MPENV_EXPORT_FULL_TEAM_POLICY_ASSIGNMENTS = 35,
+    MPENV_EXPORT_EVENT_LOG = 36,
+    MPENV_EXPORT_PACKED_STEP_SNAPSHOT = 37,
+    MPENV_EXPORT_FILTERS_STATE = 38,
+    MPENV_EXPORT_REWARD_HYPER_PARAMS = 39,
+    MPENV_NUM_REFERENCE_EXPORTS = 40,
+
+    /* Extensions (not in the reference ExportID): */
+    MPENV_EXPORT_SIM_CONTROL = 64,   /* TrainControl i32[3] (mgr.cpp:1975-1978) */
+    MPENV_EXPORT_DEBUG_AGENT_F32 = 65, /* [A][MPENV_DBG_AF_COUNT] internal state */
+    MPENV_EXPORT_DEBUG_AGENT_I32 = 66, /* [A][MPENV_DBG_AI_COUNT] */
+    MPENV_EXPORT_DEBUG_WORLD_I32 = 67, /* [W][MPENV_DBG_WI_COUNT] */
+    MPENV_EXPORT_DEBUG_WORLD_F32 = 68, /* [W][MPENV_DBG_WF_COUNT] */
+    MPENV_EXPORT_DEBUG_EXPLORE = 69,   /* [A][81*81] u32 ExploreTracker.visited */
+    MPENV_EXPORT_DEBUG_CRUMBS = 70     /* [W][MPENV_MAX_CRUMBS][8] f32 breadcrumb pool */
+};
+
+/* Debug-state column layouts (parity tests compare these bit-exactly). */
+enum mpenv_dbg_agent_f32 {
+    MPENV_DBG_AF_POS = 0,     /* 3 */
+    MPENV_DBG_AF_VEL = 3,     /* 3 */
+    MPENV_DBG_AF_ROT = 6,     /* 4 (w,x,y,z) */
+    MPENV_DBG_AF_AIM = 10,    /* yaw, pitch, rot w,x,y,z */
+    MPENV_DBG_AF_MAXVEL = 16,
+    MPENV_DBG_AF_MINDIST_ZONE = 17,
+    MPENV_DBG_AF_FIRED_T = 18,
+    MPENV_DBG_AF_BC_PENALTY = 19,
+    MPENV_DBG_AF_START = 20,  /* 3 */
+    MPENV_DBG_AF_COUNT = 23
+};
+enum mpenv_dbg_agent_i32 {
+    MPENV_DBG_AI_CUR_POSE = 0,
+    MPENV_DBG_AI_TGT_POSE = 1,
+    MPENV_DBG_AI_TRANSITION = 2,
+    MPENV_DBG_AI_RNG_A = 3,
+    MPENV_DBG_AI_RNG_B = 4,
+    MPENV_DBG_AI_RNG_CTR = 5,
+    MPENV_DBG_AI_LANDED_ON = 6,     /* agent index in world, or -1 */
+    MPENV_DBG_AI_RESPAWN_STEPS = 7,
+    MPENV_DBG_AI_AUTOHEAL_STEPS = 8,
+    MPENV_DBG_AI_FLAGS = 9,         /* bit0 successfulKill, 1 wasKilled, 2 inZone, 3 hasDied, 4 reloadedFullMag */
+    MPENV_DBG_AI_WAS_SHOT = 10,
+    MPENV_DBG_AI_WEAPON = 11,
+    MPENV_DBG_AI_BC_LAST = 12,
+    MPENV_DBG_AI_BC_STEPS = 13,
+    MPENV_DBG_AI_CANSEE = 14,       /* bitmask over opponents */
+    MPENV_DBG_AI_NEW_CELLS = 15,
+    MPENV_DBG_AI_COUNT = 16
+};
+enum mpenv_dbg_world_i32 {
+    MPENV_DBG_WI_TEAM_A = 0,
+    MPENV_DBG_WI_CUR_STEP = 1,
+    MPENV_DBG_WI_FINISHED = 2,
+    MPENV_DBG_WI_CUR_ZONE = 3,
+    MPENV_DBG_WI_CONTROLLING = 4,
+    MPENV_DBG_WI_CONTESTED = 5,
+    MPENV_DBG_WI_CAPTURED = 6,
+    MPENV_DBG_WI_EARNED = 7,
+    MPENV_DBG_WI_ZONE_STEPS = 8,
+    MPENV_DBG_WI_STEPS_UNTIL_POINT = 9,
+    MPENV_DBG_WI_EPISODE = 10,
+    MPENV_DBG_WI_EPISODE_COUNTER = 11,
+    MPENV_DBG_WI_RNG_A = 12,
+    MPENV_DBG_WI_RNG_B = 13,
+    MPENV_DBG_WI_RNG_CTR = 14,
+    MPENV_DBG_WI_NUM_CRUMBS = 15,
+    MPENV_DBG_WI_FILTER_ACTIVE0 = 16,
+    MPENV_DBG_WI_FILTER_ACTIVE1 = 17,
+    MPENV_DBG_WI_FILTER_LAST0 = 18,
+    MPENV_DBG_WI_FILTER_LAST1 = 19,
+    MPENV_DBG_WI_CRUMB_OVERFLOW = 20,
+    MPENV_DBG_WI_COUNT = 21
+};
+enum mpenv_dbg_world_f32 {
+    MPENV_DBG_WF_TEAM_REWARD0 = 0,
+    MPENV_DBG_WF_TEAM_REWARD1 = 1,
+    MPENV_DBG_WF_GOAL_MIN0 = 2,
+    MPENV_DBG_WF_GOAL_MIN1 = 3,
+    MPENV_DBG_WF_GOAL_TEAM0 = 4,
+    MPENV_DBG_WF_GOAL_TEAM1 = 5,
+    MPENV_DBG_WF_COUNT = 6
+};
+
+/* Fixed-capacity per-world breadcrumb pool (reference: dynamic
+ * BreadcrumbEntity archetype, sim.cpp:4845-4926).  Live crumbs per world are
+ * bounded by ~6 per agent; creations beyond capacity are
+ * dropped and counted in MPENV_DBG_WI_CRUMB_OVERFLOW. */
+#define MPENV_MAX_CRUMBS 128
+
+/* Tensor element types (madrona::py::TensorElementType subset) */
+#define MPENV_DTYPE_INT32 0
+#define MPENV_DTYPE_FLOAT32 1
+#define MPENV_DTYPE_UINT32 2
+
+typedef struct mpenv_config {
+    int32_t exec_mode;          /* MPENV_EXEC_* */
+    int32_t gpu_id;
+    uint32_t num_worlds;        /* worlds owned by this manager */
+    uint32_t rand_seed;
+    int32_t auto_reset;
+    uint32_t sim_flags;
+    int32_t task_type;          /* MPENV_TASK_* (only ZONE is implemented) */
+    uint32_t team_size;         /* 1..6 */
+    uint32_t num_pbt_policies;
+    uint32_t policy_history_size;
+    const char *scene_path;     /* dir with collisions/navmesh/spawns/zones.bin */
+    int32_t train_flank;
+    const char *replay_log_path;     /* NULL = none */
+    const char *record_log_path;     /* NULL = none */
+    const char *event_log_path;      /* NULL = none */
+    const char *curriculum_data_path;/* NULL = none */
+    /* Extension for sharding worlds across GPUs: the global index of this
+     * manager's world 0.  RNG keys use global world IDs (sim.cpp:743-746),
+     * so a shard reproduces exactly the worlds of a single big run. */
+    uint32_t world_id_offset;
+} mpenv_config;
+
+typedef struct mpenv_manager mpenv_manager;
+
+/* Manager::Manager (mgr.hpp:57-58 / mgr.cpp:1914-1919) */
+int mpenv_create(const mpenv_config *cfg, mpenv_manager **out);
+/* Manager::~Manager (mgr.cpp:1921) */
+void mpenv_destroy(mpenv_manager *mgr);
+/* Manager::init (mgr.cpp:1923-1946): forced reset of every world + Init graph */
+int mpenv_init(mpenv_manager *mgr);
+/* Manager::step (mgr.cpp:1948-1951): one synchronous world-batched step */
+int mpenv_step(mpenv_manager *mgr);
+/* Asynchronous step on a caller-owned hipStream_t (no host sync). */
+int mpenv_step_async(mpenv_manager *mgr, void *hip_stream);
+/* Manager::gpuStreamInit / gpuStreamStep (mgr.cpp:507-645): XLA custom-call
+ * ABI.  buffers = TrainInterface inputs then outputs, in the order of
+ * mpenv_train_interface(). */
+int mpenv_gpu_stream_init(mpenv_manager *mgr, void *hip_stream, void **buffers);
+int mpenv_gpu_stream_step(mpenv_manager *mgr, void *hip_stream, void **buffers);
+
+/* Manager::*Tensor() getters (mgr.cpp:1965-2381): zero-copy view of an
+ * engine-owned buffer.  dims must hold 8 entries. gpu_id = -1 for host. */
+int mpenv_export_tensor(mpenv_manager *mgr, int32_t export_id, void **ptr,
+                        int32_t *dtype, int32_t *ndim, int64_t *dims,
+                        int32_t *gpu_id);
+
+/* TrainInterface (mgr.cpp:2383-2431): number of named inputs / outputs and
+ * their (name, export id).  Index order is the gpuStream buffers order. */
+int mpenv_train_interface_size(int32_t *num_inputs, int32_t *num_outputs);
+int mpenv_train_interface_entry(int32_t is_output, int32_t idx,
+                                const char **name, int32_t *export_id);
+
+/* Step-input copy (TrainInterface::cudaCopyStepInputs of gpuStreamStep,
+ * mgr.cpp:625) from a device buffer laid out [A][6] i32 (4 discrete +
+ * 2 discrete-aim actions per agent), asynchronous on hip_stream. */
+int mpenv_copy_actions(mpenv_manager *mgr, const int32_t *src_device, void *hip_stream);
+
+/* Manager::triggerReset (mgr.cpp:2484-2500) */
+int mpenv_trigger_reset(mpenv_manager *mgr, int32_t world_idx);
+/* Manager::setPvPAction (mgr.cpp:2518-2566) */
+int mpenv_set_pvp_action(mpenv_manager *mgr, int32_t world_idx, int32_t agent_idx,
+                         const int32_t discrete[4], const float aim[2],
+                         const int32_t aim_discrete[2]);
+/* Manager::setHP (mgr.cpp:2585-2601) */
+int mpenv_set_hp(mpenv_manager *mgr, int32_t world_idx, int32_t agent_idx, int32_t hp);
+/* Manager::setAgentPolicy / setUniformAgentPolicy (mgr.cpp:2619-2658) */
+int mpenv_set_agent_policy(mpenv_manager *mgr, int32_t world_idx, int32_t agent_idx,
+                           int32_t policy);
+int mpenv_set_uniform_agent_policy(mpenv_manager *mgr, int32_t policy);
+/* Manager::isReplayFinished (mgr.cpp:2603-2617) */
+int mpenv_is_replay_finished(mpenv_manager *mgr, int32_t *finished);
+
+/* Number of worlds / agents per world of a manager. */
+int mpenv_dims(mpenv_manager *mgr, int32_t *num_worlds, int32_t *agents_per_world);
+
+/* Measurement hook: average device time (ms) of each step kernel over the
+ * steps since the last call, measured with HIP events on the step stream.
+ * names[i] point to static strings.  Returns the number of kernels. */
+int mpenv_kernel_timings(mpenv_manager *mgr, int32_t max_n, const char **names,
+                         float *avg_ms, int32_t *launches);
+int mpenv_enable_kernel_timing(mpenv_manager *mgr, int32_t enable);
+
+/* Scene BVH as the engine builds it (map_importer.cpp:364-419 replacement):
+ * 64-byte nodes and float3 vertices (3 per triangle).  Call with null
+ * outputs to query sizes.  Used by the parity oracle and tests. */
+int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes,
+                    float *verts_out, int32_t *num_verts, int32_t *max_stack);
+
+const char *mpenv_last_error(void);
+int32_t mpenv_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPENV_H */

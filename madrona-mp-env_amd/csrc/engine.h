@@ -1,0 +1,175 @@
+// engine.h — device state layout of the MI355X engine.
+//
+// The reference stores per-entity components in Madrona ECS archetype
+// columns (PvPAgent, types.hpp:932-995) and per-world singletons
+// (sim.hpp:81-191).  Here every per-agent internal field is its own
+// structure-of-arrays column indexed by the global agent id
+// g = world * N + agent (N = 2 * teamSize, team 0 offsets first,
+// level_gen.cpp:148-162), so lanes that own consecutive agents issue
+// coalesced loads.  Exported components keep the reference's
+// array-of-struct column layout (tensor dims of mgr.cpp:1965-2381) because
+// they are the drop-in boundary.
+#pragma once
+
+#include <cstdint>
+
+#include "mpenv_core.h"
+#include "scene.h"
+
+namespace mpenv {
+
+constexpr int kMaxTeamSize = 6;
+constexpr int kMaxAgents = 2 * kMaxTeamSize;
+constexpr int kMaxZones = 5;
+constexpr int kGridW = 81;
+constexpr int kGridCells = kGridW * kGridW;
+constexpr int kSelfObs = 43;
+constexpr int kOtherObs = 32;
+constexpr int kFwdRays = 64;   // 2 x 32
+constexpr int kRearRays = 16;  // 2 x 8
+constexpr int kLidarRays = kFwdRays + kRearRays;
+constexpr int kMaxCrumbs = 128;
+constexpr int kMaxSpawns = 32;   // per spawn list (simple_map: 8/8/16)
+constexpr int kMaxBVHStack = 16; // register byte-stack capacity
+
+#define MP_AGENT_F32(X) \
+    X(px) X(py) X(pz) X(vx) X(vy) X(vz) X(rw) X(rx) X(ry) X(rz) \
+    X(ayaw) X(apitch) X(aw) X(ax) X(ay) X(az) X(maxVel) X(minDistZone) \
+    X(firedT) X(bcPenalty) X(sx) X(sy) X(sz) X(dyv) X(dpv)
+
+#define MP_AGENT_I32(X) \
+    X(curPose) X(tgtPose) X(transRem) X(rngA) X(rngB) X(rngCtr) X(landedOn) \
+    X(respawnSteps) X(autohealSteps) X(flags) X(wasShot) X(weapon) X(bcLast) \
+    X(bcSteps) X(newCells)
+
+#define MP_WORLD_I32(X) \
+    X(teamA) X(curStep) X(finished) X(curZone) X(controlling) X(contested) \
+    X(captured) X(earned) X(zoneSteps) X(stepsUntilPoint) X(episode) \
+    X(episodeCounter) X(wRngA) X(wRngB) X(wRngCtr) X(filtAct0) X(filtAct1) \
+    X(filtMatched0) X(filtMatched1) X(episodeCurr) X(numCrumbs) X(nextCrumbId) \
+    X(crumbOverflow) X(curTier) X(curSpawnIdx) X(spawnCurriculum)
+
+#define MP_WORLD_F32(X) \
+    X(teamRew0) X(teamRew1) X(goalMin0) X(goalMin1) X(goalTeam0) X(goalTeam1)
+
+// Agent flag bits (CombatState booleans, types.hpp:510-528)
+enum : int32_t {
+    kFlagSuccessfulKill = 1,
+    kFlagWasKilled = 2,
+    kFlagInZone = 4,
+    kFlagHasDied = 8,
+    kFlagReloadedFullMag = 16,
+};
+
+struct DevState {
+    int32_t W, N, T;
+    int64_t A;
+
+#define MP_DECL_F(n) float *n;
+#define MP_DECL_I(n) int32_t *n;
+    MP_AGENT_F32(MP_DECL_F)
+    MP_AGENT_I32(MP_DECL_I)
+    MP_WORLD_I32(MP_DECL_I)
+    MP_WORLD_F32(MP_DECL_F)
+#undef MP_DECL_F
+#undef MP_DECL_I
+
+    float *dmg;            // [6][A] DamageDealt
+    uint8_t *canSee;       // [A][6] OpponentsVisibility
+    uint32_t *visited;     // [A][81*81] ExploreTracker
+    int32_t *filtLast;     // [W][2][3] FiltersMatchState::lastMatches (3 filters used)
+    int32_t *zoneStats;    // [W][5][5]
+    uint32_t *spawnTrack;  // [W][3][kMaxSpawns] SpawnUsageCounter
+    float4 *crumbs;        // [W][kMaxCrumbs][2] {x,y,z,penalty},{team,offset,id,-}
+
+    // Exported columns (reference layouts)
+    int32_t *reset;        // [W]
+    int32_t *worldCurr;    // [W]
+    int32_t *matchResult;  // [W][30]
+    int32_t *exploreAction;// [A][4]
+    int32_t *discreteAction; // [A][4]
+    float *aimAction;      // [A][2]
+    int32_t *discreteAim;  // [A][2]
+    int32_t *policy;       // [A]
+    int32_t *botAction;    // [A][7]
+    float *reward;         // [A]
+    int32_t *done;         // [A]
+    float *selfObs;        // [A][43]
+    float *filters;        // [A]
+    float *tmObs;          // [A][5][32]
+    float *oppObs;         // [A][6][32]
+    float *lkObs;          // [A][6][32]
+    float *selfPos;        // [A][3]
+    float *tmPos;          // [A][5][3]
+    float *oppPos;         // [A][6][3]
+    float *lkPos;          // [A][6][3]
+    float *masks;          // [A][6]
+    float *fwdLidar;       // [A][2][32][4]
+    float *rearLidar;      // [A][2][8][4]
+    float *agentMap;       // [A][16][16][4] (never written, as in the reference)
+    float *hp;             // [A]
+    float *alive;          // [A]
+    int32_t *magazine;     // [A][2]
+    float *rewardCoefs;    // [A][9]
+    int32_t *trainCtrl;    // [3]
+};
+
+struct ZOBBDev {
+    mp::Vec3 pMin, pMax;
+    float rotation;
+};
+
+struct GoalRegionDev {
+    ZOBBDev sub[3];
+    int32_t numSub;
+    int32_t attackerTeam;
+    float rewardStrength;
+};
+
+// Read-only scene + task constants, passed by value as a kernel argument.
+struct SceneDev {
+    const BVHNode *nodes;
+    const float *verts;     // 3 floats per vertex, 3 vertices per triangle
+    int32_t numNodes;
+    int32_t numVerts;
+    mp::AABB worldBounds;
+    float maxDist;
+    float frustum[4];
+    const Spawn *aSpawns;
+    const Spawn *bSpawns;
+    const Spawn *commonRespawns;
+    int32_t numA, numB, numCommon, numDefaultA, numDefaultB;
+    mp::AABB zoneAABB[kMaxZones];
+    float zoneRot[kMaxZones];
+    int32_t numZones;
+    GoalRegionDev goals[4];
+    int32_t numGoals;
+    uint32_t simFlags;
+    int32_t autoReset;
+    uint32_t worldOffset;
+    mp::RandKey initRandKey;
+};
+
+// Host launchers (kernels.hip)
+struct LaunchCtx {
+    void *stream;       // hipStream_t
+    void *events[16];   // optional per-kernel timing events (start/stop pairs)
+    int timing;         // record events when nonzero
+};
+
+enum KernelId { kKSim = 0, kKVis = 1, kKObs = 2, kKLidar = 3, kNumTimedKernels = 4 };
+
+const char *kernelName(int k);
+size_t bvhLdsBytes(const SceneDev &sc);
+
+int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t ctor_train_ctrl[3], void *stream);
+int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream);
+int launchSimStep(const DevState &s, const SceneDev &sc, void *stream);
+int launchVisibility(const DevState &s, const SceneDev &sc, void *stream);
+int launchObservations(const DevState &s, const SceneDev &sc, void *stream);
+int launchLidar(const DevState &s, const SceneDev &sc, void *stream);
+int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, float *wf, uint32_t *explore,
+                      float *crumbs, void *stream);
+int launchFillActions(const DevState &s, const int32_t *src6, void *stream);
+
+} // namespace mpenv

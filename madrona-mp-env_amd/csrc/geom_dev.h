@@ -1,0 +1,426 @@
+// geom_dev.h — gfx950 device geometry: compressed 4-wide BVH traversal with
+// nodes and triangles staged in LDS, a register-resident byte stack, and the
+// agent-capsule test (mesh_bvh.inl:110-1127, utils.cpp:10-138).
+//
+// Design:
+//   * the whole collision BVH (simple_map: 61 x 64 B nodes + 756 x 12 B
+//     vertices = 13 KB) is copied into LDS once per workgroup; every
+//     traversal reads LDS only (ds_read), never HBM;
+//   * the traversal stack is a 16-entry byte stack held in two 64-bit
+//     registers (node indices < 256) — no scratch memory, no LDS stack;
+//   * child-visit order and every float expression match the reference
+//     (and the CPU oracle) exactly, so hits are bit-identical.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+
+#pragma clang fp contract(off)
+
+namespace mpenv {
+
+#define MP_LDS __attribute__((address_space(3)))
+
+struct LBVH {
+    const MP_LDS BVHNode *nodes;
+    const MP_LDS float *verts;
+};
+
+// Byte stack: push shifts left by 8 across a 128-bit register pair.
+struct ByteStack {
+    uint64_t lo, hi;
+    int n;
+};
+
+__device__ __forceinline__ void bsPush(ByteStack &s, uint32_t v)
+{
+    s.hi = (s.hi << 8) | (s.lo >> 56);
+    s.lo = (s.lo << 8) | (uint64_t)v;
+    s.n += 1;
+}
+
+__device__ __forceinline__ uint32_t bsPop(ByteStack &s)
+{
+    uint32_t v = (uint32_t)(s.lo & 0xffu);
+    s.lo = (s.lo >> 8) | (s.hi << 56);
+    s.hi >>= 8;
+    s.n -= 1;
+    return v;
+}
+
+// Stage nodes + vertices into dynamic LDS (all threads participate).
+__device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc)
+{
+    const int node_words = sc.numNodes * 16; // 64 B per node
+    const uint4 *src_n = reinterpret_cast<const uint4 *>(sc.nodes);
+    uint4 *dst_n = reinterpret_cast<uint4 *>(smem);
+    for (int k = threadIdx.x; k < node_words / 4; k += blockDim.x) dst_n[k] = src_n[k];
+    const int vert_words = sc.numVerts * 3;
+    const uint32_t *src_v = reinterpret_cast<const uint32_t *>(sc.verts);
+    uint32_t *dst_v = reinterpret_cast<uint32_t *>(smem + (size_t)node_words * 4);
+    for (int k = threadIdx.x; k < vert_words; k += blockDim.x) dst_v[k] = src_v[k];
+    __syncthreads();
+    LBVH b;
+    b.nodes = (const MP_LDS BVHNode *)(smem);
+    b.verts = (const MP_LDS float *)(smem + (size_t)node_words * 4);
+    return b;
+}
+
+__device__ __forceinline__ void loadTri(const LBVH &b, int tri, mp::Vec3 &a, mp::Vec3 &bb, mp::Vec3 &c)
+{
+    const MP_LDS float *p = b.verts + tri * 9;
+    a = mp::v3(p[0], p[1], p[2]);
+    bb = mp::v3(p[3], p[4], p[5]);
+    c = mp::v3(p[6], p[7], p[8]);
+}
+
+struct RayTxfmD {
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+};
+
+// mesh_bvh.inl:584-620 (shear constants only; see oracle)
+__device__ __forceinline__ RayTxfmD rayTxfm(mp::Vec3 d, mp::Vec3 inv_d)
+{
+    float abs_x = mp::fabs_(d.x), abs_y = mp::fabs_(d.y), abs_z = mp::fabs_(d.z);
+    int kz;
+    if (abs_x > abs_y && abs_x > abs_z) kz = 0;
+    else if (abs_y > abs_z) kz = 1;
+    else kz = 2;
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    if (mp::comp(d, kz) < 0.f) { int t = kx; kx = ky; ky = t; }
+    RayTxfmD t;
+    t.kx = kx; t.ky = ky; t.kz = kz;
+    t.Sx = mp::comp(d, kx) * mp::comp(inv_d, kz);
+    t.Sy = mp::comp(d, ky) * mp::comp(inv_d, kz);
+    t.Sz = mp::comp(inv_d, kz);
+    return t;
+}
+
+// mesh_bvh.inl:433-554, backface culling
+__device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, const RayTxfmD &tx, mp::Vec3 org,
+                                       float t_max, float &out_t)
+{
+    using namespace mp;
+    const Vec3 A = ta - org, B = tb - org, C = tc - org;
+    const float Az_ = comp(A, tx.kz), Bz_ = comp(B, tx.kz), Cz_ = comp(C, tx.kz);
+    const float Ax = fma_(-tx.Sx, Az_, comp(A, tx.kx));
+    const float Ay = fma_(-tx.Sy, Az_, comp(A, tx.ky));
+    const float Bx = fma_(-tx.Sx, Bz_, comp(B, tx.kx));
+    const float By = fma_(-tx.Sy, Bz_, comp(B, tx.ky));
+    const float Cx = fma_(-tx.Sx, Cz_, comp(C, tx.kx));
+    const float Cy = fma_(-tx.Sy, Cz_, comp(C, tx.ky));
+    float U = fma_(Cx, By, -(Cy * Bx));
+    float V = fma_(Ax, Cy, -(Ay * Cx));
+    float W = fma_(Bx, Ay, -(By * Ax));
+    if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        double CxBy = (double)Cx * (double)By;
+        double CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        double AxCy = (double)Ax * (double)Cy;
+        double AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        double BxAy = (double)Bx * (double)Ay;
+        double ByAx = (double)By * (double)Ax;
+        W = (float)(BxAy - ByAx);
+        if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
+    }
+    float det = U + V + W;
+    if (det == 0.f) return false;
+    const float Az = tx.Sz * Az_;
+    const float Bz = tx.Sz * Bz_;
+    const float Cz = tx.Sz * Cz_;
+    const float T = fma_(U, Az, fma_(V, Bz, W * Cz));
+    if (T < 0.0f || T > t_max * det) return false;
+    const float rcpDet = 1.0f / det;
+    out_t = T * rcpDet;
+    return true;
+}
+
+__device__ __forceinline__ float expScaleD(int8_t e) { return mp::u2f((uint32_t)((int32_t)e + 127) << 23); }
+
+// MeshBVH::traceRay (mesh_bvh.inl:110-208) over the LDS-resident BVH.
+// Returns hit flag; *t_out = closest hit t when hit.
+__device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out)
+{
+    using namespace mp;
+    const float diveps = 0.0000001f;
+    Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
+    RayTxfmD tx = rayTxfm(ray_d, inv_d);
+    // Loop-invariant in the reference (recomputed per node there; same bits).
+    const float rayXInv = copysign_(ray_d.x == 0 ? 1 / diveps : 1 / ray_d.x, ray_d.x);
+    const float rayYInv = copysign_(ray_d.y == 0 ? 1 / diveps : 1 / ray_d.y, ray_d.y);
+    const float rayZInv = copysign_(ray_d.z == 0 ? 1 / diveps : 1 / ray_d.z, ray_d.z);
+
+    float t_max = kFltMax;
+    bool ray_hit = false;
+    ByteStack st;
+    st.lo = 0; st.hi = 0; st.n = 0;
+    bsPush(st, 0);
+    while (st.n > 0) {
+        const uint32_t node_idx = bsPop(st);
+        const MP_LDS BVHNode &node = b.nodes[node_idx];
+        const float dirQuantX = expScaleD(node.expX) * rayXInv;
+        const float dirQuantY = expScaleD(node.expY) * rayYInv;
+        const float dirQuantZ = expScaleD(node.expZ) * rayZInv;
+        const float originQuantX = (node.minX - ray_o.x) * rayXInv;
+        const float originQuantY = (node.minY - ray_o.y) * rayYInv;
+        const float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int32_t child = node.children[i];
+            if (child == -1) continue;
+            float t_near_x = node.qMinX[i] * dirQuantX + originQuantX;
+            float t_near_y = node.qMinY[i] * dirQuantY + originQuantY;
+            float t_near_z = node.qMinZ[i] * dirQuantZ + originQuantZ;
+            float t_far_x = node.qMaxX[i] * dirQuantX + originQuantX;
+            float t_far_y = node.qMaxY[i] * dirQuantY + originQuantY;
+            float t_far_z = node.qMaxZ[i] * dirQuantZ + originQuantZ;
+            float t_near = fmax_(fmin_(t_near_x, t_far_x),
+                                 fmax_(fmin_(t_near_y, t_far_y), fmax_(fmin_(t_near_z, t_far_z), 0.f)));
+            float t_far = fmin_(fmax_(t_far_x, t_near_x),
+                                fmin_(fmax_(t_far_y, t_near_y), fmin_(fmax_(t_far_z, t_near_z), t_max)));
+            if (t_near <= t_far) {
+                if (child & 0x80000000) {
+                    const int leaf = child & 0x7fffffff;
+                    const int ntri = node.triSize[i];
+                    bool hit_tri = false;
+                    float hit_t = 0.f;
+                    float leaf_tmax = t_max;
+                    for (int k = 0; k < ntri; k++) {
+                        Vec3 a, bb, c;
+                        loadTri(b, leaf + k, a, bb, c);
+                        if (rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t)) {
+                            hit_tri = true;
+                            leaf_tmax = hit_t;
+                        }
+                    }
+                    if (hit_tri) {
+                        ray_hit = true;
+                        t_max = hit_t;
+                    }
+                } else {
+                    bsPush(st, (uint32_t)child);
+                }
+            }
+        }
+    }
+    t_out = t_max;
+    return ray_hit;
+}
+
+// mesh_bvh.inl:817-855
+__device__ __forceinline__ bool sphereNodeCheckD(mp::Vec3 o, mp::Vec3 inv_d, float t_max, float r, mp::AABB aabb)
+{
+    using namespace mp;
+    AABB e = aabb;
+    e.pMin.x -= r; e.pMin.y -= r; e.pMin.z -= r;
+    e.pMax.x += r; e.pMax.y += r; e.pMax.z += r;
+    float t_min = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float inv_d_i = comp(inv_d, i);
+        float b_min, b_max;
+        if (!__builtin_signbit(inv_d_i)) {
+            b_min = comp(e.pMin, i); b_max = comp(e.pMax, i);
+        } else {
+            b_min = comp(e.pMax, i); b_max = comp(e.pMin, i);
+        }
+        float i_min = (b_min - comp(o, i)) * inv_d_i;
+        float i_max = (b_max - comp(o, i)) * inv_d_i;
+        t_min = i_min > t_min ? i_min : t_min;
+        t_max = i_max < t_max ? i_max : t_max;
+    }
+    return t_min < t_max;
+}
+
+// mesh_bvh.inl:885-1127 (same quirks as the oracle restatement)
+__device__ __forceinline__ float sphereTriD(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, mp::Vec3 ray_o, mp::Vec3 ray_d,
+                                            float t_max, float r, mp::Vec3 &out_n)
+{
+    using namespace mp;
+    const Vec3 e01 = tb - ta, e02 = tc - ta, e12 = tc - tb;
+    const Vec3 v0 = ta - ray_o, v1 = tb - ray_o, v2 = tc - ray_o;
+    Vec3 nu = computeTriangleGeoNormal(e01, e02, e12);
+    float n_len = length(nu);
+    Vec3 n = nu / n_len;
+    const float n_dot_d = dot(n, ray_d);
+    const float r2 = r * r;
+
+    if (fabs_(dot(v0, n)) <= r) {
+        Vec3 q = triangleClosestPointToOrigin(v0, v1, v2, e01, e02);
+        float q_len2 = length2(q);
+        if (q_len2 <= r2) {
+            float q_len = sqrt_(q_len2);
+            out_n = q_len > 0.0f ? q / q_len : kUp;
+            return 0.f;
+        }
+    } else {
+        float abs_n_dot_d = fabs_(n_dot_d);
+        if (abs_n_dot_d > 1.0e-6f) {
+            float sgn = copysign_(1.f, n_dot_d);
+            Vec3 extruded_delta = sgn * r * n;
+            Vec3 v0e = v0 - extruded_delta;
+            float plane_t = dot(v0e, n) / n_dot_d;
+            if (plane_t * abs_n_dot_d < -r || plane_t >= t_max) return t_max;
+            if (plane_t >= 0.0f) {
+                Vec3 e = cross(ray_d, v0e);
+                float v = -dot(e02, e) * sgn;
+                float w = dot(e01, e) * sgn;
+                if (v >= 0.f && w >= 0.f && v + w <= n_len * abs_n_dot_d) {
+                    out_n = -sgn * n;
+                    return plane_t;
+                }
+            }
+        }
+    }
+
+    const float edge_eps = 1e-6f;
+    const float d_len2 = length2(ray_d);
+    float hit_t = t_max;
+    // testEdge x3
+    {
+        const Vec3 axes[3] = { e01, e02, e12 };
+        const Vec3 bases[3] = { v0, v0, v1 };
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            Vec3 axis = axes[k];
+            Vec3 start = -bases[k];
+            const float s_dot_a = dot(start, axis);
+            const float d_dot_a = dot(ray_d, axis);
+            const float e_dot_a = s_dot_a + d_dot_a;
+            if (s_dot_a < 0.0f && e_dot_a < 0.0f) continue;
+            const float a_len2 = length2(axis);
+            if (s_dot_a > a_len2 && e_dot_a > a_len2) continue;
+            float a = a_len2 * d_len2 - d_dot_a * d_dot_a;
+            if (fabs_(a) < edge_eps) continue;
+            float bq = a_len2 * dot(start, ray_d) - d_dot_a * s_dot_a;
+            float c = a_len2 * (length2(start) - r2) - s_dot_a * s_dot_a;
+            float det = bq * bq - a * c;
+            if (det < 0.0f) continue;
+            float t = -(bq + sqrt_(det)) / a;
+            if (t < 0.0f || t >= hit_t) continue;
+            if (s_dot_a + t * d_dot_a < 0.0f || s_dot_a + t * d_dot_a > a_len2) continue;
+            hit_t = t;
+        }
+    }
+    // testVert x3 (mesh_bvh.inl:1073-1104 quirk: ray_o - relative vertex)
+    {
+        const Vec3 vs[3] = { v0, v1, v2 };
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            Vec3 m = ray_o - vs[k];
+            float bq = dot(m, ray_d);
+            float c = dot(m, m) - r2;
+            if (c > 0.0f && bq > 0.0f) continue;
+            float discr = bq * bq - c;
+            if (discr < 0.0f) continue;
+            float t = -bq - sqrt_(discr);
+            if (t < 0.f) { hit_t = 0.f; continue; }
+            if (t >= hit_t) continue;
+            hit_t = t;
+        }
+    }
+    if (hit_t >= t_max) return t_max;
+    Vec3 hp = ray_d * hit_t;
+    Vec3 ct = triangleClosestPointToOrigin(v0 - hp, v1 - hp, v2 - hp, e01, e02);
+    out_n = normalize(ct);
+    return hit_t;
+}
+
+struct SphereHit {
+    float t;
+    mp::Vec3 n; // valid only when t < FLT_MAX (the reference writes the normal only on a hit)
+};
+
+// MeshBVH::sphereCast (mesh_bvh.inl:743-815).
+__device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r)
+{
+    using namespace mp;
+    Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
+    Vec3 closest = v3(0.f, 0.f, 0.f);
+    const float t_max0 = kFltMax;
+    float hit_t = t_max0;
+    ByteStack st;
+    st.lo = 0; st.hi = 0; st.n = 0;
+    bsPush(st, 0);
+    while (st.n > 0) {
+        const uint32_t node_idx = bsPop(st);
+        const MP_LDS BVHNode &node = b.nodes[node_idx];
+        const float sx = expScaleD(node.expX), sy = expScaleD(node.expY), sz = expScaleD(node.expZ);
+        for (int i = 0; i < 4; i++) {
+            const int32_t child = node.children[i];
+            if (child == -1) continue;
+            AABB cb;
+            cb.pMin = v3(node.minX + sx * node.qMinX[i], node.minY + sy * node.qMinY[i], node.minZ + sz * node.qMinZ[i]);
+            cb.pMax = v3(node.minX + sx * node.qMaxX[i], node.minY + sy * node.qMaxY[i], node.minZ + sz * node.qMaxZ[i]);
+            if (sphereNodeCheckD(ray_o, inv_d, hit_t, r, cb)) {
+                if (child & 0x80000000) {
+                    const int leaf = child & 0x7fffffff;
+                    const int ntri = node.triSize[i];
+                    Vec3 leaf_n = v3(0.f, 0.f, 0.f);
+                    float leaf_t = hit_t;
+                    for (int k = 0; k < ntri; k++) {
+                        Vec3 a, bb, c;
+                        loadTri(b, leaf + k, a, bb, c);
+                        leaf_t = sphereTriD(a, bb, c, ray_o, ray_d, leaf_t, r, leaf_n);
+                    }
+                    if (leaf_t < hit_t) {
+                        hit_t = leaf_t;
+                        closest = leaf_n;
+                    }
+                } else {
+                    bsPush(st, (uint32_t)child);
+                }
+            }
+        }
+    }
+    SphereHit h;
+    h.t = hit_t;
+    h.n = closest;
+    return h;
+}
+
+constexpr float kCapsuleRadius = 15.f;         // consts::agentRadius
+constexpr float kCapsuleSegment = 65.f - 30.f; // standHeight - 2 * agentRadius
+
+struct WorldHit {
+    bool hit;
+    float t;
+    int entity; // agent index within the world, -1 none
+};
+
+// traceRayAgainstWorld (utils.cpp:10-72): BVH then the world's N capsules.
+// Capsule bases are read from the SoA position columns (cached).
+__device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__restrict__ px,
+                                                const float *__restrict__ py, const float *__restrict__ pz,
+                                                int64_t g0, int N, mp::Vec3 org, mp::Vec3 d)
+{
+    using namespace mp;
+    float min_t = kFltMax;
+    float tb;
+    bool hit = bvhTraceRayD(b, org, d, tb);
+    if (hit) min_t = tb;
+    int ent = -1;
+    for (int j = 0; j < N; j++) {
+        Vec3 co = v3(px[g0 + j], py[g0 + j], pz[g0 + j]);
+        co.z += kCapsuleRadius;
+        Vec3 tr = org - co;
+        float t = intersectRayZOriginCapsule(tr, d, kCapsuleRadius, kCapsuleSegment);
+        if (t != 0 && t < min_t) {
+            min_t = t;
+            hit = true;
+            ent = j;
+        }
+    }
+    WorldHit h;
+    h.hit = hit;
+    h.t = min_t;
+    h.entity = ent;
+    return h;
+}
+
+} // namespace mpenv

@@ -1,0 +1,1787 @@
+// kernels.hip — the world-batched Zone step as hand-written gfx950 kernels.
+//
+// The reference runs ~40 ECS systems per step, each a device-wide
+// ParallelForNode with a grid barrier in between (sim.cpp:5342-5842;
+// NVRTC megakernel).  Every dependency between those systems is *within a
+// world* (SURVEY.md §8e), so here a workgroup owns a tile of worlds and the
+// system chain becomes LDS/L1-local __syncthreads() barriers.  The step is
+// four kernels:
+//
+//   k_sim    world tile, lane = agent: movement + sphere casts, fire, damage,
+//            respawn, heal, zone, breadcrumbs, match info, goals, explore,
+//            rewards, done, reset  (sim.cpp:5347-5841 up to resetSystem)
+//   k_vis    lane = (agent, opponent): frustum + line-of-sight rays
+//            (opponentsWriteVisibilitySystem, sim.cpp:2526-2560)
+//   k_obs    lane = agent: opponent masks + all observation tensors
+//            (sim.cpp:2562-3052)
+//   k_lidar  lane = ray: 80 lidar rays per agent (sim.cpp:3324-3506)
+//
+// All traversals read an LDS-resident copy of the BVH (geom_dev.h).  Every
+// arithmetic expression follows the reference (and the CPU oracle) term by
+// term with -ffp-contract=off so that results are bit-identical.
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+#include "geom_dev.h"
+
+#pragma clang fp contract(off)
+
+namespace mpenv {
+
+using namespace mp;
+
+// ----------------------------------------------------- consts.hpp:7-72
+namespace c {
+constexpr int kNumStepsPerZone = 600;
+constexpr int kZonePointInterval = 20;
+constexpr int kZoneWinPoints = 125;
+constexpr int kPoseTransitionSpeed = 10;
+constexpr float kAgentRadius = 15.f;
+constexpr float kStandHeight = 65.f;
+constexpr float kCrouchHeight = 47.f;
+constexpr float kProneHeight = 30.f;
+constexpr float kMaxRunVelocity = 400.f;
+constexpr float kMaxWalkVelocity = 200.f;
+constexpr float kMaxCrouchVelocity = 50.f;
+constexpr float kMaxProneVelocity = 20.f;
+constexpr float kDeaccelerateRate = 1000.f;
+constexpr int kRespawnInvincibleSteps = 5;
+constexpr int kOutOfCombatSteps = 150;
+constexpr float kAutohealPerStep = 5.f;
+constexpr int kEpisodeLen = 3000;
+constexpr int kNumMoveAmountBuckets = 3;
+constexpr int kNumMoveAngleBuckets = 8;
+constexpr float kDeltaT = 0.05f;
+constexpr int kDiscreteAimYawBuckets = 13;
+constexpr int kDiscreteAimPitchBuckets = 7;
+constexpr int kGridMax = 40;
+// mgr.cpp:1383-1395 weapon stats
+constexpr int kMagSize = 30;
+constexpr int kReloadTime = 30;
+constexpr float kDmgPerBullet = 10.f;
+constexpr float kAccuracyScale = 0.005f;
+constexpr int kNumWeaponTypes = 1;
+} // namespace c
+
+enum { kStand = 0, kCrouch = 1, kProne = 2 };
+constexpr uint32_t kFlagNoRespawn = 1u << 3;
+constexpr uint32_t kFlagSpawnInMiddle = 1u << 0;
+constexpr uint32_t kFlagRandomizeHP = 1u << 1;
+constexpr uint32_t kFlagHardcodedSpawns = 1u << 6;
+constexpr uint32_t kFlagEnableCurriculum = 1u << 5;
+constexpr int32_t kFlagCrumbRequest = 64; // transient (leave -> append)
+
+__device__ __forceinline__ float viewHeightD(int pose)
+{
+    float top = pose == kStand ? c::kStandHeight : (pose == kCrouch ? c::kCrouchHeight : c::kProneHeight);
+    return top - c::kAgentRadius;
+}
+
+__device__ __forceinline__ int32_t f2iSatD(float f)
+{
+    if (!(f == f)) return 0;
+    if (f >= 2147483520.f) return INT32_MAX;
+    if (f <= -2147483648.f) return INT32_MIN;
+    return (int32_t)f;
+}
+
+// ------------------------------------------------------ SoA accessors
+__device__ __forceinline__ Vec3 ldPos(const DevState &S, int64_t g) { return v3(S.px[g], S.py[g], S.pz[g]); }
+__device__ __forceinline__ void stPos(const DevState &S, int64_t g, Vec3 p) { S.px[g] = p.x; S.py[g] = p.y; S.pz[g] = p.z; }
+__device__ __forceinline__ Vec3 ldVel(const DevState &S, int64_t g) { return v3(S.vx[g], S.vy[g], S.vz[g]); }
+__device__ __forceinline__ void stVel(const DevState &S, int64_t g, Vec3 v) { S.vx[g] = v.x; S.vy[g] = v.y; S.vz[g] = v.z; }
+__device__ __forceinline__ Quat ldRot(const DevState &S, int64_t g) { return quat(S.rw[g], S.rx[g], S.ry[g], S.rz[g]); }
+__device__ __forceinline__ void stRot(const DevState &S, int64_t g, Quat q) { S.rw[g] = q.w; S.rx[g] = q.x; S.ry[g] = q.y; S.rz[g] = q.z; }
+__device__ __forceinline__ Quat ldAimRot(const DevState &S, int64_t g) { return quat(S.aw[g], S.ax[g], S.ay[g], S.az[g]); }
+__device__ __forceinline__ void stAimRot(const DevState &S, int64_t g, Quat q) { S.aw[g] = q.w; S.ax[g] = q.x; S.ay[g] = q.y; S.az[g] = q.z; }
+__device__ __forceinline__ RNG ldRng(const DevState &S, int64_t g)
+{
+    RNG r; r.key.a = (uint32_t)S.rngA[g]; r.key.b = (uint32_t)S.rngB[g]; r.ctr = (uint32_t)S.rngCtr[g];
+    return r;
+}
+__device__ __forceinline__ void stRng(const DevState &S, int64_t g, const RNG &r)
+{
+    S.rngA[g] = (int32_t)r.key.a; S.rngB[g] = (int32_t)r.key.b; S.rngCtr[g] = (int32_t)r.ctr;
+}
+__device__ __forceinline__ RNG ldWRng(const DevState &S, int w)
+{
+    RNG r; r.key.a = (uint32_t)S.wRngA[w]; r.key.b = (uint32_t)S.wRngB[w]; r.ctr = (uint32_t)S.wRngCtr[w];
+    return r;
+}
+__device__ __forceinline__ void stWRng(const DevState &S, int w, const RNG &r)
+{
+    S.wRngA[w] = (int32_t)r.key.a; S.wRngB[w] = (int32_t)r.key.b; S.wRngCtr[w] = (int32_t)r.ctr;
+}
+__device__ __forceinline__ void setFlag(const DevState &S, int64_t g, int32_t bit, bool v)
+{
+    int32_t f = S.flags[g];
+    S.flags[g] = v ? (f | bit) : (f & ~bit);
+}
+
+struct AimD {
+    float yaw, pitch;
+    Quat rot;
+};
+
+// utils.cpp:140-167 computeAim
+__device__ __forceinline__ AimD computeAimD(float yaw, float pitch)
+{
+    if (yaw < -kPi) yaw += 2.f * kPi;
+    else if (yaw > kPi) yaw -= 2.f * kPi;
+    if (pitch < -0.25f * kPi) pitch = -0.25f * kPi;
+    if (pitch > 0.25f * kPi) pitch = 0.25f * kPi;
+    Quat r = angleAxis(yaw, kUp) * angleAxis(pitch, kRight);
+    r = qnormalize(r);
+    AimD a;
+    a.yaw = yaw; a.pitch = pitch; a.rot = r;
+    return a;
+}
+
+__device__ __forceinline__ void stAim(const DevState &S, int64_t g, const AimD &a)
+{
+    S.ayaw[g] = a.yaw; S.apitch[g] = a.pitch; stAimRot(S, g, a.rot);
+}
+
+// ====================================================== per-agent systems
+// sim.cpp:2057-2091 applyBotActionsSystem
+__device__ void applyBotActionsD(const DevState &S, int64_t g)
+{
+    if (S.policy[g] != -1) return;
+    const int32_t *hb = &S.botAction[7 * g];
+    S.discreteAction[4 * g + 0] = hb[0];
+    S.discreteAction[4 * g + 1] = hb[1];
+    S.discreteAction[4 * g + 2] = hb[4];
+    S.discreteAction[4 * g + 3] = hb[6];
+    const float turn_delta = 10.f / (float)(5 / 2);
+    S.aimAction[2 * g] = turn_delta * (float)(hb[2] - 5 / 2);
+    S.aimAction[2 * g + 1] = turn_delta * (float)(hb[3] - 5 / 2);
+}
+
+// sim.cpp:2093-2199 pvpMovementSystem
+__device__ void pvpMovementD(const DevState &S, int64_t g)
+{
+    if (S.alive[g] == 0.f) return;
+    const int32_t a_amount = S.discreteAction[4 * g + 0];
+    const int32_t a_angle = S.discreteAction[4 * g + 1];
+    const int32_t a_stand = S.discreteAction[4 * g + 3];
+    Vec3 vel = ldVel(S, g);
+    {
+        float v_len = length(vel);
+        if (v_len > 0.f) {
+            Vec3 norm_v = vel / v_len;
+            v_len -= c::kDeaccelerateRate * c::kDeltaT;
+            v_len = fmaxD(0.f, v_len);
+            vel = norm_v * v_len;
+        }
+    }
+    int cur = S.curPose[g], tgt = S.tgtPose[g], tr = S.transRem[g];
+    if (tr > 0) {
+        tr -= 1;
+        if (tr == 0) cur = tgt;
+    }
+    if (a_stand != tgt) {
+        tgt = a_stand;
+        int dst = tgt - cur;
+        dst = dst < 0 ? -dst : dst;
+        tr = dst * (c::kPoseTransitionSpeed / 2);
+    }
+    S.curPose[g] = cur; S.tgtPose[g] = tgt; S.transRem[g] = tr;
+
+    float accel_max = 3000;
+    if (cur == kCrouch) accel_max = 100;
+    else if (cur == kProne) accel_max = 50;
+    float move_amount = (float)a_amount * (accel_max / (float)(c::kNumMoveAmountBuckets - 1));
+    const float per_bucket = 2.f * kPi / float(c::kNumMoveAngleBuckets);
+    float move_angle = float(a_angle) * per_bucket;
+    float f_x = move_amount * sinf_(move_angle);
+    float f_y = move_amount * cosf_(move_angle);
+    vel = vel + rotateVec(ldRot(S, g), v3(f_x, f_y, 0)) * c::kDeltaT;
+    if (move_amount != 0) S.respawnSteps[g] = 0;
+    float v_len = length(vel);
+    if (v_len == 0.f) {
+        stVel(S, g, vel);
+        return;
+    }
+    float max_vel = S.maxVel[g];
+    {
+        const float max_change = 510.f;
+        float tgt_v;
+        if (cur == kStand) tgt_v = a_amount == 2 ? c::kMaxRunVelocity : c::kMaxWalkVelocity;
+        else if (cur == kCrouch) tgt_v = c::kMaxCrouchVelocity;
+        else tgt_v = c::kMaxProneVelocity;
+        float diff = tgt_v - max_vel;
+        float adj = fmaxD(fminD(diff, max_change), -max_change);
+        max_vel += adj;
+    }
+    S.maxVel[g] = max_vel;
+    Vec3 v_norm = vel / v_len;
+    v_len = fminD(v_len, max_vel);
+    stVel(S, g, v_norm * v_len);
+}
+
+// sim.cpp:2266-2370 continuous then discrete aim
+__device__ void pvpAimD(const DevState &S, int64_t g)
+{
+    if (S.alive[g] == 0.f) return;
+    float yaw = S.ayaw[g], pitch = S.apitch[g];
+    yaw += S.aimAction[2 * g] * c::kDeltaT;
+    pitch += S.aimAction[2 * g + 1] * c::kDeltaT;
+    AimD a = computeAimD(yaw, pitch);
+    yaw = a.yaw; pitch = a.pitch;
+    // pvpContinuousAimSystem writes Rotation too; it is overwritten below.
+    const float yaw_turn[7] = { 0, 0.00390625f * kPi, 0.0078125f * kPi, 0.015625f * kPi,
+                                0.03125f * kPi, 0.0625f * kPi, 0.125f * kPi };
+    const float pitch_turn[4] = { 0, 0.0078125f * kPi, 0.015625f * kPi, 0.03125f * kPi };
+    int yb = S.discreteAim[2 * g] - c::kDiscreteAimYawBuckets / 2;
+    int yba = yb < 0 ? -yb : yb;
+    if (yb < 0) yaw -= yaw_turn[yba];
+    else yaw += yaw_turn[yba];
+    int pb = S.discreteAim[2 * g + 1] - c::kDiscreteAimPitchBuckets / 2;
+    int pba = pb < 0 ? -pb : pb;
+    if (pb < 0) pitch -= pitch_turn[pba];
+    else pitch += pitch_turn[pba];
+    a = computeAimD(yaw, pitch);
+    stAim(S, g, a);
+    stRot(S, g, qnormalize(angleAxis(a.yaw, kUp)));
+}
+
+__device__ __forceinline__ Vec3 rotate2DD(Vec3 dir, float radians) // sim.cpp:874-879
+{
+    float cc = cosf_(radians);
+    float s = sinf_(radians);
+    return v3(cc * dir.x - s * dir.y, s * dir.x + cc * dir.y, 0);
+}
+
+// sim.cpp:889-1039 applyVelocitySystem + updateMoveStateSystem
+__device__ void applyVelocityD(const DevState &S, const LBVH &bvh, int64_t g)
+{
+    const Vec3 x = ldPos(S, g);
+    Vec3 v = ldVel(S, g);
+    v.z = 0;
+    Vec3 new_pos = x;
+    Vec3 new_vel = v3(0.f, 0.f, 0.f);
+    const int pose = S.curPose[g];
+    float v_len = length(v);
+    do {
+        if (v_len == 0.f) break;
+        Vec3 v_norm = v / v_len;
+        float move_dist = v_len * c::kDeltaT;
+        const float buffer = 0.05f * c::kAgentRadius;
+        const float r = c::kAgentRadius;
+        float top = c::kStandHeight - r;
+        float low_check = c::kProneHeight;
+        if (pose == kCrouch) {
+            top = c::kCrouchHeight - r;
+        } else if (pose == kProne) {
+            top = low_check;
+            low_check = c::kProneHeight - r + buffer;
+        }
+
+        Vec3 ray_o = x;
+        ray_o.z += top;
+        Vec3 normal = v3(0.f, 0.f, 0.f);
+        {
+            SphereHit h = bvhSphereCastD(bvh, ray_o, -kUp, r);
+            if (h.t < kFltMax) normal = h.n;
+        }
+        if (normal.z > 0.0f && (double)normal.z < 0.7 && dot(normal, v_norm) < 0.0f) break;
+
+        ray_o = x + v_norm * buffer * 0.5f;
+        ray_o.z += low_check;
+        float low_dist;
+        {
+            SphereHit h = bvhSphereCastD(bvh, ray_o, v_norm, r);
+            low_dist = h.t;
+            if (h.t < kFltMax) normal = h.n;
+        }
+        float high_dist = low_dist;
+        bool high_hit = false;
+        if (pose != kProne) {
+            ray_o.z = x.z + top;
+            SphereHit h = bvhSphereCastD(bvh, ray_o, v_norm, r);
+            high_dist = h.t;
+            if (high_dist < low_dist) {
+                low_dist = high_dist;
+                normal = h.n;
+                high_hit = true;
+            }
+        }
+        bool stuck = low_dist == 0.0f || high_dist == 0.0f;
+        low_dist = fmaxD(0.0f, low_dist - buffer);
+        high_dist = fmaxD(0.0f, high_dist - buffer);
+        Vec3 hit_pos = x + v_norm * fminD(low_dist, move_dist);
+
+        if (move_dist > low_dist) {
+            Vec3 slide_dir = normalize(cross(kUp, normal));
+            if (dot(slide_dir, v_norm) < 0) slide_dir = -slide_dir;
+            ray_o = x + v_norm * low_dist;
+            ray_o.z += high_hit ? top : low_check;
+            float slide = bvhSphereCastD(bvh, ray_o, slide_dir, r).t;
+            slide = fmaxD(0.0f, slide - buffer);
+            float max_move = move_dist - low_dist;
+            slide = fminD(slide, max_move);
+            if (slide > 0.0f) hit_pos = hit_pos + slide_dir * slide;
+        }
+
+        Vec3 ground_check = hit_pos;
+        ground_check.z += top;
+        float ground_dist = bvhSphereCastD(bvh, ground_check, -kUp, r).t;
+        if (ground_dist == kFltMax) break;
+
+        if (ground_dist <= 0.0f || stuck) {
+            float furthest = 0.0f;
+            int best_dir = -1;
+            for (int dir = 0; dir < 4; dir++) {
+                Vec3 dv = rotate2DD(v_norm, (float)dir * 3.14159f * 0.5f);
+                ray_o = x - dv * r * 2.0f;
+                ray_o.z += low_check;
+                float hd = bvhSphereCastD(bvh, ray_o, dv, r).t;
+                if (hd > furthest) {
+                    furthest = hd;
+                    best_dir = dir;
+                }
+            }
+            if (best_dir != -1) {
+                Vec3 dv = rotate2DD(v_norm, (float)best_dir * 3.14159f * 0.5f);
+                hit_pos = x + dv * (fminD(furthest - r * 2.0f, -buffer));
+                ground_check = hit_pos;
+                ground_check.z += top;
+                ground_dist = bvhSphereCastD(bvh, ground_check, -kUp, r).t;
+                if (ground_dist == kFltMax) break;
+            }
+        }
+
+        float fall_dist = fminD(ground_dist, top) + r;
+        Vec3 np = ground_check;
+        np.z -= fall_dist;
+        Vec3 to_new = np - x;
+        float to_new_dist = length(to_new);
+        if (to_new_dist == 0.f) break;
+        new_pos = np;
+        new_vel = to_new / c::kDeltaT;
+    } while (false);
+    // updateMoveStateSystem (sim.cpp:1030-1039)
+    stPos(S, g, new_pos);
+    stVel(S, g, new_vel);
+}
+
+// sim.cpp:1041-1104 fallSystem + updateMoveStatePostFallSystem
+__device__ void fallD(const DevState &S, const LBVH &bvh, int64_t g)
+{
+    if (S.alive[g] == 0.f) return;
+    const float fall_rate = 386.08858267717f;
+    const float cast_offset = c::kAgentRadius;
+    Vec3 pos = ldPos(S, g);
+    Vec3 ray_o = pos;
+    ray_o.z += c::kAgentRadius + cast_offset;
+    float ground = bvhSphereCastD(bvh, ray_o, -kUp, c::kAgentRadius).t;
+    if (ground == kFltMax || ground < cast_offset) return;
+    float fall = fminD(ground - cast_offset, fall_rate * c::kDeltaT);
+    pos.z -= fall;
+    S.pz[g] = pos.z;
+}
+
+// sim.cpp:1443-1615 fireSystem
+__device__ void fireD(const DevState &S, const LBVH &bvh, int w, int i)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    const int64_t g = g0 + i;
+    S.landedOn[g] = -1;
+    S.firedT[g] = -kFltMax;
+    int32_t flags = S.flags[g] & ~(kFlagSuccessfulKill | kFlagReloadedFullMag);
+    if (S.alive[g] == 0.f) {
+        S.flags[g] = flags;
+        return;
+    }
+    int32_t mag0 = S.magazine[2 * g], mag1 = S.magazine[2 * g + 1];
+    const int fire = S.discreteAction[4 * g + 2];
+    if (fire == 2) {
+        if (mag0 == c::kMagSize) flags |= kFlagReloadedFullMag;
+        mag0 = c::kMagSize;
+        mag1 = c::kReloadTime;
+    }
+    bool reloading = mag1 > 0;
+    if (reloading) mag1 -= 1;
+    bool should_fire = false;
+    if (!reloading && mag0 > 0) should_fire = fire == 1;
+    if (!should_fire) {
+        S.magazine[2 * g] = mag0;
+        S.magazine[2 * g + 1] = mag1;
+        S.flags[g] = flags;
+        return;
+    }
+    mag0 -= 1;
+    S.magazine[2 * g] = mag0;
+    S.magazine[2 * g + 1] = mag1;
+
+    Vec3 fire_from = ldPos(S, g);
+    fire_from.z += viewHeightD(S.curPose[g]);
+    RNG rng = ldRng(S, g);
+    float u1 = rngUniform(rng);
+    float u2 = rngUniform(rng);
+    stRng(S, g, rng);
+    float z1 = sqrt_(-2.f * logf_(u1)) * cosf_(2.f * kPi * u2);
+    float z2 = sqrt_(-2.f * logf_(u1)) * sinf_(2.f * kPi * u2);
+    const float acc = c::kAccuracyScale;
+    const float bias = 1.5f;
+    float up_delta = fminD(fmaxD((z1 + bias) * acc, 0.f), 4.f * acc);
+    float right_delta = fminD(fmaxD(z2 * acc, -4.f * acc), 4.f * acc);
+    AimD a = computeAimD(S.ayaw[g] + right_delta, S.apitch[g] + up_delta);
+    stAim(S, g, a);
+    Vec3 fire_dir = rotateVec(a.rot, kFwd);
+
+    WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, fire_from, fire_dir);
+    S.firedT[g] = h.hit ? h.t : kFltMax;
+    bool success = h.hit;
+    const int team = i / S.T, offset = i - team * S.T;
+    if (h.entity == -1) {
+        success = false;
+    } else {
+        const int tteam = h.entity / S.T;
+        if (success && tteam == team) success = false;
+        if (success && S.respawnSteps[g0 + h.entity] > 0) success = false;
+    }
+    if (success) {
+        S.landedOn[g] = h.entity;
+        if (S.hp[g0 + h.entity] <= c::kDmgPerBullet) flags |= kFlagSuccessfulKill;
+        S.dmg[(int64_t)offset * S.A + g0 + h.entity] = c::kDmgPerBullet;
+    }
+    S.flags[g] = flags;
+}
+
+// sim.cpp:1794-1836 applyDmgSystem
+__device__ void applyDmgD(const DevState &S, int64_t g)
+{
+    int32_t flags = S.flags[g] & ~kFlagWasKilled;
+    int was_shot = 0;
+    int rs = S.respawnSteps[g];
+    if (rs > 0) S.respawnSteps[g] = rs - 1;
+    float hp = S.hp[g];
+    for (int k = 0; k < S.T; k++) {
+        const int64_t di = (int64_t)k * S.A + g;
+        float d = S.dmg[di];
+        if (d > 0.f) {
+            was_shot += 1;
+            S.autohealSteps[g] = c::kOutOfCombatSteps;
+        }
+        hp -= d;
+        S.dmg[di] = 0.f;
+    }
+    S.wasShot[g] = was_shot;
+    if (S.alive[g] == 1.f && hp <= 0.f) flags |= kFlagWasKilled | kFlagHasDied;
+    if (hp <= 0.f) {
+        hp = 0.f;
+        S.alive[g] = 0.f;
+        stPos(S, g, v3(0, 0, 10000.f));
+        stVel(S, g, v3(0, 0, 0));
+    } else {
+        S.alive[g] = 1.f;
+    }
+    S.hp[g] = hp;
+    S.flags[g] = flags;
+}
+
+// sim.cpp:1875-1890 autoHealSystem
+__device__ void autoHealD(const DevState &S, int64_t g)
+{
+    if (S.alive[g] == 0.f) return;
+    int ah = S.autohealSteps[g];
+    float hp = S.hp[g];
+    if (ah == 0 && hp < 100.f) {
+        S.hp[g] = fminD(100.f, hp + c::kAutohealPerStep);
+    } else if (ah > 0) {
+        S.autohealSteps[g] = ah - 1;
+    }
+}
+
+// ====================================================== spawning / reset
+// utils.cpp:273-479 standardSpawnPoint (Zone task)
+__device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w, int ai, bool is_respawn,
+                                    bool use_middle, RNG &rng, Vec3 &out_pt, float &out_yaw)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    const int team = ai / S.T;
+    const uint32_t cur_step = (uint32_t)S.curStep[w];
+    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * kMaxSpawns];
+
+    const Spawn *options;
+    auto spawnAgent = [&](int idx) {
+        Spawn s = options[idx];
+        float x_rnd = rngUniform(rng);
+        float y_rnd = rngUniform(rng);
+        float z_rnd = rngUniform(rng);
+        float yaw_rnd = rngUniform(rng);
+        float x_min = s.region.pMin.x, x_diff = s.region.pMax.x - x_min;
+        float y_min = s.region.pMin.y, y_diff = s.region.pMax.y - y_min;
+        float z_min = s.region.pMin.z, z_diff = s.region.pMax.z - z_min;
+        out_pt = v3(x_min + x_rnd * x_diff, y_min + y_rnd * y_diff, z_min + z_rnd * z_diff);
+        out_yaw = s.yawMin + yaw_rnd * (s.yawMax - s.yawMin);
+    };
+
+    if (!is_respawn || sc.numCommon == 0) {
+        uint32_t *tracker;
+        int num_default, num_extra, num_spawns;
+        if (team == S.teamA[w]) {
+            options = sc.aSpawns;
+            num_default = sc.numDefaultA;
+            num_extra = sc.numA - sc.numDefaultA;
+            tracker = track;
+        } else {
+            options = sc.bSpawns;
+            num_default = sc.numDefaultB;
+            num_extra = sc.numB - sc.numDefaultB;
+            tracker = track + kMaxSpawns;
+        }
+        if (use_middle) {
+            options += num_default;
+            num_spawns = num_extra;
+        } else {
+            num_spawns = num_default;
+        }
+        int init_idx = -1;
+        for (int k = 0; k < 5; k++) {
+            int idx = rngI32(rng, 0, num_spawns);
+            if (tracker[idx] == cur_step) continue;
+            init_idx = idx;
+            break;
+        }
+        if (init_idx == -1) init_idx = rngI32(rng, 0, num_spawns);
+        spawnAgent(init_idx);
+        tracker[init_idx] = cur_step;
+        return;
+    }
+
+    options = sc.commonRespawns;
+    uint32_t *rtrack = track + 2 * kMaxSpawns;
+    const int cz = S.curZone[w];
+    AABB za = sc.zoneAABB[cz];
+    Vec3 zone_center = 0.5f * (za.pMin + za.pMax);
+    float best_score = kFltMax;
+    int best_idx = -1;
+    for (int s = 0; s < sc.numCommon; s++) {
+        uint32_t last_used = rtrack[s];
+        if (last_used == cur_step) continue;
+        float score = 0.f;
+        uint32_t elapsed = (uint32_t)(c::kDeltaT * float(cur_step - last_used));
+        const float elapsed_weight = 0.1f, dist_weight = 0.01f;
+        if (elapsed < 3.f) score += elapsed_weight * (3.f - elapsed);
+        Spawn sp = options[s];
+        Vec3 spawn_pt = 0.5f * (sp.region.pMin + sp.region.pMax);
+        for (int j = 0; j < N; j++) {
+            if (j == ai) continue;
+            if (S.alive[g0 + j] == 0.f) continue;
+            float dist = distance(spawn_pt, ldPos(S, g0 + j));
+            if (dist < 4.f * c::kAgentRadius) {
+                score += 100000.f;
+            } else {
+                if (j / S.T == team) continue;
+                score += dist_weight * (1.f / dist);
+            }
+        }
+        float dz = distance(spawn_pt, zone_center);
+        if (dz < 100.f) score += 1000000.f;
+        if (score < best_score) {
+            best_idx = s;
+            best_score = score;
+        }
+    }
+    if (best_idx < 0) best_idx = 0;
+    spawnAgent(best_idx);
+    rtrack[best_idx] = cur_step;
+}
+
+// utils.cpp:734-948 spawnAgents
+__device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool is_respawn)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    int num_dead = 0;
+    for (int i = 0; i < N; i++)
+        if (S.alive[g0 + i] == 0.f) num_dead++;
+    if (num_dead == 0) return;
+    RNG base = ldWRng(S, w);
+    (void)rngI32(base, 0, 0); // episodes[sampleI32(0, numEpisodes = 0)]
+    bool use_middle = false;
+    if (sc.simFlags & kFlagSpawnInMiddle) use_middle = rngUniform(base) < 0.5f;
+    const bool randomize_hp = (sc.simFlags & kFlagRandomizeHP) != 0;
+    const int cz = S.curZone[w];
+
+    // Dead set fixed before the loop (utils.cpp:767-780).
+    uint32_t dead_mask = 0;
+    for (int i = 0; i < N; i++)
+        if (S.alive[g0 + i] == 0.f) dead_mask |= 1u << i;
+
+    for (int ai = 0; ai < N; ai++) {
+        if (!(dead_mask & (1u << ai))) continue;
+        const int64_t g = g0 + ai;
+        Vec3 spawn_pt;
+        float spawn_yaw;
+        RNG rng = ldRng(S, g);
+        standardSpawnPointD(S, sc, w, ai, is_respawn, use_middle, rng, spawn_pt, spawn_yaw);
+        stRng(S, g, rng);
+        stPos(S, g, spawn_pt);
+        stRot(S, g, qnormalize(angleAxis(spawn_yaw, kUp)));
+        stAim(S, g, computeAimD(spawn_yaw, 0.f));
+        stVel(S, g, v3(0.f, 0.f, 0.f));
+        S.weapon[g] = rngI32(base, 0, c::kNumWeaponTypes);
+        if (randomize_hp) {
+            int tenth = rngI32(base, 1, 11);
+            S.hp[g] = float(tenth * 10);
+            S.magazine[2 * g] = rngI32(base, 0, c::kMagSize);
+            S.magazine[2 * g + 1] = 0;
+        } else {
+            S.hp[g] = 100.f;
+            S.magazine[2 * g] = c::kMagSize;
+            S.magazine[2 * g + 1] = 0;
+        }
+        S.respawnSteps[g] = is_respawn ? 0 : c::kRespawnInvincibleSteps;
+        S.autohealSteps[g] = 0;
+        {
+            AABB za = sc.zoneAABB[cz];
+            Vec3 zone_center = (za.pMax + za.pMin) / 2.f;
+            Quat to_zone = qinv(angleAxis(sc.zoneRot[cz], kUp));
+            za.pMin = rotateVec(to_zone, za.pMin);
+            za.pMax = rotateVec(to_zone, za.pMax);
+            Vec3 pz = rotateVec(to_zone, spawn_pt);
+            spawn_pt.z += c::kStandHeight / 2.f;
+            setFlag(S, g, kFlagInZone, aabbContains(za, pz));
+            S.minDistZone[g] = distance(spawn_pt, zone_center);
+        }
+        S.curPose[g] = kStand; S.tgtPose[g] = kStand; S.transRem[g] = 0;
+        S.maxVel[g] = c::kMaxWalkVelocity;
+        S.dyv[g] = 0.f; S.dpv[g] = 0.f;
+        S.alive[g] = 1.f;
+    }
+    stWRng(S, w, base);
+}
+
+// level_gen.cpp:330-582 resetPersistentEntities
+__device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, int w, RandKey episode_key)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    for (int i = 0; i < N; i++) {
+        const int64_t g = g0 + i;
+        stPos(S, g, v3(kFltMax, kFltMax, kFltMax));
+        RNG r = makeRNG(splitI(episode_key, (uint32_t)(i + 1)));
+        stRng(S, g, r);
+        S.landedOn[g] = -1;
+        S.respawnSteps[g] = 0;
+        S.autohealSteps[g] = 0;
+        S.wasShot[g] = 0;
+        S.firedT[g] = -kFltMax;
+        S.flags[g] = S.flags[g] & kFlagInZone; // successfulKill/wasKilled/hasDied/reloadedFullMag = false
+        S.alive[g] = 0.f;
+        float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
+        for (int k = 0; k < 6 * kOtherObs / 4; k++) lk[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < 18; k++) S.lkPos[g * 18 + k] = -1000.f;
+        S.bcPenalty[g] = 0.f;
+        S.bcLast[g] = -1;
+        S.bcSteps[g] = 0;
+    }
+    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * kMaxSpawns];
+    for (int k = 0; k < 3 * kMaxSpawns; k++) track[k] = 0xFFFFFFFFu;
+    spawnAgentsD(S, sc, w, false);
+
+    RNG base = ldWRng(S, w);
+    for (int i = 0; i < N; i++) {
+        const int64_t g = g0 + i;
+        S.sx[g] = S.px[g]; S.sy[g] = S.py[g]; S.sz[g] = S.pz[g];
+        for (int k = 0; k < 4; k++) S.discreteAction[4 * g + k] = 0;
+        S.aimAction[2 * g] = 0.f; S.aimAction[2 * g + 1] = 0.f;
+        S.newCells[g] = 0;
+        // level_gen.cpp:427-446: nine discarded coefficient draws.
+        base.ctr += 9;
+        float *rc = &S.rewardCoefs[9 * g];
+        rc[0] = 0.f; rc[1] = 0.5f; rc[2] = 0.005f; rc[3] = 0.05f; rc[4] = 0.01f;
+        rc[5] = 0.1f; rc[6] = 0.0005f; rc[7] = 1.f; rc[8] = 0.1f;
+    }
+    stWRng(S, w, base);
+    // GoalRegionsState (level_gen.cpp:472-485)
+    S.goalMin0[w] = kFltMax;
+    S.goalMin1[w] = kFltMax;
+    S.goalTeam0[w] = 0.f;
+    S.goalTeam1[w] = 0.f;
+}
+
+// sim.cpp:732-833 initWorld
+__device__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool triggered_reset, const int32_t *tc)
+{
+    const uint32_t world_id = sc.worldOffset + (uint32_t)w;
+    S.episodeCurr[w] = S.worldCurr[w];
+    const uint32_t ep = (uint32_t)S.episode[w];
+    RandKey episode_key = splitI(sc.initRandKey, ep, world_id);
+    RNG base = makeRNG(splitI(episode_key, 0));
+    bool flip = false;
+    if (tc[2]) flip = rngUniform(base) < 0.5f;
+    S.teamA[w] = flip ? 1 : 0;
+    if (triggered_reset && tc[1]) S.curStep[w] = rngI32(base, 0, c::kEpisodeLen - 1);
+    else S.curStep[w] = 0;
+    S.finished[w] = 0;
+    const float use_prob = 1.0f;
+    const float tier_probs[5] = { 0.f, 0.f, 0.3f, 0.3f, 0.4f };
+    S.spawnCurriculum[w] = rngUniform(base) < use_prob ? 1 : 0;
+    float cdf[5];
+    float running = 0.f;
+    for (int i = 0; i < 5; i++) { running += tier_probs[i]; cdf[i] = running; }
+    float sel = running * rngUniform(base);
+    for (int i = 0; i < 5; i++) {
+        if (sel < cdf[i]) { S.curTier[w] = i; break; }
+    }
+    S.curSpawnIdx[w] = rngI32(base, 0, 0);
+    if (sc.simFlags & kFlagHardcodedSpawns) (void)rngI32(base, 0, 4);
+    S.curZone[w] = rngI32(base, 0, sc.numZones);
+    S.controlling[w] = -1;
+    S.contested[w] = 0;
+    S.captured[w] = 0;
+    S.earned[w] = 0;
+    S.zoneSteps[w] = c::kNumStepsPerZone;
+    S.stepsUntilPoint[w] = c::kZonePointInterval;
+    stWRng(S, w, base);
+    resetPersistentEntitiesD(S, sc, w, episode_key);
+    S.filtAct0[w] = 0; S.filtAct1[w] = 0;
+    S.filtMatched0[w] = 0; S.filtMatched1[w] = 0;
+}
+
+// sim.cpp:835-872 resetSystem
+__device__ void resetSystemD(const DevState &S, const SceneDev &sc, int w)
+{
+    const int32_t force = S.reset[w];
+    int32_t should = force;
+    if (sc.autoReset && S.finished[w]) should = 1;
+    if (should == 0) return;
+    S.reset[w] = 0;
+    const int32_t ep = S.episodeCounter[w];
+    S.episode[w] = ep;
+    S.episodeCounter[w] = ep + 1;
+    if (sc.simFlags & kFlagEnableCurriculum) {
+        if ((uint32_t)ep < 50) {
+            RNG base = ldWRng(S, w);
+            if (rngUniform(base) < ((uint32_t)ep + 1) / (float)50) S.worldCurr[w] = 1;
+            else S.worldCurr[w] = 0;
+            stWRng(S, w, base);
+        } else {
+            S.worldCurr[w] = 1;
+        }
+    }
+    initWorldD(S, sc, w, force == 1, S.trainCtrl);
+}
+
+// ====================================================== per-world systems
+// sim.cpp:1892-1976 zoneSystem
+__device__ void zoneSystemD(const DevState &S, const SceneDev &sc, int w)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    int cz = S.curZone[w];
+    int ctrl = S.controlling[w];
+    int zsr = S.zoneSteps[w];
+    int sup = S.stepsUntilPoint[w];
+    bool captured = S.captured[w] != 0;
+    if (ctrl != -1) zsr -= 1;
+    if (zsr == 0) {
+        cz += 1;
+        if (cz == sc.numZones) cz = 0;
+        captured = false;
+        zsr = c::kNumStepsPerZone;
+        sup = c::kZonePointInterval;
+        AABB za = sc.zoneAABB[cz];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        for (int i = 0; i < N; i++) S.minDistZone[g0 + i] = distance(ldPos(S, g0 + i), center);
+    }
+    AABB za = sc.zoneAABB[cz];
+    Quat to_zone = qinv(angleAxis(sc.zoneRot[cz], kUp));
+    za.pMin = rotateVec(to_zone, za.pMin);
+    za.pMax = rotateVec(to_zone, za.pMax);
+    int na = 0, nb = 0;
+    for (int i = 0; i < N; i++) {
+        Vec3 p = ldPos(S, g0 + i);
+        p.z += c::kStandHeight / 2.f;
+        Vec3 pz = rotateVec(to_zone, p);
+        bool in = aabbContains(za, pz);
+        setFlag(S, g0 + i, kFlagInZone, in);
+        if (!in) continue;
+        if (i / S.T == 0) na += 1;
+        else nb += 1;
+    }
+    sup -= 1;
+    bool contested = na > 0 && nb > 0;
+    if (contested || (na == 0 && nb == 0)) {
+        ctrl = -1;
+        captured = false;
+        sup = c::kZonePointInterval;
+    } else if (na > 0 && nb == 0) {
+        if (ctrl != 0) { ctrl = 0; captured = false; sup = c::kZonePointInterval; }
+    } else if (na == 0 && nb > 0) {
+        if (ctrl != 1) { ctrl = 1; captured = false; sup = c::kZonePointInterval; }
+    }
+    S.curZone[w] = cz;
+    S.controlling[w] = ctrl;
+    S.zoneSteps[w] = zsr;
+    S.stepsUntilPoint[w] = sup;
+    S.captured[w] = captured ? 1 : 0;
+    S.contested[w] = contested ? 1 : 0;
+}
+
+__device__ __forceinline__ float4 *crumbPtr(const DevState &S, int w) { return &S.crumbs[(int64_t)w * kMaxCrumbs * 2]; }
+
+// sim.cpp:4845-4889 leaveBreadcrumbsSystem, agent part: refresh own last
+// crumb or request a new one (appended in agent order by the world lane).
+__device__ void leaveBreadcrumbAgentD(const DevState &S, int w, int64_t g)
+{
+    S.bcPenalty[g] = 0.f;
+    const Vec3 pos = ldPos(S, g);
+    const int32_t last = S.bcLast[g];
+    bool updated = false;
+    if (last != -1) {
+        float4 *cr = crumbPtr(S, w);
+        const int n = S.numCrumbs[w];
+        for (int k = 0; k < n; k++) {
+            float4 meta = cr[2 * k + 1];
+            if (__float_as_int(meta.z) != last) continue;
+            float4 p = cr[2 * k];
+            if (distance(pos, v3(p.x, p.y, p.z)) < c::kAgentRadius * 4) {
+                cr[2 * k].w = 1.f;
+                updated = true;
+                S.bcSteps[g] = 0;
+            }
+            break;
+        }
+    }
+    if (!updated) {
+        int steps = S.bcSteps[g] + 1;
+        if (steps > 10) {
+            S.flags[g] |= kFlagCrumbRequest;
+            steps = 0;
+        }
+        S.bcSteps[g] = steps;
+    }
+}
+
+// World part of leaveBreadcrumbsSystem: append requested crumbs in agent order.
+__device__ void appendCrumbsD(const DevState &S, int w)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    float4 *cr = crumbPtr(S, w);
+    int n = S.numCrumbs[w];
+    int next_id = S.nextCrumbId[w];
+    for (int i = 0; i < N; i++) {
+        const int64_t g = g0 + i;
+        int32_t f = S.flags[g];
+        if (!(f & kFlagCrumbRequest)) continue;
+        S.flags[g] = f & ~kFlagCrumbRequest;
+        if (n < kMaxCrumbs) {
+            const int team = i / S.T, off = i - team * S.T;
+            cr[2 * n] = make_float4(S.px[g], S.py[g], S.pz[g], 1.f);
+            cr[2 * n + 1] = make_float4((float)team, (float)off, __int_as_float(next_id), 0.f);
+            S.bcLast[g] = next_id;
+            next_id += 1;
+            n += 1;
+        } else {
+            S.crumbOverflow[w] += 1;
+            S.bcLast[g] = -1;
+        }
+    }
+    S.numCrumbs[w] = n;
+    S.nextCrumbId[w] = next_id;
+}
+
+// sim.cpp:4892-4926 accumulateBreadcrumbPenaltiesSystem, gathered per agent
+// (crumbs in creation order).
+__device__ void accumulateCrumbsD(const DevState &S, int w, int i)
+{
+    const int64_t g = (int64_t)w * S.N + i;
+    const int team = i / S.T, off = i - team * S.T;
+    const Vec3 pos = ldPos(S, g);
+    const float4 *cr = crumbPtr(S, w);
+    const int n = S.numCrumbs[w];
+    float total = S.bcPenalty[g];
+    for (int k = 0; k < n; k++) {
+        float4 meta = cr[2 * k + 1];
+        if ((int)meta.x != team || (int)meta.y == off) continue;
+        float4 p = cr[2 * k];
+        if (distance(pos, v3(p.x, p.y, p.z)) <= c::kAgentRadius * 4.f) total += p.w;
+    }
+    S.bcPenalty[g] = total;
+}
+
+__device__ void decayCrumbsD(const DevState &S, int w)
+{
+    float4 *cr = crumbPtr(S, w);
+    const int n = S.numCrumbs[w];
+    int m = 0;
+    for (int k = 0; k < n; k++) {
+        float4 p = cr[2 * k];
+        float4 meta = cr[2 * k + 1];
+        p.w -= 0.025f;
+        if (!(p.w <= 0.f)) {
+            cr[2 * m] = p;
+            cr[2 * m + 1] = meta;
+            m += 1;
+        }
+    }
+    S.numCrumbs[w] = m;
+}
+
+// sim.cpp:128-291 updateFiltersState
+__device__ void updateFiltersD(const DevState &S, int w, int cur_step)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    int32_t *last = &S.filtLast[(int64_t)w * 6]; // [team][filter]
+    uint32_t act[2] = { (uint32_t)S.filtAct0[w], (uint32_t)S.filtAct1[w] };
+    const int16_t fmin_x[3] = { -1272, 852, -32768 }, fmin_y[3] = { -866, -851, -32768 };
+    const int16_t fmax_x[3] = { -825, 1280, 32767 }, fmax_y[3] = { 696, 593, 32767 };
+    const int min_num[2] = { 5, 1 };
+    for (int fi = 0; fi < 3; fi++) {
+        for (int t = 0; t < 2; t++) {
+            if (act[t] & (1u << fi)) {
+                if (cur_step - last[t * 3 + fi] > 0) act[t] &= ~(1u << fi);
+            }
+        }
+        if (fi == 2) {
+            for (int p = 0; p < N; p++) {
+                const int lo = S.landedOn[g0 + p];
+                if (lo == -1) continue;
+                const int team = p / S.T;
+                Vec3 ap = ldPos(S, g0 + p), tp = ldPos(S, g0 + lo);
+                if (ap.x < fmin_x[fi] || ap.y < fmin_y[fi] || ap.x > fmax_x[fi] || ap.y > fmax_y[fi] ||
+                    tp.x < fmin_x[fi] || tp.y < fmin_y[fi] || tp.x > fmax_x[fi] || tp.y > fmax_y[fi]) continue;
+                act[team] |= 1u << fi;
+                last[team * 3 + fi] = cur_step;
+            }
+        } else {
+            int cnt[2] = { 0, 0 };
+            for (int p = 0; p < N; p++) {
+                Vec3 pos = ldPos(S, g0 + p);
+                if (pos.x < fmin_x[fi] || pos.y < fmin_y[fi] || pos.x > fmax_x[fi] || pos.y > fmax_y[fi]) continue;
+                cnt[p / S.T] += 1;
+            }
+            for (int t = 0; t < 2; t++) {
+                if (cnt[t] >= min_num[fi]) {
+                    act[t] |= 1u << fi;
+                    last[t * 3 + fi] = cur_step;
+                }
+            }
+        }
+    }
+    S.filtAct0[w] = (int32_t)act[0];
+    S.filtAct1[w] = (int32_t)act[1];
+    if (__builtin_popcount(act[0]) == 3) S.filtMatched0[w] = cur_step;
+    if (__builtin_popcount(act[1]) == 3) S.filtMatched1[w] = cur_step;
+}
+
+// sim.cpp:4470-4673 zoneMatchInfoSystem
+__device__ void zoneMatchInfoD(const DevState &S, int w)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    int32_t *mr = &S.matchResult[(int64_t)w * 30];
+    int32_t *zs_all = &S.zoneStats[(int64_t)w * 25];
+    const int cur_step = S.curStep[w] + 1;
+    bool finished = false;
+    if (cur_step >= c::kEpisodeLen || S.reset[w] == 1) finished = true;
+    if (cur_step == 1) {
+        mr[0] = -1; mr[1] = 0; mr[2] = 0; mr[3] = 0; mr[4] = 0;
+    }
+    for (int i = 0; i < N; i++) {
+        if (S.flags[g0 + i] & kFlagWasKilled) mr[1 + ((i / S.T) ^ 1)] += 1;
+    }
+    bool earned = false;
+    bool new_captured = false;
+    const int ctrl = S.controlling[w];
+    int sup = S.stepsUntilPoint[w];
+    bool captured = S.captured[w] != 0;
+    if (sup == 0) {
+        sup = c::kZonePointInterval;
+        if (!captured) {
+            captured = true;
+            new_captured = true;
+        }
+        if (ctrl >= 0) mr[3 + ctrl] += 1;
+        earned = true;
+    }
+    S.stepsUntilPoint[w] = sup;
+    S.captured[w] = captured ? 1 : 0;
+    S.earned[w] = earned ? 1 : 0;
+    if (mr[3] >= c::kZoneWinPoints || mr[4] >= c::kZoneWinPoints) finished = true;
+    {
+        int32_t *zs = &zs_all[S.curZone[w] * 5];
+        zs[4] += 1;
+        if (captured && ctrl >= 0) zs[1 + ctrl] += 1;
+        if (S.contested[w]) zs[3] += 1;
+        if (new_captured) zs[0] += 1;
+        updateFiltersD(S, w, cur_step);
+    }
+    if (finished) {
+        if (mr[3] > mr[4]) mr[0] = 0;
+        else if (mr[4] > mr[3]) mr[0] = 1;
+        else mr[0] = 2;
+        for (int k = 0; k < 25; k++) mr[5 + k] = zs_all[k];
+        for (int k = 0; k < 25; k++) zs_all[k] = 0;
+    }
+    S.curStep[w] = cur_step;
+    S.finished[w] = finished ? 1 : 0;
+}
+
+// sim.cpp:3998-4087 distToZOBB + evaluateGoalRegionsSystem
+__device__ float distToZOBBD(const ZOBBDev &z, Vec3 pos)
+{
+    Quat to_frame = qinv(angleAxis(z.rotation, kUp));
+    Vec3 pmin = rotateVec(to_frame, z.pMin);
+    Vec3 pmax = rotateVec(to_frame, z.pMax);
+    Vec3 p = rotateVec(to_frame, pos);
+    float sq = 0.f;
+    for (int i = 0; i < 3; i++) {
+        float v = comp(p, i);
+        if (v < comp(pmin, i)) { float d = comp(pmin, i) - v; sq += d * d; }
+        if (v > comp(pmax, i)) { float d = v - comp(pmax, i); sq += d * d; }
+    }
+    return sqrt_(sq);
+}
+
+__device__ void goalRegionsD(const DevState &S, const SceneDev &sc, int w)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    float team_step[2] = { 0.f, 0.f };
+    float mins[2] = { S.goalMin0[w], S.goalMin1[w] };
+    const int attacker = S.teamA[w];
+    for (int r = 0; r < sc.numGoals && r < 2; r++) {
+        const GoalRegionDev &gr = sc.goals[r];
+        const int region_team = gr.attackerTeam ? attacker : (attacker ^ 1);
+        float max_min = -kFltMax;
+        for (int s = 0; s < gr.numSub; s++) {
+            float min_d = kFltMax;
+            for (int i = 0; i < N; i++) {
+                if (i / S.T != region_team) continue;
+                float d = distToZOBBD(gr.sub[s], ldPos(S, g0 + i));
+                if (d < min_d) min_d = d;
+            }
+            if (min_d > max_min) max_min = min_d;
+        }
+        float prev = mins[r];
+        if (prev == kFltMax) {
+            mins[r] = max_min;
+        } else {
+            float diff = prev - max_min;
+            if (diff > 0.f) {
+                mins[r] = max_min;
+                team_step[region_team] += diff * gr.rewardStrength;
+            }
+        }
+    }
+    S.goalMin0[w] = mins[0];
+    S.goalMin1[w] = mins[1];
+    S.goalTeam0[w] = team_step[0];
+    S.goalTeam1[w] = team_step[1];
+}
+
+// sim.cpp:3508-3536 exploreVisitedSystem
+__device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
+{
+    Vec3 delta = ldPos(S, g) - v3(S.sx[g], S.sy[g], S.sz[g]);
+    int32_t x = f2iSatD((delta.x + 0.5f) / (c::kAgentRadius * 2.f));
+    int32_t y = f2iSatD((delta.y + 0.5f) / (c::kAgentRadius * 2.f));
+    int64_t cx = (int64_t)x + c::kGridMax, cy = (int64_t)y + c::kGridMax;
+    if (cx < 0 || cx >= kGridW || cy < 0 || cy >= kGridW) return;
+    uint32_t *cell = &S.visited[g * kGridCells + cy * kGridW + cx];
+    const uint32_t cur = (uint32_t)S.episode[w];
+    if (*cell != cur) {
+        *cell = cur;
+        if (length2(delta) > 2.f) S.newCells[g] += 1;
+    }
+}
+
+// sim.cpp:3849-3996 zoneRewardSystem (+ learnShootingRewardSystem 3707-3732)
+__device__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
+{
+    const int64_t g0 = (int64_t)w * S.N;
+    const int64_t g = g0 + i;
+    int32_t flags = S.flags[g];
+    const int landed = S.landedOn[g];
+    float r = 0.f;
+    if (S.worldCurr[w] == 0) {
+        if (landed != -1) r += 0.5f;
+        else if (S.firedT[g] >= 0.f) r -= 0.05f;
+        if (flags & kFlagReloadedFullMag) r -= 0.5f;
+        S.reward[g] = r;
+        return;
+    }
+    const float *rc = &S.rewardCoefs[9 * g];
+    const float shot = rc[1], explore = rc[2], in_zone = rc[3], ctrl_s = rc[5], zdist = rc[6], earned_s = rc[7],
+                crumb = rc[8];
+    const int team = i / S.T, off = i - team * S.T;
+    const Vec3 pos = ldPos(S, g);
+    r -= crumb * S.bcPenalty[g];
+    if (flags & kFlagReloadedFullMag) r -= 0.5f;
+    if (flags & kFlagSuccessfulKill) r += 1.f;
+    if (landed != -1) r += shot * 1.f;
+    if (flags & kFlagWasKilled) r -= 1.5f;
+    if (S.wasShot[g] > 0) r -= shot * 1.f;
+    uint32_t nn = (uint32_t)S.newCells[g];
+    S.newCells[g] = 0;
+    if (nn > 0) r += float(nn) * explore;
+    if (flags & kFlagInZone) {
+        r += in_zone;
+    } else {
+        AABB za = sc.zoneAABB[S.curZone[w]];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        float dist = distance(center, pos);
+        float md = S.minDistZone[g];
+        if (dist < md) {
+            float scale = zdist;
+            if (!(flags & kFlagHasDied)) scale *= 10.f;
+            r += scale * (md - dist);
+            S.minDistZone[g] = dist;
+        }
+    }
+    const int ctrl = S.controlling[w];
+    const bool earned = S.earned[w] != 0;
+    if (ctrl != -1) {
+        if (ctrl == team) {
+            r += ctrl_s;
+            if (earned) r += earned_s;
+        } else {
+            r -= ctrl_s;
+            if (earned) r -= earned_s;
+        }
+    }
+    if (S.alive[g] == 0.f) {
+        S.flags[g] = flags & ~(kFlagSuccessfulKill | kFlagWasKilled);
+        S.landedOn[g] = -1;
+        S.wasShot[g] = 0;
+        S.firedT[g] = -kFltMax;
+        S.reward[g] = r;
+        return;
+    }
+    {
+        float poly = 0.f;
+        const int num_teammates = S.T - 1;
+        for (int k = 0; k < num_teammates - 1; k++) {
+            const int64_t t1 = g0 + team * S.T + (k < off ? k : k + 1);
+            const int64_t t2 = g0 + team * S.T + (k + 1 < off ? k + 1 : k + 2);
+            float e1x = S.px[t1] - pos.x, e1y = S.py[t1] - pos.y;
+            float e2x = S.px[t2] - pos.x, e2y = S.py[t2] - pos.y;
+            float tri = e1x * e2y - e1y * e2x;
+            poly += fabs_(tri);
+        }
+        float dx = sc.worldBounds.pMax.x - sc.worldBounds.pMin.x;
+        float dy = sc.worldBounds.pMax.y - sc.worldBounds.pMin.y;
+        float area = dx * dy;
+        float frac = poly / (2.f * area);
+        r += frac * 1e-2f;
+    }
+    S.reward[g] = r;
+}
+
+// ====================================================== kernels
+constexpr int kBlock = 256;
+
+// Persistent-entity setup + the Sim constructor's initWorld(ctx, true)
+// (sim.cpp:5850-5980, level_gen.cpp:19-328).  One thread per world.
+__global__ void __launch_bounds__(64) k_construct(DevState S, SceneDev sc, int32_t tc0, int32_t tc1, int32_t tc2)
+{
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= S.W) return;
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    for (int i = 0; i < N; i++) {
+        const int64_t g = g0 + i;
+        S.policy[g] = 0;
+        S.aimAction[2 * g] = 0.f; S.aimAction[2 * g + 1] = 0.f;
+        S.discreteAim[2 * g] = c::kDiscreteAimYawBuckets / 2;
+        S.discreteAim[2 * g + 1] = c::kDiscreteAimPitchBuckets / 2;
+        S.dyv[g] = 0.f; S.dpv[g] = 0.f;
+        for (int k = 0; k < kMaxTeamSize; k++) S.dmg[(int64_t)k * S.A + g] = 0.f;
+        stRot(S, g, quat(1, 0, 0, 0));
+        stAimRot(S, g, quat(1, 0, 0, 0));
+        S.landedOn[g] = -1;
+        S.bcLast[g] = -1;
+        S.flags[g] = 0;
+    }
+    S.episode[w] = 0;
+    S.episodeCounter[w] = 0;
+    S.curTier[w] = 0;
+    S.curSpawnIdx[w] = 0;
+    S.numCrumbs[w] = 0;
+    S.nextCrumbId[w] = 0;
+    S.crumbOverflow[w] = 0;
+    S.reset[w] = 0;
+    for (int k = 0; k < 6; k++) S.filtLast[(int64_t)w * 6 + k] = 0;
+    S.worldCurr[w] = 1; // WorldCurriculum::FullMatch (sim.cpp:5959)
+    const int32_t tc[3] = { tc0, tc1, tc2 };
+    initWorldD(S, sc, w, true, tc);
+    for (int k = 0; k < 25; k++) S.zoneStats[(int64_t)w * 25 + k] = 0;
+    S.filtAct0[w] = 0; S.filtAct1[w] = 0;
+    S.filtMatched0[w] = -1; S.filtMatched1[w] = -1;
+}
+
+// ExploreTracker initial contents (level_gen.cpp:166-171; cells outside the
+// y<40, x<40 quadrant start at 0).
+__global__ void __launch_bounds__(256) k_init_explore(uint32_t *visited, int64_t total)
+{
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
+        int cell = (int)(k % kGridCells);
+        int y = cell / kGridW, x = cell - y * kGridW;
+        visited[k] = (y < c::kGridMax && x < c::kGridMax) ? 0xFFFFFFFFu : 0u;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
+{
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= S.W) return;
+    resetSystemD(S, sc, w);
+}
+
+// The Step graph up to and including resetSystem, one workgroup per tile of
+// floor(256 / N) worlds, one lane per agent.
+__global__ void __launch_bounds__(kBlock) k_sim(DevState S, SceneDev sc)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const LBVH bvh = stageBVH(smem, sc);
+    const int N = S.N;
+    const int wpb = kBlock / N;
+    const int wl = threadIdx.x / N;
+    const int i = threadIdx.x - wl * N;
+    const int w = blockIdx.x * wpb + wl;
+    const bool act = (wl < wpb) && (w < S.W);
+    const bool wlane = act && i == 0;
+    const int64_t g = (int64_t)w * N + i;
+
+    if (act) {
+        // planAStarAISystem (sim.cpp:5041-5172) acts only for AgentPolicy == -1
+        // (bots) and is not part of round 1.
+        applyBotActionsD(S, g);
+        pvpMovementD(S, g);
+        pvpAimD(S, g);
+        applyVelocityD(S, bvh, g);
+        fallD(S, bvh, g);
+    }
+    __syncthreads();
+    if (act) fireD(S, bvh, w, i);
+    __syncthreads();
+    if (act) applyDmgD(S, g);
+    __syncthreads();
+    if (wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
+    __syncthreads();
+    if (act) autoHealD(S, g);
+    __syncthreads();
+    if (wlane) zoneSystemD(S, sc, w);
+    __syncthreads();
+    if (act) leaveBreadcrumbAgentD(S, w, g);
+    __syncthreads();
+    if (wlane) appendCrumbsD(S, w);
+    __syncthreads();
+    if (act) accumulateCrumbsD(S, w, i);
+    __syncthreads();
+    if (wlane) {
+        decayCrumbsD(S, w);
+        zoneMatchInfoD(S, w);
+        goalRegionsD(S, sc, w);
+    }
+    __syncthreads();
+    if (act) {
+        exploreVisitedD(S, w, g);
+        zoneRewardD(S, sc, w, i);
+    }
+    __syncthreads();
+    if (wlane) {
+        // pvpTeamRewardSystem (sim.cpp:4292-4313)
+        float tr[2] = { 0.f, 0.f };
+        int ts[2] = { 0, 0 };
+        for (int j = 0; j < N; j++) {
+            int t = j / S.T;
+            tr[t] += S.reward[(int64_t)w * N + j];
+            ts[t] += 1;
+        }
+        tr[0] /= float(ts[0]);
+        tr[1] /= float(ts[1]);
+        S.teamRew0[w] = tr[0];
+        S.teamRew1[w] = tr[1];
+    }
+    __syncthreads();
+    if (act) {
+        // pvpFinalRewardSystem (sim.cpp:4315-4339) + doneSystem (4712-4717)
+        const int team = i / S.T;
+        float my = S.reward[g];
+        float team_r = team == 0 ? S.teamRew0[w] : S.teamRew1[w];
+        float spirit = S.rewardCoefs[9 * g];
+        S.reward[g] = my * (1.f - spirit) + team_r * spirit;
+        S.done[g] = S.finished[w] ? 1 : 0;
+    }
+    __syncthreads();
+    if (wlane) resetSystemD(S, sc, w);
+}
+
+// utils.cpp:169-184 inFrustum
+__device__ __forceinline__ bool inFrustumD(const SceneDev &sc, Vec3 vp)
+{
+    bool in = true;
+    in = in && vp.y * sc.frustum[1] - fabs_(vp.x) * sc.frustum[0] > -c::kAgentRadius;
+    in = in && vp.y * sc.frustum[3] - fabs_(vp.z) * sc.frustum[2] > -c::kAgentRadius;
+    return in;
+}
+
+// opponentsWriteVisibilitySystem (sim.cpp:2526-2560) with isAgentVisible
+// (utils.cpp:186-271).  Lane = (agent, opponent slot); the four sample
+// points stop at the first visible one (the reference tests all four but
+// only the boolean is consumed).
+__global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const LBVH bvh = stageBVH(smem, sc);
+    const int T = S.T, N = S.N;
+    const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= S.A * T) return;
+    const int64_t g = lane / T;
+    const int k = (int)(lane - g * T);
+    const int w = (int)(g / N);
+    const int i = (int)(g - (int64_t)w * N);
+    const int64_t g0 = (int64_t)w * N;
+    const int team = i / T;
+    const int target = (team ^ 1) * T + k;
+    const int64_t gt = g0 + target;
+    bool vis = false;
+    if (S.alive[g] != 0.f && S.alive[gt] != 0.f) {
+        Vec3 org = ldPos(S, g);
+        org.z += viewHeightD(S.curPose[g]);
+        const Quat aim_rot = ldAimRot(S, g);
+        const Quat inv_rot = qinv(aim_rot);
+        const Vec3 base = ldPos(S, gt);
+        const float vh = viewHeightD(S.curPose[gt]);
+        const Vec3 aim_right = rotateVec(aim_rot, kRight);
+        const Vec3 delta_right = aim_right * 0.9f * c::kAgentRadius;
+        Vec3 pts[4];
+        pts[0] = base; pts[0].z += c::kAgentRadius;             // bottom
+        pts[1] = base; pts[1].z += vh;                          // top
+        pts[2] = base; pts[2].z += vh; pts[2] = pts[2] - delta_right; // left
+        pts[3] = base; pts[3].z += vh; pts[3] = pts[3] + delta_right; // right
+        for (int p = 0; p < 4 && !vis; p++) {
+            Vec3 to_test = pts[p] - org;
+            Vec3 view = rotateVec(inv_rot, to_test);
+            if (view.y <= 0.f) continue;
+            if (!inFrustumD(sc, view)) continue;
+            float len = length(to_test);
+            if (len < c::kAgentRadius) continue;
+            to_test = to_test / len;
+            WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, org, to_test);
+            if (h.hit && h.entity == target) vis = true;
+        }
+    }
+    reinterpret_cast<uint8_t *>(S.canSee)[g * kMaxTeamSize + k] = vis ? 1 : 0;
+}
+
+__device__ __forceinline__ Vec3 normalizedPosD(const SceneDev &sc, Vec3 p) // sim.cpp:2693-2718
+{
+    float min_x = sc.worldBounds.pMin.x, min_y = sc.worldBounds.pMin.y, min_z = sc.worldBounds.pMin.z;
+    float max_x = sc.worldBounds.pMax.x, max_y = sc.worldBounds.pMax.y, max_z = sc.worldBounds.pMax.z;
+    float xr = max_x - min_x, yr = max_y - min_y, zr = max_z - min_z;
+    float x = (p.x - min_x) / xr, y = (p.y - min_y) / yr, z = (p.z - min_z) / zr;
+    return v3(clampf(x, 0.f, 1.f), clampf(y, 0.f, 1.f), clampf(z, 0.f, 1.f));
+}
+
+struct SelfFrame {
+    Vec3 pos;
+    Quat invRot;
+    float yaw, pitch;
+};
+
+__device__ __forceinline__ void relAnglesD(const SelfFrame &sf, Vec3 to, float &dist_out, float &yaw_out,
+                                           float &pitch_out)
+{
+    float d = length(to);
+    if (d < 1e-2f) {
+        dist_out = 0.f; yaw_out = 0.f; pitch_out = 0.f;
+        return;
+    }
+    to = to / d;
+    float new_yaw = -atan2f_(to.x, to.y);
+    float new_pitch = asinf_(clampf(to.z, -1.f, 1.f));
+    float yaw_delta = new_yaw - sf.yaw;
+    float pitch_delta = new_pitch - sf.pitch;
+    if (yaw_delta > kPi) yaw_delta -= 2.f * kPi;
+    else if (yaw_delta < -kPi) yaw_delta += 2.f * kPi;
+    dist_out = d; yaw_out = yaw_delta; pitch_out = pitch_delta;
+}
+
+// fillCommonOb (sim.cpp:2720-2774) into a register array; returns alive.
+__device__ __forceinline__ bool fillCommonD(const DevState &S, const SceneDev &sc, const SelfFrame &sf, int64_t gj,
+                                            float *ob, float *pos_ob)
+{
+    ob[0] = 1.f;
+    if (!S.alive[gj]) return false;
+    ob[1] = 1.f;
+    Vec3 np = normalizedPosD(sc, ldPos(S, gj));
+    ob[2] = np.x; ob[3] = np.y; ob[4] = np.z;
+    pos_ob[0] = np.x; pos_ob[1] = np.y; pos_ob[2] = np.z;
+    ob[5] = 0.5f * ((S.ayaw[gj] / kPi) + 1.f);
+    ob[6] = 0.5f * (S.apitch[gj] / (0.25f * kPi) + 1.f);
+    Vec3 rv = rotateVec(sf.invRot, ldVel(S, gj));
+    ob[7] = rv.x; ob[8] = rv.y; ob[9] = rv.z;
+    ob[10] = S.dyv[gj]; ob[11] = S.dpv[gj];
+    const int cp = S.curPose[gj], tp = S.tgtPose[gj];
+    ob[12] = cp == kStand ? 1.f : 0.f;
+    ob[13] = cp == kCrouch ? 1.f : 0.f;
+    ob[14] = cp == kProne ? 1.f : 0.f;
+    ob[15] = tp == kStand ? 1.f : 0.f;
+    ob[16] = tp == kCrouch ? 1.f : 0.f;
+    ob[17] = tp == kProne ? 1.f : 0.f;
+    ob[18] = (float)S.transRem[gj] / (float)c::kPoseTransitionSpeed;
+    ob[19] = (S.flags[gj] & kFlagInZone) ? 1.f : 0.f;
+    const int wt = S.weapon[gj];
+    ob[20] = wt == 0 ? 1.f : 0.f;
+    ob[21] = wt == 1 ? 1.f : 0.f;
+    ob[22] = wt == 2 ? 1.f : 0.f;
+    return true;
+}
+
+__device__ __forceinline__ void fillCombatD(const DevState &S, int64_t gj, float *ob)
+{
+    ob[0] = (float)S.hp[gj] / 100.f;
+    ob[1] = (float)S.magazine[2 * gj];
+    ob[2] = (float)S.magazine[2 * gj + 1];
+    ob[3] = float(S.autohealSteps[gj]) / float(c::kOutOfCombatSteps);
+}
+
+__device__ __forceinline__ void fillOtherD(const DevState &S, const SelfFrame &sf, int64_t gj, float *ob)
+{
+    relAnglesD(sf, ldPos(S, gj) - sf.pos, ob[23], ob[24], ob[25]);
+    float rfy = S.ayaw[gj] - sf.yaw;
+    float rfp = S.apitch[gj] - sf.pitch;
+    if (rfy > kPi) rfy -= 2.f * kPi;
+    else if (rfy < -kPi) rfy += 2.f * kPi;
+    ob[26] = rfy;
+    ob[27] = rfp;
+}
+
+__device__ __forceinline__ void storeVec(float *dst, const float *src, int n)
+{
+    for (int k = 0; k < n; k++) dst[k] = src[k];
+}
+
+// pvpOpponentMasksSystem (sim.cpp:2562-2614) + pvpObservationsSystem
+// (sim.cpp:2645-3052).  Lane = agent.
+__global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= S.A) return;
+    const int T = S.T, N = S.N;
+    const int w = (int)(g / N);
+    const int i = (int)(g - (int64_t)w * N);
+    const int64_t g0 = (int64_t)w * N;
+    const int team = i / T, off = i - team * T;
+    const uint8_t *cansee = reinterpret_cast<const uint8_t *>(S.canSee);
+    const bool self_alive = S.alive[g] != 0.f;
+
+    // ---- masks
+    float mask[kMaxTeamSize];
+    for (int k = 0; k < kMaxTeamSize; k++) {
+        mask[k] = 0.f;
+        if (!self_alive || k >= T) continue;
+        const int64_t go = g0 + (team ^ 1) * T + k;
+        if (S.alive[go] == 0.f) continue;
+        bool can_see = cansee[g * kMaxTeamSize + k] != 0;
+        for (int t = 0; t < T - 1 && !can_see; t++) {
+            const int64_t gt = g0 + team * T + (t < off ? t : t + 1);
+            if (cansee[gt * kMaxTeamSize + k]) can_see = true;
+        }
+        if (can_see) mask[k] = 1.f;
+        if (S.firedT[go] >= 0) mask[k] = 1.f;
+    }
+    storeVec(&S.masks[g * 6], mask, 6);
+
+    // ---- observations
+    const int cur_step = S.curStep[w];
+    const int fm = team == 0 ? S.filtMatched0[w] : S.filtMatched1[w];
+    S.filters[g] = (cur_step - fm < 5) ? 1.f : 0.f;
+
+    SelfFrame sf;
+    sf.pos = ldPos(S, g);
+    sf.invRot = qinv(ldRot(S, g));
+    sf.yaw = S.ayaw[g];
+    sf.pitch = S.apitch[g];
+
+    float ob[kSelfObs];
+    float pos3[3];
+    for (int k = 0; k < kSelfObs; k++) ob[k] = 0.f;
+    pos3[0] = pos3[1] = pos3[2] = -1000.f;
+    const bool alive_ok = fillCommonD(S, sc, sf, g, ob, pos3);
+    if (alive_ok) {
+        fillCombatD(S, g, &ob[23]);
+        float *zo = &ob[27];
+        const int cz = S.curZone[w];
+        AABB za = sc.zoneAABB[cz];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        Vec3 nc = normalizedPosD(sc, center);
+        zo[0] = nc.x; zo[1] = nc.y; zo[2] = nc.z;
+        relAnglesD(sf, center - sf.pos, zo[3], zo[4], zo[5]);
+        const int ctrl = S.controlling[w];
+        zo[6] = (ctrl == team) ? 1.f : 0.f;
+        zo[7] = (ctrl != -1 && ctrl != team) ? 1.f : 0.f;
+        zo[8] = S.contested[w] ? 1.f : 0.f;
+        zo[9] = S.captured[w] ? 1.f : 0.f;
+        zo[10] = float(S.stepsUntilPoint[w]) / float(c::kZonePointInterval);
+        zo[11] = float(S.zoneSteps[w]) / float(c::kNumStepsPerZone);
+        zo[12] = cz == 0 ? 1.f : 0.f;
+        zo[13] = cz == 1 ? 1.f : 0.f;
+        zo[14] = cz == 2 ? 1.f : 0.f;
+        zo[15] = cz == 3 ? 1.f : 0.f;
+    }
+    storeVec(&S.selfObs[g * kSelfObs], ob, kSelfObs);
+    storeVec(&S.selfPos[g * 3], pos3, 3);
+
+    // teammates
+    for (int k = 0; k < kMaxTeamSize - 1; k++) {
+        float tob[kOtherObs];
+        float tpos[3];
+        for (int q = 0; q < kOtherObs; q++) tob[q] = 0.f;
+        tpos[0] = tpos[1] = tpos[2] = -1000.f;
+        if (alive_ok && k < T - 1) {
+            const int64_t gj = g0 + team * T + (k < off ? k : k + 1);
+            if (fillCommonD(S, sc, sf, gj, tob, tpos)) {
+                fillOtherD(S, sf, gj, tob);
+                fillCombatD(S, gj, &tob[28]);
+            }
+        }
+        storeVec(&S.tmObs[(g * 5 + k) * kOtherObs], tob, kOtherObs);
+        storeVec(&S.tmPos[(g * 5 + k) * 3], tpos, 3);
+    }
+
+    // opponents (+ last known)
+    for (int k = 0; k < kMaxTeamSize; k++) {
+        float oob[kOtherObs];
+        float opos[3];
+        for (int q = 0; q < kOtherObs; q++) oob[q] = 0.f;
+        opos[0] = opos[1] = opos[2] = -1000.f;
+        float *lk = &S.lkObs[(g * 6 + k) * kOtherObs];
+        float *lkp = &S.lkPos[(g * 6 + k) * 3];
+        if (alive_ok && k < T) {
+            const int64_t gj = g0 + (team ^ 1) * T + k;
+            if (!fillCommonD(S, sc, sf, gj, oob, opos)) {
+                for (int q = 0; q < kOtherObs; q++) lk[q] = 0.f;
+                lkp[0] = lkp[1] = lkp[2] = -1000.f;
+            } else {
+                fillOtherD(S, sf, gj, oob);
+                if (S.flags[gj] & kFlagWasKilled) {
+                    for (int q = 0; q < kOtherObs; q++) lk[q] = 0.f;
+                    lkp[0] = lkp[1] = lkp[2] = -1000.f;
+                }
+                oob[28] = (float)S.wasShot[gj];
+                oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
+                oob[30] = cansee[g * kMaxTeamSize + k] ? 1.f : 0.f;
+                const bool knows = mask[k] == 1.f;
+                oob[31] = knows ? 1.f : 0.f;
+                if (knows) {
+                    storeVec(lk, oob, kOtherObs);
+                    storeVec(lkp, opos, 3);
+                }
+            }
+        }
+        storeVec(&S.oppObs[(g * 6 + k) * kOtherObs], oob, kOtherObs);
+        storeVec(&S.oppPos[(g * 6 + k) * 3], opos, 3);
+    }
+}
+
+// pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray; a workgroup walks
+// kLidarIters x 256 consecutive rays (the 80 rays of an agent are adjacent).
+constexpr int kLidarIters = 8;
+
+__global__ void __launch_bounds__(kBlock) k_lidar(DevState S, SceneDev sc)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const LBVH bvh = stageBVH(smem, sc);
+    const int N = S.N, T = S.T;
+    const int64_t total = S.A * kLidarRays;
+    const int64_t base = (int64_t)blockIdx.x * (kBlock * kLidarIters);
+    for (int it = 0; it < kLidarIters; it++) {
+        const int64_t r = base + it * kBlock + threadIdx.x;
+        if (r >= total) break;
+        const int64_t g = r / kLidarRays;
+        const int k = (int)(r - g * kLidarRays);
+        const int w = (int)(g / N);
+        const int i = (int)(g - (int64_t)w * N);
+        const int64_t g0 = (int64_t)w * N;
+        const bool fwd = k < kFwdRays;
+        const int kk = fwd ? k : k - kFwdRays;
+        const int width = fwd ? 32 : 8;
+        const int h = kk / width, x = kk - h * width;
+        const Quat q = fwd ? ldAimRot(S, g) : ldRot(S, g);
+        const Vec3 dir_fwd = rotateVec(q, kFwd);
+        const Vec3 dir_right = rotateVec(q, kRight);
+        const float top = viewHeightD(S.curPose[g]) + c::kAgentRadius;
+        Vec3 ray_o = ldPos(S, g);
+        ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
+        const float range = fwd ? 0.75f * kPi : -kPi;
+        const float offset = fwd ? 0.5f * (1.f - 0.75f) * kPi : 0.f;
+        float theta = range * (float(x) / float(width - 1)) + offset;
+        float dx = -cosf_(theta);
+        float dy = sinf_(theta);
+        Vec3 dir = normalize(dx * dir_right + dy * dir_fwd);
+        WorldHit hw = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, ray_o, dir);
+        float4 out;
+        if (hw.hit) {
+            const bool wall = hw.entity == -1;
+            const bool tm = !wall && (hw.entity / T) == (i / T);
+            out = make_float4(fminD(hw.t, sc.maxDist), wall ? 1.f : 0.f, tm ? 1.f : 0.f, (!wall && !tm) ? 1.f : 0.f);
+        } else {
+            out = make_float4(-1.f, 0.f, 0.f, 0.f);
+        }
+        float4 *dst = fwd ? reinterpret_cast<float4 *>(S.fwdLidar) + g * kFwdRays + kk
+                          : reinterpret_cast<float4 *>(S.rearLidar) + g * kRearRays + kk;
+        *dst = out;
+    }
+}
+
+// Debug gather of internal state into the MPENV_EXPORT_DEBUG_* layouts.
+__global__ void __launch_bounds__(256) k_debug(DevState S, float *af, int32_t *ai, int32_t *wi, float *wf,
+                                               uint32_t *explore, float *crumbs)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < S.A) {
+        const int64_t g = t;
+        float *f = &af[g * 23];
+        f[0] = S.px[g]; f[1] = S.py[g]; f[2] = S.pz[g];
+        f[3] = S.vx[g]; f[4] = S.vy[g]; f[5] = S.vz[g];
+        f[6] = S.rw[g]; f[7] = S.rx[g]; f[8] = S.ry[g]; f[9] = S.rz[g];
+        f[10] = S.ayaw[g]; f[11] = S.apitch[g];
+        f[12] = S.aw[g]; f[13] = S.ax[g]; f[14] = S.ay[g]; f[15] = S.az[g];
+        f[16] = S.maxVel[g]; f[17] = S.minDistZone[g]; f[18] = S.firedT[g]; f[19] = S.bcPenalty[g];
+        f[20] = S.sx[g]; f[21] = S.sy[g]; f[22] = S.sz[g];
+        int32_t *n = &ai[g * 16];
+        n[0] = S.curPose[g]; n[1] = S.tgtPose[g]; n[2] = S.transRem[g];
+        n[3] = S.rngA[g]; n[4] = S.rngB[g]; n[5] = S.rngCtr[g];
+        n[6] = S.landedOn[g]; n[7] = S.respawnSteps[g]; n[8] = S.autohealSteps[g];
+        n[9] = S.flags[g] & 31;
+        n[10] = S.wasShot[g]; n[11] = S.weapon[g]; n[12] = S.bcLast[g]; n[13] = S.bcSteps[g];
+        const uint8_t *cs = reinterpret_cast<const uint8_t *>(S.canSee) + g * kMaxTeamSize;
+        int m = 0;
+        for (int k = 0; k < kMaxTeamSize; k++) m |= cs[k] ? (1 << k) : 0;
+        n[14] = m;
+        n[15] = S.newCells[g];
+        if (explore) {
+            for (int k = 0; k < kGridCells; k++) explore[g * kGridCells + k] = S.visited[g * kGridCells + k];
+        }
+    }
+    if (t < S.W) {
+        const int w = (int)t;
+        int32_t *n = &wi[(int64_t)w * 21];
+        n[0] = S.teamA[w]; n[1] = S.curStep[w]; n[2] = S.finished[w]; n[3] = S.curZone[w];
+        n[4] = S.controlling[w]; n[5] = S.contested[w]; n[6] = S.captured[w]; n[7] = S.earned[w];
+        n[8] = S.zoneSteps[w]; n[9] = S.stepsUntilPoint[w]; n[10] = S.episode[w]; n[11] = S.episodeCounter[w];
+        n[12] = S.wRngA[w]; n[13] = S.wRngB[w]; n[14] = S.wRngCtr[w]; n[15] = S.numCrumbs[w];
+        n[16] = S.filtAct0[w]; n[17] = S.filtAct1[w]; n[18] = S.filtMatched0[w]; n[19] = S.filtMatched1[w];
+        n[20] = S.crumbOverflow[w];
+        float *f = &wf[(int64_t)w * 6];
+        f[0] = S.teamRew0[w]; f[1] = S.teamRew1[w]; f[2] = S.goalMin0[w]; f[3] = S.goalMin1[w];
+        f[4] = S.goalTeam0[w]; f[5] = S.goalTeam1[w];
+        float *cdst = &crumbs[(int64_t)w * kMaxCrumbs * 8];
+        const float4 *cr = crumbPtr(S, w);
+        const int nc = S.numCrumbs[w];
+        for (int k = 0; k < kMaxCrumbs; k++) {
+            float *e = &cdst[k * 8];
+            if (k < nc) {
+                float4 p = cr[2 * k], meta = cr[2 * k + 1];
+                e[0] = p.x; e[1] = p.y; e[2] = p.z; e[3] = p.w;
+                e[4] = meta.x; e[5] = meta.y; e[6] = (float)__float_as_int(meta.z); e[7] = 1.f;
+            } else {
+                for (int q = 0; q < 8; q++) e[q] = 0.f;
+            }
+        }
+    }
+}
+
+// Copy one step of the action tape ([A][6] i32: 4 discrete + 2 aim) into the
+// engine's action columns (the cudaCopyStepInputs of gpuStreamStep,
+// mgr.cpp:625).
+__global__ void __launch_bounds__(256) k_fill_actions(DevState S, const int32_t *src)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= S.A) return;
+    const int32_t *s = src + 6 * g;
+    int4 d = make_int4(s[0], s[1], s[2], s[3]);
+    reinterpret_cast<int4 *>(S.discreteAction)[g] = d;
+    reinterpret_cast<int2 *>(S.discreteAim)[g] = make_int2(s[4], s[5]);
+}
+
+// ============================================================ host side
+const char *kernelName(int k)
+{
+    static const char *names[kNumTimedKernels] = { "k_sim", "k_vis", "k_obs", "k_lidar" };
+    return (k >= 0 && k < kNumTimedKernels) ? names[k] : "?";
+}
+
+size_t bvhLdsBytes(const SceneDev &sc) { return (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 12; }
+
+static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
+
+int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t total = s.A * kGridCells;
+    int blocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_init_explore, dim3(blocks), dim3(256), 0, st, s.visited, total);
+    if (check(hipGetLastError())) return -1;
+    hipLaunchKernelGGL(k_construct, dim3((s.W + 63) / 64), dim3(64), 0, st, s, sc, tc[0], tc[1], tc[2]);
+    return check(hipGetLastError());
+}
+
+int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream)
+{
+    hipLaunchKernelGGL(k_reset_only, dim3((s.W + 63) / 64), dim3(64), 0, (hipStream_t)stream, s, sc);
+    return check(hipGetLastError());
+}
+
+int launchSimStep(const DevState &s, const SceneDev &sc, void *stream)
+{
+    const int wpb = kBlock / s.N;
+    const int blocks = (s.W + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k_sim, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
+    return check(hipGetLastError());
+}
+
+int launchVisibility(const DevState &s, const SceneDev &sc, void *stream)
+{
+    const int64_t lanes = s.A * s.T;
+    const int blocks = (int)((lanes + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_vis, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
+    return check(hipGetLastError());
+}
+
+int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
+{
+    const int blocks = (int)((s.A + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, s, sc);
+    return check(hipGetLastError());
+}
+
+int launchLidar(const DevState &s, const SceneDev &sc, void *stream)
+{
+    const int64_t rays = s.A * kLidarRays;
+    const int64_t per_block = (int64_t)kBlock * kLidarIters;
+    const int blocks = (int)((rays + per_block - 1) / per_block);
+    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
+    return check(hipGetLastError());
+}
+
+int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, float *wf, uint32_t *explore,
+                      float *crumbs, void *stream)
+{
+    const int64_t n = s.A > s.W ? s.A : s.W;
+    hipLaunchKernelGGL(k_debug, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, s, af, ai, wi,
+                       wf, explore, crumbs);
+    return check(hipGetLastError());
+}
+
+int launchFillActions(const DevState &s, const int32_t *src6, void *stream)
+{
+    hipLaunchKernelGGL(k_fill_actions, dim3((unsigned)((s.A + 255) / 256)), dim3(256), 0, (hipStream_t)stream, s,
+                       src6);
+    return check(hipGetLastError());
+}
+
+} // namespace mpenv

@@ -1,0 +1,688 @@
+// manager.cpp — the Manager (src/mgr.hpp:31-161, src/mgr.cpp) for the gfx950
+// engine, exposed through the C ABI of include/mpenv.h.
+//
+// Owns every device buffer (engine-owned tensors, zero-copy views handed to
+// callers as in mgr.cpp:295-301/655-661), the scene upload, and the step
+// launch sequence on a HIP stream.  There is no CPU execution path: a CPU
+// ExecMode is rejected (the reference's CPU TaskGraph executor is restated
+// only by the test oracle).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "mpenv.h"
+#include "scene.h"
+
+using namespace mpenv;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_CHECK(expr)                                                                   \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + \
+                                     " at " #expr);                                       \
+        }                                                                                 \
+    } while (0)
+
+// Order of TrainInterface inputs/outputs (mgr.cpp:2383-2431).
+struct TIEntry {
+    const char *name;
+    int32_t id;
+};
+const TIEntry kTIInputs[] = {
+    { "discrete", MPENV_EXPORT_PVP_DISCRETE_ACTION },
+    { "aim", MPENV_EXPORT_PVP_DISCRETE_AIM_ACTION },
+    { "resets", MPENV_EXPORT_RESET },
+    { "simCtrl", MPENV_EXPORT_SIM_CONTROL },
+    { "pbt.policy_assignments", MPENV_EXPORT_AGENT_POLICY },
+};
+const TIEntry kTIOutputs[] = {
+    { "fwd_lidar", MPENV_EXPORT_FWD_LIDAR },
+    { "rear_lidar", MPENV_EXPORT_REAR_LIDAR },
+    { "hp", MPENV_EXPORT_HP },
+    { "magazine", MPENV_EXPORT_MAGAZINE },
+    { "alive", MPENV_EXPORT_ALIVE },
+    { "self", MPENV_EXPORT_SELF_OBSERVATION },
+    { "filters_state", MPENV_EXPORT_FILTERS_STATE },
+    { "teammates", MPENV_EXPORT_TEAMMATE_OBSERVATIONS },
+    { "opponents", MPENV_EXPORT_OPPONENT_OBSERVATIONS },
+    { "opponents_last_known", MPENV_EXPORT_OPPONENT_LAST_KNOWN_OBSERVATIONS },
+    { "self_pos", MPENV_EXPORT_SELF_POSITION },
+    { "teammate_positions", MPENV_EXPORT_TEAMMATE_POSITIONS },
+    { "opponent_positions", MPENV_EXPORT_OPPONENT_POSITIONS },
+    { "opponent_last_known_positions", MPENV_EXPORT_OPPONENT_LAST_KNOWN_POSITIONS },
+    { "opponent_masks", MPENV_EXPORT_OPPONENT_MASKS },
+    { "agent_map", MPENV_EXPORT_AGENT_MAP },
+    { "unmasked_agent_map", MPENV_EXPORT_AGENT_MAP },
+    { "reward_coefs", MPENV_EXPORT_REWARD_HYPER_PARAMS },
+    { "rewards", MPENV_EXPORT_REWARD },
+    { "dones", MPENV_EXPORT_DONE },
+    { "pbt.episode_results", MPENV_EXPORT_MATCH_RESULT },
+};
+constexpr int kNumTIInputs = sizeof(kTIInputs) / sizeof(kTIInputs[0]);
+constexpr int kNumTIOutputs = sizeof(kTIOutputs) / sizeof(kTIOutputs[0]);
+
+struct TensorDesc {
+    void *ptr = nullptr;
+    int32_t dtype = MPENV_DTYPE_FLOAT32;
+    std::vector<int64_t> dims;
+    size_t bytes() const
+    {
+        size_t n = 4;
+        for (int64_t d : dims) n *= (size_t)d;
+        return n;
+    }
+};
+
+} // namespace
+
+struct mpenv_manager {
+    mpenv_config cfg;
+    std::string scenePath;
+    int gpu = 0;
+    Scene scene;
+    SceneDev sc;
+    DevState S;
+    hipStream_t stream = nullptr;
+    std::vector<void *> allocations;
+
+    // Debug gather buffers (allocated lazily)
+    float *dbgAF = nullptr, *dbgWF = nullptr, *dbgCrumbs = nullptr;
+    int32_t *dbgAI = nullptr, *dbgWI = nullptr;
+    uint32_t *dbgExplore = nullptr;
+
+    // Kernel timing
+    bool timing = false;
+    std::vector<hipEvent_t> eventPool;
+    size_t eventsUsed = 0;
+
+    ~mpenv_manager()
+    {
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (hipEvent_t e : eventPool) (void)hipEventDestroy(e);
+        for (void *p : allocations) (void)hipFree(p);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    template <typename T>
+    T *alloc(size_t count)
+    {
+        size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+        void *p = nullptr;
+        HIP_CHECK(hipMalloc(&p, bytes));
+        HIP_CHECK(hipMemsetAsync(p, 0, bytes, stream));
+        allocations.push_back(p);
+        return static_cast<T *>(p);
+    }
+
+    hipEvent_t nextEvent()
+    {
+        if (eventsUsed == eventPool.size()) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            eventPool.push_back(e);
+        }
+        return eventPool[eventsUsed++];
+    }
+
+    void record(hipStream_t st)
+    {
+        if (timing) HIP_CHECK(hipEventRecord(nextEvent(), st));
+    }
+
+    void runStep(hipStream_t st)
+    {
+        record(st);
+        if (launchSimStep(S, sc, st)) throw std::runtime_error("k_sim launch failed");
+        record(st);
+        if (launchVisibility(S, sc, st)) throw std::runtime_error("k_vis launch failed");
+        record(st);
+        if (launchObservations(S, sc, st)) throw std::runtime_error("k_obs launch failed");
+        record(st);
+        if (launchLidar(S, sc, st)) throw std::runtime_error("k_lidar launch failed");
+        record(st);
+    }
+
+    void runInitGraph(hipStream_t st)
+    {
+        // triggerReset on every world (mgr.cpp:1936-1938) then the Init graph
+        // (sim.cpp:5322-5340): resetSystem + observations + lidar.
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)S.reset, 1, (size_t)S.W, st));
+        if (launchResetOnly(S, sc, st)) throw std::runtime_error("k_reset launch failed");
+        if (launchVisibility(S, sc, st)) throw std::runtime_error("k_vis launch failed");
+        if (launchObservations(S, sc, st)) throw std::runtime_error("k_obs launch failed");
+        if (launchLidar(S, sc, st)) throw std::runtime_error("k_lidar launch failed");
+    }
+
+    bool exportDesc(int32_t id, TensorDesc &d);
+    void gatherDebug();
+};
+
+bool mpenv_manager::exportDesc(int32_t id, TensorDesc &d)
+{
+    const int64_t A = S.A, W = S.W;
+    auto set = [&](void *p, int32_t dt, std::initializer_list<int64_t> dims) {
+        d.ptr = p;
+        d.dtype = dt;
+        d.dims.assign(dims.begin(), dims.end());
+        return true;
+    };
+    switch (id) {
+    case MPENV_EXPORT_RESET: return set(S.reset, MPENV_DTYPE_INT32, { W, 1 });
+    case MPENV_EXPORT_WORLD_CURRICULUM: return set(S.worldCurr, MPENV_DTYPE_INT32, { W, 1 });
+    case MPENV_EXPORT_EXPLORE_ACTION: return set(S.exploreAction, MPENV_DTYPE_INT32, { A, 4 });
+    case MPENV_EXPORT_PVP_DISCRETE_ACTION: return set(S.discreteAction, MPENV_DTYPE_INT32, { A, 4 });
+    case MPENV_EXPORT_PVP_AIM_ACTION: return set(S.aimAction, MPENV_DTYPE_FLOAT32, { A, 1, 2 });
+    case MPENV_EXPORT_PVP_DISCRETE_AIM_ACTION: return set(S.discreteAim, MPENV_DTYPE_INT32, { A, 2 });
+    case MPENV_EXPORT_REWARD: return set(S.reward, MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_DONE: return set(S.done, MPENV_DTYPE_INT32, { A, 1 });
+    case MPENV_EXPORT_MATCH_RESULT: return set(S.matchResult, MPENV_DTYPE_INT32, { W, 30 });
+    case MPENV_EXPORT_AGENT_POLICY: return set(S.policy, MPENV_DTYPE_INT32, { A, 1 });
+    case MPENV_EXPORT_SELF_OBSERVATION: return set(S.selfObs, MPENV_DTYPE_FLOAT32, { A, kSelfObs });
+    case MPENV_EXPORT_TEAMMATE_OBSERVATIONS: return set(S.tmObs, MPENV_DTYPE_FLOAT32, { A, 5, kOtherObs });
+    case MPENV_EXPORT_OPPONENT_OBSERVATIONS: return set(S.oppObs, MPENV_DTYPE_FLOAT32, { A, 6, kOtherObs });
+    case MPENV_EXPORT_OPPONENT_LAST_KNOWN_OBSERVATIONS: return set(S.lkObs, MPENV_DTYPE_FLOAT32, { A, 6, kOtherObs });
+    case MPENV_EXPORT_SELF_POSITION: return set(S.selfPos, MPENV_DTYPE_FLOAT32, { A, 3 });
+    case MPENV_EXPORT_TEAMMATE_POSITIONS: return set(S.tmPos, MPENV_DTYPE_FLOAT32, { A, 5, 3 });
+    case MPENV_EXPORT_OPPONENT_POSITIONS: return set(S.oppPos, MPENV_DTYPE_FLOAT32, { A, 6, 3 });
+    case MPENV_EXPORT_OPPONENT_LAST_KNOWN_POSITIONS: return set(S.lkPos, MPENV_DTYPE_FLOAT32, { A, 6, 3 });
+    case MPENV_EXPORT_OPPONENT_MASKS: return set(S.masks, MPENV_DTYPE_FLOAT32, { A, 6, 1 });
+    case MPENV_EXPORT_FWD_LIDAR: return set(S.fwdLidar, MPENV_DTYPE_FLOAT32, { A, 2, 32, 4 });
+    case MPENV_EXPORT_REAR_LIDAR: return set(S.rearLidar, MPENV_DTYPE_FLOAT32, { A, 2, 8, 4 });
+    case MPENV_EXPORT_AGENT_MAP:
+    case MPENV_EXPORT_UNMASKED_AGENT_MAP: return set(S.agentMap, MPENV_DTYPE_FLOAT32, { A, 16, 16, 4 });
+    case MPENV_EXPORT_HP: return set(S.hp, MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_ALIVE: return set(S.alive, MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_MAGAZINE: return set(S.magazine, MPENV_DTYPE_INT32, { A, 2 });
+    case MPENV_EXPORT_FILTERS_STATE: return set(S.filters, MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_REWARD_HYPER_PARAMS: return set(S.rewardCoefs, MPENV_DTYPE_FLOAT32, { A, 9 });
+    case MPENV_EXPORT_SIM_CONTROL: return set(S.trainCtrl, MPENV_DTYPE_INT32, { 3 });
+    case MPENV_EXPORT_DEBUG_AGENT_F32: gatherDebug(); return set(dbgAF, MPENV_DTYPE_FLOAT32, { A, MPENV_DBG_AF_COUNT });
+    case MPENV_EXPORT_DEBUG_AGENT_I32: gatherDebug(); return set(dbgAI, MPENV_DTYPE_INT32, { A, MPENV_DBG_AI_COUNT });
+    case MPENV_EXPORT_DEBUG_WORLD_I32: gatherDebug(); return set(dbgWI, MPENV_DTYPE_INT32, { W, MPENV_DBG_WI_COUNT });
+    case MPENV_EXPORT_DEBUG_WORLD_F32: gatherDebug(); return set(dbgWF, MPENV_DTYPE_FLOAT32, { W, MPENV_DBG_WF_COUNT });
+    case MPENV_EXPORT_DEBUG_EXPLORE: gatherDebug(); return set(dbgExplore, MPENV_DTYPE_UINT32, { A, kGridCells });
+    case MPENV_EXPORT_DEBUG_CRUMBS: gatherDebug(); return set(dbgCrumbs, MPENV_DTYPE_FLOAT32, { W, kMaxCrumbs, 8 });
+    default: return false;
+    }
+}
+
+void mpenv_manager::gatherDebug()
+{
+    if (!dbgAF) {
+        dbgAF = alloc<float>((size_t)S.A * MPENV_DBG_AF_COUNT);
+        dbgAI = alloc<int32_t>((size_t)S.A * MPENV_DBG_AI_COUNT);
+        dbgWI = alloc<int32_t>((size_t)S.W * MPENV_DBG_WI_COUNT);
+        dbgWF = alloc<float>((size_t)S.W * MPENV_DBG_WF_COUNT);
+        dbgExplore = alloc<uint32_t>((size_t)S.A * kGridCells);
+        dbgCrumbs = alloc<float>((size_t)S.W * kMaxCrumbs * 8);
+    }
+    if (launchDebugGather(S, dbgAF, dbgAI, dbgWI, dbgWF, dbgExplore, dbgCrumbs, stream))
+        throw std::runtime_error("debug gather launch failed");
+    HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+static void buildSceneDev(mpenv_manager &m)
+{
+    Scene &s = m.scene;
+    SceneDev &sc = m.sc;
+    std::memset(&sc, 0, sizeof(sc));
+    if (s.nodes.size() > 256) throw std::runtime_error("BVH has more than 256 nodes (byte-stack limit)");
+    if (s.maxStack > kMaxBVHStack) throw std::runtime_error("BVH too deep for the 16-entry register stack");
+    if (s.zoneAABBs.empty() || s.zoneAABBs.size() > (size_t)kMaxZones) throw std::runtime_error("bad zone count");
+    if (s.aSpawns.size() > (size_t)kMaxSpawns || s.bSpawns.size() > (size_t)kMaxSpawns ||
+        s.commonRespawns.size() > (size_t)kMaxSpawns)
+        throw std::runtime_error("too many spawns for the per-world usage tracker");
+    if (s.aSpawns.empty() || s.bSpawns.empty()) throw std::runtime_error("scene needs A and B spawns");
+
+    BVHNode *d_nodes = m.alloc<BVHNode>(s.nodes.size());
+    HIP_CHECK(hipMemcpy(d_nodes, s.nodes.data(), sizeof(BVHNode) * s.nodes.size(), hipMemcpyHostToDevice));
+    float *d_verts = m.alloc<float>(s.bvhVerts.size() * 3);
+    HIP_CHECK(hipMemcpy(d_verts, s.bvhVerts.data(), sizeof(float) * 3 * s.bvhVerts.size(), hipMemcpyHostToDevice));
+    auto upSpawns = [&](const std::vector<Spawn> &v) {
+        Spawn *p = m.alloc<Spawn>(std::max<size_t>(v.size(), 1));
+        if (!v.empty()) HIP_CHECK(hipMemcpy(p, v.data(), sizeof(Spawn) * v.size(), hipMemcpyHostToDevice));
+        return p;
+    };
+    sc.nodes = d_nodes;
+    sc.verts = d_verts;
+    sc.numNodes = (int32_t)s.nodes.size();
+    sc.numVerts = (int32_t)s.bvhVerts.size();
+    sc.worldBounds = s.worldBounds;
+    // sim.cpp:5855 maxDist; 5869-5882 frustumData
+    sc.maxDist = mp::length(s.worldBounds.pMax - s.worldBounds.pMin);
+    {
+        float aspect = 16.f / 9.f;
+        float ang = 90.f / 2.f * (mp::kPi / 180.f);
+        float f = 1.f / (mp::sinf_(ang) / mp::cosf_(ang));
+        float wx = f / aspect, wy = 1.f, hx = f, hy = 1.f;
+        float wi = 1.f / mp::sqrt_(wx * wx + wy * wy);
+        float hi = 1.f / mp::sqrt_(hx * hx + hy * hy);
+        sc.frustum[0] = wx * wi; sc.frustum[1] = wy * wi;
+        sc.frustum[2] = hx * hi; sc.frustum[3] = hy * hi;
+    }
+    sc.aSpawns = upSpawns(s.aSpawns);
+    sc.bSpawns = upSpawns(s.bSpawns);
+    sc.commonRespawns = upSpawns(s.commonRespawns);
+    sc.numA = (int32_t)s.aSpawns.size();
+    sc.numB = (int32_t)s.bSpawns.size();
+    sc.numCommon = (int32_t)s.commonRespawns.size();
+    sc.numDefaultA = (int32_t)s.numDefaultASpawns;
+    sc.numDefaultB = (int32_t)s.numDefaultBSpawns;
+    sc.numZones = (int32_t)s.zoneAABBs.size();
+    for (int z = 0; z < sc.numZones; z++) {
+        sc.zoneAABB[z] = s.zoneAABBs[z];
+        sc.zoneRot[z] = s.zoneRotations[z];
+    }
+    sc.numGoals = (int32_t)s.goalRegions.size();
+    for (int gi = 0; gi < sc.numGoals && gi < 4; gi++) {
+        const GoalRegion &g = s.goalRegions[gi];
+        GoalRegionDev &d = sc.goals[gi];
+        for (int k = 0; k < 3; k++) {
+            d.sub[k].pMin = g.subRegions[k].pMin;
+            d.sub[k].pMax = g.subRegions[k].pMax;
+            d.sub[k].rotation = g.subRegions[k].rotation;
+        }
+        d.numSub = g.numSubRegions;
+        d.attackerTeam = g.attackerTeam;
+        d.rewardStrength = g.rewardStrength;
+    }
+    sc.simFlags = m.cfg.sim_flags;
+    sc.autoReset = m.cfg.auto_reset;
+    sc.worldOffset = m.cfg.world_id_offset;
+    // mgr.cpp:1736-1737
+    sc.initRandKey = mp::splitI(mp::initKey(m.cfg.rand_seed), 0);
+}
+
+static void allocState(mpenv_manager &m)
+{
+    DevState &S = m.S;
+    const size_t A = (size_t)S.A, W = (size_t)S.W;
+#define MP_ALLOC_AF(n) S.n = m.alloc<float>(A);
+#define MP_ALLOC_AI(n) S.n = m.alloc<int32_t>(A);
+#define MP_ALLOC_WI(n) S.n = m.alloc<int32_t>(W);
+#define MP_ALLOC_WF(n) S.n = m.alloc<float>(W);
+    MP_AGENT_F32(MP_ALLOC_AF)
+    MP_AGENT_I32(MP_ALLOC_AI)
+    MP_WORLD_I32(MP_ALLOC_WI)
+    MP_WORLD_F32(MP_ALLOC_WF)
+#undef MP_ALLOC_AF
+#undef MP_ALLOC_AI
+#undef MP_ALLOC_WI
+#undef MP_ALLOC_WF
+    S.dmg = m.alloc<float>(A * kMaxTeamSize);
+    S.canSee = m.alloc<uint8_t>(A * kMaxTeamSize);
+    S.visited = m.alloc<uint32_t>(A * kGridCells);
+    S.filtLast = m.alloc<int32_t>(W * 6);
+    S.zoneStats = m.alloc<int32_t>(W * 25);
+    S.spawnTrack = m.alloc<uint32_t>(W * 3 * kMaxSpawns);
+    S.crumbs = m.alloc<float4>(W * kMaxCrumbs * 2);
+    S.reset = m.alloc<int32_t>(W);
+    S.worldCurr = m.alloc<int32_t>(W);
+    S.matchResult = m.alloc<int32_t>(W * 30);
+    S.exploreAction = m.alloc<int32_t>(A * 4);
+    S.discreteAction = m.alloc<int32_t>(A * 4);
+    S.aimAction = m.alloc<float>(A * 2);
+    S.discreteAim = m.alloc<int32_t>(A * 2);
+    S.policy = m.alloc<int32_t>(A);
+    S.botAction = m.alloc<int32_t>(A * 7);
+    S.reward = m.alloc<float>(A);
+    S.done = m.alloc<int32_t>(A);
+    S.selfObs = m.alloc<float>(A * kSelfObs);
+    S.filters = m.alloc<float>(A);
+    S.tmObs = m.alloc<float>(A * 5 * kOtherObs);
+    S.oppObs = m.alloc<float>(A * 6 * kOtherObs);
+    S.lkObs = m.alloc<float>(A * 6 * kOtherObs);
+    S.selfPos = m.alloc<float>(A * 3);
+    S.tmPos = m.alloc<float>(A * 15);
+    S.oppPos = m.alloc<float>(A * 18);
+    S.lkPos = m.alloc<float>(A * 18);
+    S.masks = m.alloc<float>(A * 6);
+    S.fwdLidar = m.alloc<float>(A * kFwdRays * 4);
+    S.rearLidar = m.alloc<float>(A * kRearRays * 4);
+    S.agentMap = m.alloc<float>(A * 16 * 16 * 4);
+    S.hp = m.alloc<float>(A);
+    S.alive = m.alloc<float>(A);
+    S.magazine = m.alloc<int32_t>(A * 2);
+    S.rewardCoefs = m.alloc<float>(A * 9);
+    S.trainCtrl = m.alloc<int32_t>(3);
+}
+
+extern "C" {
+
+int32_t mpenv_abi_version(void) { return MPENV_ABI_VERSION; }
+
+const char *mpenv_last_error(void) { return g_last_error.c_str(); }
+
+int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
+{
+    if (!cfg || !out) return fail(MPENV_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (cfg->exec_mode != MPENV_EXEC_CUDA)
+        return fail(MPENV_ERR_UNSUPPORTED, "ExecMode.CPU is not supported: this engine runs only on the GPU (HIP)");
+    if (cfg->task_type != MPENV_TASK_ZONE)
+        return fail(MPENV_ERR_UNSUPPORTED, "only Task.Zone is implemented");
+    if (cfg->team_size < 1 || cfg->team_size > kMaxTeamSize)
+        return fail(MPENV_ERR_INVALID, "team_size must be in [1, 6]");
+    if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");
+    if (!cfg->scene_path) return fail(MPENV_ERR_INVALID, "scene_path is required");
+    const uint32_t unsupported = MPENV_SIMFLAG_NAVMESH_SPAWN | MPENV_SIMFLAG_ENABLE_CURRICULUM |
+                                 MPENV_SIMFLAG_HARDCODED_SPAWNS | MPENV_SIMFLAG_FULL_TEAM_POLICY |
+                                 MPENV_SIMFLAG_SUB_ZONES;
+    if (cfg->sim_flags & unsupported)
+        return fail(MPENV_ERR_UNSUPPORTED, "sim_flags contains a flag this build does not implement");
+    if (cfg->replay_log_path || cfg->record_log_path || cfg->event_log_path || cfg->curriculum_data_path ||
+        cfg->train_flank)
+        return fail(MPENV_ERR_UNSUPPORTED, "record/replay/event logs, curricula and flank rewards are not implemented");
+
+    mpenv_manager *m = nullptr;
+    try {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+            return fail(MPENV_ERR_HIP, "no HIP device available");
+        if (cfg->gpu_id < 0 || cfg->gpu_id >= ndev) return fail(MPENV_ERR_INVALID, "gpu_id out of range");
+        HIP_CHECK(hipSetDevice(cfg->gpu_id));
+        m = new mpenv_manager();
+        m->cfg = *cfg;
+        m->scenePath = cfg->scene_path;
+        m->cfg.scene_path = m->scenePath.c_str();
+        m->gpu = cfg->gpu_id;
+        HIP_CHECK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+        m->scene = loadScene(m->scenePath, (cfg->sim_flags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) != 0);
+        buildSceneDev(*m);
+        m->S.W = (int32_t)cfg->num_worlds;
+        m->S.T = (int32_t)cfg->team_size;
+        m->S.N = 2 * m->S.T;
+        m->S.A = (int64_t)m->S.W * m->S.N;
+        allocState(*m);
+        // TrainControl from sim flags (mgr.cpp:1397-1413)
+        int32_t tc[3] = { (cfg->sim_flags & MPENV_SIMFLAG_SIM_EVAL_MODE) ? 1 : 0,
+                          (cfg->sim_flags & MPENV_SIMFLAG_STAGGER_STARTS) ? 1 : 0,
+                          (cfg->sim_flags & MPENV_SIMFLAG_RANDOM_FLIP_TEAMS) ? 1 : 0 };
+        HIP_CHECK(hipMemcpyAsync(m->S.trainCtrl, tc, sizeof(tc), hipMemcpyHostToDevice, m->stream));
+        if (launchConstruct(m->S, m->sc, tc, m->stream)) throw std::runtime_error("construct launch failed");
+        HIP_CHECK(hipStreamSynchronize(m->stream));
+        *out = m;
+        return MPENV_OK;
+    } catch (const std::exception &e) {
+        delete m;
+        std::string msg = e.what();
+        bool io = msg.find("open") != std::string::npos || msg.find("truncated") != std::string::npos;
+        return fail(io ? MPENV_ERR_IO : MPENV_ERR_HIP, msg);
+    }
+}
+
+void mpenv_destroy(mpenv_manager *m) { delete m; }
+
+int mpenv_init(mpenv_manager *m)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    try {
+        m->runInitGraph(m->stream);
+        HIP_CHECK(hipStreamSynchronize(m->stream));
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_step_async(mpenv_manager *m, void *stream)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    try {
+        m->runStep(stream ? (hipStream_t)stream : m->stream);
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_step(mpenv_manager *m)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    try {
+        m->runStep(m->stream);
+        HIP_CHECK(hipStreamSynchronize(m->stream));
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_export_tensor(mpenv_manager *m, int32_t id, void **ptr, int32_t *dtype, int32_t *ndim, int64_t *dims,
+                        int32_t *gpu_id)
+{
+    if (!m || !ptr || !dtype || !ndim || !dims) return fail(MPENV_ERR_INVALID, "null argument");
+    TensorDesc d;
+    try {
+        if (!m->exportDesc(id, d)) return fail(MPENV_ERR_INVALID, "unknown export id " + std::to_string(id));
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    *ptr = d.ptr;
+    *dtype = d.dtype;
+    *ndim = (int32_t)d.dims.size();
+    for (size_t k = 0; k < d.dims.size(); k++) dims[k] = d.dims[k];
+    if (gpu_id) *gpu_id = m->gpu;
+    return MPENV_OK;
+}
+
+int mpenv_train_interface_size(int32_t *num_inputs, int32_t *num_outputs)
+{
+    if (num_inputs) *num_inputs = kNumTIInputs;
+    if (num_outputs) *num_outputs = kNumTIOutputs;
+    return MPENV_OK;
+}
+
+int mpenv_train_interface_entry(int32_t is_output, int32_t idx, const char **name, int32_t *export_id)
+{
+    const TIEntry *tab = is_output ? kTIOutputs : kTIInputs;
+    int n = is_output ? kNumTIOutputs : kNumTIInputs;
+    if (idx < 0 || idx >= n) return fail(MPENV_ERR_INVALID, "train interface index out of range");
+    if (name) *name = tab[idx].name;
+    if (export_id) *export_id = tab[idx].id;
+    return MPENV_OK;
+}
+
+static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs, bool outputs)
+{
+    int k = 0;
+    for (int i = 0; i < kNumTIInputs; i++, k++) {
+        if (!inputs) continue;
+        TensorDesc d;
+        m->exportDesc(kTIInputs[i].id, d);
+        if (buffers[k]) HIP_CHECK(hipMemcpyAsync(d.ptr, buffers[k], d.bytes(), hipMemcpyDeviceToDevice, st));
+    }
+    for (int i = 0; i < kNumTIOutputs; i++, k++) {
+        if (!outputs) continue;
+        TensorDesc d;
+        m->exportDesc(kTIOutputs[i].id, d);
+        if (buffers[k]) HIP_CHECK(hipMemcpyAsync(buffers[k], d.ptr, d.bytes(), hipMemcpyDeviceToDevice, st));
+    }
+    return 0;
+}
+
+// mgr.cpp:507-612
+int mpenv_gpu_stream_init(mpenv_manager *m, void *stream, void **buffers)
+{
+    if (!m || !buffers) return fail(MPENV_ERR_INVALID, "null argument");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : m->stream;
+        m->runInitGraph(st);
+        copyTI(m, st, buffers, false, true);
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    return MPENV_OK;
+}
+
+// mgr.cpp:614-645
+int mpenv_gpu_stream_step(mpenv_manager *m, void *stream, void **buffers)
+{
+    if (!m || !buffers) return fail(MPENV_ERR_INVALID, "null argument");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : m->stream;
+        copyTI(m, st, buffers, true, false);
+        m->runStep(st);
+        copyTI(m, st, buffers, false, true);
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_copy_actions(mpenv_manager *m, const int32_t *src, void *stream)
+{
+    if (!m || !src) return fail(MPENV_ERR_INVALID, "null argument");
+    if (launchFillActions(m->S, src, stream ? stream : (void *)m->stream))
+        return fail(MPENV_ERR_HIP, "action copy launch failed");
+    return MPENV_OK;
+}
+
+static int checkAgent(mpenv_manager *m, int32_t w, int32_t a)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    if (w < 0 || w >= m->S.W) return fail(MPENV_ERR_INVALID, "world index out of range");
+    if (a < 0 || a >= m->S.N) return fail(MPENV_ERR_INVALID, "agent index out of range");
+    return MPENV_OK;
+}
+
+int mpenv_trigger_reset(mpenv_manager *m, int32_t w)
+{
+    if (int rc = checkAgent(m, w, 0)) return rc;
+    int32_t one = 1;
+    if (hipMemcpy(m->S.reset + w, &one, 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(MPENV_ERR_HIP, "hipMemcpy failed");
+    return MPENV_OK;
+}
+
+int mpenv_set_pvp_action(mpenv_manager *m, int32_t w, int32_t a, const int32_t discrete[4], const float aim[2],
+                         const int32_t aim_discrete[2])
+{
+    if (int rc = checkAgent(m, w, a)) return rc;
+    const int64_t g = (int64_t)w * m->S.N + a;
+    bool ok = true;
+    if (discrete) ok &= hipMemcpy(m->S.discreteAction + 4 * g, discrete, 16, hipMemcpyHostToDevice) == hipSuccess;
+    if (aim) ok &= hipMemcpy(m->S.aimAction + 2 * g, aim, 8, hipMemcpyHostToDevice) == hipSuccess;
+    if (aim_discrete) ok &= hipMemcpy(m->S.discreteAim + 2 * g, aim_discrete, 8, hipMemcpyHostToDevice) == hipSuccess;
+    return ok ? MPENV_OK : fail(MPENV_ERR_HIP, "hipMemcpy failed");
+}
+
+int mpenv_set_hp(mpenv_manager *m, int32_t w, int32_t a, int32_t hp)
+{
+    if (int rc = checkAgent(m, w, a)) return rc;
+    float v = (float)hp;
+    if (hipMemcpy(m->S.hp + (int64_t)w * m->S.N + a, &v, 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(MPENV_ERR_HIP, "hipMemcpy failed");
+    return MPENV_OK;
+}
+
+int mpenv_set_agent_policy(mpenv_manager *m, int32_t w, int32_t a, int32_t policy)
+{
+    if (int rc = checkAgent(m, w, a)) return rc;
+    if (hipMemcpy(m->S.policy + (int64_t)w * m->S.N + a, &policy, 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(MPENV_ERR_HIP, "hipMemcpy failed");
+    return MPENV_OK;
+}
+
+int mpenv_set_uniform_agent_policy(mpenv_manager *m, int32_t policy)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    if (hipMemsetD32((hipDeviceptr_t)m->S.policy, policy, (size_t)m->S.A) != hipSuccess)
+        return fail(MPENV_ERR_HIP, "hipMemsetD32 failed");
+    return MPENV_OK;
+}
+
+int mpenv_is_replay_finished(mpenv_manager *m, int32_t *finished)
+{
+    (void)m;
+    if (finished) *finished = 1;
+    return fail(MPENV_ERR_UNSUPPORTED, "replay logs are not implemented");
+}
+
+int mpenv_dims(mpenv_manager *m, int32_t *num_worlds, int32_t *agents_per_world)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    if (num_worlds) *num_worlds = m->S.W;
+    if (agents_per_world) *agents_per_world = m->S.N;
+    return MPENV_OK;
+}
+
+int mpenv_enable_kernel_timing(mpenv_manager *m, int32_t enable)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    m->timing = enable != 0;
+    m->eventsUsed = 0;
+    return MPENV_OK;
+}
+
+int mpenv_kernel_timings(mpenv_manager *m, int32_t max_n, const char **names, float *avg_ms, int32_t *launches)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    const int nk = kNumTimedKernels;
+    std::vector<double> sum(nk, 0.0);
+    int steps = 0;
+    try {
+        HIP_CHECK(hipDeviceSynchronize());
+        // events per step: nk + 1 boundaries
+        const size_t per = (size_t)nk + 1;
+        for (size_t base = 0; base + per <= m->eventsUsed; base += per) {
+            for (int k = 0; k < nk; k++) {
+                float ms = 0.f;
+                HIP_CHECK(hipEventElapsedTime(&ms, m->eventPool[base + k], m->eventPool[base + k + 1]));
+                sum[k] += ms;
+            }
+            steps++;
+        }
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    m->eventsUsed = 0;
+    for (int k = 0; k < nk && k < max_n; k++) {
+        if (names) names[k] = kernelName(k);
+        if (avg_ms) avg_ms[k] = steps ? (float)(sum[k] / steps) : 0.f;
+        if (launches) launches[k] = steps;
+    }
+    return nk;
+}
+
+// Host-side access to the scene BVH (for the parity oracle and tests).
+int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes, float *verts_out,
+                    int32_t *num_verts, int32_t *max_stack)
+{
+    try {
+        Scene s = loadScene(scene_path);
+        if (num_nodes) {
+            if (nodes_out && *num_nodes >= (int32_t)s.nodes.size())
+                std::memcpy(nodes_out, s.nodes.data(), s.nodes.size() * sizeof(BVHNode));
+            *num_nodes = (int32_t)s.nodes.size();
+        }
+        if (num_verts) {
+            if (verts_out && *num_verts >= (int32_t)s.bvhVerts.size())
+                std::memcpy(verts_out, s.bvhVerts.data(), s.bvhVerts.size() * 12);
+            *num_verts = (int32_t)s.bvhVerts.size();
+        }
+        if (max_stack) *max_stack = s.maxStack;
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_IO, e.what());
+    }
+    return MPENV_OK;
+}
+
+} // extern "C"

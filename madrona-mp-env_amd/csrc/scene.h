@@ -1,0 +1,92 @@
+// scene.h — host-side map data: the four .bin formats of
+// map_importer.cpp:35-567 and the compressed 4-wide BVH of mesh_bvh.hpp:56-86,
+// built by our own SAH builder (the reference uses Embree's rtcBuildBVH,
+// mesh_bvh_builder.cpp:218-737; Embree is absent here, and hit results are
+// builder-independent up to exact ties).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mpenv_core.h"
+
+namespace mpenv {
+
+// mesh_bvh.hpp:61-86 (MeshBVH::Node, 64 bytes).  Quantised child boxes:
+// child AABB = min + 2^exp * q.  children[i] has bit 31 set for a leaf whose
+// low bits give the leaf's first triangle; sentinel = -1.
+struct BVHNode {
+    float minX, minY, minZ;
+    int8_t expX, expY, expZ;
+    uint8_t internalNodes;
+    uint8_t triSize[4];
+    uint8_t qMinX[4];
+    uint8_t qMinY[4];
+    uint8_t qMinZ[4];
+    uint8_t qMaxX[4];
+    uint8_t qMaxY[4];
+    uint8_t qMaxZ[4];
+    int32_t children[4];
+    int32_t parentID;
+};
+static_assert(sizeof(BVHNode) == 64, "BVHNode must be 64 bytes");
+
+// Spawn (types.hpp:60-64): 32 bytes on disk.
+struct Spawn {
+    mp::AABB region;
+    float yawMin, yawMax;
+};
+static_assert(sizeof(Spawn) == 32, "Spawn must be 32 bytes");
+
+struct GoalZOBB {
+    mp::Vec3 pMin, pMax;
+    float rotation;
+};
+
+// GoalRegion (types.hpp:798-806) as filled by hardcodedGoalRegions
+// (mgr.cpp:913-944).
+struct GoalRegion {
+    GoalZOBB subRegions[3];
+    int32_t numSubRegions;
+    int32_t attackerTeam; // bool in the reference
+    float rewardStrength;
+};
+
+struct Scene {
+    mp::AABB worldBounds;
+
+    // Collision triangles after filterMeshes (map_importer.cpp:126-221),
+    // de-indexed: tri i = verts[3i..3i+2].
+    std::vector<mp::Vec3> triVerts;
+
+    // BVH (nodes + per-leaf de-indexed vertices, 3 per triangle).
+    std::vector<BVHNode> nodes;
+    std::vector<mp::Vec3> bvhVerts;
+    mp::AABB rootAABB;
+    int32_t numLeaves = 0;
+    int32_t maxDepth = 0;      // deepest inner-node level (root = 1)
+    int32_t maxStack = 0;      // bound on traversal stack occupancy
+
+    std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
+    uint32_t numDefaultASpawns = 0, numDefaultBSpawns = 0;
+
+    std::vector<mp::AABB> zoneAABBs;
+    std::vector<float> zoneRotations;
+
+    std::vector<mp::Vec3> navVerts;
+    std::vector<uint32_t> navFaceCounts;
+    std::vector<uint32_t> navIndices;
+
+    std::vector<GoalRegion> goalRegions;
+};
+
+// Loads <dir>/{collisions,navmesh,spawns,zones}.bin (bindings.cpp:56-81) and
+// builds the BVH.  Throws std::runtime_error on I/O failure (the reference
+// FATALs, map_importer.cpp:229-231).
+Scene loadScene(const std::string &scene_dir, bool spawn_in_middle = false);
+
+// Builds the compressed 4-wide BVH over de-indexed triangles.
+void buildBVH(const std::vector<mp::Vec3> &tri_verts, Scene &out);
+
+} // namespace mpenv

@@ -1,0 +1,2407 @@
+// oracle.cpp — TEST INFRASTRUCTURE ONLY (parity checker, CPU baseline).
+//
+// A single-threaded, plain-C++ restatement of the reference's world-batched
+// Zone step: the TaskGraphID::Step graph of Sim::setupTasks
+// (src/sim.cpp:5342-5842) and the Init graph (sim.cpp:5322-5340), plus the
+// per-world constructor (sim.cpp:5850-5980), world generation
+// (src/level_gen.cpp:19-582), the ray/sphere/visibility/spawn helpers
+// (src/utils.cpp:10-948) and the compressed-BVH traversal
+// (src/mesh_bvh.inl:110-1127).  Every function cites the reference lines it
+// follows.  Systems run in the reference's insertion order, world by world
+// (worlds never interact), so a world-partitioned thread
+// pool gives the same results as the reference's per-node barriers.
+//
+// Only the Madrona layer (vector/quaternion math, transcendentals, RNG,
+// geo:: helpers — not vendored in the reference) comes from the shared
+// definition header mpenv_core.h; everything restating madrona-mp-env code
+// lives here and is independent of the GPU kernels it checks.
+//
+// Reference quirks reproduced on purpose: the
+// sphere-cast vertex test's double origin shift (mesh_bvh.inl:1073-1104),
+// the escape-move sign (sim.cpp:1004), respawn scoring's integer "elapsed"
+// (utils.cpp:418-428), spawn z offset after the zone-frame test
+// (utils.cpp:899-903), dead agents still casting lidar and dropping
+// breadcrumbs.  Deliberate, documented definitions: breadcrumb penalties
+// accumulate in creation order (the reference uses an order-dependent float
+// atomic, sim.cpp:4915); sphereCastLeaf tests triSize triangles (the
+// reference always reads 2, mesh_bvh.inl:867); ExploreTracker cells outside
+// the initialised quadrant start at 0; uninitialised locals (the first
+// slope-cast normal, sim.cpp:927) start at zero.
+#include "oracle.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mpenv.h"
+#include "mpenv_core.h"
+
+using namespace mp;
+
+namespace {
+
+// ----------------------------------------------------- consts.hpp:7-72
+constexpr int kMaxTeamSize = 6;
+constexpr int kMaxZones = 5;
+constexpr int kNumStepsPerZone = 600;
+constexpr int kZonePointInterval = 20;
+constexpr int kZoneWinPoints = 125;
+constexpr int kPoseTransitionSpeed = 10;
+constexpr float kAgentRadius = 15.f;
+constexpr float kStandHeight = 65.f;
+constexpr float kCrouchHeight = 47.f;
+constexpr float kProneHeight = 30.f;
+constexpr float kMaxRunVelocity = 400.f;
+constexpr float kMaxWalkVelocity = 200.f;
+constexpr float kMaxCrouchVelocity = 50.f;
+constexpr float kMaxProneVelocity = 20.f;
+constexpr float kDeaccelerateRate = 1000.f;
+constexpr int kRespawnInvincibleSteps = 5;
+constexpr int kOutOfCombatSteps = 150;
+constexpr float kAutohealPerStep = 5.f;
+constexpr int kEpisodeLen = 3000;
+constexpr int kNumMoveAmountBuckets = 3;
+constexpr int kNumMoveAngleBuckets = 8;
+constexpr float kDeltaT = 0.05f;
+constexpr int kDiscreteAimYawBuckets = 13;
+constexpr int kDiscreteAimPitchBuckets = 7;
+constexpr int kFwdW = 32, kFwdH = 2, kRearW = 8, kRearH = 2;
+constexpr int kGridW = 81, kGridMax = 40;
+
+// Weapon stats (mgr.cpp:1383-1395): one weapon type.
+constexpr int kMagSize = 30;
+constexpr int kReloadTime = 30;
+constexpr float kDmgPerBullet = 10.f;
+constexpr float kAccuracyScale = 0.005f;
+constexpr int kNumWeaponTypes = 1;
+
+// Observation struct sizes (types.hpp:275-423).
+constexpr int kSelfObs = 43, kOtherObs = 32, kLidarData = 4;
+
+enum Pose { kStand = 0, kCrouch = 1, kProne = 2 };
+
+// ----------------------------------------------- mesh_bvh.hpp:61-86 Node
+struct Node {
+    float minX, minY, minZ;
+    int8_t expX, expY, expZ;
+    uint8_t internalNodes;
+    uint8_t triSize[4];
+    uint8_t qMinX[4], qMinY[4], qMinZ[4];
+    uint8_t qMaxX[4], qMaxY[4], qMaxZ[4];
+    int32_t children[4];
+    int32_t parentID;
+};
+static_assert(sizeof(Node) == 64, "node layout");
+
+struct Spawn {
+    AABB region;
+    float yawMin, yawMax;
+};
+
+struct ZOBB {
+    Vec3 pMin, pMax;
+    float rotation;
+};
+
+struct GoalRegion {
+    ZOBB subRegions[3];
+    int numSubRegions;
+    bool attackerTeam;
+    float rewardStrength;
+};
+
+float viewHeight(int pose) // utils.hpp:37-56
+{
+    float top = pose == kStand ? kStandHeight : (pose == kCrouch ? kCrouchHeight : kProneHeight);
+    return top - kAgentRadius;
+}
+
+int32_t f2iSat(float f) // float->int conversion with defined NaN/overflow
+{
+    if (!(f == f)) return 0;
+    if (f >= 2147483520.f) return INT32_MAX;
+    if (f <= -2147483648.f) return INT32_MIN;
+    return (int32_t)f;
+}
+
+// ------------------------------------------------------------ state
+struct Agent {
+    Vec3 pos;
+    Quat rot;
+    Vec3 vel;
+    Vec3 newPos, newVel;
+    float maxVelocity;
+    int curPose, tgtPose, transitionRemaining;
+    float dmg[kMaxTeamSize];
+    float aimYaw, aimPitch;
+    Quat aimRot;
+    int team, offset;
+    RNG rng;
+    int landedShotOn;  // agent index within world, -1 = Entity::none()
+    int remainingRespawnSteps, remainingStepsBeforeAutoheal;
+    bool successfulKill;
+    int wasShotCount;
+    bool wasKilled;
+    float firedShotT;
+    bool inZone;
+    float minDistToZone;
+    bool hasDiedDuringEpisode;
+    bool reloadedFullMag;
+    int weaponType;
+    float totalPenalty;
+    int64_t lastBreadcrumb;
+    int stepsSinceLastNewBreadcrumb;
+    Vec3 startPos;
+    std::vector<uint32_t> visited;
+    uint32_t numNewCellsVisited;
+    float daimYawVel, daimPitchVel;
+    bool canSee[kMaxTeamSize];
+};
+
+struct Crumb {
+    Vec3 pos;
+    float penalty;
+    int team, offset;
+    uint32_t id;
+};
+
+struct World {
+    // MatchInfo (types.hpp:127-134)
+    int teamA, curStep;
+    bool isFinished;
+    bool enableSpawnCurriculum;
+    uint32_t curCurriculumTier, curCurriculumSpawnIdx;
+    // ZoneState (types.hpp:563-572)
+    int curZone, curControllingTeam;
+    bool isContested, isCaptured, earnedPoint;
+    int zoneStepsRemaining, stepsUntilPoint;
+    // Sim data (sim.hpp:81-191)
+    uint32_t curEpisodeIdx, worldEpisodeCounter;
+    RNG baseRNG;
+    int zoneStats[kMaxZones][5];
+    uint64_t filtersActive[2];
+    int filtersLastMatches[2][64];
+    int filtersLastMatchedStep[2];
+    int episodeCurriculum;
+    uint64_t matchID;
+    // SpawnUsageCounter (types.hpp:95-100)
+    uint32_t initASpawnsLastUsedTick[128], initBSpawnsLastUsedTick[128], respawnLastUsedTick[128];
+    // GoalRegionsState (types.hpp:808-814)
+    bool regionsActive[10];
+    float minDistToRegions[10];
+    float teamStepRewards[2];
+    // TeamRewardState
+    float teamRewards[2];
+    std::vector<Crumb> crumbs;
+    uint32_t nextCrumbId;
+    int crumbOverflow;
+};
+
+struct Oracle {
+    oracle_config cfg;
+    std::string scenePath;
+    int W, N, teamSize;
+    uint32_t worldOffset;
+    bool autoReset;
+    uint32_t simFlags;
+    RandKey initRandKey;
+
+    AABB worldBounds;
+    float maxDist;
+    float frustum[4];
+    std::vector<Node> nodes;
+    std::vector<Vec3> verts;
+    std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
+    uint32_t numDefaultASpawns, numDefaultBSpawns;
+    std::vector<AABB> zoneAABBs;
+    std::vector<float> zoneRot;
+    std::vector<GoalRegion> goalRegions;
+    int32_t trainControl[3];
+
+    std::vector<Agent> agents;
+    std::vector<World> worlds;
+
+    // Exported buffers, laid out as the reference's exported columns.
+    std::vector<int32_t> resetBuf, worldCurriculum, matchResult, exploreAction, discreteAction,
+        discreteAim, policy, done, magazine, botAction;
+    std::vector<float> aimAction, reward, selfObs, filtersObs, teammateObs, opponentObs, lastKnownObs,
+        selfPos, teammatePos, opponentPos, lastKnownPos, masks, fwdLidar, rearLidar, agentMap, hp,
+        alive, rewardCoefs;
+    std::vector<float> dbgAF, dbgWF, dbgCrumbs;
+    std::vector<int32_t> dbgAI, dbgWI;
+    std::vector<uint32_t> dbgExplore;
+
+    Agent &agent(int w, int i) { return agents[(size_t)w * N + i]; }
+    size_t gi(int w, int i) const { return (size_t)w * N + i; }
+};
+
+// ============================================================== geometry
+// mesh_bvh.inl:584-741 computeRayIsectTxfm — only kx/ky/kz and the shear
+// constants feed the traversal; the near/far error terms are unused by
+// traceRay and are omitted.
+struct RayTxfm {
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+};
+
+RayTxfm computeRayIsectTxfm(Vec3 d, Vec3 inv_d)
+{
+    float abs_x = fabs_(d.x), abs_y = fabs_(d.y), abs_z = fabs_(d.z);
+    int kz;
+    if (abs_x > abs_y && abs_x > abs_z) kz = 0;
+    else if (abs_y > abs_z) kz = 1;
+    else kz = 2;
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    if (comp(d, kz) < 0.f) std::swap(kx, ky);
+    RayTxfm t;
+    t.kx = kx; t.ky = ky; t.kz = kz;
+    t.Sx = comp(d, kx) * comp(inv_d, kz);
+    t.Sy = comp(d, ky) * comp(inv_d, kz);
+    t.Sz = comp(inv_d, kz);
+    return t;
+}
+
+// mesh_bvh.inl:433-554 (backface culling on, line 3)
+bool rayTriangleIntersection(Vec3 ta, Vec3 tb, Vec3 tc, const RayTxfm &tx, Vec3 org, float t_max,
+                             float *out_t)
+{
+    const Vec3 A = ta - org, B = tb - org, C = tc - org;
+    const float Ax = fma_(-tx.Sx, comp(A, tx.kz), comp(A, tx.kx));
+    const float Ay = fma_(-tx.Sy, comp(A, tx.kz), comp(A, tx.ky));
+    const float Bx = fma_(-tx.Sx, comp(B, tx.kz), comp(B, tx.kx));
+    const float By = fma_(-tx.Sy, comp(B, tx.kz), comp(B, tx.ky));
+    const float Cx = fma_(-tx.Sx, comp(C, tx.kz), comp(C, tx.kx));
+    const float Cy = fma_(-tx.Sy, comp(C, tx.kz), comp(C, tx.ky));
+    float U = fma_(Cx, By, -(Cy * Bx));
+    float V = fma_(Ax, Cy, -(Ay * Cx));
+    float Wb = fma_(Bx, Ay, -(By * Ax));
+    if (U < 0.0f || V < 0.0f || Wb < 0.0f) return false;
+    if (U == 0.0f || V == 0.0f || Wb == 0.0f) {
+        double CxBy = (double)Cx * (double)By;
+        double CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        double AxCy = (double)Ax * (double)Cy;
+        double AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        double BxAy = (double)Bx * (double)Ay;
+        double ByAx = (double)By * (double)Ax;
+        Wb = (float)(BxAy - ByAx);
+        if (U < 0.0f || V < 0.0f || Wb < 0.0f) return false;
+    }
+    float det = U + V + Wb;
+    if (det == 0.f) return false;
+    const float Az = tx.Sz * comp(A, tx.kz);
+    const float Bz = tx.Sz * comp(B, tx.kz);
+    const float Cz = tx.Sz * comp(C, tx.kz);
+    const float T = fma_(U, Az, fma_(V, Bz, Wb * Cz));
+    if (T < 0.0f || T > t_max * det) return false;
+    const float rcpDet = 1.0f / det;
+    *out_t = T * rcpDet;
+    return true;
+}
+
+float expScale(int8_t e) { return u2f((uint32_t)((int32_t)e + 127) << 23); }
+
+// mesh_bvh.inl:110-208 (MeshBVH::traceRay) + 360-431 (traceRayLeaf)
+bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_max = kFltMax)
+{
+    const float diveps = 0.0000001f;
+    Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
+    RayTxfm tx = computeRayIsectTxfm(ray_d, inv_d);
+
+    int32_t stack[64];
+    int sp = 0;
+    stack[sp++] = 0;
+    bool ray_hit = false;
+    while (sp > 0) {
+        int32_t node_idx = stack[--sp];
+        const Node &node = o.nodes[node_idx];
+        float rayXInv = copysign_(ray_d.x == 0 ? 1 / diveps : 1 / ray_d.x, ray_d.x);
+        float rayYInv = copysign_(ray_d.y == 0 ? 1 / diveps : 1 / ray_d.y, ray_d.y);
+        float rayZInv = copysign_(ray_d.z == 0 ? 1 / diveps : 1 / ray_d.z, ray_d.z);
+        float dirQuantX = expScale(node.expX) * rayXInv;
+        float dirQuantY = expScale(node.expY) * rayYInv;
+        float dirQuantZ = expScale(node.expZ) * rayZInv;
+        float originQuantX = (node.minX - ray_o.x) * rayXInv;
+        float originQuantY = (node.minY - ray_o.y) * rayYInv;
+        float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
+        for (int i = 0; i < 4; i++) {
+            if (node.children[i] == -1) continue;
+            float t_near_x = node.qMinX[i] * dirQuantX + originQuantX;
+            float t_near_y = node.qMinY[i] * dirQuantY + originQuantY;
+            float t_near_z = node.qMinZ[i] * dirQuantZ + originQuantZ;
+            float t_far_x = node.qMaxX[i] * dirQuantX + originQuantX;
+            float t_far_y = node.qMaxY[i] * dirQuantY + originQuantY;
+            float t_far_z = node.qMaxZ[i] * dirQuantZ + originQuantZ;
+            float t_near = fmax_(fmin_(t_near_x, t_far_x),
+                                 fmax_(fmin_(t_near_y, t_far_y), fmax_(fmin_(t_near_z, t_far_z), 0.f)));
+            float t_far = fmin_(fmax_(t_far_x, t_near_x),
+                                fmin_(fmax_(t_far_y, t_near_y), fmin_(fmax_(t_far_z, t_near_z), t_max)));
+            if (t_near <= t_far) {
+                if (node.children[i] & 0x80000000) {
+                    int32_t leaf_idx = node.children[i] & ~0x80000000;
+                    // traceRayLeaf
+                    bool hit_tri = false;
+                    float hit_t = 0.f;
+                    float leaf_tmax = t_max;
+                    for (int k = 0; k < node.triSize[i]; k++) {
+                        Vec3 a = o.verts[(leaf_idx + k) * 3 + 0];
+                        Vec3 b = o.verts[(leaf_idx + k) * 3 + 1];
+                        Vec3 c = o.verts[(leaf_idx + k) * 3 + 2];
+                        if (rayTriangleIntersection(a, b, c, tx, ray_o, leaf_tmax, &hit_t)) {
+                            hit_tri = true;
+                            leaf_tmax = hit_t;
+                        }
+                    }
+                    if (hit_tri) {
+                        ray_hit = true;
+                        t_max = hit_t;
+                    }
+                } else {
+                    stack[sp++] = node.children[i];
+                }
+            }
+        }
+    }
+    *t_hit = t_max;
+    return ray_hit;
+}
+
+// mesh_bvh.inl:817-855
+bool sphereCastNodeCheck(Vec3 o, Vec3 inv_d, float t_max, float r, AABB aabb)
+{
+    AABB e = aabb;
+    e.pMin.x -= r; e.pMin.y -= r; e.pMin.z -= r;
+    e.pMax.x += r; e.pMax.y += r; e.pMax.z += r;
+    float t_min = 0.f;
+    for (int i = 0; i < 3; i++) {
+        float inv_d_i = comp(inv_d, i);
+        float b_min, b_max;
+        if (!__builtin_signbit(inv_d_i)) {
+            b_min = comp(e.pMin, i); b_max = comp(e.pMax, i);
+        } else {
+            b_min = comp(e.pMax, i); b_max = comp(e.pMin, i);
+        }
+        float i_min = (b_min - comp(o, i)) * inv_d_i;
+        float i_max = (b_max - comp(o, i)) * inv_d_i;
+        t_min = i_min > t_min ? i_min : t_min;
+        t_max = i_max < t_max ? i_max : t_max;
+    }
+    return t_min < t_max;
+}
+
+// mesh_bvh.inl:885-1127 (Jolt-derived swept sphere vs triangle)
+float sphereCastTriangle(Vec3 ta, Vec3 tb, Vec3 tc, Vec3 ray_o, Vec3 ray_d, float t_max, float r,
+                         Vec3 *out_n)
+{
+    const Vec3 e01 = tb - ta, e02 = tc - ta, e12 = tc - tb;
+    const Vec3 v0 = ta - ray_o, v1 = tb - ray_o, v2 = tc - ray_o;
+    Vec3 nu = computeTriangleGeoNormal(e01, e02, e12);
+    float n_len = length(nu);
+    Vec3 n = nu / n_len;
+    const float n_dot_d = dot(n, ray_d);
+    const float r2 = r * r;
+
+    if (fabs_(dot(v0, n)) <= r) {
+        Vec3 q = triangleClosestPointToOrigin(v0, v1, v2, e01, e02);
+        float q_len2 = length2(q);
+        if (q_len2 <= r2) {
+            float q_len = sqrt_(q_len2);
+            *out_n = q_len > 0.0f ? q / q_len : kUp;
+            return 0.f;
+        }
+    } else {
+        float abs_n_dot_d = fabs_(n_dot_d);
+        if (abs_n_dot_d > 1.0e-6f) {
+            float sgn = copysign_(1.f, n_dot_d);
+            Vec3 extruded_delta = sgn * r * n;
+            Vec3 v0e = v0 - extruded_delta;
+            float plane_t = dot(v0e, n) / n_dot_d;
+            if (plane_t * abs_n_dot_d < -r || plane_t >= t_max) return t_max;
+            if (plane_t >= 0.0f) {
+                Vec3 e = cross(ray_d, v0e);
+                float v = -dot(e02, e) * sgn;
+                float w = dot(e01, e) * sgn;
+                if (v >= 0.f && w >= 0.f && v + w <= n_len * abs_n_dot_d) {
+                    *out_n = -sgn * n;
+                    return plane_t;
+                }
+            }
+        }
+    }
+
+    const float edge_eps = 1e-6f;
+    const float d_len2 = length2(ray_d);
+    auto testEdge = [&](Vec3 axis, Vec3 base, float hit_t) {
+        Vec3 start = -base;
+        const float s_dot_a = dot(start, axis);
+        const float d_dot_a = dot(ray_d, axis);
+        const float e_dot_a = s_dot_a + d_dot_a;
+        if (s_dot_a < 0.0f && e_dot_a < 0.0f) return hit_t;
+        const float a_len2 = length2(axis);
+        if (s_dot_a > a_len2 && e_dot_a > a_len2) return hit_t;
+        float a = a_len2 * d_len2 - d_dot_a * d_dot_a;
+        if (fabs_(a) < edge_eps) return hit_t;
+        float b = a_len2 * dot(start, ray_d) - d_dot_a * s_dot_a;
+        float c = a_len2 * (length2(start) - r2) - s_dot_a * s_dot_a;
+        float det = b * b - a * c;
+        if (det < 0.0f) return hit_t;
+        float t = -(b + sqrt_(det)) / a;
+        if (t < 0.0f || t >= hit_t) return hit_t;
+        if (s_dot_a + t * d_dot_a < 0.0f || s_dot_a + t * d_dot_a > a_len2) return hit_t;
+        return t;
+    };
+    // Faithful to mesh_bvh.inl:1073-1104: v is already relative to ray_o but
+    // is subtracted from ray_o again.
+    auto testVert = [&](Vec3 v, float hit_t) {
+        Vec3 m = ray_o - v;
+        float b = dot(m, ray_d);
+        float c = dot(m, m) - r2;
+        if (c > 0.0f && b > 0.0f) return hit_t;
+        float discr = b * b - c;
+        if (discr < 0.0f) return hit_t;
+        float t = -b - sqrt_(discr);
+        if (t < 0.f) return 0.f;
+        if (t >= hit_t) return hit_t;
+        return t;
+    };
+
+    float hit_t = t_max;
+    hit_t = testEdge(e01, v0, hit_t);
+    hit_t = testEdge(e02, v0, hit_t);
+    hit_t = testEdge(e12, v1, hit_t);
+    hit_t = testVert(v0, hit_t);
+    hit_t = testVert(v1, hit_t);
+    hit_t = testVert(v2, hit_t);
+    if (hit_t >= t_max) return t_max;
+    Vec3 hp = ray_d * hit_t;
+    Vec3 ct = triangleClosestPointToOrigin(v0 - hp, v1 - hp, v2 - hp, e01, e02);
+    *out_n = normalize(ct);
+    return hit_t;
+}
+
+// mesh_bvh.inl:743-815 (MeshBVH::sphereCast) + 857-883 (sphereCastLeaf,
+// testing triSize triangles: see file header).
+float bvhSphereCast(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float r, Vec3 *out_n,
+                    float t_max = kFltMax)
+{
+    Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
+    int32_t stack[64];
+    int sp = 0;
+    stack[sp++] = 0;
+    Vec3 closest = v3(0.f, 0.f, 0.f);
+    float hit_t = t_max;
+    while (sp > 0) {
+        int32_t node_idx = stack[--sp];
+        const Node &node = o.nodes[node_idx];
+        for (int i = 0; i < 4; i++) {
+            if (node.children[i] == -1) continue;
+            float sx = u2f((uint32_t)((int32_t)node.expX + 127) << 23);
+            float sy = u2f((uint32_t)((int32_t)node.expY + 127) << 23);
+            float sz = u2f((uint32_t)((int32_t)node.expZ + 127) << 23);
+            AABB child;
+            child.pMin = v3(node.minX + sx * node.qMinX[i], node.minY + sy * node.qMinY[i],
+                            node.minZ + sz * node.qMinZ[i]);
+            child.pMax = v3(node.minX + sx * node.qMaxX[i], node.minY + sy * node.qMaxY[i],
+                            node.minZ + sz * node.qMaxZ[i]);
+            if (sphereCastNodeCheck(ray_o, inv_d, hit_t, r, child)) {
+                if (node.children[i] & 0x80000000) {
+                    int32_t leaf_idx = node.children[i] & ~0x80000000;
+                    Vec3 leaf_n = v3(0.f, 0.f, 0.f);
+                    float leaf_t = hit_t;
+                    for (int k = 0; k < node.triSize[i]; k++) {
+                        Vec3 a = o.verts[(leaf_idx + k) * 3 + 0];
+                        Vec3 b = o.verts[(leaf_idx + k) * 3 + 1];
+                        Vec3 c = o.verts[(leaf_idx + k) * 3 + 2];
+                        leaf_t = sphereCastTriangle(a, b, c, ray_o, ray_d, leaf_t, r, &leaf_n);
+                    }
+                    if (leaf_t < hit_t) {
+                        hit_t = leaf_t;
+                        closest = leaf_n;
+                    }
+                } else {
+                    stack[sp++] = node.children[i];
+                }
+            }
+        }
+    }
+    if (hit_t < t_max) *out_n = closest;
+    return hit_t;
+}
+
+// ============================================================ utils.cpp
+struct HitResult {
+    bool hit;
+    float t;
+    int entity; // agent index in world, -1 none
+};
+
+// utils.cpp:10-72 traceRayAgainstWorld
+HitResult traceRayAgainstWorld(const Oracle &o, int w, Vec3 org, Vec3 d)
+{
+    float min_hit_t = kFltMax;
+    float t_bvh;
+    bool hit = bvhTraceRay(o, org, d, &t_bvh);
+    if (hit) min_hit_t = t_bvh;
+    int hit_entity = -1;
+    for (int j = 0; j < o.N; j++) {
+        const Agent &a = o.agents[o.gi(w, j)];
+        Vec3 capsule_origin = a.pos;
+        capsule_origin.z += kAgentRadius;
+        Vec3 translated = org - capsule_origin;
+        float t = intersectRayZOriginCapsule(translated, d, kAgentRadius, kStandHeight - 2.f * kAgentRadius);
+        if (t != 0 && t < min_hit_t) {
+            min_hit_t = t;
+            hit = true;
+            hit_entity = j;
+        }
+    }
+    return { hit, min_hit_t, hit_entity };
+}
+
+// utils.cpp:75-138 sphereCastWorld (agent capsules disabled, #if 0)
+float sphereCastWorld(const Oracle &o, Vec3 org, Vec3 d, float r, Vec3 &normal)
+{
+    return bvhSphereCast(o, org, d, r, &normal);
+}
+
+float sphereCastWorld(const Oracle &o, Vec3 org, Vec3 d, float r)
+{
+    Vec3 n = v3(0.f, 0.f, 0.f);
+    return bvhSphereCast(o, org, d, r, &n);
+}
+
+struct AimS {
+    float yaw, pitch;
+    Quat rot;
+};
+
+// utils.cpp:140-167 computeAim
+AimS computeAim(float yaw, float pitch)
+{
+    if (yaw < -kPi) yaw += 2.f * kPi;
+    else if (yaw > kPi) yaw -= 2.f * kPi;
+    if (pitch < -0.25f * kPi) pitch = -0.25f * kPi;
+    if (pitch > 0.25f * kPi) pitch = 0.25f * kPi;
+    Quat r = angleAxis(yaw, kUp) * angleAxis(pitch, kRight);
+    r = qnormalize(r);
+    return { yaw, pitch, r };
+}
+
+// utils.cpp:169-184
+bool inFrustum(const Oracle &o, Vec3 vp)
+{
+    bool in = true;
+    in = in && vp.y * o.frustum[1] - fabs_(vp.x) * o.frustum[0] > -kAgentRadius;
+    in = in && vp.y * o.frustum[3] - fabs_(vp.z) * o.frustum[2] > -kAgentRadius;
+    return in;
+}
+
+// utils.cpp:186-271 isAgentVisible (only the boolean result is consumed in
+// the Zone task; the running mean of visible points is not needed)
+bool isAgentVisible(const Oracle &o, int w, Vec3 org, Quat aim_rot, int target)
+{
+    const Agent &t = o.agents[o.gi(w, target)];
+    Vec3 base = t.pos;
+    auto testVisible = [&](Vec3 p) {
+        Vec3 to_test = p - org;
+        Vec3 view = rotateVec(qinv(aim_rot), to_test);
+        if (view.y <= 0.f) return false;
+        if (!inFrustum(o, view)) return false;
+        float len = length(to_test);
+        if (len < kAgentRadius) return false;
+        to_test = to_test / len;
+        HitResult h = traceRayAgainstWorld(o, w, org, to_test);
+        if (!h.hit) return false;
+        return h.entity == target;
+    };
+    float vh = viewHeight(t.curPose);
+    Vec3 aim_right = rotateVec(aim_rot, kRight);
+    Vec3 delta_right = aim_right * 0.9f * kAgentRadius;
+    Vec3 bottom = base; bottom.z += kAgentRadius;
+    Vec3 top = base; top.z += vh;
+    Vec3 right = base; right.z += vh; right = right + delta_right;
+    Vec3 left = base; left.z += vh; left = left - delta_right;
+    int num_visible = 0;
+    if (testVisible(bottom)) num_visible++;
+    if (testVisible(top)) num_visible++;
+    if (testVisible(left)) num_visible++;
+    if (testVisible(right)) num_visible++;
+    return num_visible > 0;
+}
+
+// utils.cpp:273-479 standardSpawnPoint (Zone task: no TDM episode branch)
+void standardSpawnPoint(Oracle &o, int w, int ai, bool is_respawn, bool use_middle_spawn, Vec3 *out_pt,
+                        float *out_yaw)
+{
+    World &wd = o.worlds[w];
+    Agent &ag = o.agent(w, ai);
+    RNG &rng = ag.rng;
+
+    const Spawn *options;
+    int num_spawns;
+    auto spawnAgent = [&](int idx) {
+        Spawn s = options[idx];
+        float x_rnd = rngUniform(rng);
+        float y_rnd = rngUniform(rng);
+        float z_rnd = rngUniform(rng);
+        float yaw_rnd = rngUniform(rng);
+        float x_min = s.region.pMin.x, x_diff = s.region.pMax.x - x_min;
+        float y_min = s.region.pMin.y, y_diff = s.region.pMax.y - y_min;
+        float z_min = s.region.pMin.z, z_diff = s.region.pMax.z - z_min;
+        *out_pt = v3(x_min + x_rnd * x_diff, y_min + y_rnd * y_diff, z_min + z_rnd * z_diff);
+        *out_yaw = s.yawMin + yaw_rnd * (s.yawMax - s.yawMin);
+    };
+
+    if (!is_respawn || o.commonRespawns.empty()) {
+        uint32_t *tracker;
+        int num_default, num_extra;
+        if (ag.team == wd.teamA) {
+            options = o.aSpawns.data();
+            num_default = (int)o.numDefaultASpawns;
+            num_extra = (int)o.aSpawns.size() - num_default;
+            tracker = wd.initASpawnsLastUsedTick;
+        } else {
+            options = o.bSpawns.data();
+            num_default = (int)o.numDefaultBSpawns;
+            num_extra = (int)o.bSpawns.size() - num_default;
+            tracker = wd.initBSpawnsLastUsedTick;
+        }
+        if (use_middle_spawn) {
+            options += num_default;
+            num_spawns = num_extra;
+        } else {
+            num_spawns = num_default;
+        }
+        int init_idx = -1;
+        for (int i = 0; i < 5; i++) {
+            int idx = rngI32(rng, 0, num_spawns);
+            if (tracker[idx] == (uint32_t)wd.curStep) continue;
+            init_idx = idx;
+            break;
+        }
+        if (init_idx == -1) init_idx = rngI32(rng, 0, num_spawns);
+        spawnAgent(init_idx);
+        tracker[init_idx] = (uint32_t)wd.curStep;
+        return;
+    }
+
+    options = o.commonRespawns.data();
+    num_spawns = (int)o.commonRespawns.size();
+    AABB zone_aabb = o.zoneAABBs[wd.curZone];
+    Vec3 zone_center = 0.5f * (zone_aabb.pMin + zone_aabb.pMax);
+
+    float best_score = kFltMax;
+    int best_idx = -1;
+    for (int s = 0; s < num_spawns; s++) {
+        uint32_t last_used = wd.respawnLastUsedTick[s];
+        if (last_used == (uint32_t)wd.curStep) continue;
+        float score = 0.f;
+        uint32_t elapsed = (uint32_t)(kDeltaT * float((uint32_t)wd.curStep - last_used));
+        const float elapsed_weight = 0.1f, dist_weight = 0.01f;
+        if (elapsed < 3.f) score += elapsed_weight * (3.f - elapsed);
+        Spawn sp = options[s];
+        Vec3 spawn_pt = 0.5f * (sp.region.pMin + sp.region.pMax);
+        for (int j = 0; j < o.N; j++) {
+            if (j == ai) continue;
+            const Agent &other = o.agent(w, j);
+            if (o.alive[o.gi(w, j)] == 0.f) continue;
+            float dist = distance(spawn_pt, other.pos);
+            if (dist < 4.f * kAgentRadius) {
+                score += 100000.f;
+            } else {
+                if (other.team == ag.team) continue;
+                score += dist_weight * (1.f / dist);
+            }
+        }
+        float dz = distance(spawn_pt, zone_center);
+        if (dz < 100.f) score += 1000000.f;
+        if (score < best_score) {
+            best_idx = s;
+            best_score = score;
+        }
+    }
+    if (best_idx < 0) best_idx = 0; // assert(best_spawn_idx != -1) in the reference
+    spawnAgent(best_idx);
+    wd.respawnLastUsedTick[best_idx] = (uint32_t)wd.curStep;
+}
+
+// utils.cpp:734-948 spawnAgents (Zone task, default flags)
+void spawnAgents(Oracle &o, int w, bool is_respawn)
+{
+    World &wd = o.worlds[w];
+    int dead[2 * kMaxTeamSize];
+    int num_dead = 0;
+    for (int i = 0; i < o.N; i++) {
+        if (o.alive[o.gi(w, i)] == 0.f) dead[num_dead++] = i;
+    }
+    if (num_dead == 0) return;
+
+    RNG &base = wd.baseRNG;
+    (void)rngI32(base, 0, 0); // episodes[sampleI32(0, numEpisodes = 0)] (utils.cpp:788-789)
+
+    bool use_middle = false;
+    if (o.simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) use_middle = rngUniform(base) < 0.5f;
+    const bool randomize_hp = (o.simFlags & MPENV_SIMFLAG_RANDOMIZE_HP_MAGAZINE) != 0;
+
+    for (int d = 0; d < num_dead; d++) {
+        int ai = dead[d];
+        Agent &ag = o.agent(w, ai);
+        size_t g = o.gi(w, ai);
+        Vec3 spawn_pt;
+        float spawn_yaw;
+        float spawn_pitch = 0.f;
+        standardSpawnPoint(o, w, ai, is_respawn, use_middle, &spawn_pt, &spawn_yaw);
+
+        ag.pos = spawn_pt;
+        ag.rot = qnormalize(angleAxis(spawn_yaw, kUp));
+        AimS aim = computeAim(spawn_yaw, spawn_pitch);
+        ag.aimYaw = aim.yaw; ag.aimPitch = aim.pitch; ag.aimRot = aim.rot;
+        ag.vel = v3(0.f, 0.f, 0.f);
+
+        ag.weaponType = rngI32(base, 0, kNumWeaponTypes);
+        if (randomize_hp) {
+            int tenth = rngI32(base, 1, 11);
+            o.hp[g] = float(tenth * 10);
+            o.magazine[2 * g] = rngI32(base, 0, kMagSize);
+            o.magazine[2 * g + 1] = 0;
+        } else {
+            o.hp[g] = 100.f;
+            o.magazine[2 * g] = kMagSize;
+            o.magazine[2 * g + 1] = 0;
+        }
+        ag.remainingRespawnSteps = is_respawn ? 0 : kRespawnInvincibleSteps;
+        ag.remainingStepsBeforeAutoheal = 0;
+
+        {
+            AABB zone_aabb = o.zoneAABBs[wd.curZone];
+            Vec3 zone_center = (zone_aabb.pMax + zone_aabb.pMin) / 2.f;
+            float rot_angle = o.zoneRot[wd.curZone];
+            Quat to_zone = qinv(angleAxis(rot_angle, kUp));
+            zone_aabb.pMin = rotateVec(to_zone, zone_aabb.pMin);
+            zone_aabb.pMax = rotateVec(to_zone, zone_aabb.pMax);
+            Vec3 pos_in_zone = rotateVec(to_zone, spawn_pt);
+            spawn_pt.z += kStandHeight / 2.f;
+            ag.inZone = aabbContains(zone_aabb, pos_in_zone);
+            ag.minDistToZone = distance(spawn_pt, zone_center);
+        }
+
+        ag.curPose = kStand; ag.tgtPose = kStand; ag.transitionRemaining = 0;
+        ag.newPos = ag.pos;
+        ag.newVel = v3(0.f, 0.f, 0.f);
+        ag.maxVelocity = kMaxWalkVelocity;
+        ag.daimYawVel = 0.f; ag.daimPitchVel = 0.f;
+        o.alive[g] = 1.f;
+    }
+}
+
+// ====================================================== level_gen.cpp
+// level_gen.cpp:19-328 createPersistentEntities (agents only: static
+// geometry, zone/camera/sub-zone entities are visualisation-only)
+void createPersistentEntities(Oracle &o, int w)
+{
+    for (int i = 0; i < o.N; i++) {
+        Agent &ag = o.agent(w, i);
+        size_t g = o.gi(w, i);
+        ag.visited.assign((size_t)kGridW * kGridW, 0u);
+        for (int y = 0; y < kGridMax; y++)
+            for (int x = 0; x < kGridMax; x++)
+                ag.visited[(size_t)y * kGridW + x] = 0xFFFFFFFFu;
+        o.policy[g] = 0;
+        o.aimAction[2 * g] = 0.f; o.aimAction[2 * g + 1] = 0.f;
+        o.discreteAim[2 * g] = kDiscreteAimYawBuckets / 2;
+        o.discreteAim[2 * g + 1] = kDiscreteAimPitchBuckets / 2;
+        ag.daimYawVel = 0.f; ag.daimPitchVel = 0.f;
+        ag.team = i / o.teamSize;
+        ag.offset = i - ag.team * o.teamSize;
+        for (int j = 0; j < kMaxTeamSize; j++) ag.dmg[j] = 0.f;
+    }
+}
+
+// level_gen.cpp:330-582 resetPersistentEntities
+void resetPersistentEntities(Oracle &o, int w, RandKey episode_key)
+{
+    World &wd = o.worlds[w];
+    RNG &base = wd.baseRNG;
+    for (int i = 0; i < o.N; i++) {
+        Agent &ag = o.agent(w, i);
+        size_t g = o.gi(w, i);
+        ag.pos = v3(kFltMax, kFltMax, kFltMax);
+        ag.rng = makeRNG(splitI(episode_key, (uint32_t)(i + 1)));
+        ag.landedShotOn = -1;
+        ag.remainingRespawnSteps = 0;
+        ag.remainingStepsBeforeAutoheal = 0;
+        ag.successfulKill = false;
+        ag.wasShotCount = 0;
+        ag.wasKilled = false;
+        ag.firedShotT = -kFltMax;
+        ag.hasDiedDuringEpisode = false;
+        ag.reloadedFullMag = false;
+        o.alive[g] = 0.f;
+        for (int j = 0; j < kMaxTeamSize; j++) {
+            float *lk = &o.lastKnownObs[(g * kMaxTeamSize + j) * kOtherObs];
+            std::fill(lk, lk + kOtherObs, 0.f);
+            float *lkp = &o.lastKnownPos[(g * kMaxTeamSize + j) * 3];
+            lkp[0] = lkp[1] = lkp[2] = -1000.f;
+        }
+        ag.totalPenalty = 0.f;
+        ag.lastBreadcrumb = -1;
+        ag.stepsSinceLastNewBreadcrumb = 0;
+    }
+    for (int i = 0; i < 128; i++) {
+        wd.initASpawnsLastUsedTick[i] = 0xFFFFFFFFu;
+        wd.initBSpawnsLastUsedTick[i] = 0xFFFFFFFFu;
+        wd.respawnLastUsedTick[i] = 0xFFFFFFFFu;
+    }
+    spawnAgents(o, w, false);
+
+    for (int i = 0; i < o.N; i++) {
+        Agent &ag = o.agent(w, i);
+        size_t g = o.gi(w, i);
+        ag.startPos = ag.pos;
+        for (int k = 0; k < 4; k++) o.discreteAction[4 * g + k] = 0;
+        o.aimAction[2 * g] = 0.f; o.aimAction[2 * g + 1] = 0.f;
+        ag.numNewCellsVisited = 0;
+        auto sampleCoef = [&base](float a, float b) { return a + (b - a) * rngUniform(base); };
+        // level_gen.cpp:434-444: nine draws, then overwritten with defaults (446)
+        (void)sampleCoef(0.f, 1.f);
+        (void)sampleCoef(0.01f, 0.2f);
+        (void)sampleCoef(0.0001f, 0.005f);
+        (void)sampleCoef(0.0f, 0.05f);
+        (void)sampleCoef(0.0f, 0.01f);
+        (void)sampleCoef(0.0f, 0.1f);
+        (void)sampleCoef(0.0f, 0.01f);
+        (void)sampleCoef(0.1f, 2.0f);
+        (void)sampleCoef(0.01f, 0.5f);
+        float *rc = &o.rewardCoefs[9 * g];
+        rc[0] = 0.f; rc[1] = 0.5f; rc[2] = 0.005f; rc[3] = 0.05f; rc[4] = 0.01f;
+        rc[5] = 0.1f; rc[6] = 0.0005f; rc[7] = 1.f; rc[8] = 0.1f;
+    }
+
+    for (int i = 0; i < (int)o.goalRegions.size(); i++) {
+        wd.regionsActive[i] = true;
+        wd.minDistToRegions[i] = kFltMax;
+    }
+    wd.teamStepRewards[0] = 0.f;
+    wd.teamStepRewards[1] = 0.f;
+}
+
+// sim.cpp:732-833 initWorld
+void initWorld(Oracle &o, int w, bool triggered_reset)
+{
+    World &wd = o.worlds[w];
+    const uint32_t world_id = o.worldOffset + (uint32_t)w;
+    wd.episodeCurriculum = o.worldCurriculum[w];
+    wd.matchID = ((uint64_t)world_id << 32) | (uint64_t)wd.curEpisodeIdx;
+
+    RandKey episode_key = splitI(o.initRandKey, wd.curEpisodeIdx, world_id);
+    wd.baseRNG = makeRNG(splitI(episode_key, 0));
+    RNG &base = wd.baseRNG;
+
+    bool flip = false;
+    if (o.trainControl[2]) flip = rngUniform(base) < 0.5f;
+    wd.teamA = flip ? 1 : 0;
+    if (triggered_reset && o.trainControl[1]) {
+        wd.curStep = rngI32(base, 0, kEpisodeLen - 1);
+    } else {
+        wd.curStep = 0;
+    }
+    wd.isFinished = false;
+
+    // CurriculumState (sim.cpp:5915-5924)
+    const float use_prob = 1.0f;
+    const float tier_probs[5] = { 0.f, 0.f, 0.3f, 0.3f, 0.4f };
+    wd.enableSpawnCurriculum = rngUniform(base) < use_prob;
+    float cdf[5];
+    float running = 0.f;
+    for (int i = 0; i < 5; i++) { running += tier_probs[i]; cdf[i] = running; }
+    float sel = running * rngUniform(base);
+    for (int i = 0; i < 5; i++) {
+        if (sel < cdf[i]) { wd.curCurriculumTier = (uint32_t)i; break; }
+    }
+    // SpawnCurriculum tiers are only consumed by the disabled
+    // curriculumSpawnPoint (utils.cpp:652-732); only the draw matters.
+    wd.curCurriculumSpawnIdx = (uint32_t)rngI32(base, 0, 0);
+
+    if (o.simFlags & MPENV_SIMFLAG_HARDCODED_SPAWNS) (void)rngI32(base, 0, 4);
+
+    wd.curZone = rngI32(base, 0, (int)o.zoneAABBs.size());
+    wd.curControllingTeam = -1;
+    wd.isContested = false;
+    wd.isCaptured = false;
+    wd.earnedPoint = false;
+    wd.zoneStepsRemaining = kNumStepsPerZone;
+    wd.stepsUntilPoint = kZonePointInterval;
+
+    resetPersistentEntities(o, w, episode_key);
+
+    for (int t = 0; t < 2; t++) {
+        wd.filtersActive[t] = 0;
+        wd.filtersLastMatchedStep[t] = 0;
+    }
+}
+
+// sim.cpp:835-872 resetSystem
+void resetSystem(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    int32_t force_reset = o.resetBuf[w];
+    int32_t should_reset = force_reset;
+    if (o.autoReset && wd.isFinished) should_reset = 1;
+    if (should_reset != 0) {
+        o.resetBuf[w] = 0;
+        wd.curEpisodeIdx = wd.worldEpisodeCounter++;
+        if (o.simFlags & MPENV_SIMFLAG_ENABLE_CURRICULUM) {
+            if (wd.curEpisodeIdx < 50) {
+                if (rngUniform(wd.baseRNG) < (wd.curEpisodeIdx + 1) / (float)50) o.worldCurriculum[w] = 1;
+                else o.worldCurriculum[w] = 0;
+            } else {
+                o.worldCurriculum[w] = 1;
+            }
+        }
+        initWorld(o, w, force_reset == 1);
+    }
+}
+
+// ====================================================== step systems
+Vec3 rotate2D(Vec3 dir, float radians) // sim.cpp:874-879
+{
+    float c = cosf_(radians);
+    float s = sinf_(radians);
+    return v3(c * dir.x - s * dir.y, s * dir.x + c * dir.y, 0);
+}
+
+// sim.cpp:2093-2199 pvpMovementSystem
+void pvpMovementSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    if (o.alive[g] == 0.f) return;
+    const int32_t *action = &o.discreteAction[4 * g];
+    {
+        Vec3 v = ag.vel;
+        float v_len = length(v);
+        if (v_len > 0.f) {
+            Vec3 norm_v = v / v_len;
+            v_len -= kDeaccelerateRate * kDeltaT;
+            v_len = fmaxD(0.f, v_len);
+            ag.vel = norm_v * v_len;
+        }
+    }
+    if (ag.transitionRemaining > 0) {
+        ag.transitionRemaining -= 1;
+        if (ag.transitionRemaining == 0) ag.curPose = ag.tgtPose;
+    }
+    int action_pose = action[3];
+    if (action_pose != ag.tgtPose) {
+        ag.tgtPose = action_pose;
+        int dst = std::abs(ag.tgtPose - ag.curPose);
+        ag.transitionRemaining = dst * (kPoseTransitionSpeed / 2);
+    }
+    int32_t move_amount_d = action[0];
+    int32_t move_angle_d = action[1];
+    float accel_max = 3000;
+    if (ag.curPose == kCrouch) accel_max = 100;
+    else if (ag.curPose == kProne) accel_max = 50;
+    float move_amount = (float)move_amount_d * (accel_max / (float)(kNumMoveAmountBuckets - 1));
+    const float per_bucket = 2.f * kPi / float(kNumMoveAngleBuckets);
+    float move_angle = float(move_angle_d) * per_bucket;
+    float f_x = move_amount * sinf_(move_angle);
+    float f_y = move_amount * cosf_(move_angle);
+    ag.vel = ag.vel + rotateVec(ag.rot, v3(f_x, f_y, 0)) * kDeltaT;
+    if (move_amount != 0) ag.remainingRespawnSteps = 0;
+    float v_len = length(ag.vel);
+    if (v_len == 0.f) return;
+    {
+        const float max_change = 510.f;
+        float tgt;
+        if (ag.curPose == kStand) tgt = move_amount_d == 2 ? kMaxRunVelocity : kMaxWalkVelocity;
+        else if (ag.curPose == kCrouch) tgt = kMaxCrouchVelocity;
+        else tgt = kMaxProneVelocity;
+        float diff = tgt - ag.maxVelocity;
+        float adj = fmaxD(fminD(diff, max_change), -max_change);
+        ag.maxVelocity += adj;
+    }
+    Vec3 v_norm = ag.vel / v_len;
+    v_len = fminD(v_len, ag.maxVelocity);
+    ag.vel = v_norm * v_len;
+}
+
+// sim.cpp:2266-2282 pvpContinuousAimSystem
+void pvpContinuousAimSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    if (o.alive[g] == 0.f) return;
+    ag.aimYaw += o.aimAction[2 * g] * kDeltaT;
+    ag.aimPitch += o.aimAction[2 * g + 1] * kDeltaT;
+    AimS a = computeAim(ag.aimYaw, ag.aimPitch);
+    ag.aimYaw = a.yaw; ag.aimPitch = a.pitch; ag.aimRot = a.rot;
+    ag.rot = qnormalize(angleAxis(ag.aimYaw, kUp));
+}
+
+// sim.cpp:2284-2370 pvpDiscreteAimSystem
+void pvpDiscreteAimSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    if (o.alive[g] == 0.f) return;
+    static const float yaw_turn[7] = { 0, 0.00390625f * kPi, 0.0078125f * kPi, 0.015625f * kPi,
+                                       0.03125f * kPi, 0.0625f * kPi, 0.125f * kPi };
+    static const float pitch_turn[4] = { 0, 0.0078125f * kPi, 0.015625f * kPi, 0.03125f * kPi };
+    int yb = o.discreteAim[2 * g] - kDiscreteAimYawBuckets / 2;
+    if (yb < 0) ag.aimYaw -= yaw_turn[std::abs(yb)];
+    else ag.aimYaw += yaw_turn[std::abs(yb)];
+    int pb = o.discreteAim[2 * g + 1] - kDiscreteAimPitchBuckets / 2;
+    if (pb < 0) ag.aimPitch -= pitch_turn[std::abs(pb)];
+    else ag.aimPitch += pitch_turn[std::abs(pb)];
+    AimS a = computeAim(ag.aimYaw, ag.aimPitch);
+    ag.aimYaw = a.yaw; ag.aimPitch = a.pitch; ag.aimRot = a.rot;
+    ag.rot = qnormalize(angleAxis(ag.aimYaw, kUp));
+}
+
+// sim.cpp:2057-2091 applyBotActionsSystem
+void applyBotActionsSystem(Oracle &o, int w, int i)
+{
+    size_t g = o.gi(w, i);
+    if (o.policy[g] != -1) return;
+    const int32_t *hb = &o.botAction[7 * g];
+    o.discreteAction[4 * g + 0] = hb[0];
+    o.discreteAction[4 * g + 1] = hb[1];
+    o.discreteAction[4 * g + 2] = hb[4];
+    o.discreteAction[4 * g + 3] = hb[6];
+    const float turn_delta = 10.f / (float)(5 / 2);
+    o.aimAction[2 * g] = turn_delta * (float)(hb[2] - 5 / 2);
+    o.aimAction[2 * g + 1] = turn_delta * (float)(hb[3] - 5 / 2);
+}
+
+// sim.cpp:889-1028 applyVelocitySystem (+ updateMoveStateSystem 1030-1039)
+void applyVelocitySystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    Vec3 x = ag.pos;
+    Vec3 v = ag.vel;
+    v.z = 0;
+    ag.newPos = x;
+    ag.newVel = v3(0.f, 0.f, 0.f);
+    float v_len = length(v);
+    if (v_len == 0.f) return;
+    Vec3 v_norm = v / v_len;
+    float move_dist = v_len * kDeltaT;
+
+    const float buffer = 0.05f * kAgentRadius;
+    const float r = kAgentRadius;
+    float top = kStandHeight - r;
+    float low_check = kProneHeight;
+    if (ag.curPose == kCrouch) {
+        top = kCrouchHeight - r;
+    } else if (ag.curPose == kProne) {
+        top = low_check;
+        low_check = kProneHeight - r + buffer;
+    }
+
+    Vec3 ray_o = x;
+    ray_o.z += top;
+    Vec3 normal = v3(0.f, 0.f, 0.f);
+    sphereCastWorld(o, ray_o, -kUp, r, normal);
+    if (normal.z > 0.0f && normal.z < 0.7 && dot(normal, v_norm) < 0.0f) return;
+
+    ray_o = x + v_norm * buffer * 0.5f;
+    ray_o.z += low_check;
+    float low_dist = sphereCastWorld(o, ray_o, v_norm, r, normal);
+    float high_dist = low_dist;
+    bool high_hit = false;
+    if (ag.curPose != kProne) {
+        ray_o.z = x.z + top;
+        Vec3 high_normal = v3(0.f, 0.f, 0.f);
+        high_dist = sphereCastWorld(o, ray_o, v_norm, r, high_normal);
+        if (high_dist < low_dist) {
+            low_dist = high_dist;
+            normal = high_normal;
+            high_hit = true;
+        }
+    }
+    bool stuck = low_dist == 0.0f || high_dist == 0.0f;
+    low_dist = fmaxD(0.0f, low_dist - buffer);
+    high_dist = fmaxD(0.0f, high_dist - buffer);
+    Vec3 hit_pos = x + v_norm * fminD(low_dist, move_dist);
+
+    if (move_dist > low_dist) {
+        Vec3 slide_dir = normalize(cross(kUp, normal));
+        if (dot(slide_dir, v_norm) < 0) slide_dir = -slide_dir;
+        ray_o = x + v_norm * low_dist;
+        ray_o.z += high_hit ? top : low_check;
+        float slide = sphereCastWorld(o, ray_o, slide_dir, r);
+        slide = fmaxD(0.0f, slide - buffer);
+        float max_move = move_dist - low_dist;
+        slide = fminD(slide, max_move);
+        if (slide > 0.0f) hit_pos = hit_pos + slide_dir * slide;
+    }
+
+    Vec3 ground_check = hit_pos;
+    ground_check.z += top;
+    float ground_dist = sphereCastWorld(o, ground_check, -kUp, r);
+    if (ground_dist == kFltMax) return;
+
+    if (ground_dist <= 0.0f || stuck) {
+        float furthest = 0.0f;
+        int best_dir = -1;
+        for (int dir = 0; dir < 4; dir++) {
+            Vec3 dv = rotate2D(v_norm, (float)dir * 3.14159f * 0.5f);
+            ray_o = x - dv * r * 2.0f;
+            ray_o.z += low_check;
+            float hd = sphereCastWorld(o, ray_o, dv, r);
+            if (hd > furthest) {
+                furthest = hd;
+                best_dir = dir;
+            }
+        }
+        if (best_dir != -1) {
+            Vec3 dv = rotate2D(v_norm, (float)best_dir * 3.14159f * 0.5f);
+            hit_pos = x + dv * (fminD(furthest - r * 2.0f, -buffer));
+            ground_check = hit_pos;
+            ground_check.z += top;
+            ground_dist = sphereCastWorld(o, ground_check, -kUp, r);
+            if (ground_dist == kFltMax) return;
+        }
+    }
+
+    float fall_dist = fminD(ground_dist, top) + r;
+    Vec3 new_pos = ground_check;
+    new_pos.z -= fall_dist;
+    Vec3 to_new = new_pos - x;
+    float to_new_dist = length(to_new);
+    if (to_new_dist == 0.f) return;
+    ag.newPos = new_pos;
+    ag.newVel = to_new / kDeltaT;
+}
+
+// sim.cpp:1041-1095 fallSystem (+ updateMoveStatePostFallSystem 1097-1104)
+void fallSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    if (o.alive[g] == 0.f) {
+        ag.newPos = ag.pos;
+        return;
+    }
+    const float fall_rate = 386.08858267717f;
+    const float cast_offset = kAgentRadius;
+    Vec3 ray_o = ag.pos;
+    ray_o.z += kAgentRadius + cast_offset;
+    float ground = sphereCastWorld(o, ray_o, -kUp, kAgentRadius);
+    if (ground == kFltMax || ground < cast_offset) {
+        ag.newPos = ag.pos;
+        return;
+    }
+    float fall = fminD(ground - cast_offset, fall_rate * kDeltaT);
+    Vec3 np = ag.pos;
+    np.z -= fall;
+    ag.newPos = np;
+}
+
+// sim.cpp:1443-1615 fireSystem
+void fireSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    ag.landedShotOn = -1;
+    ag.successfulKill = false;
+    ag.firedShotT = -kFltMax;
+    ag.reloadedFullMag = false;
+    if (o.alive[g] == 0.f) return;
+    int32_t *mag = &o.magazine[2 * g];
+    int fire = o.discreteAction[4 * g + 2];
+    if (fire == 2) {
+        if (mag[0] == kMagSize) ag.reloadedFullMag = true;
+        mag[0] = kMagSize;
+        mag[1] = kReloadTime;
+    }
+    bool reload_in_progress = mag[1] > 0;
+    if (reload_in_progress) mag[1] -= 1;
+    bool should_fire = false;
+    if (!reload_in_progress && mag[0] > 0) should_fire = fire == 1;
+    if (!should_fire) return;
+    mag[0] -= 1;
+
+    Vec3 fire_from = ag.pos;
+    fire_from.z += viewHeight(ag.curPose);
+    float u1 = rngUniform(ag.rng);
+    float u2 = rngUniform(ag.rng);
+    float z1 = sqrt_(-2.f * logf_(u1)) * cosf_(2.f * kPi * u2);
+    float z2 = sqrt_(-2.f * logf_(u1)) * sinf_(2.f * kPi * u2);
+    float acc = kAccuracyScale;
+    float bias = 1.5f;
+    float up_delta = fminD(fmaxD((z1 + bias) * acc, 0.f), 4.f * acc);
+    float right_delta = fminD(fmaxD(z2 * acc, -4.f * acc), 4.f * acc);
+    ag.aimYaw += right_delta;
+    ag.aimPitch += up_delta;
+    AimS a = computeAim(ag.aimYaw, ag.aimPitch);
+    ag.aimYaw = a.yaw; ag.aimPitch = a.pitch; ag.aimRot = a.rot;
+    Vec3 fire_dir = rotateVec(ag.aimRot, kFwd);
+
+    HitResult h = traceRayAgainstWorld(o, w, fire_from, fire_dir);
+    ag.firedShotT = h.hit ? h.t : kFltMax;
+    bool success = h.hit;
+    if (h.entity == -1) {
+        success = false;
+    } else {
+        const Agent &tgt = o.agent(w, h.entity);
+        if (success && tgt.team == ag.team) success = false;
+        if (success && tgt.remainingRespawnSteps > 0) success = false;
+    }
+    if (!success) return;
+    ag.landedShotOn = h.entity;
+    if (o.hp[o.gi(w, h.entity)] <= kDmgPerBullet) ag.successfulKill = true;
+    o.agent(w, h.entity).dmg[ag.offset] = kDmgPerBullet;
+}
+
+// sim.cpp:1794-1836 applyDmgSystem
+void applyDmgSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    ag.wasShotCount = 0;
+    ag.wasKilled = false;
+    if (ag.remainingRespawnSteps > 0) ag.remainingRespawnSteps -= 1;
+    for (int k = 0; k < o.teamSize; k++) {
+        if (ag.dmg[k] > 0.f) {
+            ag.wasShotCount += 1;
+            ag.remainingStepsBeforeAutoheal = kOutOfCombatSteps;
+        }
+        o.hp[g] -= ag.dmg[k];
+        ag.dmg[k] = 0.f;
+    }
+    if (o.alive[g] == 1.f && o.hp[g] <= 0.f) {
+        ag.wasKilled = true;
+        ag.hasDiedDuringEpisode = true;
+    }
+    if (o.hp[g] <= 0.f) {
+        o.hp[g] = 0.f;
+        o.alive[g] = 0.f;
+        ag.pos = v3(0, 0, 10000.f);
+        ag.vel = v3(0, 0, 0);
+    } else {
+        o.alive[g] = 1.f;
+    }
+}
+
+// sim.cpp:1875-1890 autoHealSystem
+void autoHealSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    if (o.alive[g] == 0.f) return;
+    if (ag.remainingStepsBeforeAutoheal == 0 && o.hp[g] < 100.f) {
+        o.hp[g] = fminD(100.f, o.hp[g] + kAutohealPerStep);
+    } else if (ag.remainingStepsBeforeAutoheal > 0) {
+        ag.remainingStepsBeforeAutoheal -= 1;
+    }
+}
+
+// sim.cpp:1892-1976 zoneSystem
+void zoneSystem(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    if (wd.curControllingTeam != -1) wd.zoneStepsRemaining -= 1;
+    if (wd.zoneStepsRemaining == 0) {
+        wd.curZone += 1;
+        if (wd.curZone == (int)o.zoneAABBs.size()) wd.curZone = 0;
+        wd.isCaptured = false;
+        wd.zoneStepsRemaining = kNumStepsPerZone;
+        wd.stepsUntilPoint = kZonePointInterval;
+        AABB za = o.zoneAABBs[wd.curZone];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        for (int i = 0; i < o.N; i++) {
+            Agent &ag = o.agent(w, i);
+            ag.minDistToZone = distance(ag.pos, center);
+        }
+    }
+    AABB za = o.zoneAABBs[wd.curZone];
+    float rot_angle = o.zoneRot[wd.curZone];
+    Quat to_zone = qinv(angleAxis(rot_angle, kUp));
+    za.pMin = rotateVec(to_zone, za.pMin);
+    za.pMax = rotateVec(to_zone, za.pMax);
+    int na = 0, nb = 0;
+    for (int i = 0; i < o.N; i++) {
+        Agent &ag = o.agent(w, i);
+        Vec3 p = ag.pos;
+        p.z += kStandHeight / 2.f;
+        Vec3 pz = rotateVec(to_zone, p);
+        if (!aabbContains(za, pz)) {
+            ag.inZone = false;
+            continue;
+        }
+        ag.inZone = true;
+        if (ag.team == 0) na += 1;
+        if (ag.team == 1) nb += 1;
+    }
+    wd.stepsUntilPoint -= 1;
+    wd.isContested = na > 0 && nb > 0;
+    if (wd.isContested || (na == 0 && nb == 0)) {
+        wd.curControllingTeam = -1;
+        wd.isCaptured = false;
+        wd.stepsUntilPoint = kZonePointInterval;
+    } else if (na > 0 && nb == 0) {
+        if (wd.curControllingTeam != 0) {
+            wd.curControllingTeam = 0;
+            wd.isCaptured = false;
+            wd.stepsUntilPoint = kZonePointInterval;
+        }
+    } else if (na == 0 && nb > 0) {
+        if (wd.curControllingTeam != 1) {
+            wd.curControllingTeam = 1;
+            wd.isCaptured = false;
+            wd.stepsUntilPoint = kZonePointInterval;
+        }
+    }
+}
+
+// sim.cpp:4845-4889 leaveBreadcrumbsSystem
+void leaveBreadcrumbsSystem(Oracle &o, int w, int i)
+{
+    World &wd = o.worlds[w];
+    Agent &ag = o.agent(w, i);
+    ag.totalPenalty = 0.f;
+    const float penalty = 1.f;
+    const int frequency = 10;
+    bool updated = false;
+    if (ag.lastBreadcrumb != -1) {
+        for (Crumb &c : wd.crumbs) {
+            if ((int64_t)c.id != ag.lastBreadcrumb) continue;
+            if (distance(ag.pos, c.pos) < kAgentRadius * 4) {
+                c.penalty = penalty;
+                updated = true;
+                ag.stepsSinceLastNewBreadcrumb = 0;
+            }
+            break;
+        }
+    }
+    if (!updated) {
+        ag.stepsSinceLastNewBreadcrumb += 1;
+        if (ag.stepsSinceLastNewBreadcrumb > frequency) {
+            if ((int)wd.crumbs.size() < MPENV_MAX_CRUMBS) {
+                Crumb c;
+                c.pos = ag.pos;
+                c.penalty = penalty;
+                c.team = ag.team;
+                c.offset = ag.offset;
+                c.id = wd.nextCrumbId++;
+                wd.crumbs.push_back(c);
+                ag.lastBreadcrumb = c.id;
+            } else {
+                wd.crumbOverflow += 1;
+                ag.lastBreadcrumb = -1;
+            }
+            ag.stepsSinceLastNewBreadcrumb = 0;
+        }
+    }
+}
+
+// sim.cpp:4892-4926 accumulateBreadcrumbPenaltiesSystem (crumbs visited in
+// creation order; sim.cpp:5572/5581 CompactArchetypeNode keeps that order)
+void accumulateBreadcrumbPenalties(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    std::vector<Crumb> kept;
+    kept.reserve(wd.crumbs.size());
+    for (Crumb &c : wd.crumbs) {
+        for (int team = 0; team < 2; team++) {
+            for (int off = 0; off < o.teamSize; off++) {
+                if (c.team != team) continue;
+                if (c.offset == off) continue;
+                Agent &ag = o.agent(w, team * o.teamSize + off);
+                if (distance(ag.pos, c.pos) <= kAgentRadius * 4.f) {
+                    ag.totalPenalty += c.penalty;
+                }
+            }
+        }
+        c.penalty -= 0.025f;
+        if (!(c.penalty <= 0.f)) kept.push_back(c);
+    }
+    wd.crumbs.swap(kept);
+}
+
+// sim.cpp:128-291 updateFiltersState
+void updateFiltersState(Oracle &o, int w, int cur_step)
+{
+    World &wd = o.worlds[w];
+    struct Filt { int type; int16_t minx, miny, maxx, maxy; int minNum; };
+    // type 0 = PlayerInRegion, 1 = PlayerShotEvent (full-range regions)
+    const Filt filters[3] = {
+        { 0, -1272, -866, -825, 696, 5 },
+        { 0, 852, -851, 1280, 593, 1 },
+        { 1, -32768, -32768, 32767, 32767, 0 },
+    };
+    const int window = 0;
+    for (int fi = 0; fi < 3; fi++) {
+        const Filt &f = filters[fi];
+        for (int t = 0; t < 2; t++) {
+            if ((wd.filtersActive[t] & (1ull << fi)) != 0) {
+                if (cur_step - wd.filtersLastMatches[t][fi] > window) {
+                    wd.filtersActive[t] &= ~(1ull << fi);
+                }
+            }
+        }
+        if (f.type == 1) {
+            for (int p = 0; p < o.N; p++) {
+                const Agent &ag = o.agent(w, p);
+                int team = p / o.teamSize;
+                if (ag.landedShotOn == -1) continue;
+                Vec3 ap = ag.pos;
+                Vec3 tp = o.agent(w, ag.landedShotOn).pos;
+                if (ap.x < f.minx || ap.y < f.miny || ap.x > f.maxx || ap.y > f.maxy ||
+                    tp.x < f.minx || tp.y < f.miny || tp.x > f.maxx || tp.y > f.maxy) continue;
+                wd.filtersActive[team] |= (1ull << fi);
+                wd.filtersLastMatches[team][fi] = cur_step;
+            }
+        } else {
+            int cnt[2] = { 0, 0 };
+            for (int p = 0; p < o.N; p++) {
+                const Agent &ag = o.agent(w, p);
+                int team = p / o.teamSize;
+                Vec3 pos = ag.pos;
+                if (pos.x < f.minx || pos.y < f.miny || pos.x > f.maxx || pos.y > f.maxy) continue;
+                cnt[team] += 1;
+            }
+            for (int t = 0; t < 2; t++) {
+                if (cnt[t] >= f.minNum) {
+                    wd.filtersActive[t] |= (1ull << fi);
+                    wd.filtersLastMatches[t][fi] = cur_step;
+                }
+            }
+        }
+    }
+    for (int t = 0; t < 2; t++) {
+        if (__builtin_popcountll(wd.filtersActive[t]) == 3) wd.filtersLastMatchedStep[t] = cur_step;
+    }
+}
+
+// sim.cpp:4470-4673 zoneMatchInfoSystem
+void zoneMatchInfoSystem(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    int32_t *mr = &o.matchResult[(size_t)w * 30];
+    int cur_step = wd.curStep + 1;
+    bool finished = false;
+    if (cur_step >= kEpisodeLen || o.resetBuf[w] == 1) finished = true;
+    if (cur_step == 1) {
+        mr[0] = -1; mr[1] = 0; mr[2] = 0; mr[3] = 0; mr[4] = 0;
+    }
+    for (int i = 0; i < o.N; i++) {
+        const Agent &ag = o.agent(w, i);
+        if (ag.wasKilled) mr[1 + (ag.team ^ 1)] += 1;
+    }
+    wd.earnedPoint = false;
+    bool new_captured = false;
+    if (wd.stepsUntilPoint == 0) {
+        wd.stepsUntilPoint = kZonePointInterval;
+        if (!wd.isCaptured) {
+            wd.isCaptured = true;
+            new_captured = true;
+        }
+        if (wd.curControllingTeam >= 0) mr[3 + wd.curControllingTeam] += 1;
+        wd.earnedPoint = true;
+    }
+    if (mr[3] >= kZoneWinPoints || mr[4] >= kZoneWinPoints) finished = true;
+    {
+        int *zs = wd.zoneStats[wd.curZone];
+        zs[4] += 1; // numTotalActiveSteps
+        if (wd.isCaptured && wd.curControllingTeam >= 0) zs[1 + wd.curControllingTeam] += 1;
+        if (wd.isContested) zs[3] += 1;
+        if (new_captured) zs[0] += 1;
+        updateFiltersState(o, w, cur_step);
+    }
+    if (finished) {
+        if (mr[3] > mr[4]) mr[0] = 0;
+        else if (mr[4] > mr[3]) mr[0] = 1;
+        else mr[0] = 2;
+        for (int z = 0; z < kMaxZones; z++)
+            for (int k = 0; k < 5; k++) mr[5 + 5 * z + k] = wd.zoneStats[z][k];
+        for (int z = 0; z < kMaxZones; z++)
+            for (int k = 0; k < 5; k++) wd.zoneStats[z][k] = 0;
+    }
+    wd.curStep = cur_step;
+    wd.isFinished = finished;
+}
+
+// sim.cpp:3998-4021 distToZOBB
+float distToZOBB(ZOBB z, Vec3 pos)
+{
+    Quat to_frame = qinv(angleAxis(z.rotation, kUp));
+    Vec3 pmin = rotateVec(to_frame, z.pMin);
+    Vec3 pmax = rotateVec(to_frame, z.pMax);
+    Vec3 p = rotateVec(to_frame, pos);
+    float sq = 0.f;
+    for (int i = 0; i < 3; i++) {
+        float v = comp(p, i);
+        if (v < comp(pmin, i)) { float d = comp(pmin, i) - v; sq += d * d; }
+        if (v > comp(pmax, i)) { float d = v - comp(pmax, i); sq += d * d; }
+    }
+    return sqrt_(sq);
+}
+
+// sim.cpp:4023-4087 evaluateGoalRegionsSystem
+void evaluateGoalRegionsSystem(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    wd.teamStepRewards[0] = 0.f;
+    wd.teamStepRewards[1] = 0.f;
+    int attacker = wd.teamA;
+    for (int r = 0; r < (int)o.goalRegions.size(); r++) {
+        const GoalRegion &gr = o.goalRegions[r];
+        int region_team = gr.attackerTeam ? attacker : (attacker ^ 1);
+        float max_min = -kFltMax;
+        for (int s = 0; s < gr.numSubRegions; s++) {
+            float min_d = kFltMax;
+            for (int i = 0; i < o.N; i++) {
+                const Agent &ag = o.agent(w, i);
+                if (ag.team != region_team) continue;
+                float d = distToZOBB(gr.subRegions[s], ag.pos);
+                if (d < min_d) min_d = d;
+            }
+            if (min_d > max_min) max_min = min_d;
+        }
+        float prev = wd.minDistToRegions[r];
+        if (prev == kFltMax) {
+            wd.minDistToRegions[r] = max_min;
+        } else {
+            float diff = prev - max_min;
+            if (diff > 0.f) {
+                wd.minDistToRegions[r] = max_min;
+                wd.teamStepRewards[region_team] += diff * gr.rewardStrength;
+            }
+        }
+    }
+}
+
+// sim.cpp:3508-3536 exploreVisitedSystem
+void exploreVisitedSystem(Oracle &o, int w, int i)
+{
+    World &wd = o.worlds[w];
+    Agent &ag = o.agent(w, i);
+    Vec3 delta = ag.pos - ag.startPos;
+    int32_t x = f2iSat((delta.x + 0.5f) / (kAgentRadius * 2.f));
+    int32_t y = f2iSat((delta.y + 0.5f) / (kAgentRadius * 2.f));
+    int64_t cx = (int64_t)x + kGridMax, cy = (int64_t)y + kGridMax;
+    if (cx < 0 || cx >= kGridW || cy < 0 || cy >= kGridW) return;
+    uint32_t &cell = ag.visited[(size_t)cy * kGridW + (size_t)cx];
+    uint32_t cur = wd.curEpisodeIdx;
+    if (cell != cur) {
+        cell = cur;
+        if (length2(delta) > 2.f) ag.numNewCellsVisited += 1;
+    }
+}
+
+// sim.cpp:3707-3732 learnShootingRewardSystem
+void learnShootingReward(Agent &ag, float &r)
+{
+    if (ag.landedShotOn != -1) r += 0.5f;
+    else if (ag.firedShotT >= 0.f) r -= 0.05f;
+    if (ag.reloadedFullMag) r -= 0.5f;
+}
+
+// sim.cpp:3849-3996 zoneRewardSystem
+void zoneRewardSystem(Oracle &o, int w, int i)
+{
+    World &wd = o.worlds[w];
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    float r = 0.f;
+    if (o.worldCurriculum[w] == 0) { // LearnShooting
+        learnShootingReward(ag, r);
+        o.reward[g] = r;
+        return;
+    }
+    const float *rc = &o.rewardCoefs[9 * g];
+    const float shot = rc[1], explore = rc[2], in_zone = rc[3], ctrl = rc[5], zdist = rc[6],
+                earned = rc[7], crumb = rc[8];
+    r -= crumb * ag.totalPenalty;
+    if (ag.reloadedFullMag) r -= 0.5f;
+    if (ag.successfulKill) r += 1.f;
+    if (ag.landedShotOn != -1) r += shot * 1.f;
+    if (ag.wasKilled) r -= 1.5f;
+    if (ag.wasShotCount > 0) r -= shot * 1.f;
+    uint32_t nn = ag.numNewCellsVisited;
+    ag.numNewCellsVisited = 0;
+    if (nn > 0) r += float(nn) * explore;
+    if (ag.inZone) {
+        r += in_zone;
+    } else {
+        AABB za = o.zoneAABBs[wd.curZone];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        float dist = distance(center, ag.pos);
+        if (dist < ag.minDistToZone) {
+            float scale = zdist;
+            if (!ag.hasDiedDuringEpisode) scale *= 10.f;
+            r += scale * (ag.minDistToZone - dist);
+            ag.minDistToZone = dist;
+        }
+    }
+    if (wd.curControllingTeam != -1) {
+        if (wd.curControllingTeam == ag.team) {
+            r += ctrl;
+            if (wd.earnedPoint) r += earned;
+        } else {
+            r -= ctrl;
+            if (wd.earnedPoint) r -= earned;
+        }
+    }
+    if (o.alive[g] == 0.f) {
+        ag.successfulKill = false;
+        ag.landedShotOn = -1;
+        ag.wasKilled = false;
+        ag.wasShotCount = 0;
+        ag.firedShotT = -kFltMax;
+        o.reward[g] = r;
+        return;
+    }
+    {
+        float poly = 0.f;
+        const int num_teammates = o.teamSize - 1;
+        for (int k = 0; k < num_teammates - 1; k++) {
+            int t1 = ag.team * o.teamSize + (k < ag.offset ? k : k + 1);
+            int t2 = ag.team * o.teamSize + (k + 1 < ag.offset ? k + 1 : k + 2);
+            Vec3 p1 = o.agent(w, t1).pos, p2 = o.agent(w, t2).pos;
+            float e1x = p1.x - ag.pos.x, e1y = p1.y - ag.pos.y;
+            float e2x = p2.x - ag.pos.x, e2y = p2.y - ag.pos.y;
+            float tri = e1x * e2y - e1y * e2x;
+            poly += fabs_(tri);
+        }
+        float dx = o.worldBounds.pMax.x - o.worldBounds.pMin.x;
+        float dy = o.worldBounds.pMax.y - o.worldBounds.pMin.y;
+        float area = dx * dy;
+        float frac = poly / (2.f * area);
+        r += frac * 1e-2f;
+    }
+    o.reward[g] = r;
+}
+
+// sim.cpp:4292-4313 pvpTeamRewardSystem + 4315-4339 pvpFinalRewardSystem
+void teamAndFinalReward(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    float tr[2] = { 0, 0 };
+    int ts[2] = { 0, 0 };
+    for (int i = 0; i < o.N; i++) {
+        int t = o.agent(w, i).team;
+        tr[t] += o.reward[o.gi(w, i)];
+        ts[t] += 1;
+    }
+    tr[0] /= float(ts[0]);
+    tr[1] /= float(ts[1]);
+    wd.teamRewards[0] = tr[0];
+    wd.teamRewards[1] = tr[1];
+    for (int i = 0; i < o.N; i++) {
+        size_t g = o.gi(w, i);
+        float my = o.reward[g];
+        float team_r = wd.teamRewards[o.agent(w, i).team];
+        float spirit = o.rewardCoefs[9 * g + 0];
+        o.reward[g] = my * (1.f - spirit) + team_r * spirit;
+    }
+}
+
+// sim.cpp:2526-2560 opponentsWriteVisibilitySystem
+void opponentsWriteVisibility(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    Vec3 ray_o = ag.pos;
+    ray_o.z += viewHeight(ag.curPose);
+    int opp_team = ag.team ^ 1;
+    for (int k = 0; k < kMaxTeamSize; k++) {
+        ag.canSee[k] = false;
+        if (o.alive[g] == 0.f) continue;
+        if (k >= o.teamSize) continue;
+        int opp = opp_team * o.teamSize + k;
+        if (o.alive[o.gi(w, opp)] == 0.f) continue;
+        if (isAgentVisible(o, w, ray_o, ag.aimRot, opp)) ag.canSee[k] = true;
+    }
+}
+
+// sim.cpp:2562-2614 pvpOpponentMasksSystem
+void opponentMasks(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    int opp_team = ag.team ^ 1;
+    for (int k = 0; k < kMaxTeamSize; k++) {
+        float &m = o.masks[g * kMaxTeamSize + k];
+        m = 0.f;
+        if (o.alive[g] == 0.f) continue;
+        if (k >= o.teamSize) continue;
+        int opp = opp_team * o.teamSize + k;
+        if (o.alive[o.gi(w, opp)] == 0.f) continue;
+        bool can_see = ag.canSee[k];
+        for (int t = 0; t < kMaxTeamSize - 1; t++) {
+            if (t >= o.teamSize - 1) continue;
+            int tm = ag.team * o.teamSize + (t < ag.offset ? t : t + 1);
+            if (o.agent(w, tm).canSee[k]) {
+                can_see = true;
+                break;
+            }
+        }
+        if (can_see) m = 1.f;
+        if (o.agent(w, opp).firedShotT >= 0) m = 1.f;
+    }
+}
+
+Vec3 normalizedPos(const Oracle &o, Vec3 p) // sim.cpp:2693-2718
+{
+    float min_x = o.worldBounds.pMin.x, min_y = o.worldBounds.pMin.y, min_z = o.worldBounds.pMin.z;
+    float max_x = o.worldBounds.pMax.x, max_y = o.worldBounds.pMax.y, max_z = o.worldBounds.pMax.z;
+    float xr = max_x - min_x, yr = max_y - min_y, zr = max_z - min_z;
+    float x = (p.x - min_x) / xr, y = (p.y - min_y) / yr, z = (p.z - min_z) / zr;
+    return v3(clampf(x, 0.f, 1.f), clampf(y, 0.f, 1.f), clampf(z, 0.f, 1.f));
+}
+
+// sim.cpp:2645-3052 pvpObservationsSystem
+void pvpObservations(Oracle &o, int w, int i)
+{
+    World &wd = o.worlds[w];
+    Agent &self = o.agent(w, i);
+    size_t g = o.gi(w, i);
+
+    o.filtersObs[g] = (wd.curStep - wd.filtersLastMatchedStep[self.team] < 5) ? 1.f : 0.f;
+
+    float *self_ob = &o.selfObs[g * kSelfObs];
+    float *self_pos = &o.selfPos[g * 3];
+    std::fill(self_ob, self_ob + kSelfObs, 0.f);
+    self_pos[0] = self_pos[1] = self_pos[2] = -1000.f;
+    for (int k = 0; k < kMaxTeamSize - 1; k++) {
+        float *p = &o.teammatePos[(g * 5 + k) * 3];
+        p[0] = p[1] = p[2] = -1000.f;
+        float *ob = &o.teammateObs[(g * 5 + k) * kOtherObs];
+        std::fill(ob, ob + kOtherObs, 0.f);
+    }
+    for (int k = 0; k < kMaxTeamSize; k++) {
+        float *p = &o.opponentPos[(g * 6 + k) * 3];
+        p[0] = p[1] = p[2] = -1000.f;
+        float *ob = &o.opponentObs[(g * 6 + k) * kOtherObs];
+        std::fill(ob, ob + kOtherObs, 0.f);
+    }
+
+    const Vec3 self_pos_v = self.pos;
+    const Quat self_rot = self.rot;
+    const float self_yaw = self.aimYaw, self_pitch = self.aimPitch;
+
+    auto fillCommon = [&](float *ob, float *pos_ob, int j) {
+        ob[0] = 1.f; // isValid
+        size_t gj = o.gi(w, j);
+        if (!o.alive[gj]) return false;
+        const Agent &a = o.agent(w, j);
+        ob[1] = 1.f;
+        Vec3 np = normalizedPos(o, a.pos);
+        ob[2] = np.x; ob[3] = np.y; ob[4] = np.z;
+        pos_ob[0] = np.x; pos_ob[1] = np.y; pos_ob[2] = np.z;
+        ob[5] = 0.5f * ((a.aimYaw / kPi) + 1.f);
+        ob[6] = 0.5f * (a.aimPitch / (0.25f * kPi) + 1.f);
+        Vec3 rv = rotateVec(qinv(self_rot), a.vel);
+        ob[7] = rv.x; ob[8] = rv.y; ob[9] = rv.z;
+        ob[10] = a.daimYawVel; ob[11] = a.daimPitchVel;
+        ob[12] = a.curPose == kStand ? 1.f : 0.f;
+        ob[13] = a.curPose == kCrouch ? 1.f : 0.f;
+        ob[14] = a.curPose == kProne ? 1.f : 0.f;
+        ob[15] = a.tgtPose == kStand ? 1.f : 0.f;
+        ob[16] = a.tgtPose == kCrouch ? 1.f : 0.f;
+        ob[17] = a.tgtPose == kProne ? 1.f : 0.f;
+        ob[18] = (float)a.transitionRemaining / (float)kPoseTransitionSpeed;
+        ob[19] = a.inZone ? 1.f : 0.f;
+        ob[20 + a.weaponType] = 1.f;
+        return true;
+    };
+    auto fillCombat = [&](float *ob, int j) {
+        size_t gj = o.gi(w, j);
+        const Agent &a = o.agent(w, j);
+        ob[0] = (float)o.hp[gj] / 100.f;
+        ob[1] = (float)o.magazine[2 * gj];
+        ob[2] = (float)o.magazine[2 * gj + 1];
+        ob[3] = float(a.remainingStepsBeforeAutoheal) / float(kOutOfCombatSteps);
+    };
+    auto relAngles = [&](Vec3 to, float *dist_out, float *yaw_out, float *pitch_out, float eps) {
+        float d = length(to);
+        if (d < eps) {
+            *dist_out = 0.f; *yaw_out = 0.f; *pitch_out = 0.f;
+            return;
+        }
+        to = to / d;
+        float new_yaw = -atan2f_(to.x, to.y);
+        float new_pitch = asinf_(clampf(to.z, -1.f, 1.f));
+        float yaw_delta = new_yaw - self_yaw;
+        float pitch_delta = new_pitch - self_pitch;
+        if (yaw_delta > kPi) yaw_delta -= 2.f * kPi;
+        else if (yaw_delta < -kPi) yaw_delta += 2.f * kPi;
+        *dist_out = d; *yaw_out = yaw_delta; *pitch_out = pitch_delta;
+    };
+    auto fillOther = [&](float *ob, int j) {
+        const Agent &a = o.agent(w, j);
+        relAngles(a.pos - self_pos_v, &ob[23], &ob[24], &ob[25], 1e-2f);
+        float rfy = a.aimYaw - self_yaw;
+        float rfp = a.aimPitch - self_pitch;
+        if (rfy > kPi) rfy -= 2.f * kPi;
+        else if (rfy < -kPi) rfy += 2.f * kPi;
+        ob[26] = rfy;
+        ob[27] = rfp;
+    };
+
+    if (!fillCommon(self_ob, self_pos, i)) return;
+    fillCombat(&self_ob[23], i);
+    {
+        float *zo = &self_ob[27];
+        AABB za = o.zoneAABBs[wd.curZone];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        Vec3 nc = normalizedPos(o, center);
+        zo[0] = nc.x; zo[1] = nc.y; zo[2] = nc.z;
+        relAngles(center - self_pos_v, &zo[3], &zo[4], &zo[5], 1e-2f);
+        zo[6] = (wd.curControllingTeam == self.team) ? 1.f : 0.f;
+        zo[7] = (wd.curControllingTeam != -1 && wd.curControllingTeam != self.team) ? 1.f : 0.f;
+        zo[8] = wd.isContested ? 1.f : 0.f;
+        zo[9] = wd.isCaptured ? 1.f : 0.f;
+        zo[10] = float(wd.stepsUntilPoint) / float(kZonePointInterval);
+        zo[11] = float(wd.zoneStepsRemaining) / float(kNumStepsPerZone);
+        if (wd.curZone >= 0 && wd.curZone < 4) zo[12 + wd.curZone] = 1.f;
+    }
+
+    for (int k = 0; k < o.teamSize - 1; k++) {
+        int j = self.team * o.teamSize + (k < self.offset ? k : k + 1);
+        float *ob = &o.teammateObs[(g * 5 + k) * kOtherObs];
+        float *pos_ob = &o.teammatePos[(g * 5 + k) * 3];
+        if (!fillCommon(ob, pos_ob, j)) continue;
+        fillOther(ob, j);
+        fillCombat(&ob[28], j);
+    }
+
+    for (int k = 0; k < o.teamSize; k++) {
+        int j = (self.team ^ 1) * o.teamSize + k;
+        float *ob = &o.opponentObs[(g * 6 + k) * kOtherObs];
+        float *lk = &o.lastKnownObs[(g * 6 + k) * kOtherObs];
+        float *pos_ob = &o.opponentPos[(g * 6 + k) * 3];
+        float *lk_pos = &o.lastKnownPos[(g * 6 + k) * 3];
+        if (!fillCommon(ob, pos_ob, j)) {
+            std::fill(lk, lk + kOtherObs, 0.f);
+            lk_pos[0] = lk_pos[1] = lk_pos[2] = -1000.f;
+            continue;
+        }
+        fillOther(ob, j);
+        const Agent &a = o.agent(w, j);
+        if (a.wasKilled) {
+            std::fill(lk, lk + kOtherObs, 0.f);
+            lk_pos[0] = lk_pos[1] = lk_pos[2] = -1000.f;
+        }
+        ob[28] = (float)a.wasShotCount;
+        ob[29] = a.firedShotT >= 0.f ? 1.f : 0.f;
+        ob[30] = self.canSee[k] ? 1.f : 0.f;
+        bool knows = o.masks[g * 6 + k] == 1.f;
+        ob[31] = knows ? 1.f : 0.f;
+        if (knows) {
+            std::copy(ob, ob + kOtherObs, lk);
+            lk_pos[0] = pos_ob[0]; lk_pos[1] = pos_ob[1]; lk_pos[2] = pos_ob[2];
+        }
+    }
+}
+
+// sim.cpp:3324-3506 pvpLidarSystem
+void pvpLidar(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    Vec3 fwd_fwd = rotateVec(ag.aimRot, kFwd);
+    Vec3 fwd_right = rotateVec(ag.aimRot, kRight);
+    Vec3 rear_fwd = rotateVec(ag.rot, kFwd);
+    Vec3 rear_right = rotateVec(ag.rot, kRight);
+    auto trace = [&](int idx, int num, Vec3 ray_o, Vec3 fwd, Vec3 right, float range, float offset,
+                     float *out) {
+        float theta = range * (float(idx) / float(num - 1)) + offset;
+        float x = -cosf_(theta);
+        float y = sinf_(theta);
+        Vec3 dir = normalize(x * right + y * fwd);
+        HitResult h = traceRayAgainstWorld(o, w, ray_o, dir);
+        if (h.hit) {
+            bool wall = h.entity == -1;
+            bool tm = !wall && o.agent(w, h.entity).team == ag.team;
+            out[0] = fminD(h.t, o.maxDist);
+            out[1] = wall ? 1.f : 0.f;
+            out[2] = tm ? 1.f : 0.f;
+            out[3] = (!wall && !tm) ? 1.f : 0.f;
+        } else {
+            out[0] = -1.f; out[1] = 0.f; out[2] = 0.f; out[3] = 0.f;
+        }
+    };
+    float top = viewHeight(ag.curPose) + kAgentRadius;
+    for (int h = 0; h < kFwdH; h++) {
+        Vec3 ray_o = ag.pos;
+        ray_o.z += kAgentRadius + (top - 2.f * kAgentRadius) * (float(h) / float(kFwdH - 1));
+        for (int x = 0; x < kFwdW; x++) {
+            trace(x, kFwdW, ray_o, fwd_fwd, fwd_right, 0.75f * kPi, 0.5f * (1.f - 0.75f) * kPi,
+                  &o.fwdLidar[((g * kFwdH + h) * kFwdW + x) * kLidarData]);
+        }
+    }
+    for (int h = 0; h < kRearH; h++) {
+        Vec3 ray_o = ag.pos;
+        ray_o.z += kAgentRadius + (top - 2.f * kAgentRadius) * (float(h) / float(kRearH - 1));
+        for (int x = 0; x < kRearW; x++) {
+            trace(x, kRearW, ray_o, rear_fwd, rear_right, -kPi, 0.f,
+                  &o.rearLidar[((g * kRearH + h) * kRearW + x) * kLidarData]);
+        }
+    }
+}
+
+// sim.cpp:5174-5320 resetAndObsTasks (per world)
+void resetAndObs(Oracle &o, int w)
+{
+    resetSystem(o, w);
+    for (int i = 0; i < o.N; i++) opponentsWriteVisibility(o, w, i);
+    for (int i = 0; i < o.N; i++) opponentMasks(o, w, i);
+    for (int i = 0; i < o.N; i++) pvpObservations(o, w, i);
+    for (int i = 0; i < o.N; i++) pvpLidar(o, w, i);
+}
+
+// sim.cpp:5342-5842 setupStepTasks, Task::Zone, default flags
+void stepWorld(Oracle &o, int w)
+{
+    const int N = o.N;
+    // planAStarAISystem (sim.cpp:5041-5172) runs only for AgentPolicy == -1;
+    // bots are not implemented in round 1.
+    for (int i = 0; i < N; i++) applyBotActionsSystem(o, w, i);
+    for (int i = 0; i < N; i++) pvpMovementSystem(o, w, i);
+    for (int i = 0; i < N; i++) pvpContinuousAimSystem(o, w, i);
+    for (int i = 0; i < N; i++) pvpDiscreteAimSystem(o, w, i);
+    for (int i = 0; i < N; i++) applyVelocitySystem(o, w, i);
+    for (int i = 0; i < N; i++) {
+        Agent &ag = o.agent(w, i);
+        ag.pos = ag.newPos;
+        ag.vel = ag.newVel;
+    }
+    for (int i = 0; i < N; i++) fallSystem(o, w, i);
+    for (int i = 0; i < N; i++) o.agent(w, i).pos = o.agent(w, i).newPos;
+    for (int i = 0; i < N; i++) fireSystem(o, w, i);
+    for (int i = 0; i < N; i++) applyDmgSystem(o, w, i);
+    if (!(o.simFlags & MPENV_SIMFLAG_NO_RESPAWN)) spawnAgents(o, w, true);
+    for (int i = 0; i < N; i++) autoHealSystem(o, w, i);
+    zoneSystem(o, w);
+    for (int i = 0; i < N; i++) leaveBreadcrumbsSystem(o, w, i);
+    accumulateBreadcrumbPenalties(o, w);
+    zoneMatchInfoSystem(o, w);
+    evaluateGoalRegionsSystem(o, w);
+    for (int i = 0; i < N; i++) exploreVisitedSystem(o, w, i);
+    for (int i = 0; i < N; i++) zoneRewardSystem(o, w, i);
+    teamAndFinalReward(o, w);
+    for (int i = 0; i < N; i++) o.done[o.gi(w, i)] = o.worlds[w].isFinished ? 1 : 0;
+    resetAndObs(o, w);
+}
+
+// sim.cpp:5850-5980 Sim::Sim
+void constructWorld(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    wd.curEpisodeIdx = 0;
+    wd.worldEpisodeCounter = 0;
+    wd.curCurriculumTier = 0;
+    wd.curCurriculumSpawnIdx = 0;
+    wd.nextCrumbId = 0;
+    wd.crumbOverflow = 0;
+    wd.crumbs.clear();
+    o.resetBuf[w] = 0;
+    for (int t = 0; t < 2; t++)
+        for (int k = 0; k < 64; k++) wd.filtersLastMatches[t][k] = 0;
+    createPersistentEntities(o, w);
+    o.worldCurriculum[w] = 1; // FullMatch (sim.cpp:5959)
+    initWorld(o, w, true);
+    for (int z = 0; z < kMaxZones; z++)
+        for (int k = 0; k < 5; k++) wd.zoneStats[z][k] = 0;
+    wd.matchID = ~0ull;
+    for (int t = 0; t < 2; t++) {
+        wd.filtersActive[t] = 0;
+        wd.filtersLastMatchedStep[t] = -1;
+    }
+}
+
+template <typename T>
+void readVec(std::ifstream &f, std::vector<T> &v, size_t n)
+{
+    v.resize(n);
+    if (n) f.read(reinterpret_cast<char *>(v.data()), (std::streamsize)(n * sizeof(T)));
+    if (!f) throw std::runtime_error("oracle: truncated scene file");
+}
+
+// map_importer.cpp:508-567 (spawns, zones) and 223-256 (world bounds)
+void loadScene(Oracle &o)
+{
+    {
+        std::ifstream f(o.scenePath + "/collisions.bin", std::ios::binary);
+        if (!f) throw std::runtime_error("oracle: cannot open collisions.bin");
+        float wb[6];
+        f.read(reinterpret_cast<char *>(wb), sizeof(wb));
+        o.worldBounds.pMin = v3(wb[0], wb[1], wb[2]);
+        o.worldBounds.pMax = v3(wb[3], wb[4], wb[5]);
+    }
+    {
+        std::ifstream f(o.scenePath + "/spawns.bin", std::ios::binary);
+        if (!f) throw std::runtime_error("oracle: cannot open spawns.bin");
+        std::vector<Spawn> *dst[3] = { &o.aSpawns, &o.bSpawns, &o.commonRespawns };
+        for (int k = 0; k < 3; k++) {
+            uint32_t n = 0;
+            f.read(reinterpret_cast<char *>(&n), 4);
+            readVec(f, *dst[k], n);
+        }
+        o.numDefaultASpawns = (uint32_t)o.aSpawns.size();
+        o.numDefaultBSpawns = (uint32_t)o.bSpawns.size();
+    }
+    {
+        std::ifstream f(o.scenePath + "/zones.bin", std::ios::binary);
+        if (!f) throw std::runtime_error("oracle: cannot open zones.bin");
+        uint32_t n = 0;
+        f.read(reinterpret_cast<char *>(&n), 4);
+        readVec(f, o.zoneAABBs, n);
+        readVec(f, o.zoneRot, n);
+    }
+    // mgr.cpp:913-944 hardcodedGoalRegions
+    const float top = -56.f + kStandHeight * 1.5f;
+    GoalRegion g0 = {};
+    g0.subRegions[0] = { v3(625, 510, -64), v3(900, 540, top), 0.f };
+    g0.numSubRegions = 1; g0.attackerTeam = true; g0.rewardStrength = 1.f;
+    GoalRegion g1 = {};
+    g1.subRegions[0] = { v3(938, 440, -56), v3(1030, 539, top), 0.f };
+    g1.subRegions[1] = { v3(545, 102, -64), v3(630, 134, top), 0.f };
+    g1.numSubRegions = 2; g1.attackerTeam = true; g1.rewardStrength = 1.f;
+    o.goalRegions = { g0, g1 };
+}
+
+void refreshDebug(Oracle &o)
+{
+    const size_t A = (size_t)o.W * o.N;
+    for (size_t g = 0; g < A; g++) {
+        const Agent &a = o.agents[g];
+        float *f = &o.dbgAF[g * MPENV_DBG_AF_COUNT];
+        f[0] = a.pos.x; f[1] = a.pos.y; f[2] = a.pos.z;
+        f[3] = a.vel.x; f[4] = a.vel.y; f[5] = a.vel.z;
+        f[6] = a.rot.w; f[7] = a.rot.x; f[8] = a.rot.y; f[9] = a.rot.z;
+        f[10] = a.aimYaw; f[11] = a.aimPitch;
+        f[12] = a.aimRot.w; f[13] = a.aimRot.x; f[14] = a.aimRot.y; f[15] = a.aimRot.z;
+        f[16] = a.maxVelocity; f[17] = a.minDistToZone; f[18] = a.firedShotT; f[19] = a.totalPenalty;
+        f[20] = a.startPos.x; f[21] = a.startPos.y; f[22] = a.startPos.z;
+        int32_t *n = &o.dbgAI[g * MPENV_DBG_AI_COUNT];
+        n[0] = a.curPose; n[1] = a.tgtPose; n[2] = a.transitionRemaining;
+        n[3] = (int32_t)a.rng.key.a; n[4] = (int32_t)a.rng.key.b; n[5] = (int32_t)a.rng.ctr;
+        n[6] = a.landedShotOn; n[7] = a.remainingRespawnSteps; n[8] = a.remainingStepsBeforeAutoheal;
+        n[9] = (a.successfulKill ? 1 : 0) | (a.wasKilled ? 2 : 0) | (a.inZone ? 4 : 0) |
+               (a.hasDiedDuringEpisode ? 8 : 0) | (a.reloadedFullMag ? 16 : 0);
+        n[10] = a.wasShotCount; n[11] = a.weaponType; n[12] = (int32_t)a.lastBreadcrumb;
+        n[13] = a.stepsSinceLastNewBreadcrumb;
+        int cs = 0;
+        for (int k = 0; k < kMaxTeamSize; k++) cs |= a.canSee[k] ? (1 << k) : 0;
+        n[14] = cs; n[15] = (int32_t)a.numNewCellsVisited;
+        std::copy(a.visited.begin(), a.visited.end(), &o.dbgExplore[g * kGridW * kGridW]);
+    }
+    for (int w = 0; w < o.W; w++) {
+        const World &wd = o.worlds[w];
+        int32_t *n = &o.dbgWI[(size_t)w * MPENV_DBG_WI_COUNT];
+        n[0] = wd.teamA; n[1] = wd.curStep; n[2] = wd.isFinished; n[3] = wd.curZone;
+        n[4] = wd.curControllingTeam; n[5] = wd.isContested; n[6] = wd.isCaptured; n[7] = wd.earnedPoint;
+        n[8] = wd.zoneStepsRemaining; n[9] = wd.stepsUntilPoint; n[10] = (int32_t)wd.curEpisodeIdx;
+        n[11] = (int32_t)wd.worldEpisodeCounter; n[12] = (int32_t)wd.baseRNG.key.a;
+        n[13] = (int32_t)wd.baseRNG.key.b; n[14] = (int32_t)wd.baseRNG.ctr; n[15] = (int32_t)wd.crumbs.size();
+        n[16] = (int32_t)wd.filtersActive[0]; n[17] = (int32_t)wd.filtersActive[1];
+        n[18] = wd.filtersLastMatchedStep[0]; n[19] = wd.filtersLastMatchedStep[1];
+        n[20] = wd.crumbOverflow;
+        float *f = &o.dbgWF[(size_t)w * MPENV_DBG_WF_COUNT];
+        f[0] = wd.teamRewards[0]; f[1] = wd.teamRewards[1];
+        f[2] = wd.minDistToRegions[0]; f[3] = wd.minDistToRegions[1];
+        f[4] = wd.teamStepRewards[0]; f[5] = wd.teamStepRewards[1];
+        float *c = &o.dbgCrumbs[(size_t)w * MPENV_MAX_CRUMBS * 8];
+        std::fill(c, c + MPENV_MAX_CRUMBS * 8, 0.f);
+        for (size_t k = 0; k < wd.crumbs.size(); k++) {
+            const Crumb &cr = wd.crumbs[k];
+            float *e = &c[k * 8];
+            e[0] = cr.pos.x; e[1] = cr.pos.y; e[2] = cr.pos.z; e[3] = cr.penalty;
+            e[4] = (float)cr.team; e[5] = (float)cr.offset; e[6] = (float)cr.id; e[7] = 1.f;
+        }
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+void *oracle_create(const oracle_config *cfg)
+{
+    try {
+        Oracle *o = new Oracle();
+        o->cfg = *cfg;
+        o->scenePath = cfg->scene_path;
+        o->W = (int)cfg->num_worlds;
+        o->teamSize = (int)cfg->team_size;
+        o->N = 2 * o->teamSize;
+        o->worldOffset = cfg->world_id_offset;
+        o->autoReset = cfg->auto_reset != 0;
+        o->simFlags = cfg->sim_flags;
+        // mgr.cpp:1736-1738
+        RandKey init_key = initKey(cfg->rand_seed);
+        o->initRandKey = splitI(init_key, 0);
+        // mgr.cpp:1397-1413 TrainControl from flags
+        o->trainControl[0] = (cfg->sim_flags & MPENV_SIMFLAG_SIM_EVAL_MODE) ? 1 : 0;
+        o->trainControl[1] = (cfg->sim_flags & MPENV_SIMFLAG_STAGGER_STARTS) ? 1 : 0;
+        o->trainControl[2] = (cfg->sim_flags & MPENV_SIMFLAG_RANDOM_FLIP_TEAMS) ? 1 : 0;
+        loadScene(*o);
+        o->nodes.resize(cfg->num_nodes);
+        std::memcpy(o->nodes.data(), cfg->bvh_nodes, sizeof(Node) * cfg->num_nodes);
+        o->verts.resize(cfg->num_bvh_verts);
+        for (int i = 0; i < cfg->num_bvh_verts; i++)
+            o->verts[i] = v3(cfg->bvh_verts[3 * i], cfg->bvh_verts[3 * i + 1], cfg->bvh_verts[3 * i + 2]);
+        // sim.cpp:5855 maxDist; 5869-5882 frustumData
+        o->maxDist = length(o->worldBounds.pMax - o->worldBounds.pMin);
+        {
+            float aspect = 16.f / 9.f;
+            float ang = 90.f / 2.f * (kPi / 180.f);
+            float f = 1.f / (sinf_(ang) / cosf_(ang));
+            float wx = f / aspect, wy = 1.f;
+            float hx = f, hy = 1.f;
+            float wi = 1.f / sqrt_(wx * wx + wy * wy);
+            float hi = 1.f / sqrt_(hx * hx + hy * hy);
+            o->frustum[0] = wx * wi; o->frustum[1] = wy * wi;
+            o->frustum[2] = hx * hi; o->frustum[3] = hy * hi;
+        }
+        const size_t A = (size_t)o->W * o->N, W = (size_t)o->W;
+        o->agents.resize(A);
+        for (Agent &a : o->agents) {
+            std::memset(&a.pos, 0, offsetof(Agent, visited) - offsetof(Agent, pos));
+            a.rot = quat(1, 0, 0, 0);
+            a.aimRot = quat(1, 0, 0, 0);
+            a.landedShotOn = -1;
+            a.lastBreadcrumb = -1;
+            a.numNewCellsVisited = 0;
+            a.daimYawVel = a.daimPitchVel = 0.f;
+            for (bool &b : a.canSee) b = false;
+        }
+        o->worlds.resize(W);
+        o->resetBuf.assign(W, 0);
+        o->worldCurriculum.assign(W, 0);
+        o->matchResult.assign(W * 30, 0);
+        o->exploreAction.assign(A * 4, 0);
+        o->discreteAction.assign(A * 4, 0);
+        o->discreteAim.assign(A * 2, 0);
+        o->policy.assign(A, 0);
+        o->done.assign(A, 0);
+        o->magazine.assign(A * 2, 0);
+        o->botAction.assign(A * 7, 0);
+        o->aimAction.assign(A * 2, 0.f);
+        o->reward.assign(A, 0.f);
+        o->selfObs.assign(A * kSelfObs, 0.f);
+        o->filtersObs.assign(A, 0.f);
+        o->teammateObs.assign(A * 5 * kOtherObs, 0.f);
+        o->opponentObs.assign(A * 6 * kOtherObs, 0.f);
+        o->lastKnownObs.assign(A * 6 * kOtherObs, 0.f);
+        o->selfPos.assign(A * 3, -1000.f);
+        o->teammatePos.assign(A * 5 * 3, -1000.f);
+        o->opponentPos.assign(A * 6 * 3, -1000.f);
+        o->lastKnownPos.assign(A * 6 * 3, -1000.f);
+        o->masks.assign(A * 6, 0.f);
+        o->fwdLidar.assign(A * kFwdH * kFwdW * 4, 0.f);
+        o->rearLidar.assign(A * kRearH * kRearW * 4, 0.f);
+        o->agentMap.assign(A * 16 * 16 * 4, 0.f);
+        o->hp.assign(A, 0.f);
+        o->alive.assign(A, 0.f);
+        o->rewardCoefs.assign(A * 9, 0.f);
+        o->dbgAF.assign(A * MPENV_DBG_AF_COUNT, 0.f);
+        o->dbgAI.assign(A * MPENV_DBG_AI_COUNT, 0);
+        o->dbgWI.assign(W * MPENV_DBG_WI_COUNT, 0);
+        o->dbgWF.assign(W * MPENV_DBG_WF_COUNT, 0.f);
+        o->dbgExplore.assign(A * kGridW * kGridW, 0u);
+        o->dbgCrumbs.assign(W * MPENV_MAX_CRUMBS * 8, 0.f);
+        for (int w = 0; w < o->W; w++) constructWorld(*o, w);
+        return o;
+    } catch (const std::exception &e) {
+        fprintf(stderr, "oracle_create failed: %s\n", e.what());
+        return nullptr;
+    }
+}
+
+void oracle_destroy(void *h) { delete static_cast<Oracle *>(h); }
+
+int oracle_export(void *h, int32_t id, void **ptr, int32_t *dtype, int32_t *ndim, int64_t *dims)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    const int64_t A = (int64_t)o.W * o.N, W = o.W;
+    auto set = [&](void *p, int32_t dt, std::initializer_list<int64_t> d) {
+        *ptr = p;
+        *dtype = dt;
+        *ndim = (int32_t)d.size();
+        int k = 0;
+        for (int64_t x : d) dims[k++] = x;
+        return 0;
+    };
+    switch (id) {
+    case MPENV_EXPORT_RESET: return set(o.resetBuf.data(), MPENV_DTYPE_INT32, { W, 1 });
+    case MPENV_EXPORT_WORLD_CURRICULUM: return set(o.worldCurriculum.data(), MPENV_DTYPE_INT32, { W, 1 });
+    case MPENV_EXPORT_EXPLORE_ACTION: return set(o.exploreAction.data(), MPENV_DTYPE_INT32, { A, 4 });
+    case MPENV_EXPORT_PVP_DISCRETE_ACTION: return set(o.discreteAction.data(), MPENV_DTYPE_INT32, { A, 4 });
+    case MPENV_EXPORT_PVP_AIM_ACTION: return set(o.aimAction.data(), MPENV_DTYPE_FLOAT32, { A, 1, 2 });
+    case MPENV_EXPORT_PVP_DISCRETE_AIM_ACTION: return set(o.discreteAim.data(), MPENV_DTYPE_INT32, { A, 2 });
+    case MPENV_EXPORT_REWARD: return set(o.reward.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_DONE: return set(o.done.data(), MPENV_DTYPE_INT32, { A, 1 });
+    case MPENV_EXPORT_MATCH_RESULT: return set(o.matchResult.data(), MPENV_DTYPE_INT32, { W, 30 });
+    case MPENV_EXPORT_AGENT_POLICY: return set(o.policy.data(), MPENV_DTYPE_INT32, { A, 1 });
+    case MPENV_EXPORT_SELF_OBSERVATION: return set(o.selfObs.data(), MPENV_DTYPE_FLOAT32, { A, kSelfObs });
+    case MPENV_EXPORT_TEAMMATE_OBSERVATIONS: return set(o.teammateObs.data(), MPENV_DTYPE_FLOAT32, { A, 5, kOtherObs });
+    case MPENV_EXPORT_OPPONENT_OBSERVATIONS: return set(o.opponentObs.data(), MPENV_DTYPE_FLOAT32, { A, 6, kOtherObs });
+    case MPENV_EXPORT_OPPONENT_LAST_KNOWN_OBSERVATIONS: return set(o.lastKnownObs.data(), MPENV_DTYPE_FLOAT32, { A, 6, kOtherObs });
+    case MPENV_EXPORT_SELF_POSITION: return set(o.selfPos.data(), MPENV_DTYPE_FLOAT32, { A, 3 });
+    case MPENV_EXPORT_TEAMMATE_POSITIONS: return set(o.teammatePos.data(), MPENV_DTYPE_FLOAT32, { A, 5, 3 });
+    case MPENV_EXPORT_OPPONENT_POSITIONS: return set(o.opponentPos.data(), MPENV_DTYPE_FLOAT32, { A, 6, 3 });
+    case MPENV_EXPORT_OPPONENT_LAST_KNOWN_POSITIONS: return set(o.lastKnownPos.data(), MPENV_DTYPE_FLOAT32, { A, 6, 3 });
+    case MPENV_EXPORT_OPPONENT_MASKS: return set(o.masks.data(), MPENV_DTYPE_FLOAT32, { A, 6, 1 });
+    case MPENV_EXPORT_FWD_LIDAR: return set(o.fwdLidar.data(), MPENV_DTYPE_FLOAT32, { A, kFwdH, kFwdW, 4 });
+    case MPENV_EXPORT_REAR_LIDAR: return set(o.rearLidar.data(), MPENV_DTYPE_FLOAT32, { A, kRearH, kRearW, 4 });
+    case MPENV_EXPORT_AGENT_MAP:
+    case MPENV_EXPORT_UNMASKED_AGENT_MAP: return set(o.agentMap.data(), MPENV_DTYPE_FLOAT32, { A, 16, 16, 4 });
+    case MPENV_EXPORT_HP: return set(o.hp.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_ALIVE: return set(o.alive.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_MAGAZINE: return set(o.magazine.data(), MPENV_DTYPE_INT32, { A, 2 });
+    case MPENV_EXPORT_FILTERS_STATE: return set(o.filtersObs.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
+    case MPENV_EXPORT_REWARD_HYPER_PARAMS: return set(o.rewardCoefs.data(), MPENV_DTYPE_FLOAT32, { A, 9 });
+    case MPENV_EXPORT_SIM_CONTROL: return set(o.trainControl, MPENV_DTYPE_INT32, { 3 });
+    case MPENV_EXPORT_DEBUG_AGENT_F32: return set(o.dbgAF.data(), MPENV_DTYPE_FLOAT32, { A, MPENV_DBG_AF_COUNT });
+    case MPENV_EXPORT_DEBUG_AGENT_I32: return set(o.dbgAI.data(), MPENV_DTYPE_INT32, { A, MPENV_DBG_AI_COUNT });
+    case MPENV_EXPORT_DEBUG_WORLD_I32: return set(o.dbgWI.data(), MPENV_DTYPE_INT32, { W, MPENV_DBG_WI_COUNT });
+    case MPENV_EXPORT_DEBUG_WORLD_F32: return set(o.dbgWF.data(), MPENV_DTYPE_FLOAT32, { W, MPENV_DBG_WF_COUNT });
+    case MPENV_EXPORT_DEBUG_EXPLORE: return set(o.dbgExplore.data(), MPENV_DTYPE_UINT32, { A, kGridW * kGridW });
+    case MPENV_EXPORT_DEBUG_CRUMBS: return set(o.dbgCrumbs.data(), MPENV_DTYPE_FLOAT32, { W, MPENV_MAX_CRUMBS, 8 });
+    default: return -1;
+    }
+}
+
+void oracle_init(void *h)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    for (int w = 0; w < o.W; w++) o.resetBuf[w] = 1; // triggerReset (mgr.cpp:1936-1938)
+    for (int w = 0; w < o.W; w++) resetAndObs(o, w); // Init graph (sim.cpp:5322-5340)
+}
+
+void oracle_step(void *h)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    for (int w = 0; w < o.W; w++) stepWorld(o, w);
+}
+
+void oracle_step_worlds(void *h, int32_t w0, int32_t w1)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    for (int w = w0; w < w1; w++) stepWorld(o, w);
+}
+
+void oracle_refresh_debug(void *h) { refreshDebug(*static_cast<Oracle *>(h)); }
+
+double oracle_run_threaded(void *h, int32_t nsteps, int32_t nthreads, const int32_t *ring, int32_t ring_len)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    const size_t A = (size_t)o.W * o.N;
+    if (nthreads < 1) nthreads = 1;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; t++) {
+        int w0 = (int)((int64_t)o.W * t / nthreads), w1 = (int)((int64_t)o.W * (t + 1) / nthreads);
+        pool.emplace_back([&o, w0, w1, nsteps, ring, ring_len, A]() {
+            for (int s = 0; s < nsteps; s++) {
+                const int32_t *src = ring + (size_t)(s % ring_len) * A * 6;
+                for (size_t g = (size_t)w0 * o.N; g < (size_t)w1 * o.N; g++) {
+                    for (int k = 0; k < 4; k++) o.discreteAction[4 * g + k] = src[6 * g + k];
+                    o.discreteAim[2 * g] = src[6 * g + 4];
+                    o.discreteAim[2 * g + 1] = src[6 * g + 5];
+                }
+                for (int w = w0; w < w1; w++) stepWorld(o, w);
+            }
+        });
+    }
+    for (auto &th : pool) th.join();
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+int oracle_trace_ray(void *h, const float *org, const float *d, float *t_out)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    return bvhTraceRay(o, v3(org[0], org[1], org[2]), v3(d[0], d[1], d[2]), t_out) ? 1 : 0;
+}
+
+float oracle_sphere_cast(void *h, const float *org, const float *d, float r, float *n_out)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    Vec3 n = v3(0.f, 0.f, 0.f);
+    float t = bvhSphereCast(o, v3(org[0], org[1], org[2]), v3(d[0], d[1], d[2]), r, &n);
+    n_out[0] = n.x; n_out[1] = n.y; n_out[2] = n.z;
+    return t;
+}
+
+int oracle_trace_ray_brute(void *h, const float *org, const float *d, float *t_out)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    Vec3 ro = v3(org[0], org[1], org[2]), rd = v3(d[0], d[1], d[2]);
+    Vec3 inv_d = v3(1.f / rd.x, 1.f / rd.y, 1.f / rd.z);
+    RayTxfm tx = computeRayIsectTxfm(rd, inv_d);
+    float t_max = kFltMax;
+    bool hit = false;
+    for (size_t t = 0; t + 2 < o.verts.size(); t += 3) {
+        float th;
+        if (rayTriangleIntersection(o.verts[t], o.verts[t + 1], o.verts[t + 2], tx, ro, t_max, &th)) {
+            hit = true;
+            t_max = th;
+        }
+    }
+    *t_out = t_max;
+    return hit ? 1 : 0;
+}
+
+float oracle_sphere_cast_brute(void *h, const float *org, const float *d, float r)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    Vec3 ro = v3(org[0], org[1], org[2]), rd = v3(d[0], d[1], d[2]);
+    float t_max = kFltMax;
+    for (size_t t = 0; t + 2 < o.verts.size(); t += 3) {
+        Vec3 n;
+        t_max = sphereCastTriangle(o.verts[t], o.verts[t + 1], o.verts[t + 2], ro, rd, t_max, r, &n);
+    }
+    return t_max;
+}
+
+void oracle_eval_math(int32_t fn, const float *in, const float *in2, float *out, int32_t n)
+{
+    for (int32_t k = 0; k < n; k++) {
+        float x = in[k];
+        switch (fn) {
+        case 0: out[k] = sinf_(x); break;
+        case 1: out[k] = cosf_(x); break;
+        case 2: out[k] = atan2f_(x, in2[k]); break;
+        case 3: out[k] = asinf_(x); break;
+        case 4: out[k] = logf_(x); break;
+        case 5: out[k] = sqrt_(x); break;
+        case 6: out[k] = x / in2[k]; break;
+        default: out[k] = 0.f; break;
+        }
+    }
+}
+
+void oracle_threefry(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t *out2)
+{
+    RandKey r = threefry2x32(initKey(k0, k1), c0, c1);
+    out2[0] = r.a;
+    out2[1] = r.b;
+}
+
+void oracle_tape_actions(uint32_t seed, uint32_t step, uint32_t first_agent, int32_t n, int32_t *out6)
+{
+    for (int32_t k = 0; k < n; k++) tapeActions(seed, step, first_agent + (uint32_t)k, &out6[6 * k], &out6[6 * k + 4]);
+}
+
+float oracle_capsule(const float *o, const float *d, float r, float h)
+{
+    return intersectRayZOriginCapsule(v3(o[0], o[1], o[2]), v3(d[0], d[1], d[2]), r, h);
+}
+
+} // extern "C"

@@ -1,0 +1,73 @@
+/*
+ * oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * C interface of the CPU restatement ("oracle") of the reference's
+ * world-batched Zone step.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library; the product
+ * (madrona-mp-env_amd/) never links or calls it.
+ */
+#ifndef MPENV_ORACLE_H
+#define MPENV_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_config {
+    uint32_t num_worlds;
+    uint32_t rand_seed;
+    int32_t auto_reset;
+    uint32_t sim_flags;
+    uint32_t team_size;
+    uint32_t world_id_offset;
+    const char *scene_path;
+    /* BVH built by the product's builder (same bytes the GPU traverses):
+     * 64-byte nodes (mesh_bvh.hpp:61-86) and 3 float3 vertices per triangle. */
+    const void *bvh_nodes;
+    int32_t num_nodes;
+    const float *bvh_verts;
+    int32_t num_bvh_verts;
+} oracle_config;
+
+void *oracle_create(const oracle_config *cfg);
+void oracle_destroy(void *h);
+int oracle_export(void *h, int32_t export_id, void **ptr, int32_t *dtype,
+                  int32_t *ndim, int64_t *dims);
+/* Manager::init: forced reset of every world then the Init graph. */
+void oracle_init(void *h);
+/* One Step graph over all worlds. */
+void oracle_step(void *h);
+/* One Step graph over worlds [w0, w1) (caller guarantees disjoint ranges). */
+void oracle_step_worlds(void *h, int32_t w0, int32_t w1);
+/* Refresh MPENV_EXPORT_DEBUG_* buffers from internal state. */
+void oracle_refresh_debug(void *h);
+/* CPU baseline timing: runs nsteps steps over all worlds with nthreads
+ * std::threads (static world partition, like ThreadPoolExecutor,
+ * mgr.cpp:1863-1871).  Before each step the discrete/aim actions of step s
+ * are copied from ring[(s % ring_len)] (layout [ring_len][A][6] i32:
+ * 4 discrete + 2 aim).  Returns wall seconds. */
+double oracle_run_threaded(void *h, int32_t nsteps, int32_t nthreads,
+                           const int32_t *ring, int32_t ring_len);
+
+/* Geometry hooks for known-answer tests (mesh_bvh.inl restatement). */
+int oracle_trace_ray(void *h, const float *o, const float *d, float *t_out);
+float oracle_sphere_cast(void *h, const float *o, const float *d, float r,
+                         float *normal_out);
+int oracle_trace_ray_brute(void *h, const float *o, const float *d, float *t_out);
+float oracle_sphere_cast_brute(void *h, const float *o, const float *d, float r);
+
+/* Known-answer hooks for the shared Madrona-layer definitions
+ * (mpenv_core.h): fn 0 sin, 1 cos, 2 atan2(in, in2), 3 asin, 4 log,
+ * 5 sqrt, 6 x / in2. */
+void oracle_eval_math(int32_t fn, const float *in, const float *in2, float *out, int32_t n);
+void oracle_threefry(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t *out2);
+void oracle_tape_actions(uint32_t seed, uint32_t step, uint32_t first_agent, int32_t n, int32_t *out6);
+float oracle_capsule(const float *o, const float *d, float r, float h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

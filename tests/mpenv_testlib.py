@@ -1,0 +1,297 @@
+"""ctypes harness over the two C ABIs used by the tests.
+
+* libmpenv.so (the product, include/mpenv.h) — the gfx950 engine.
+* liboracle.so (oracle/oracle.h) — TEST INFRASTRUCTURE: the CPU restatement
+  of the reference step used as the parity checker.
+
+Nothing here is imported by the product.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "madrona-mp-env_amd")
+SCENE = os.environ.get("MPENV_SCENE", os.path.join(ROOT, "scenes", "simple_map"))
+
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+import build_native  # noqa: E402
+import mpenv_tape  # noqa: E402
+
+# ---------------------------------------------------------------- constants
+EXPORT = dict(
+    RESET=0, WORLD_CURRICULUM=1, EXPLORE_ACTION=2, PVP_DISCRETE_ACTION=3, PVP_AIM_ACTION=4,
+    PVP_DISCRETE_AIM_ACTION=5, REWARD=6, DONE=7, MATCH_RESULT=8, AGENT_POLICY=9,
+    SELF_OBSERVATION=10, TEAMMATE_OBSERVATIONS=11, OPPONENT_OBSERVATIONS=12,
+    OPPONENT_LAST_KNOWN_OBSERVATIONS=13, SELF_POSITION=14, TEAMMATE_POSITIONS=15,
+    OPPONENT_POSITIONS=16, OPPONENT_LAST_KNOWN_POSITIONS=17, OPPONENT_MASKS=18, FWD_LIDAR=19,
+    REAR_LIDAR=20, AGENT_MAP=21, UNMASKED_AGENT_MAP=22, HP=23, ALIVE=24, MAGAZINE=25,
+    FILTERS_STATE=38, REWARD_HYPER_PARAMS=39, SIM_CONTROL=64, DEBUG_AGENT_F32=65,
+    DEBUG_AGENT_I32=66, DEBUG_WORLD_I32=67, DEBUG_WORLD_F32=68, DEBUG_EXPLORE=69,
+    DEBUG_CRUMBS=70,
+)
+
+# Exports compared between engine and oracle after every step.
+STEP_OUTPUTS = [
+    "FWD_LIDAR", "REAR_LIDAR", "HP", "MAGAZINE", "ALIVE", "SELF_OBSERVATION", "FILTERS_STATE",
+    "TEAMMATE_OBSERVATIONS", "OPPONENT_OBSERVATIONS", "OPPONENT_LAST_KNOWN_OBSERVATIONS",
+    "SELF_POSITION", "TEAMMATE_POSITIONS", "OPPONENT_POSITIONS", "OPPONENT_LAST_KNOWN_POSITIONS",
+    "OPPONENT_MASKS", "REWARD", "DONE", "MATCH_RESULT", "REWARD_HYPER_PARAMS", "RESET",
+    "WORLD_CURRICULUM", "PVP_DISCRETE_ACTION", "PVP_DISCRETE_AIM_ACTION", "PVP_AIM_ACTION",
+]
+DEBUG_OUTPUTS = ["DEBUG_AGENT_F32", "DEBUG_AGENT_I32", "DEBUG_WORLD_I32", "DEBUG_WORLD_F32",
+                 "DEBUG_CRUMBS"]
+
+DTYPES = {0: np.int32, 1: np.float32, 2: np.uint32}
+
+SIMFLAG_STAGGER_STARTS = 1 << 4
+SIMFLAG_RANDOM_FLIP_TEAMS = 1 << 7
+
+
+class OracleConfig(C.Structure):
+    _fields_ = [
+        ("num_worlds", C.c_uint32), ("rand_seed", C.c_uint32), ("auto_reset", C.c_int32),
+        ("sim_flags", C.c_uint32), ("team_size", C.c_uint32), ("world_id_offset", C.c_uint32),
+        ("scene_path", C.c_char_p), ("bvh_nodes", C.c_void_p), ("num_nodes", C.c_int32),
+        ("bvh_verts", C.c_void_p), ("num_bvh_verts", C.c_int32),
+    ]
+
+
+class MpenvConfig(C.Structure):
+    _fields_ = [
+        ("exec_mode", C.c_int32), ("gpu_id", C.c_int32), ("num_worlds", C.c_uint32),
+        ("rand_seed", C.c_uint32), ("auto_reset", C.c_int32), ("sim_flags", C.c_uint32),
+        ("task_type", C.c_int32), ("team_size", C.c_uint32), ("num_pbt_policies", C.c_uint32),
+        ("policy_history_size", C.c_uint32), ("scene_path", C.c_char_p), ("train_flank", C.c_int32),
+        ("replay_log_path", C.c_char_p), ("record_log_path", C.c_char_p),
+        ("event_log_path", C.c_char_p), ("curriculum_data_path", C.c_char_p),
+        ("world_id_offset", C.c_uint32),
+    ]
+
+
+_libs = {}
+
+
+def ensure_built():
+    build_native.build_all()
+
+
+def lib_mpenv():
+    if "mpenv" not in _libs:
+        ensure_built()
+        lib = C.CDLL(build_native.LIB)
+        lib.mpenv_create.argtypes = [C.POINTER(MpenvConfig), C.POINTER(C.c_void_p)]
+        lib.mpenv_destroy.argtypes = [C.c_void_p]
+        for fn in ("mpenv_init", "mpenv_step"):
+            getattr(lib, fn).argtypes = [C.c_void_p]
+        lib.mpenv_step_async.argtypes = [C.c_void_p, C.c_void_p]
+        lib.mpenv_export_tensor.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p),
+                                            C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                            C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+        lib.mpenv_last_error.restype = C.c_char_p
+        lib.mpenv_scene_bvh.argtypes = [C.c_char_p, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.mpenv_trigger_reset.argtypes = [C.c_void_p, C.c_int32]
+        lib.mpenv_set_hp.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
+        lib.mpenv_enable_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
+        lib.mpenv_kernel_timings.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_char_p),
+                                             C.POINTER(C.c_float), C.POINTER(C.c_int32)]
+        _libs["mpenv"] = lib
+    return _libs["mpenv"]
+
+
+def lib_oracle():
+    if "oracle" not in _libs:
+        ensure_built()
+        lib = C.CDLL(build_native.ORACLE_LIB)
+        lib.oracle_create.argtypes = [C.POINTER(OracleConfig)]
+        lib.oracle_create.restype = C.c_void_p
+        lib.oracle_destroy.argtypes = [C.c_void_p]
+        lib.oracle_export.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p),
+                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_int64)]
+        for fn in ("oracle_init", "oracle_step", "oracle_refresh_debug"):
+            getattr(lib, fn).argtypes = [C.c_void_p]
+        lib.oracle_step_worlds.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        lib.oracle_run_threaded.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32]
+        lib.oracle_run_threaded.restype = C.c_double
+        fp = C.POINTER(C.c_float)
+        lib.oracle_trace_ray.argtypes = [C.c_void_p, fp, fp, fp]
+        lib.oracle_trace_ray_brute.argtypes = [C.c_void_p, fp, fp, fp]
+        lib.oracle_sphere_cast.argtypes = [C.c_void_p, fp, fp, C.c_float, fp]
+        lib.oracle_sphere_cast.restype = C.c_float
+        lib.oracle_sphere_cast_brute.argtypes = [C.c_void_p, fp, fp, C.c_float]
+        lib.oracle_sphere_cast_brute.restype = C.c_float
+        lib.oracle_eval_math.argtypes = [C.c_int32, fp, fp, fp, C.c_int32]
+        lib.oracle_threefry.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)]
+        lib.oracle_tape_actions.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32,
+                                            C.POINTER(C.c_int32)]
+        lib.oracle_capsule.argtypes = [fp, fp, C.c_float, C.c_float]
+        lib.oracle_capsule.restype = C.c_float
+        _libs["oracle"] = lib
+    return _libs["oracle"]
+
+
+def fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def scene_bvh(scene=SCENE):
+    lib = lib_mpenv()
+    nn, nv, ms = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+    rc = lib.mpenv_scene_bvh(scene.encode(), None, C.byref(nn), None, C.byref(nv), C.byref(ms))
+    assert rc == 0, lib.mpenv_last_error()
+    nodes = np.zeros(nn.value * 64, dtype=np.uint8)
+    verts = np.zeros(nv.value * 3, dtype=np.float32)
+    rc = lib.mpenv_scene_bvh(scene.encode(), nodes.ctypes.data, C.byref(nn), verts.ctypes.data,
+                             C.byref(nv), C.byref(ms))
+    assert rc == 0, lib.mpenv_last_error()
+    return nodes, verts, ms.value
+
+
+class Oracle:
+    """CPU restatement of the reference step (test infrastructure)."""
+
+    def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
+                 world_id_offset=0, scene=SCENE):
+        self.lib = lib_oracle()
+        self.nodes, self.verts, _ = scene_bvh(scene)
+        cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
+                           world_id_offset, scene.encode(), self.nodes.ctypes.data,
+                           len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3)
+        self.h = self.lib.oracle_create(C.byref(cfg))
+        assert self.h, "oracle_create failed"
+        self.W, self.N = num_worlds, 2 * team_size
+
+    def close(self):
+        if self.h:
+            self.lib.oracle_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def view(self, name):
+        """Zero-copy numpy view of an oracle export."""
+        ptr, dt, nd = C.c_void_p(), C.c_int32(), C.c_int32()
+        dims = (C.c_int64 * 8)()
+        rc = self.lib.oracle_export(self.h, EXPORT[name], C.byref(ptr), C.byref(dt), C.byref(nd), dims)
+        assert rc == 0, name
+        shape = tuple(dims[i] for i in range(nd.value))
+        n = int(np.prod(shape))
+        ctype = {0: C.c_int32, 1: C.c_float, 2: C.c_uint32}[dt.value]
+        buf = (ctype * n).from_address(ptr.value)
+        return np.ctypeslib.as_array(buf).reshape(shape)
+
+    def get(self, name):
+        if name.startswith("DEBUG"):
+            self.lib.oracle_refresh_debug(self.h)
+        return self.view(name).copy()
+
+    def set_actions(self, acts6):
+        self.view("PVP_DISCRETE_ACTION")[:] = acts6[:, :4]
+        self.view("PVP_DISCRETE_AIM_ACTION")[:] = acts6[:, 4:6]
+
+    def init(self):
+        self.lib.oracle_init(self.h)
+
+    def step(self):
+        self.lib.oracle_step(self.h)
+
+
+class HipMem:
+    """Device->host copies through libamdhip64 (no torch needed)."""
+
+    def __init__(self):
+        self.hip = C.CDLL("libamdhip64.so")
+        self.hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        self.hip.hipDeviceSynchronize.argtypes = []
+
+    def d2h(self, ptr, nbytes, out):
+        rc = self.hip.hipMemcpy(out.ctypes.data, ptr, nbytes, 2)
+        assert rc == 0, f"hipMemcpy D2H failed: {rc}"
+
+    def h2d(self, ptr, arr):
+        arr = np.ascontiguousarray(arr)
+        rc = self.hip.hipMemcpy(ptr, arr.ctypes.data, arr.nbytes, 1)
+        assert rc == 0, f"hipMemcpy H2D failed: {rc}"
+
+
+class Engine:
+    """The gfx950 engine through its C ABI (include/mpenv.h)."""
+
+    def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
+                 world_id_offset=0, scene=SCENE, gpu_id=0):
+        self.lib = lib_mpenv()
+        self.mem = HipMem()
+        self._scene = scene.encode()
+        cfg = MpenvConfig(1, gpu_id, num_worlds, rand_seed, int(auto_reset), sim_flags, 2,
+                          team_size, 0, 0, self._scene, 0, None, None, None, None, world_id_offset)
+        h = C.c_void_p()
+        rc = self.lib.mpenv_create(C.byref(cfg), C.byref(h))
+        assert rc == 0, self.lib.mpenv_last_error().decode()
+        self.h = h
+        self.W, self.N = num_worlds, 2 * team_size
+
+    def close(self):
+        if self.h:
+            self.lib.mpenv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def desc(self, name):
+        ptr, dt, nd, gpu = C.c_void_p(), C.c_int32(), C.c_int32(), C.c_int32()
+        dims = (C.c_int64 * 8)()
+        rc = self.lib.mpenv_export_tensor(self.h, EXPORT[name], C.byref(ptr), C.byref(dt),
+                                          C.byref(nd), dims, C.byref(gpu))
+        assert rc == 0, self.lib.mpenv_last_error().decode()
+        return ptr.value, DTYPES[dt.value], tuple(dims[i] for i in range(nd.value))
+
+    def get(self, name):
+        ptr, dt, shape = self.desc(name)
+        out = np.empty(shape, dtype=dt)
+        self.mem.d2h(ptr, out.nbytes, out)
+        return out
+
+    def put(self, name, arr):
+        ptr, dt, shape = self.desc(name)
+        arr = np.ascontiguousarray(arr, dtype=dt).reshape(shape)
+        self.mem.h2d(ptr, arr)
+
+    def set_actions(self, acts6):
+        self.put("PVP_DISCRETE_ACTION", acts6[:, :4])
+        self.put("PVP_DISCRETE_AIM_ACTION", acts6[:, 4:6])
+
+    def init(self):
+        rc = self.lib.mpenv_init(self.h)
+        assert rc == 0, self.lib.mpenv_last_error().decode()
+
+    def step(self):
+        rc = self.lib.mpenv_step(self.h)
+        assert rc == 0, self.lib.mpenv_last_error().decode()
+
+
+def compare(a, b, name, float_rtol=0.0):
+    """Bit-exact for integer/bool data; floats exact unless float_rtol > 0."""
+    assert a.shape == b.shape, (name, a.shape, b.shape)
+    if a.dtype.kind == "f":
+        same = (a == b) | (np.isnan(a) & np.isnan(b))
+        if float_rtol > 0:
+            same |= np.abs(a - b) <= float_rtol * np.maximum(np.abs(a), np.abs(b))
+        if not same.all():
+            idx = np.argwhere(~same)
+            i0 = tuple(idx[0])
+            raise AssertionError(
+                f"{name}: {len(idx)} mismatches, first at {i0}: engine={a[i0]!r} oracle={b[i0]!r}")
+    else:
+        if not np.array_equal(a, b):
+            idx = np.argwhere(a != b)
+            i0 = tuple(idx[0])
+            raise AssertionError(
+                f"{name}: {len(idx)} mismatches, first at {i0}: engine={a[i0]!r} oracle={b[i0]!r}")
