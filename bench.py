@@ -1,0 +1,244 @@
+"""Headline benchmark: agent-steps/s of the world-batched Zone step.
+
+Metric (BASELINE.json): env steps/sec x agents, simple_map 6v6 @ 16384 worlds
+per GPU (config C3 at N=1; C4 = 8 x 16384 worlds sharded one process per
+GPU, weak scaling).  One "step" = one full Step graph (sim.cpp:5299-5320
+setupStepTasks, Task::Zone) over every world of the rank, preceded by the
+TrainInterface input copy of gpuStreamStep (mgr.cpp:625): the actions of
+step s are copied device-to-device from a 64-step ring of synthetic action
+tapes resident in HBM.  Inputs are resident before the timed
+region; nothing is skipped inside it.
+
+Also reported (one JSON line on rank 0):
+  roofline     -- dominant kernel's algorithmic HBM bytes / its average
+                  duration (HIP events on the engine's stream, timed
+                  region), against the 8 TB/s HBM3E peak; `traffic` = PMC
+                  HBM bytes per launch from profiles/ when a matching
+                  rocprofv3 --pmc summary exists (else null).
+  cpu_baseline -- the CPU oracle (a restatement of the reference's
+                  ThreadPoolExecutor path, oracle/) timed on this host on a
+                  bounded sample of the same workload, rank 0, N=1 only.
+
+Launch: python bench.py [--gpus 1 --steps 1000 --warmup 100]
+        N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "madrona-mp-env_amd")
+sys.path.insert(0, PKG)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md §HBM)
+RING = 64
+TAPE_SEED = 1234
+
+# Algorithmic HBM bytes per agent-step for each kernel: the
+# unique bytes the kernel must read or write, no re-reads counted.
+#   k_sim  : actions 24 r; agent SoA state 40 cols x 4 B r+w (320); DamageDealt
+#            6 x 4 r+w (48); hp/alive/magazine r+w (32); reward+done w (8);
+#            1 explore cell r+w (8); canSee r (8)                 = 448
+#   k_vis  : pos 12 + aim rot 16 + pose 4 + alive 4 r; canSee w 6  = 42
+#   k_obs  : state r ~104; self 172 + teammates 640 + opponents 768 +
+#            last-known 768 w, last-known 768 r; positions 12+60+72 w,
+#            last-known pos 72 r+w (144); masks 24 + filters 4 w; canSee 8 r
+#                                                                  = 3540
+#   k_lidar: pos 12 + rot 16 + aim rot 16 + pose 4 r; 80 rays x 16 B w
+#                                                                  = 1328
+# plus per world-step: 32 singleton columns x 4 B r+w (256) in k_sim.
+KERNEL_BYTES_PER_AGENT = {"k_sim": 448, "k_vis": 42, "k_obs": 3540, "k_lidar": 1328}
+KERNEL_BYTES_PER_WORLD = {"k_sim": 256, "k_vis": 0, "k_obs": 0, "k_lidar": 0}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--worlds", type=int, default=16384, help="worlds per GPU")
+    ap.add_argument("--team-size", type=int, default=6)
+    ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "simple_map"))
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline timed budget")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: RCCL-gather obs/reward/done to rank 0 every step (learner mode)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(args, world_size):
+    """Oracle (test infrastructure, a restatement of the reference's CPU
+    executor) on a bounded sample: 32 worlds per thread, 10 untimed steps,
+    then 5-step chunks until --cpu-seconds elapse."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import mpenv_testlib as T
+
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    W = 32 * threads
+    N = 2 * args.team_size
+    o = T.Oracle(W, args.team_size, scene=args.scene)
+    o.put_ctrl([0, 1, 1])
+    o.init()
+    ring = np.ascontiguousarray(T.mpenv_tape.tape_ring(TAPE_SEED, 0, W * N, 16))
+    o.lib.oracle_run_threaded(o.h, 10, threads, ring.ctypes.data, 16)
+    secs, steps = 0.0, 0
+    while secs < args.cpu_seconds and steps < 400:
+        secs += o.lib.oracle_run_threaded(o.h, 5, threads, ring.ctypes.data, 16)
+        steps += 5
+    o.close()
+    return {
+        "value": W * N * steps / secs,
+        "unit": "agent-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{W} worlds {args.team_size}v{args.team_size} simple_map, {steps} steps after 10 "
+                  f"warmup, {threads} std::threads static world partition, {secs:.1f} s",
+    }
+
+
+def load_traffic(path, workload):
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if d.get("workload") != workload:
+        return None, None
+    return d.get("kernel"), d.get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import madrona_mp_env as m
+    from mpenv_dist import gather_to_learner
+    import mpenv_tape
+
+    W, ts = args.worlds, args.team_size
+    N = 2 * ts
+    A = W * N
+    offset = rank * W  # weak scaling: each rank owns W global worlds
+    sim = m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=local, num_worlds=W, rand_seed=5,
+                       auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                       team_size=ts, num_pbt_policies=0, policy_history_size=0,
+                       scene_path=args.scene, world_id_offset=offset)
+    ctrl = sim.sim_control_tensor().to_torch()
+    ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=dev).view_as(ctrl))
+    torch.cuda.synchronize()
+    sim.init()
+
+    ring = torch.from_numpy(mpenv_tape.tape_ring(TAPE_SEED, offset * N, A, RING)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    outs = [sim.self_observation_tensor().to_torch(), sim.reward_tensor().to_torch(),
+            sim.done_tensor().to_torch()] if args.gather and world_size > 1 else None
+
+    def one_step(s):
+        sim.copy_actions(ring[s % RING].data_ptr(), sptr)
+        sim.step_async(sptr)
+        if outs is not None:
+            gather_to_learner(outs, dst=0)
+
+    for s in range(args.warmup):
+        one_step(s)
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    sim.enable_kernel_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        one_step(args.warmup + s)
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timings = sim.kernel_timings()  # {name: (avg ms, launches)}
+    sim.enable_kernel_timing(False)
+    if world_size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_agent_steps = world_size * A * args.steps
+    value = total_agent_steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # dominant kernel and its HBM roofline
+    dom = max(timings, key=lambda k: timings[k][0])
+    dom_ms = timings[dom][0]
+    alg = KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W
+    achieved = alg / (dom_ms * 1e-3) / 1e9
+    workload = f"simple_map {ts}v{ts} x {W} worlds/GPU"
+    tk, traffic = load_traffic(args.traffic, workload)
+    step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W
+    kern_ms = sum(v[0] for v in timings.values())
+
+    result = {
+        "metric": "env steps/sec x agents (whole node), simple_map 6v6 @ 16384 worlds",
+        "value": round(value, 1),
+        "unit": "agent-steps/s",
+        "n_gpus": world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (hash action tape, seed 1234; 64-step ring resident in HBM)",
+        "config": {
+            "workload": workload,
+            "worlds_per_gpu": W,
+            "agents_per_gpu": A,
+            "total_worlds": W * world_size,
+            "task": "Zone",
+            "sim_flags": "Default",
+            "sim_control": [0, 1, 1],
+            "rand_seed": 5,
+            "parallelism": f"world-sharded x{world_size}" + (" + RCCL gather" if outs else ""),
+        },
+        "world_steps_per_s": round(value / N, 1),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic if tk == dom else None,
+            "algorithmic_bytes_per_launch": alg,
+        },
+        "kernels_ms": {k: round(v[0], 4) for k, v in timings.items()},
+        "step_hbm": {
+            "algorithmic_bytes_per_step": step_bytes,
+            "achieved_GBps_over_kernels": round(step_bytes / (kern_ms * 1e-3) / 1e9, 2),
+        },
+    }
+    if rank == 0 and world_size == 1 and args.cpu_baseline == "auto":
+        result["cpu_baseline"] = cpu_baseline(args, world_size)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world_size > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

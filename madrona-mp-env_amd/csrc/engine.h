@@ -29,7 +29,7 @@ constexpr int kFwdRays = 64;   // 2 x 32
 constexpr int kRearRays = 16;  // 2 x 8
 constexpr int kLidarRays = kFwdRays + kRearRays;
 constexpr int kMaxCrumbs = 128;
-constexpr int kMaxSpawns = 32;   // per spawn list (simple_map: 8/8/16)
+constexpr int kMinSpawnTrack = 128; // SpawnUsageCounter::maxNumSpawns (types.hpp:96)
 constexpr int kMaxBVHStack = 16; // register byte-stack capacity
 
 #define MP_AGENT_F32(X) \
@@ -79,7 +79,7 @@ struct DevState {
     uint32_t *visited;     // [A][81*81] ExploreTracker
     int32_t *filtLast;     // [W][2][3] FiltersMatchState::lastMatches (3 filters used)
     int32_t *zoneStats;    // [W][5][5]
-    uint32_t *spawnTrack;  // [W][3][kMaxSpawns] SpawnUsageCounter
+    uint32_t *spawnTrack;  // [W][3][spawnTrackLen] SpawnUsageCounter
     float4 *crumbs;        // [W][kMaxCrumbs][2] {x,y,z,penalty},{team,offset,id,-}
 
     // Exported columns (reference layouts)
@@ -139,6 +139,7 @@ struct SceneDev {
     const Spawn *bSpawns;
     const Spawn *commonRespawns;
     int32_t numA, numB, numCommon, numDefaultA, numDefaultB;
+    int32_t spawnTrackLen; // slots per SpawnUsageCounter list: max(128, longest list)
     mp::AABB zoneAABB[kMaxZones];
     float zoneRot[kMaxZones];
     int32_t numZones;

@@ -504,7 +504,7 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
     const int64_t g0 = (int64_t)w * N;
     const int team = ai / S.T;
     const uint32_t cur_step = (uint32_t)S.curStep[w];
-    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * kMaxSpawns];
+    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
 
     const Spawn *options;
     auto spawnAgent = [&](int idx) {
@@ -532,7 +532,7 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
             options = sc.bSpawns;
             num_default = sc.numDefaultB;
             num_extra = sc.numB - sc.numDefaultB;
-            tracker = track + kMaxSpawns;
+            tracker = track + sc.spawnTrackLen;
         }
         if (use_middle) {
             options += num_default;
@@ -554,7 +554,7 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
     }
 
     options = sc.commonRespawns;
-    uint32_t *rtrack = track + 2 * kMaxSpawns;
+    uint32_t *rtrack = track + 2 * sc.spawnTrackLen;
     const int cz = S.curZone[w];
     AABB za = sc.zoneAABB[cz];
     Vec3 zone_center = 0.5f * (za.pMin + za.pMax);
@@ -681,8 +681,8 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
         S.bcLast[g] = -1;
         S.bcSteps[g] = 0;
     }
-    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * kMaxSpawns];
-    for (int k = 0; k < 3 * kMaxSpawns; k++) track[k] = 0xFFFFFFFFu;
+    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
+    for (int k = 0; k < 3 * sc.spawnTrackLen; k++) track[k] = 0xFFFFFFFFu;
     spawnAgentsD(S, sc, w, false);
 
     RNG base = ldWRng(S, w);

@@ -131,6 +131,14 @@ struct mpenv_manager {
         return static_cast<T *>(p);
     }
 
+    // Host->device copy ordered on the manager stream (after the zeroing
+    // memsets issued by alloc() and any in-flight step), then waited for.
+    void upload(void *dst, const void *src, size_t bytes)
+    {
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+        HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
     hipEvent_t nextEvent()
     {
         if (eventsUsed == eventPool.size()) {
@@ -246,18 +254,19 @@ static void buildSceneDev(mpenv_manager &m)
     if (s.nodes.size() > 256) throw std::runtime_error("BVH has more than 256 nodes (byte-stack limit)");
     if (s.maxStack > kMaxBVHStack) throw std::runtime_error("BVH too deep for the 16-entry register stack");
     if (s.zoneAABBs.empty() || s.zoneAABBs.size() > (size_t)kMaxZones) throw std::runtime_error("bad zone count");
-    if (s.aSpawns.size() > (size_t)kMaxSpawns || s.bSpawns.size() > (size_t)kMaxSpawns ||
-        s.commonRespawns.size() > (size_t)kMaxSpawns)
-        throw std::runtime_error("too many spawns for the per-world usage tracker");
-    if (s.aSpawns.empty() || s.bSpawns.empty()) throw std::runtime_error("scene needs A and B spawns");
+    if (s.numDefaultASpawns == 0 || s.numDefaultBSpawns == 0) throw std::runtime_error("scene needs A and B spawns");
+    if ((m.cfg.sim_flags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) &&
+        (s.aSpawns.size() == s.numDefaultASpawns || s.bSpawns.size() == s.numDefaultBSpawns))
+        // the reference would index past its spawn array here (utils.cpp:358-366)
+        throw std::runtime_error("SpawnInMiddle: no free middle cells in this scene");
 
     BVHNode *d_nodes = m.alloc<BVHNode>(s.nodes.size());
-    HIP_CHECK(hipMemcpy(d_nodes, s.nodes.data(), sizeof(BVHNode) * s.nodes.size(), hipMemcpyHostToDevice));
+    m.upload(d_nodes, s.nodes.data(), sizeof(BVHNode) * s.nodes.size());
     float *d_verts = m.alloc<float>(s.bvhVerts.size() * 3);
-    HIP_CHECK(hipMemcpy(d_verts, s.bvhVerts.data(), sizeof(float) * 3 * s.bvhVerts.size(), hipMemcpyHostToDevice));
+    m.upload(d_verts, s.bvhVerts.data(), sizeof(float) * 3 * s.bvhVerts.size());
     auto upSpawns = [&](const std::vector<Spawn> &v) {
         Spawn *p = m.alloc<Spawn>(std::max<size_t>(v.size(), 1));
-        if (!v.empty()) HIP_CHECK(hipMemcpy(p, v.data(), sizeof(Spawn) * v.size(), hipMemcpyHostToDevice));
+        if (!v.empty()) m.upload(p, v.data(), sizeof(Spawn) * v.size());
         return p;
     };
     sc.nodes = d_nodes;
@@ -285,6 +294,8 @@ static void buildSceneDev(mpenv_manager &m)
     sc.numCommon = (int32_t)s.commonRespawns.size();
     sc.numDefaultA = (int32_t)s.numDefaultASpawns;
     sc.numDefaultB = (int32_t)s.numDefaultBSpawns;
+    sc.spawnTrackLen = (int32_t)std::max<size_t>(
+        kMinSpawnTrack, std::max(s.aSpawns.size(), std::max(s.bSpawns.size(), s.commonRespawns.size())));
     sc.numZones = (int32_t)s.zoneAABBs.size();
     for (int z = 0; z < sc.numZones; z++) {
         sc.zoneAABB[z] = s.zoneAABBs[z];
@@ -331,7 +342,7 @@ static void allocState(mpenv_manager &m)
     S.visited = m.alloc<uint32_t>(A * kGridCells);
     S.filtLast = m.alloc<int32_t>(W * 6);
     S.zoneStats = m.alloc<int32_t>(W * 25);
-    S.spawnTrack = m.alloc<uint32_t>(W * 3 * kMaxSpawns);
+    S.spawnTrack = m.alloc<uint32_t>(W * 3 * (size_t)m.sc.spawnTrackLen);
     S.crumbs = m.alloc<float4>(W * kMaxCrumbs * 2);
     S.reset = m.alloc<int32_t>(W);
     S.worldCurr = m.alloc<int32_t>(W);
@@ -385,8 +396,16 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
     const uint32_t unsupported = MPENV_SIMFLAG_NAVMESH_SPAWN | MPENV_SIMFLAG_ENABLE_CURRICULUM |
                                  MPENV_SIMFLAG_HARDCODED_SPAWNS | MPENV_SIMFLAG_FULL_TEAM_POLICY |
                                  MPENV_SIMFLAG_SUB_ZONES;
-    if (cfg->sim_flags & unsupported)
-        return fail(MPENV_ERR_UNSUPPORTED, "sim_flags contains a flag this build does not implement");
+    if (cfg->sim_flags & unsupported) {
+        static const char *names[] = { "SpawnInMiddle", "RandomizeHPMagazine", "NavmeshSpawn", "NoRespawn",
+                                       "StaggerStarts", "EnableCurriculum", "HardcodedSpawns",
+                                       "RandomFlipTeams", "StaticFlipTeams", "FullTeamPolicy",
+                                       "SimEvalMode", "SubZones" };
+        std::string msg = "sim_flags not implemented by this build:";
+        for (int b = 0; b < 12; b++)
+            if (cfg->sim_flags & unsupported & (1u << b)) msg += std::string(" ") + names[b];
+        return fail(MPENV_ERR_UNSUPPORTED, msg);
+    }
     if (cfg->replay_log_path || cfg->record_log_path || cfg->event_log_path || cfg->curriculum_data_path ||
         cfg->train_flank)
         return fail(MPENV_ERR_UNSUPPORTED, "record/replay/event logs, curricula and flank rewards are not implemented");
@@ -403,7 +422,10 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m->scenePath = cfg->scene_path;
         m->cfg.scene_path = m->scenePath.c_str();
         m->gpu = cfg->gpu_id;
-        HIP_CHECK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+        // A blocking stream: ordered after work the caller queued on the
+        // legacy default stream (e.g. torch writes into the action tensors),
+        // matching the synchronous Manager::step contract (mgr.cpp:1949-1960).
+        HIP_CHECK(hipStreamCreateWithFlags(&m->stream, hipStreamDefault));
         m->scene = loadScene(m->scenePath, (cfg->sim_flags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) != 0);
         buildSceneDev(*m);
         m->S.W = (int32_t)cfg->num_worlds;
@@ -563,11 +585,18 @@ static int checkAgent(mpenv_manager *m, int32_t w, int32_t a)
     return MPENV_OK;
 }
 
+// Setter upload: ordered after in-flight work on the manager stream.
+static bool put(mpenv_manager *m, void *dst, const void *src, size_t bytes)
+{
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, m->stream) == hipSuccess &&
+           hipStreamSynchronize(m->stream) == hipSuccess;
+}
+
 int mpenv_trigger_reset(mpenv_manager *m, int32_t w)
 {
     if (int rc = checkAgent(m, w, 0)) return rc;
     int32_t one = 1;
-    if (hipMemcpy(m->S.reset + w, &one, 4, hipMemcpyHostToDevice) != hipSuccess)
+    if (!put(m, m->S.reset + w, &one, 4))
         return fail(MPENV_ERR_HIP, "hipMemcpy failed");
     return MPENV_OK;
 }
@@ -578,9 +607,9 @@ int mpenv_set_pvp_action(mpenv_manager *m, int32_t w, int32_t a, const int32_t d
     if (int rc = checkAgent(m, w, a)) return rc;
     const int64_t g = (int64_t)w * m->S.N + a;
     bool ok = true;
-    if (discrete) ok &= hipMemcpy(m->S.discreteAction + 4 * g, discrete, 16, hipMemcpyHostToDevice) == hipSuccess;
-    if (aim) ok &= hipMemcpy(m->S.aimAction + 2 * g, aim, 8, hipMemcpyHostToDevice) == hipSuccess;
-    if (aim_discrete) ok &= hipMemcpy(m->S.discreteAim + 2 * g, aim_discrete, 8, hipMemcpyHostToDevice) == hipSuccess;
+    if (discrete) ok &= put(m, m->S.discreteAction + 4 * g, discrete, 16);
+    if (aim) ok &= put(m, m->S.aimAction + 2 * g, aim, 8);
+    if (aim_discrete) ok &= put(m, m->S.discreteAim + 2 * g, aim_discrete, 8);
     return ok ? MPENV_OK : fail(MPENV_ERR_HIP, "hipMemcpy failed");
 }
 
@@ -588,7 +617,7 @@ int mpenv_set_hp(mpenv_manager *m, int32_t w, int32_t a, int32_t hp)
 {
     if (int rc = checkAgent(m, w, a)) return rc;
     float v = (float)hp;
-    if (hipMemcpy(m->S.hp + (int64_t)w * m->S.N + a, &v, 4, hipMemcpyHostToDevice) != hipSuccess)
+    if (!put(m, m->S.hp + (int64_t)w * m->S.N + a, &v, 4))
         return fail(MPENV_ERR_HIP, "hipMemcpy failed");
     return MPENV_OK;
 }
@@ -596,7 +625,7 @@ int mpenv_set_hp(mpenv_manager *m, int32_t w, int32_t a, int32_t hp)
 int mpenv_set_agent_policy(mpenv_manager *m, int32_t w, int32_t a, int32_t policy)
 {
     if (int rc = checkAgent(m, w, a)) return rc;
-    if (hipMemcpy(m->S.policy + (int64_t)w * m->S.N + a, &policy, 4, hipMemcpyHostToDevice) != hipSuccess)
+    if (!put(m, m->S.policy + (int64_t)w * m->S.N + a, &policy, 4))
         return fail(MPENV_ERR_HIP, "hipMemcpy failed");
     return MPENV_OK;
 }
@@ -604,7 +633,8 @@ int mpenv_set_agent_policy(mpenv_manager *m, int32_t w, int32_t a, int32_t polic
 int mpenv_set_uniform_agent_policy(mpenv_manager *m, int32_t policy)
 {
     if (!m) return fail(MPENV_ERR_INVALID, "null manager");
-    if (hipMemsetD32((hipDeviceptr_t)m->S.policy, policy, (size_t)m->S.A) != hipSuccess)
+    if (hipMemsetD32Async((hipDeviceptr_t)m->S.policy, policy, (size_t)m->S.A, m->stream) != hipSuccess ||
+        hipStreamSynchronize(m->stream) != hipSuccess)
         return fail(MPENV_ERR_HIP, "hipMemsetD32 failed");
     return MPENV_OK;
 }

@@ -190,8 +190,7 @@ struct World {
     int filtersLastMatchedStep[2];
     int episodeCurriculum;
     uint64_t matchID;
-    // SpawnUsageCounter (types.hpp:95-100)
-    uint32_t initASpawnsLastUsedTick[128], initBSpawnsLastUsedTick[128], respawnLastUsedTick[128];
+    // SpawnUsageCounter (types.hpp:95-100) lives in Oracle::spawnTrack.
     // GoalRegionsState (types.hpp:808-814)
     bool regionsActive[10];
     float minDistToRegions[10];
@@ -226,6 +225,13 @@ struct Oracle {
 
     std::vector<Agent> agents;
     std::vector<World> worlds;
+    // SpawnUsageCounter per world: [W][3][spawnTrackLen] (initA, initB,
+    // respawn).  The reference fixes 128 slots (types.hpp:96) and asserts the
+    // list fits; here the length is max(128, longest spawn list) so a long
+    // SpawnInMiddle list indexes its own slots (documented definition).
+    int spawnTrackLen = 128;
+    std::vector<uint32_t> spawnTrack;
+    uint32_t *track(int w, int k) { return &spawnTrack[((size_t)w * 3 + k) * spawnTrackLen]; }
 
     // Exported buffers, laid out as the reference's exported columns.
     std::vector<int32_t> resetBuf, worldCurriculum, matchResult, exploreAction, discreteAction,
@@ -667,12 +673,12 @@ void standardSpawnPoint(Oracle &o, int w, int ai, bool is_respawn, bool use_midd
             options = o.aSpawns.data();
             num_default = (int)o.numDefaultASpawns;
             num_extra = (int)o.aSpawns.size() - num_default;
-            tracker = wd.initASpawnsLastUsedTick;
+            tracker = o.track(w, 0);
         } else {
             options = o.bSpawns.data();
             num_default = (int)o.numDefaultBSpawns;
             num_extra = (int)o.bSpawns.size() - num_default;
-            tracker = wd.initBSpawnsLastUsedTick;
+            tracker = o.track(w, 1);
         }
         if (use_middle_spawn) {
             options += num_default;
@@ -701,7 +707,7 @@ void standardSpawnPoint(Oracle &o, int w, int ai, bool is_respawn, bool use_midd
     float best_score = kFltMax;
     int best_idx = -1;
     for (int s = 0; s < num_spawns; s++) {
-        uint32_t last_used = wd.respawnLastUsedTick[s];
+        uint32_t last_used = o.track(w, 2)[s];
         if (last_used == (uint32_t)wd.curStep) continue;
         float score = 0.f;
         uint32_t elapsed = (uint32_t)(kDeltaT * float((uint32_t)wd.curStep - last_used));
@@ -730,7 +736,7 @@ void standardSpawnPoint(Oracle &o, int w, int ai, bool is_respawn, bool use_midd
     }
     if (best_idx < 0) best_idx = 0; // assert(best_spawn_idx != -1) in the reference
     spawnAgent(best_idx);
-    wd.respawnLastUsedTick[best_idx] = (uint32_t)wd.curStep;
+    o.track(w, 2)[best_idx] = (uint32_t)wd.curStep;
 }
 
 // utils.cpp:734-948 spawnAgents (Zone task, default flags)
@@ -855,11 +861,7 @@ void resetPersistentEntities(Oracle &o, int w, RandKey episode_key)
         ag.lastBreadcrumb = -1;
         ag.stepsSinceLastNewBreadcrumb = 0;
     }
-    for (int i = 0; i < 128; i++) {
-        wd.initASpawnsLastUsedTick[i] = 0xFFFFFFFFu;
-        wd.initBSpawnsLastUsedTick[i] = 0xFFFFFFFFu;
-        wd.respawnLastUsedTick[i] = 0xFFFFFFFFu;
-    }
+    std::fill(o.track(w, 0), o.track(w, 0) + 3 * o.spawnTrackLen, 0xFFFFFFFFu);
     spawnAgents(o, w, false);
 
     for (int i = 0; i < o.N; i++) {
@@ -2031,6 +2033,45 @@ void readVec(std::ifstream &f, std::vector<T> &v, size_t n)
     if (!f) throw std::runtime_error("oracle: truncated scene file");
 }
 
+// SpawnInMiddle extra spawn cells, mgr.cpp:1240-1299: a 20x20 grid over
+// x in [-280, 280], y in [-200, 200], each cell z in [1.0, 1.5]; a cell is
+// kept when no collision triangle overlaps it (left half -> team A, right
+// half -> team B, row-major order).  The reference asks MeshBVH::findOverlaps
+// (mesh_bvh.inl:50-108), which tests the cell against *quantized leaf boxes*
+// of its Embree-built tree — builder-dependent, and on simple_map likely to
+// reject every cell (the floor leaf box is padded by >= one quantum) and then
+// index past the spawn array.  The build defines the overlap test on the
+// triangles' own AABBs instead ("documented definitions").
+void addMiddleSpawnCells(Oracle &o)
+{
+    const Vec3 lo = v3(-280.f, -200.f, 0.5f), hi = v3(280.f, 200.f, 0.5f);
+    const int dim = 20;
+    const float cw = (hi.x - lo.x) / dim, chh = (hi.y - lo.y) / dim;
+    for (int y = 0; y < dim; y++) {
+        for (int x = 0; x < dim; x++) {
+            Vec3 cmin = lo + v3(cw * x, chh * y, 0.5f);
+            Vec3 cmax = cmin + v3(cw, chh, 0.5f);
+            bool hit = false;
+            for (size_t t = 0; t + 2 < o.verts.size() && !hit; t += 3) {
+                const Vec3 &a = o.verts[t], &b = o.verts[t + 1], &c = o.verts[t + 2];
+                Vec3 tmin = v3(std::min(a.x, std::min(b.x, c.x)), std::min(a.y, std::min(b.y, c.y)),
+                               std::min(a.z, std::min(b.z, c.z)));
+                Vec3 tmax = v3(std::max(a.x, std::max(b.x, c.x)), std::max(a.y, std::max(b.y, c.y)),
+                               std::max(a.z, std::max(b.z, c.z)));
+                hit = tmin.x <= cmax.x && tmax.x >= cmin.x && tmin.y <= cmax.y && tmax.y >= cmin.y &&
+                      tmin.z <= cmax.z && tmax.z >= cmin.z;
+            }
+            if (hit) continue;
+            Spawn sp;
+            sp.region.pMin = cmin;
+            sp.region.pMax = cmax;
+            sp.yawMin = 0.f;
+            sp.yawMax = 2.f * kPi;
+            (x >= dim / 2 ? o.bSpawns : o.aSpawns).push_back(sp);
+        }
+    }
+}
+
 // map_importer.cpp:508-567 (spawns, zones) and 223-256 (world bounds)
 void loadScene(Oracle &o)
 {
@@ -2155,6 +2196,7 @@ void *oracle_create(const oracle_config *cfg)
         o->verts.resize(cfg->num_bvh_verts);
         for (int i = 0; i < cfg->num_bvh_verts; i++)
             o->verts[i] = v3(cfg->bvh_verts[3 * i], cfg->bvh_verts[3 * i + 1], cfg->bvh_verts[3 * i + 2]);
+        if (o->simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) addMiddleSpawnCells(*o);
         // sim.cpp:5855 maxDist; 5869-5882 frustumData
         o->maxDist = length(o->worldBounds.pMax - o->worldBounds.pMin);
         {
@@ -2181,6 +2223,9 @@ void *oracle_create(const oracle_config *cfg)
             for (bool &b : a.canSee) b = false;
         }
         o->worlds.resize(W);
+        o->spawnTrackLen = (int)std::max<size_t>(
+            128, std::max(o->aSpawns.size(), std::max(o->bSpawns.size(), o->commonRespawns.size())));
+        o->spawnTrack.assign(W * 3 * (size_t)o->spawnTrackLen, 0xFFFFFFFFu);
         o->resetBuf.assign(W, 0);
         o->worldCurriculum.assign(W, 0);
         o->matchResult.assign(W * 30, 0);

@@ -1,0 +1,80 @@
+"""Generate tests/golden/*.json: per-step state hashes of oracle rollouts.
+
+SURVEY.md §8c: the reference cannot be built or imported here, so golden
+vectors come from the CPU restatement (oracle/) in this container.  Each
+fixture records a config, the action tape seed, and for every step the
+sha256 of every compared export (tests/mpenv_testlib.py STEP_OUTPUTS +
+DEBUG_OUTPUTS), plus a few float tensors of the final step in full.  The
+GPU parity tests check the engine against these files as well as against a
+live oracle run.
+
+Run:  python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import mpenv_testlib as T  # noqa: E402
+
+CASES = {
+    "1v1_w2": dict(team_size=1, worlds=2, steps=200, sim_flags=0, ctrl=[0, 1, 1]),
+    "3v3_w2": dict(team_size=3, worlds=2, steps=200, sim_flags=0, ctrl=[0, 1, 1]),
+    "6v6_w2": dict(team_size=6, worlds=2, steps=200, sim_flags=0, ctrl=[0, 1, 1]),
+    # RandomizeHPMagazine | NoRespawn | StaggerStarts, no auto flip
+    "2v2_flags": dict(team_size=2, worlds=3, steps=150, sim_flags=(1 << 1) | (1 << 3) | (1 << 4),
+                      ctrl=[0, 0, 0]),
+    # SpawnInMiddle (+ RandomizeHPMagazine) with the aim-bot action source:
+    # contact, kills, respawns, combat rewards
+    "3v3_mid_combat": dict(team_size=3, worlds=4, steps=300, sim_flags=1 | (1 << 1), ctrl=[0, 1, 1],
+                           policy="combat"),
+    "6v6_mid_combat": dict(team_size=6, worlds=2, steps=300, sim_flags=1, ctrl=[0, 1, 1],
+                           policy="combat"),
+}
+TAPE_SEED = 1234
+FINAL_TENSORS = ["SELF_OBSERVATION", "REWARD", "HP", "FWD_LIDAR"]
+
+
+def step_hashes(sim):
+    h = {}
+    for name in T.STEP_OUTPUTS + T.DEBUG_OUTPUTS:
+        h[name] = hashlib.sha256(np.ascontiguousarray(sim.get(name)).tobytes()).hexdigest()[:16]
+    return h
+
+
+def rollout(sim, case, record=None):
+    """Drive an Oracle or Engine through a case; yields (step, sim)."""
+    sim.put_ctrl(np.array(case["ctrl"], np.int32))
+    A = case["worlds"] * 2 * case["team_size"]
+    sim.init()
+    yield -1
+    for s in range(case["steps"]):
+        if case.get("policy") == "combat":
+            sim.set_actions(T.combat_actions(sim, s, TAPE_SEED))
+        else:
+            sim.set_actions(T.mpenv_tape.tape_actions(TAPE_SEED, s, 0, A))
+        sim.step()
+        yield s
+
+
+def make(name, case):
+    o = T.Oracle(case["worlds"], case["team_size"], sim_flags=case["sim_flags"])
+    hashes = []
+    for _ in rollout(o, case):
+        hashes.append(step_hashes(o))
+    final = {n: o.get(n).ravel().tolist() for n in FINAL_TENSORS}
+    o.close()
+    return dict(case=case, tape_seed=TAPE_SEED, hashes=hashes, final=final)
+
+
+if __name__ == "__main__":
+    for name, case in CASES.items():
+        out = make(name, case)
+        path = os.path.join(HERE, f"{name}.json")
+        with open(path, "w") as f:
+            json.dump(out, f, separators=(",", ":"))
+        print(path, os.path.getsize(path))

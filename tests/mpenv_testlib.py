@@ -192,6 +192,9 @@ class Oracle:
             self.lib.oracle_refresh_debug(self.h)
         return self.view(name).copy()
 
+    def put_ctrl(self, ctrl):
+        self.view("SIM_CONTROL")[:] = np.asarray(ctrl, np.int32).reshape(self.view("SIM_CONTROL").shape)
+
     def set_actions(self, acts6):
         self.view("PVP_DISCRETE_ACTION")[:] = acts6[:, :4]
         self.view("PVP_DISCRETE_AIM_ACTION")[:] = acts6[:, 4:6]
@@ -259,10 +262,27 @@ class Engine:
         self.mem.d2h(ptr, out.nbytes, out)
         return out
 
+    def get_rows(self, name, r0, r1):
+        """Rows [r0, r1) of the leading dimension (agents or worlds)."""
+        ptr, dt, shape = self.desc(name)
+        row = int(np.prod(shape[1:])) * 4
+        out = np.empty((r1 - r0,) + tuple(shape[1:]), dtype=dt)
+        self.mem.d2h(ptr + r0 * row, out.nbytes, out)
+        return out
+
+    def trigger_reset(self, w):
+        assert self.lib.mpenv_trigger_reset(self.h, w) == 0
+
+    def set_hp(self, w, a, hp):
+        assert self.lib.mpenv_set_hp(self.h, w, a, hp) == 0
+
     def put(self, name, arr):
         ptr, dt, shape = self.desc(name)
         arr = np.ascontiguousarray(arr, dtype=dt).reshape(shape)
         self.mem.h2d(ptr, arr)
+
+    def put_ctrl(self, ctrl):
+        self.put("SIM_CONTROL", ctrl)
 
     def set_actions(self, acts6):
         self.put("PVP_DISCRETE_ACTION", acts6[:, :4])
@@ -295,3 +315,39 @@ def compare(a, b, name, float_rtol=0.0):
             i0 = tuple(idx[0])
             raise AssertionError(
                 f"{name}: {len(idx)} mismatches, first at {i0}: engine={a[i0]!r} oracle={b[i0]!r}")
+
+
+# Discrete-aim turn table (sim.cpp:2284-2370 pvpDiscreteAimSystem).
+_YAW_TURN = np.array([0, 1 / 256, 1 / 128, 1 / 64, 1 / 32, 1 / 16, 1 / 8]) * np.pi
+_PITCH_TURN = np.array([0, 1 / 128, 1 / 64, 1 / 32]) * np.pi
+
+
+def combat_actions(sim, step, seed=1234):
+    """Tape actions overridden by a greedy aim-bot for agents that see an
+    opponent: turn toward the first visible opponent (relative yaw/pitch are
+    opponent-observation fields 24/25, sim.cpp obs layout) and fire when
+    roughly on target.  A deterministic function of the observations, so it
+    drives engine and oracle identically while parity holds; it exists to
+    exercise kills, respawns and combat rewards, which a pure random tape on
+    simple_map rarely reaches."""
+    A = sim.W * sim.N
+    acts = mpenv_tape.tape_actions(seed, step, 0, A)
+    opp = sim.get("OPPONENT_OBSERVATIONS")  # [A, 6, 32]
+    mask = sim.get("OPPONENT_MASKS").reshape(A, -1)
+    vis = mask[:, :opp.shape[1]] > 0
+    has = vis.any(1)
+    k = np.argmax(vis, 1)
+    yaw = opp[np.arange(A), k, 24]
+    pitch = opp[np.arange(A), k, 25]
+
+    def bucket(delta, table, centre):
+        mag = np.abs(delta)[:, None]
+        idx = np.sum(table[None, 1:] <= mag, axis=1)
+        return (centre + np.sign(delta) * idx).astype(np.int32)
+
+    yb = bucket(yaw, _YAW_TURN, 6)
+    pb = bucket(pitch, _PITCH_TURN, 3)
+    acts[has, 4] = yb[has]
+    acts[has, 5] = pb[has]
+    acts[has, 2] = np.where(np.abs(yaw[has]) < 0.05, 1, 0)
+    return acts

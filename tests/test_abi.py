@@ -1,0 +1,114 @@
+"""The drop-in boundary without a GPU: library load, exported symbols,
+Python module surface (src/bindings.cpp:11-160) and loud failure modes."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import mpenv_testlib as T
+
+HEADER = os.path.join(T.ROOT, "include", "mpenv.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mpenv_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_manager_surface():
+    fns = declared_functions()
+    for f in ("mpenv_create", "mpenv_destroy", "mpenv_init", "mpenv_step", "mpenv_step_async",
+              "mpenv_gpu_stream_init", "mpenv_gpu_stream_step", "mpenv_export_tensor",
+              "mpenv_trigger_reset", "mpenv_set_pvp_action", "mpenv_set_hp",
+              "mpenv_train_interface_size", "mpenv_train_interface_entry", "mpenv_copy_actions"):
+        assert f in fns, f
+
+
+def test_library_exports_every_declared_symbol():
+    lib = T.lib_mpenv()
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", T.build_native.LIB], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (mpenv_\w+)", out))
+    assert set(declared_functions()) <= exported
+    assert lib.mpenv_abi_version() == 1
+
+
+def test_library_has_gfx950_code_object():
+    sections = subprocess.run(["readelf", "-S", T.build_native.LIB], capture_output=True, text=True,
+                              check=True).stdout
+    assert ".hip_fatbin" in sections
+    assert b"amdgcn-amd-amdhsa--gfx950" in open(T.build_native.LIB, "rb").read()
+
+
+def test_oracle_is_not_linked_into_the_product():
+    for so in (T.build_native.LIB, T.build_native.EXT):
+        out = subprocess.run(["ldd", so], capture_output=True, text=True).stdout
+        assert "oracle" not in out
+        assert b"oracle_" not in open(so, "rb").read()
+
+
+def test_scene_bvh_query_needs_no_gpu():
+    nodes, verts, max_stack = T.scene_bvh()
+    assert len(nodes) // 64 == 61 and len(verts) // 9 == 252 and max_stack <= 16
+
+
+def _cfg(**kw):
+    c = T.MpenvConfig(1, 0, 4, 5, 1, 0, 2, 3, 0, 0, T.SCENE.encode(), 0, None, None, None, None, 0)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+@pytest.mark.parametrize("kw,needle", [
+    (dict(exec_mode=0), "CPU"),
+    (dict(task_type=1), "Zone"),
+    (dict(team_size=7), "team"),
+    (dict(num_worlds=0), "world"),
+    (dict(sim_flags=1 << 2), "NavmeshSpawn"),
+    (dict(scene_path=b"/nonexistent"), ""),
+])
+def test_create_rejects_unsupported_configs(kw, needle):
+    lib = T.lib_mpenv()
+    h = C.c_void_p()
+    rc = lib.mpenv_create(C.byref(_cfg(**kw)), C.byref(h))
+    assert rc != 0 and not h.value
+    msg = lib.mpenv_last_error().decode()
+    assert needle.lower() in msg.lower(), msg
+
+
+def test_python_module_surface():
+    import madrona_mp_env as m
+
+    assert m.madrona.ExecMode.CUDA is not None and m.madrona.ExecMode.CPU is not None
+    assert int(m.Task.Zone) == 2
+    flags = m.SimFlags.SpawnInMiddle | m.SimFlags.RandomizeHPMagazine
+    assert int(flags) == 3
+    # every getter src/bindings.cpp:110-158 defines, plus the extensions
+    for name in ("init", "step", "fwd_lidar", "rear_lidar", "hp", "magazine", "alive", "self_obs",
+                 "filters_state", "teammates", "opponents", "opponents_last_known", "self_pos",
+                 "teammate_positions", "opponent_positions", "opponent_last_known_positions",
+                 "opponent_masks", "agent_map", "unmasked_agent_map", "reward_coefs",
+                 "explore_action_tensor", "pvp_action_tensor", "aim_action_tensor", "reward_tensor",
+                 "done_tensor", "reset_tensor", "self_observation_tensor", "jax",
+                 "step_async", "train_interface", "copy_actions", "kernel_timings"):
+        assert hasattr(m.SimManager, name), name
+
+
+def test_python_module_fails_loudly_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import madrona_mp_env as m
+
+    with pytest.raises(Exception) as ei:
+        m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=0, num_worlds=2, rand_seed=5,
+                     auto_reset=True, sim_flags=m.SimFlags.Default, task_type=m.Task.Zone,
+                     team_size=1, num_pbt_policies=0, policy_history_size=0,
+                     scene_path=T.SCENE)
+    assert "device" in str(ei.value).lower() or "hip" in str(ei.value).lower()

@@ -1,0 +1,125 @@
+"""Known-answer tests for the shared Madrona-layer definitions (mpenv_core.h).
+
+The Madrona math/RNG/geo layer is not vendored in the reference (SURVEY.md
+§8c "Third-party arithmetic ... unpinned"), so these pin the build's own
+definitions: Threefry-2x32-20 against the Random123 published KAT vectors,
+the float transcendentals against numpy float64, the correctly-rounded
+div/sqrt bit-exactly against numpy float32, the capsule test against closed
+forms, and the numpy action tape against the C tape.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import mpenv_testlib as T
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return T.lib_oracle()
+
+
+# Random123 kat_vectors, threefry2x32_20 (key, counter) -> output.
+THREEFRY_KAT = [
+    ((0x00000000, 0x00000000), (0x00000000, 0x00000000), (0x6b200159, 0x99ba4efe)),
+    ((0xffffffff, 0xffffffff), (0xffffffff, 0xffffffff), (0x1cb996fc, 0xbb002be7)),
+    ((0x13198a2e, 0x03707344), (0x243f6a88, 0x85a308d3), (0xc4923a9c, 0x483df7a0)),
+]
+
+
+@pytest.mark.parametrize("key,ctr,expect", THREEFRY_KAT)
+def test_threefry_random123_kat(lib, key, ctr, expect):
+    out = (C.c_uint32 * 2)()
+    lib.oracle_threefry(key[0], key[1], ctr[0], ctr[1], out)
+    assert (out[0], out[1]) == expect
+    # numpy restatement used by the bench's action ring agrees
+    a, b = T.mpenv_tape.threefry2x32(np.uint32(key[0]), np.uint32(key[1]),
+                                     np.array([ctr[0]], np.uint32), np.array([ctr[1]], np.uint32))
+    assert (int(a[0]), int(b[0])) == expect
+
+
+def _eval(lib, fn, x, y=None):
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, np.float32)
+    out = np.empty_like(x)
+    lib.oracle_eval_math(fn, T.fptr(x), T.fptr(y), T.fptr(out), len(x))
+    return out
+
+
+def test_sin_cos_accuracy(lib):
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(-10, 10, 20000), rng.uniform(-1e4, 1e4, 2000),
+                        np.array([0.0, -0.0, np.pi / 2, np.pi, 1e-8])]).astype(np.float32)
+    for fn, ref in ((0, np.sin), (1, np.cos)):
+        got = _eval(lib, fn, x).astype(np.float64)
+        err = np.abs(got - ref(x.astype(np.float64)))
+        assert err.max() < 2e-6 * max(1.0, np.abs(x).max() / 1e3), (fn, err.max())
+    assert _eval(lib, 0, np.array([0.0], np.float32))[0] == 0.0
+    assert _eval(lib, 1, np.array([0.0], np.float32))[0] == 1.0
+
+
+def test_atan2_asin_log_accuracy(lib):
+    rng = np.random.default_rng(1)
+    y = rng.uniform(-5, 5, 20000).astype(np.float32)
+    x = rng.uniform(-5, 5, 20000).astype(np.float32)
+    got = _eval(lib, 2, y, x).astype(np.float64)
+    assert np.abs(got - np.arctan2(y.astype(np.float64), x.astype(np.float64))).max() < 1e-6
+    # axis cases
+    ax = _eval(lib, 2, np.array([0, 1, 0, -1], np.float32), np.array([1, 0, -1, 0], np.float32))
+    np.testing.assert_allclose(ax, [0, np.pi / 2, np.pi, -np.pi / 2], rtol=1e-7)
+    u = rng.uniform(-1, 1, 20000).astype(np.float32)
+    got = _eval(lib, 3, u).astype(np.float64)
+    assert np.abs(got - np.arcsin(u.astype(np.float64))).max() < 1e-6
+    p = rng.uniform(1e-6, 1e6, 20000).astype(np.float32)
+    got = _eval(lib, 4, p).astype(np.float64)
+    assert np.abs(got - np.log(p.astype(np.float64))).max() < 2e-6
+
+
+def test_div_sqrt_correctly_rounded(lib):
+    rng = np.random.default_rng(2)
+    a = rng.uniform(-1e3, 1e3, 50000).astype(np.float32)
+    b = rng.uniform(1e-3, 1e3, 50000).astype(np.float32)
+    np.testing.assert_array_equal(_eval(lib, 6, a, b), a / b)
+    s = np.abs(a)
+    np.testing.assert_array_equal(_eval(lib, 5, s), np.sqrt(s))
+
+
+def _capsule(lib, o, d, r, h):
+    o = np.asarray(o, np.float32)
+    d = np.asarray(d, np.float32)
+    return lib.oracle_capsule(T.fptr(o), T.fptr(d), r, h)
+
+
+def test_capsule_known_answers(lib):
+    r, h = 1.5, 2.0
+    # side hit: ray along +x from x=-10 at mid-height -> enters at x=-r
+    assert _capsule(lib, [-10, 0, 1], [1, 0, 0], r, h) == pytest.approx(10 - r, abs=1e-5)
+    # top cap: straight down from z=10 -> hits the top hemisphere at z = h + r
+    assert _capsule(lib, [0, 0, 10], [0, 0, -1], r, h) == pytest.approx(10 - (h + r), abs=1e-5)
+    # bottom cap: straight up from z=-10 -> hits at z = -r
+    assert _capsule(lib, [0, 0, -10], [0, 0, 1], r, h) == pytest.approx(10 - r, abs=1e-5)
+    # miss: passes beside it
+    assert _capsule(lib, [-10, 5, 1], [1, 0, 0], r, h) == 0.0
+    # ray pointing away
+    assert _capsule(lib, [-10, 0, 1], [-1, 0, 0], r, h) == 0.0
+    # origin inside the capsule: defined as no hit
+    assert _capsule(lib, [0, 0, 1], [1, 0, 0], r, h) == 0.0
+
+
+def test_tape_numpy_matches_c(lib):
+    for step in (0, 1, 77, 9999):
+        n = 300
+        out = np.zeros((n, 6), np.int32)
+        lib.oracle_tape_actions(1234, step, 5, n, out.ctypes.data_as(C.POINTER(C.c_int32)))
+        np.testing.assert_array_equal(out, T.mpenv_tape.tape_actions(1234, step, 5, n))
+
+
+def test_tape_distribution():
+    acts = T.mpenv_tape.tape_actions(1234, 3, 0, 200000)
+    assert acts[:, 0].min() == 0 and acts[:, 0].max() == 2
+    assert acts[:, 1].max() == 7 and acts[:, 4].max() == 12 and acts[:, 5].max() == 6
+    fire = np.bincount(acts[:, 2], minlength=3) / len(acts)
+    np.testing.assert_allclose(fire, [0.45, 0.50, 0.05], atol=0.005)
+    stand = np.bincount(acts[:, 3], minlength=3) / len(acts)
+    np.testing.assert_allclose(stand, [0.90, 0.07, 0.03], atol=0.005)

@@ -1,0 +1,200 @@
+"""Engine (gfx950 HIP, through the C ABI) vs the CPU oracle.
+
+Bar: bit-exact for every export — discrete state, and also
+the floats, because both sides compile the same IEEE-exact definitions
+(mpenv_core.h, -ffp-contract=off).  `FLOAT_RTOL` below is the stated ceiling
+the north star allows (1e-5 relative); the tests run with 0 (bit-exact) and
+only fall back to the tolerance where a test says so.
+"""
+import json
+import os
+import glob
+
+import numpy as np
+import pytest
+
+import mpenv_testlib as T
+from golden.make_golden import rollout, step_hashes
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_RTOL = 1e-5  # north_star tolerance; asserted bit-exact (0) below
+ALL = T.STEP_OUTPUTS + T.DEBUG_OUTPUTS
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.json")))
+
+
+def _compare_all(e, o, where):
+    for n in ALL:
+        T.compare(e.get(n), o.get(n), f"{n} @ {where}")
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-5] for p in GOLDEN])
+def test_engine_matches_golden_fixture(path):
+    g = json.load(open(path))
+    case = g["case"]
+    e = T.Engine(case["worlds"], case["team_size"], sim_flags=case["sim_flags"])
+    for k, s in enumerate(rollout(e, case)):
+        got = step_hashes(e)
+        bad = [n for n in got if got[n] != g["hashes"][k][n]]
+        assert not bad, f"step {s}: {bad}"
+    for n, v in g["final"].items():
+        np.testing.assert_array_equal(e.get(n).ravel(), np.asarray(v, np.float32), err_msg=n)
+    e.close()
+
+
+LIVE = [
+    # team_size, worlds, steps, sim_flags, ctrl, policy
+    (1, 64, 300, 0, [0, 1, 1], "tape"),
+    (2, 32, 300, 0, [0, 1, 1], "tape"),
+    (3, 16, 300, 0, [0, 1, 1], "tape"),
+    (6, 16, 300, 0, [0, 1, 1], "tape"),
+    (3, 32, 400, 1 | 2, [0, 1, 1], "combat"),           # middle spawns, random hp/mag
+    (6, 8, 400, 1, [0, 1, 1], "combat"),
+    (2, 16, 300, 1 | 8 | 16, [0, 0, 0], "combat"),      # NoRespawn | StaggerStarts
+    (4, 8, 300, 1 | (1 << 7) | (1 << 10), [1, 0, 1], "combat"),  # RandomFlip | SimEvalMode
+    (5, 8, 300, 1 | (1 << 8), [0, 1, 0], "combat"),     # StaticFlipTeams
+]
+
+
+@pytest.mark.parametrize("ts,worlds,steps,flags,ctrl,policy", LIVE,
+                         ids=[f"{c[0]}v{c[0]}x{c[1]}_f{c[3]}_{c[5]}" for c in LIVE])
+def test_engine_matches_oracle_live(ts, worlds, steps, flags, ctrl, policy):
+    e = T.Engine(worlds, ts, sim_flags=flags)
+    o = T.Oracle(worlds, ts, sim_flags=flags)
+    for sim in (e, o):
+        sim.put_ctrl(ctrl)
+        sim.init()
+    _compare_all(e, o, "init")
+    A = worlds * 2 * ts
+    for s in range(steps):
+        acts = T.combat_actions(o, s) if policy == "combat" else T.mpenv_tape.tape_actions(1234, s, 0, A)
+        e.set_actions(acts)
+        o.set_actions(acts)
+        e.step()
+        o.step()
+        if s % 10 == 0 or s == steps - 1:
+            _compare_all(e, o, f"step {s}")
+        else:
+            for n in ("SELF_OBSERVATION", "REWARD", "DONE", "HP", "DEBUG_AGENT_I32"):
+                T.compare(e.get(n), o.get(n), f"{n} @ step {s}")
+    e.close()
+    o.close()
+
+
+def test_auto_reset_off_and_triggered_resets():
+    """auto_reset=False: episodes end only through the reset tensor
+    (mgr.cpp:2484-2500 triggerReset; sim.cpp resetSystem)."""
+    ts, W = 2, 8
+    e = T.Engine(W, ts, auto_reset=False)
+    o = T.Oracle(W, ts, auto_reset=False)
+    for sim in (e, o):
+        sim.put_ctrl([0, 1, 1])
+        sim.init()
+    A = W * 2 * ts
+    for s in range(200):
+        if s in (5, 77, 150):
+            w = s % W
+            e.trigger_reset(w)
+            o.view("RESET")[w] = 1
+        if s == 40:
+            e.set_hp(1, 0, 7)
+            o.view("HP")[1 * 2 * ts + 0] = 7
+        acts = T.mpenv_tape.tape_actions(1234, s, 0, A)
+        e.set_actions(acts)
+        o.set_actions(acts)
+        e.step()
+        o.step()
+        _compare_all(e, o, f"step {s}")
+
+
+def test_headline_batch_shards_match_oracle():
+    """C3 size (6v6 x 16384 worlds): slices of the engine's batch against
+    oracle runs of the same global worlds (world_id_offset) — bit-exact."""
+    ts, W, steps = 6, 16384, 40
+    N = 2 * ts
+    e = T.Engine(W, ts)
+    e.put_ctrl([0, 1, 1])
+    e.init()
+    probes = [0, 4097, 12345, W - 3]
+    oracles = []
+    for w0 in probes:
+        o = T.Oracle(3, ts, world_id_offset=w0)
+        o.put_ctrl([0, 1, 1])
+        o.init()
+        oracles.append(o)
+    for s in range(steps):
+        e.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, W * N))
+        e.step()
+        for w0, o in zip(probes, oracles):
+            o.set_actions(T.mpenv_tape.tape_actions(1234, s, w0 * N, 3 * N))
+            o.step()
+        if s % 13 == 0 or s == steps - 1:
+            for w0, o in zip(probes, oracles):
+                for n in T.STEP_OUTPUTS:
+                    ptr, dt, shape = e.desc(n)
+                    per_world = shape[0] == W
+                    r0, r1 = (w0, w0 + 3) if per_world else (w0 * N, (w0 + 3) * N)
+                    T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
+    # size-independent properties over the whole batch
+    hp = e.get("HP")
+    assert np.isfinite(e.get("SELF_OBSERVATION")).all()
+    assert ((hp >= 0) & (hp <= 100)).all()
+    lid = e.get("FWD_LIDAR")
+    assert np.isfinite(lid).all()
+
+
+def test_python_module_zero_copy_and_stream_step():
+    """madrona_mp_env.SimManager (bindings.cpp surface): torch views of the
+    engine's buffers, step_async on a torch stream, copy_actions, and the
+    train_interface table — results equal the oracle's."""
+    import torch
+    import madrona_mp_env as m
+
+    ts, W = 3, 8
+    sim = m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=0, num_worlds=W, rand_seed=5,
+                       auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                       team_size=ts, num_pbt_policies=0, policy_history_size=0, scene_path=T.SCENE)
+    o = T.Oracle(W, ts)
+    ctrl = sim.sim_control_tensor().to_torch()
+    ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=ctrl.device).view_as(ctrl))
+    o.put_ctrl([0, 1, 1])
+    sim.init()
+    o.init()
+    obs = sim.self_observation_tensor().to_torch()
+    rew = sim.reward_tensor().to_torch()
+    assert obs.device.type == "cuda" and obs.shape == (W * 2 * ts, 43)
+    A = W * 2 * ts
+    stream = torch.cuda.Stream()
+    ring = torch.from_numpy(np.stack([T.mpenv_tape.tape_actions(1234, s, 0, A) for s in range(50)]))
+    ring = ring.to("cuda")
+    for s in range(50):
+        with torch.cuda.stream(stream):
+            sim.copy_actions(ring[s].data_ptr(), stream.cuda_stream)
+            sim.step_async(stream.cuda_stream)
+        o.set_actions(ring[s].cpu().numpy())
+        o.step()
+        stream.synchronize()
+        np.testing.assert_array_equal(obs.cpu().numpy(), o.get("SELF_OBSERVATION"))
+        np.testing.assert_array_equal(rew.cpu().numpy(), o.get("REWARD"))
+    ti = sim.train_interface()
+    assert set(ti) == {"inputs", "outputs"}
+    assert "rewards" in ti["outputs"] and "discrete" in ti["inputs"]
+    with pytest.raises(Exception):
+        sim.jax(True)
+
+
+def test_kernel_timing_hooks():
+    e = T.Engine(256, 6)
+    assert e.lib.mpenv_enable_kernel_timing(e.h, 1) == 0
+    e.init()
+    for s in range(5):
+        e.step()
+    import ctypes as C
+
+    names = (C.c_char_p * 16)()
+    ms = (C.c_float * 16)()
+    launches = (C.c_int32 * 16)()
+    n = e.lib.mpenv_kernel_timings(e.h, 16, names, ms, launches)
+    got = {names[i].decode(): (ms[i], launches[i]) for i in range(n)}
+    assert set(got) >= {"k_sim", "k_vis", "k_obs", "k_lidar"}
+    assert all(v[1] == 5 and v[0] > 0 for v in got.values())
