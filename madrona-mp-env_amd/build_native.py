@@ -80,6 +80,22 @@ def build_ext(force=False):
     return EXT
 
 
+HEADLESS = os.path.join(PKG, "headless")
+
+
+def build_headless(force=False):
+    """C++ driver over include/mpenv_manager.hpp (reference src/headless.cpp role)."""
+    src = os.path.join(CSRC, "headless.cpp")
+    deps = [src, LIB, os.path.join(INCLUDE, "mpenv.h"), os.path.join(INCLUDE, "mpenv_manager.hpp"),
+            os.path.join(CSRC, "mpenv_core.h")]
+    if not force and not _stale(HEADLESS, deps):
+        return HEADLESS
+    _run([HIPCC, "-x", "c++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+          f"-I{INCLUDE}", f"-I{CSRC}", src, "-o", HEADLESS, f"-L{PKG}", "-lmpenv",
+          "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
+    return HEADLESS
+
+
 def build_oracle(force=False):
     src = os.path.join(ORACLE, "oracle.cpp")
     deps = [src, os.path.join(ORACLE, "oracle.h"), os.path.join(CSRC, "mpenv_core.h"),
@@ -96,6 +112,7 @@ def build_oracle(force=False):
 def build_all(force=False):
     build_lib(force)
     build_ext(force)
+    build_headless(force)
     build_oracle(force)
 
 

@@ -112,3 +112,16 @@ def test_python_module_fails_loudly_without_gpu():
                      team_size=1, num_pbt_policies=0, policy_history_size=0,
                      scene_path=T.SCENE)
     assert "device" in str(ei.value).lower() or "hip" in str(ei.value).lower()
+
+
+def test_cpp_manager_headless_builds_and_fails_loudly_without_gpu():
+    """include/mpenv_manager.hpp (the mgr.hpp Manager class) compiles into the
+    headless driver; without a device it exits non-zero with a message."""
+    import torch
+
+    exe = T.build_native.HEADLESS
+    assert os.path.exists(exe)
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    r = subprocess.run([exe, "CUDA", "2", "1", T.SCENE], capture_output=True, text=True)
+    assert r.returncode != 0 and "device" in r.stderr.lower()

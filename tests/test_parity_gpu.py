@@ -198,3 +198,64 @@ def test_kernel_timing_hooks():
     got = {names[i].decode(): (ms[i], launches[i]) for i in range(n)}
     assert set(got) >= {"k_sim", "k_vis", "k_obs", "k_lidar"}
     assert all(v[1] == 5 and v[0] > 0 for v in got.values())
+
+
+def test_cpp_manager_headless_runs():
+    """The C++ Manager wrapper (include/mpenv_manager.hpp) drives the engine."""
+    import subprocess
+
+    r = subprocess.run([T.build_native.HEADLESS, "CUDA", "256", "50", T.SCENE, "--rand-actions"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "FPS" in r.stdout and float(r.stdout.split("FPS")[1].split()[0]) > 0
+
+
+def test_gpu_stream_step_buffers_abi():
+    """Manager::gpuStreamInit/gpuStreamStep (mgr.cpp:507-645): a flat
+    buffer array of TrainInterface inputs then outputs, caller-owned, on the
+    caller's stream — the XLA custom-call ABI scripts/jax_train.py uses."""
+    import ctypes as C
+    import torch
+
+    ts, W = 2, 16
+    A = W * 2 * ts
+    lib = T.lib_mpenv()
+    lib.mpenv_gpu_stream_init.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]
+    lib.mpenv_gpu_stream_step.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]
+    lib.mpenv_train_interface_entry.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_char_p),
+                                                C.POINTER(C.c_int32)]
+    e = T.Engine(W, ts)
+    o = T.Oracle(W, ts)
+    ni, no = C.c_int32(), C.c_int32()
+    assert lib.mpenv_train_interface_size(C.byref(ni), C.byref(no)) == 0
+    names, bufs = [], []
+    inv = {v: k for k, v in T.EXPORT.items()}
+    for io, n in ((0, ni.value), (1, no.value)):
+        for k in range(n):
+            nm, eid = C.c_char_p(), C.c_int32()
+            assert lib.mpenv_train_interface_entry(io, k, C.byref(nm), C.byref(eid)) == 0
+            _, dt, shape = e.desc(inv[eid.value])
+            tdt = {np.int32: torch.int32, np.float32: torch.float32}[dt]
+            names.append((io, nm.value.decode(), inv[eid.value]))
+            bufs.append(torch.zeros(shape, dtype=tdt, device="cuda"))
+    arr = (C.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+    idx = {nm: i for i, (io, nm, _) in enumerate(names)}
+    bufs[idx["simCtrl"]].copy_(torch.tensor([0, 1, 1], dtype=torch.int32).view_as(bufs[idx["simCtrl"]]))
+    o.put_ctrl([0, 1, 1])
+    stream = torch.cuda.Stream()
+    e.put_ctrl([0, 1, 1])
+    assert lib.mpenv_gpu_stream_init(e.h, C.c_void_p(stream.cuda_stream), arr) == 0
+    o.init()
+    stream.synchronize()
+    for s in range(40):
+        acts = T.mpenv_tape.tape_actions(1234, s, 0, A)
+        bufs[idx["discrete"]].copy_(torch.from_numpy(acts[:, :4].copy()).view_as(bufs[idx["discrete"]]))
+        bufs[idx["aim"]].copy_(torch.from_numpy(acts[:, 4:6].copy()).view_as(bufs[idx["aim"]]))
+        torch.cuda.synchronize()
+        assert lib.mpenv_gpu_stream_step(e.h, C.c_void_p(stream.cuda_stream), arr) == 0
+        o.set_actions(acts)
+        o.step()
+        stream.synchronize()
+        for (io, nm, ename), b in zip(names, bufs):
+            if io == 1:
+                np.testing.assert_array_equal(b.cpu().numpy(), o.get(ename), err_msg=f"{nm} @ {s}")

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Profiles the default bench workload on the GPU box (run under gpurun).
+#   1. rocprofv3 --kernel-trace --stats      -> per-kernel durations
+#   2. rocprofv3 --pmc FETCH_SIZE (own pass) -> HBM read bytes per dispatch
+#   3. rocprofv3 --pmc WRITE_SIZE (own pass) -> HBM write bytes per dispatch
+# Outputs under gpurun_out/prof_<tag>/; tools/pmc_summary.py condenses them.
+set -e
+TAG=${1:-r01}
+STEPS=${STEPS:-200}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+    python3 bench.py --steps $STEPS --warmup 20 --cpu-baseline off > $OUT/trace_bench.json
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- \
+    python3 bench.py --steps 50 --warmup 10 --cpu-baseline off > $OUT/fetch_bench.json
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- \
+    python3 bench.py --steps 50 --warmup 10 --cpu-baseline off > $OUT/write_bench.json
+find $OUT -name "*.csv" | head -50
