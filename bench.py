@@ -40,19 +40,21 @@ TAPE_SEED = 1234
 
 # Algorithmic HBM bytes per agent-step for each kernel: the
 # unique bytes the kernel must read or write, no re-reads counted.
-#   k_sim  : actions 24 r; agent SoA state 40 cols x 4 B r+w (320); DamageDealt
-#            6 x 4 r+w (48); hp/alive/magazine r+w (32); reward+done w (8);
-#            1 explore cell r+w (8); canSee r (8)                 = 448
-#   k_vis  : pos 12 + aim rot 16 + pose 4 + alive 4 r; canSee w 6  = 42
+#   k_move : actions 24 r; 20 movement columns (pos, vel, rot, aim yaw/pitch/
+#            quat, pose x3, maxVel, aim velocities) x 4 B r+w (160)  = 184
+#   k_sim  : 20 combat/bookkeeping columns r+w (160); pos/rot/alive r (32);
+#            DamageDealt 6 x 4 r+w (48); hp/magazine r+w (24); reward+done
+#            w (8); 1 explore cell r+w (8); rewardCoefs r (4)      = 284
+#   k_vis  : pos 12 + aim rot 16 + pose 4 + alive 4 r; mask w 1   = 37
 #   k_obs  : state r ~104; self 172 + teammates 640 + opponents 768 +
 #            last-known 768 w, last-known 768 r; positions 12+60+72 w,
-#            last-known pos 72 r+w (144); masks 24 + filters 4 w; canSee 8 r
-#                                                                  = 3540
+#            last-known pos 72 r+w (144); masks 24 + filters 4 w; vis 1 r
+#                                                                  = 3533
 #   k_lidar: pos 12 + rot 16 + aim rot 16 + pose 4 r; 80 rays x 16 B w
 #                                                                  = 1328
 # plus per world-step: 32 singleton columns x 4 B r+w (256) in k_sim.
-KERNEL_BYTES_PER_AGENT = {"k_sim": 448, "k_vis": 42, "k_obs": 3540, "k_lidar": 1328}
-KERNEL_BYTES_PER_WORLD = {"k_sim": 256, "k_vis": 0, "k_obs": 0, "k_lidar": 0}
+KERNEL_BYTES_PER_AGENT = {"k_move": 184, "k_sim": 284, "k_vis": 37, "k_obs": 3533, "k_lidar": 1328}
+KERNEL_BYTES_PER_WORLD = {"k_move": 0, "k_sim": 256, "k_vis": 0, "k_obs": 0, "k_lidar": 0}
 
 
 def parse():

@@ -246,6 +246,13 @@ int mpenv_train_interface_entry(int32_t is_output, int32_t idx,
  * 2 discrete-aim actions per agent), asynchronous on hip_stream. */
 int mpenv_copy_actions(mpenv_manager *mgr, const int32_t *src_device, void *hip_stream);
 
+/* Test hook (no reference counterpart): closest-hit BVH queries
+ * (MeshBVH::traceRay, mesh_bvh.inl:110-208) for n caller rays in device
+ * memory (o, d: [n][3] f32).  mode 0 = the traversal inlined in the step
+ * kernels, 1 = an out-of-line copy.  Outputs t (0 on miss) and hit. */
+int mpenv_debug_trace_rays(mpenv_manager *mgr, const float *o_device, const float *d_device, int32_t n,
+                           int32_t mode, float *t_device, int32_t *hit_device, void *hip_stream);
+
 /* Manager::triggerReset (mgr.cpp:2484-2500) */
 int mpenv_trigger_reset(mpenv_manager *mgr, int32_t world_idx);
 /* Manager::setPvPAction (mgr.cpp:2518-2566) */

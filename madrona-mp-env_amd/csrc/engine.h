@@ -75,7 +75,7 @@ struct DevState {
 #undef MP_DECL_I
 
     float *dmg;            // [6][A] DamageDealt
-    uint8_t *canSee;       // [A][6] OpponentsVisibility
+    uint8_t *visMask;      // [A] OpponentsVisibility, bit k = sees opponent k
     uint32_t *visited;     // [A][81*81] ExploreTracker
     int32_t *filtLast;     // [W][2][3] FiltersMatchState::lastMatches (3 filters used)
     int32_t *zoneStats;    // [W][5][5]
@@ -158,17 +158,20 @@ struct LaunchCtx {
     int timing;         // record events when nonzero
 };
 
-enum KernelId { kKSim = 0, kKVis = 1, kKObs = 2, kKLidar = 3, kNumTimedKernels = 4 };
+enum KernelId { kKMove = 0, kKSim = 1, kKVis = 2, kKObs = 3, kKLidar = 4, kNumTimedKernels = 5 };
 
 const char *kernelName(int k);
 size_t bvhLdsBytes(const SceneDev &sc);
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t ctor_train_ctrl[3], void *stream);
 int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream);
+int launchMove(const DevState &s, const SceneDev &sc, void *stream);
 int launchSimStep(const DevState &s, const SceneDev &sc, void *stream);
 int launchVisibility(const DevState &s, const SceneDev &sc, void *stream);
 int launchObservations(const DevState &s, const SceneDev &sc, void *stream);
 int launchLidar(const DevState &s, const SceneDev &sc, void *stream);
+int launchTraceRays(const SceneDev &sc, const float *o, const float *d, int n, int mode, float *t, int32_t *hit,
+                    void *stream);
 int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, float *wf, uint32_t *explore,
                       float *crumbs, void *stream);
 int launchFillActions(const DevState &s, const int32_t *src6, void *stream);

@@ -212,6 +212,18 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     return ray_hit;
 }
 
+// Out-of-line traversal for the ray-query test hook.
+struct RayHitD {
+    float t;
+    int hit;
+};
+__device__ __noinline__ RayHitD bvhTraceRayExactD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d)
+{
+    RayHitD r;
+    r.hit = bvhTraceRayD(b, ray_o, ray_d, r.t) ? 1 : 0;
+    return r;
+}
+
 // mesh_bvh.inl:817-855
 __device__ __forceinline__ bool sphereNodeCheckD(mp::Vec3 o, mp::Vec3 inv_d, float t_max, float r, mp::AABB aabb)
 {
@@ -405,10 +417,19 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     bool hit = bvhTraceRayD(b, org, d, tb);
     if (hit) min_t = tb;
     int ent = -1;
+    // Conservative cull: every point of a Z-capsule lies within r of its
+    // vertical axis, so a ray whose xy line passes farther than r from the
+    // axis cannot hit it and the exact test would return 0.  The 1% radius
+    // margin dwarfs the rounding of the cross product for |org - axis| up to
+    // ~60k units (world bounds are ~5.7k), so no hit is ever culled.
+    const float dxy2 = d.x * d.x + d.y * d.y;
+    const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
     for (int j = 0; j < N; j++) {
         Vec3 co = v3(px[g0 + j], py[g0 + j], pz[g0 + j]);
         co.z += kCapsuleRadius;
         Vec3 tr = org - co;
+        const float cr = tr.x * d.y - tr.y * d.x;
+        if (cr * cr > cull_r2 * dxy2) continue;
         float t = intersectRayZOriginCapsule(tr, d, kCapsuleRadius, kCapsuleSegment);
         if (t != 0 && t < min_t) {
             min_t = t;

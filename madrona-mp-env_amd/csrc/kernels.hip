@@ -1240,12 +1240,35 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 
 // The Step graph up to and including resetSystem, one workgroup per tile of
 // floor(256 / N) worlds, one lane per agent.
-__global__ void __launch_bounds__(kBlock) k_sim(DevState S, SceneDev sc)
+// Step graph part 1 (sim.cpp:5299-5320 up to updateMoveStatePostFall): the
+// per-agent systems, which read no other agent's state.  Lane = agent, no
+// barriers, so sphere-cast latency overlaps across the whole grid.
+__global__ void __launch_bounds__(kBlock) k_move(DevState S, SceneDev sc)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const LBVH bvh = stageBVH(smem, sc);
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= S.A) return;
+    // planAStarAISystem (sim.cpp:5041-5172) acts only for AgentPolicy == -1
+    // (bots) and is not part of round 1.
+    applyBotActionsD(S, g);
+    pvpMovementD(S, g);
+    pvpAimD(S, g);
+    applyVelocityD(S, bvh, g);
+    fallD(S, bvh, g);
+}
+
+// Step graph part 2 (fireSystem onward): per-world phases.  A workgroup
+// holds floor(kSimBlock / N) whole worlds, lane = agent, phases separated
+// by workgroup barriers.
+constexpr int kSimBlock = 128;
+
+__global__ void __launch_bounds__(kSimBlock) k_sim(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const LBVH bvh = stageBVH(smem, sc);
     const int N = S.N;
-    const int wpb = kBlock / N;
+    const int wpb = kSimBlock / N;
     const int wl = threadIdx.x / N;
     const int i = threadIdx.x - wl * N;
     const int w = blockIdx.x * wpb + wl;
@@ -1253,16 +1276,6 @@ __global__ void __launch_bounds__(kBlock) k_sim(DevState S, SceneDev sc)
     const bool wlane = act && i == 0;
     const int64_t g = (int64_t)w * N + i;
 
-    if (act) {
-        // planAStarAISystem (sim.cpp:5041-5172) acts only for AgentPolicy == -1
-        // (bots) and is not part of round 1.
-        applyBotActionsD(S, g);
-        pvpMovementD(S, g);
-        pvpAimD(S, g);
-        applyVelocityD(S, bvh, g);
-        fallD(S, bvh, g);
-    }
-    __syncthreads();
     if (act) fireD(S, bvh, w, i);
     __syncthreads();
     if (act) applyDmgD(S, g);
@@ -1327,53 +1340,60 @@ __device__ __forceinline__ bool inFrustumD(const SceneDev &sc, Vec3 vp)
     return in;
 }
 
-// opponentsWriteVisibilitySystem (sim.cpp:2526-2560) with isAgentVisible
-// (utils.cpp:186-271).  Lane = (agent, opponent slot); the four sample
-// points stop at the first visible one (the reference tests all four but
-// only the boolean is consumed).
+// opponentsWriteVisibilitySystem (sim.cpp:2526-2560) + isAgentVisible
+// (utils.cpp:169-271).  Lane = (agent, opponent k); each 64-lane wave holds
+// whole agents (floor(64 / T) of them), so the per-agent visibility bits are
+// gathered with one wave ballot and written as a single byte per agent.
 __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const LBVH bvh = stageBVH(smem, sc);
     const int T = S.T, N = S.N;
-    const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (lane >= S.A * T) return;
-    const int64_t g = lane / T;
-    const int k = (int)(lane - g * T);
-    const int w = (int)(g / N);
-    const int i = (int)(g - (int64_t)w * N);
-    const int64_t g0 = (int64_t)w * N;
-    const int team = i / T;
-    const int target = (team ^ 1) * T + k;
-    const int64_t gt = g0 + target;
+    const int apw = 64 / T; // agents per wave
+    const int wl = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t g = wave * apw + wl / T;
+    const int k = wl % T;
+    const bool valid = wl < apw * T && g < S.A;
     bool vis = false;
-    if (S.alive[g] != 0.f && S.alive[gt] != 0.f) {
-        Vec3 org = ldPos(S, g);
-        org.z += viewHeightD(S.curPose[g]);
-        const Quat aim_rot = ldAimRot(S, g);
-        const Quat inv_rot = qinv(aim_rot);
-        const Vec3 base = ldPos(S, gt);
-        const float vh = viewHeightD(S.curPose[gt]);
-        const Vec3 aim_right = rotateVec(aim_rot, kRight);
-        const Vec3 delta_right = aim_right * 0.9f * c::kAgentRadius;
-        Vec3 pts[4];
-        pts[0] = base; pts[0].z += c::kAgentRadius;             // bottom
-        pts[1] = base; pts[1].z += vh;                          // top
-        pts[2] = base; pts[2].z += vh; pts[2] = pts[2] - delta_right; // left
-        pts[3] = base; pts[3].z += vh; pts[3] = pts[3] + delta_right; // right
-        for (int p = 0; p < 4 && !vis; p++) {
-            Vec3 to_test = pts[p] - org;
-            Vec3 view = rotateVec(inv_rot, to_test);
-            if (view.y <= 0.f) continue;
-            if (!inFrustumD(sc, view)) continue;
-            float len = length(to_test);
-            if (len < c::kAgentRadius) continue;
-            to_test = to_test / len;
-            WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, org, to_test);
-            if (h.hit && h.entity == target) vis = true;
+    if (valid) {
+        const int w = (int)(g / N);
+        const int i = (int)(g - (int64_t)w * N);
+        const int64_t g0 = (int64_t)w * N;
+        const int team = i / T;
+        const int target = (team ^ 1) * T + k;
+        const int64_t gt = g0 + target;
+        if (S.alive[g] != 0.f && S.alive[gt] != 0.f) {
+            Vec3 org = ldPos(S, g);
+            org.z += viewHeightD(S.curPose[g]);
+            const Quat aim_rot = ldAimRot(S, g);
+            const Quat inv_rot = qinv(aim_rot);
+            const Vec3 base = ldPos(S, gt);
+            const float vh = viewHeightD(S.curPose[gt]);
+            const Vec3 aim_right = rotateVec(aim_rot, kRight);
+            const Vec3 delta_right = aim_right * 0.9f * c::kAgentRadius;
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                if (vis) break;
+                // bottom, top, left, right sample points (utils.cpp:188-200)
+                Vec3 pt = base;
+                pt.z += p == 0 ? c::kAgentRadius : vh;
+                if (p == 2) pt = pt - delta_right;
+                if (p == 3) pt = pt + delta_right;
+                Vec3 to_test = pt - org;
+                Vec3 view = rotateVec(inv_rot, to_test);
+                if (view.y <= 0.f) continue;
+                if (!inFrustumD(sc, view)) continue;
+                float len = length(to_test);
+                if (len < c::kAgentRadius) continue;
+                to_test = to_test / len;
+                WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, org, to_test);
+                if (h.hit && h.entity == target) vis = true;
+            }
         }
     }
-    reinterpret_cast<uint8_t *>(S.canSee)[g * kMaxTeamSize + k] = vis ? 1 : 0;
+    const uint64_t bits = __ballot(vis);
+    if (valid && k == 0) S.visMask[g] = (uint8_t)((bits >> wl) & ((1u << T) - 1u));
 }
 
 __device__ __forceinline__ Vec3 normalizedPosD(const SceneDev &sc, Vec3 p) // sim.cpp:2693-2718
@@ -1475,7 +1495,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
     const int i = (int)(g - (int64_t)w * N);
     const int64_t g0 = (int64_t)w * N;
     const int team = i / T, off = i - team * T;
-    const uint8_t *cansee = reinterpret_cast<const uint8_t *>(S.canSee);
+    const uint8_t *vm = S.visMask;
     const bool self_alive = S.alive[g] != 0.f;
 
     // ---- masks
@@ -1485,10 +1505,10 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
         if (!self_alive || k >= T) continue;
         const int64_t go = g0 + (team ^ 1) * T + k;
         if (S.alive[go] == 0.f) continue;
-        bool can_see = cansee[g * kMaxTeamSize + k] != 0;
+        bool can_see = (vm[g] >> k) & 1;
         for (int t = 0; t < T - 1 && !can_see; t++) {
             const int64_t gt = g0 + team * T + (t < off ? t : t + 1);
-            if (cansee[gt * kMaxTeamSize + k]) can_see = true;
+            if ((vm[gt] >> k) & 1) can_see = true;
         }
         if (can_see) mask[k] = 1.f;
         if (S.firedT[go] >= 0) mask[k] = 1.f;
@@ -1573,7 +1593,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
                 }
                 oob[28] = (float)S.wasShot[gj];
                 oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
-                oob[30] = cansee[g * kMaxTeamSize + k] ? 1.f : 0.f;
+                oob[30] = ((vm[g] >> k) & 1) ? 1.f : 0.f;
                 const bool knows = mask[k] == 1.f;
                 oob[31] = knows ? 1.f : 0.f;
                 if (knows) {
@@ -1594,7 +1614,20 @@ constexpr int kLidarIters = 8;
 __global__ void __launch_bounds__(kBlock) k_lidar(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const LBVH bvh = stageBVH(smem, sc);
+    // Ray-fan directions (sim.cpp:3324-3506): theta depends only on the ray
+    // slot, so the 32 forward + 8 rear (-cos, sin) pairs are computed once
+    // per workgroup with the same sinf_/cosf_ and read from LDS.
+    __shared__ float2 fan[32 + 8];
+    if (threadIdx.x < 40) {
+        const bool fwd = threadIdx.x < 32;
+        const int x = fwd ? threadIdx.x : threadIdx.x - 32;
+        const int width = fwd ? 32 : 8;
+        const float range = fwd ? 0.75f * kPi : -kPi;
+        const float offset = fwd ? 0.5f * (1.f - 0.75f) * kPi : 0.f;
+        const float theta = range * (float(x) / float(width - 1)) + offset;
+        fan[threadIdx.x] = make_float2(-cosf_(theta), sinf_(theta));
+    }
+    const LBVH bvh = stageBVH(smem, sc); // ends with __syncthreads
     const int N = S.N, T = S.T;
     const int64_t total = S.A * kLidarRays;
     const int64_t base = (int64_t)blockIdx.x * (kBlock * kLidarIters);
@@ -1616,12 +1649,8 @@ __global__ void __launch_bounds__(kBlock) k_lidar(DevState S, SceneDev sc)
         const float top = viewHeightD(S.curPose[g]) + c::kAgentRadius;
         Vec3 ray_o = ldPos(S, g);
         ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
-        const float range = fwd ? 0.75f * kPi : -kPi;
-        const float offset = fwd ? 0.5f * (1.f - 0.75f) * kPi : 0.f;
-        float theta = range * (float(x) / float(width - 1)) + offset;
-        float dx = -cosf_(theta);
-        float dy = sinf_(theta);
-        Vec3 dir = normalize(dx * dir_right + dy * dir_fwd);
+        const float2 cs = fan[fwd ? x : 32 + x];
+        Vec3 dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
         WorldHit hw = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, ray_o, dir);
         float4 out;
         if (hw.hit) {
@@ -1635,6 +1664,41 @@ __global__ void __launch_bounds__(kBlock) k_lidar(DevState S, SceneDev sc)
                           : reinterpret_cast<float4 *>(S.rearLidar) + g * kRearRays + kk;
         *dst = out;
     }
+}
+
+static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
+
+// Debug/test hook: closest-hit BVH queries for caller rays (mode 0 = the
+// traversal inlined into the step kernels, 1 = its out-of-line copy).
+__global__ void __launch_bounds__(kBlock) k_trace_rays(SceneDev sc, const float *o, const float *d, int n, int mode,
+                                                       float *t_out, int32_t *hit_out)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const LBVH bvh = stageBVH(smem, sc);
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const Vec3 org = v3(o[3 * r], o[3 * r + 1], o[3 * r + 2]);
+    const Vec3 dir = v3(d[3 * r], d[3 * r + 1], d[3 * r + 2]);
+    float t = 0.f;
+    bool hit;
+    if (mode == 0) {
+        hit = bvhTraceRayD(bvh, org, dir, t); // inlined, as in the step kernels
+    } else {
+        RayHitD h = bvhTraceRayExactD(bvh, org, dir);
+        hit = h.hit != 0;
+        t = h.t;
+    }
+    t_out[r] = hit ? t : 0.f;
+    hit_out[r] = hit ? 1 : 0;
+}
+
+int launchTraceRays(const SceneDev &sc, const float *o, const float *d, int n, int mode, float *t, int32_t *hit,
+                    void *stream)
+{
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_trace_rays, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), bvhLdsBytes(sc),
+                       (hipStream_t)stream, sc, o, d, n, mode, t, hit);
+    return check(hipGetLastError());
 }
 
 // Debug gather of internal state into the MPENV_EXPORT_DEBUG_* layouts.
@@ -1658,10 +1722,7 @@ __global__ void __launch_bounds__(256) k_debug(DevState S, float *af, int32_t *a
         n[6] = S.landedOn[g]; n[7] = S.respawnSteps[g]; n[8] = S.autohealSteps[g];
         n[9] = S.flags[g] & 31;
         n[10] = S.wasShot[g]; n[11] = S.weapon[g]; n[12] = S.bcLast[g]; n[13] = S.bcSteps[g];
-        const uint8_t *cs = reinterpret_cast<const uint8_t *>(S.canSee) + g * kMaxTeamSize;
-        int m = 0;
-        for (int k = 0; k < kMaxTeamSize; k++) m |= cs[k] ? (1 << k) : 0;
-        n[14] = m;
+        n[14] = S.visMask[g];
         n[15] = S.newCells[g];
         if (explore) {
             for (int k = 0; k < kGridCells; k++) explore[g * kGridCells + k] = S.visited[g * kGridCells + k];
@@ -1711,13 +1772,12 @@ __global__ void __launch_bounds__(256) k_fill_actions(DevState S, const int32_t 
 // ============================================================ host side
 const char *kernelName(int k)
 {
-    static const char *names[kNumTimedKernels] = { "k_sim", "k_vis", "k_obs", "k_lidar" };
+    static const char *names[kNumTimedKernels] = { "k_move", "k_sim", "k_vis", "k_obs", "k_lidar" };
     return (k >= 0 && k < kNumTimedKernels) ? names[k] : "?";
 }
 
 size_t bvhLdsBytes(const SceneDev &sc) { return (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 12; }
 
-static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
 {
@@ -1736,18 +1796,25 @@ int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream)
     return check(hipGetLastError());
 }
 
+int launchMove(const DevState &s, const SceneDev &sc, void *stream)
+{
+    hipLaunchKernelGGL(k_move, dim3((unsigned)((s.A + kBlock - 1) / kBlock)), dim3(kBlock), bvhLdsBytes(sc),
+                       (hipStream_t)stream, s, sc);
+    return check(hipGetLastError());
+}
+
 int launchSimStep(const DevState &s, const SceneDev &sc, void *stream)
 {
-    const int wpb = kBlock / s.N;
+    const int wpb = kSimBlock / s.N;
     const int blocks = (s.W + wpb - 1) / wpb;
-    hipLaunchKernelGGL(k_sim, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
+    hipLaunchKernelGGL(k_sim, dim3(blocks), dim3(kSimBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }
 
 int launchVisibility(const DevState &s, const SceneDev &sc, void *stream)
 {
-    const int64_t lanes = s.A * s.T;
-    const int blocks = (int)((lanes + kBlock - 1) / kBlock);
+    const int64_t waves = (s.A + (64 / s.T) - 1) / (64 / s.T);
+    const int blocks = (int)((waves * 64 + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_vis, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }

@@ -157,6 +157,8 @@ struct mpenv_manager {
     void runStep(hipStream_t st)
     {
         record(st);
+        if (launchMove(S, sc, st)) throw std::runtime_error("k_move launch failed");
+        record(st);
         if (launchSimStep(S, sc, st)) throw std::runtime_error("k_sim launch failed");
         record(st);
         if (launchVisibility(S, sc, st)) throw std::runtime_error("k_vis launch failed");
@@ -252,7 +254,8 @@ static void buildSceneDev(mpenv_manager &m)
     SceneDev &sc = m.sc;
     std::memset(&sc, 0, sizeof(sc));
     if (s.nodes.size() > 256) throw std::runtime_error("BVH has more than 256 nodes (byte-stack limit)");
-    if (s.maxStack > kMaxBVHStack) throw std::runtime_error("BVH too deep for the 16-entry register stack");
+    if (s.maxStack > kMaxBVHStack || s.maxStackAnyOrder > kMaxBVHStack)
+        throw std::runtime_error("BVH too deep for the 16-entry register stack");
     if (s.zoneAABBs.empty() || s.zoneAABBs.size() > (size_t)kMaxZones) throw std::runtime_error("bad zone count");
     if (s.numDefaultASpawns == 0 || s.numDefaultBSpawns == 0) throw std::runtime_error("scene needs A and B spawns");
     if ((m.cfg.sim_flags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) &&
@@ -338,7 +341,7 @@ static void allocState(mpenv_manager &m)
 #undef MP_ALLOC_WI
 #undef MP_ALLOC_WF
     S.dmg = m.alloc<float>(A * kMaxTeamSize);
-    S.canSee = m.alloc<uint8_t>(A * kMaxTeamSize);
+    S.visMask = m.alloc<uint8_t>(A);
     S.visited = m.alloc<uint32_t>(A * kGridCells);
     S.filtLast = m.alloc<int32_t>(W * 6);
     S.zoneStats = m.alloc<int32_t>(W * 25);
@@ -569,6 +572,16 @@ int mpenv_gpu_stream_step(mpenv_manager *m, void *stream, void **buffers)
     return MPENV_OK;
 }
 
+int mpenv_debug_trace_rays(mpenv_manager *m, const float *o, const float *d, int32_t n, int32_t mode, float *t_out,
+                           int32_t *hit_out, void *stream)
+{
+    if (!m || !o || !d || !t_out || !hit_out || n < 0) return fail(MPENV_ERR_INVALID, "bad argument");
+    hipStream_t st = stream ? (hipStream_t)stream : m->stream;
+    if (launchTraceRays(m->sc, o, d, n, mode, t_out, hit_out, st) || hipStreamSynchronize(st) != hipSuccess)
+        return fail(MPENV_ERR_HIP, "trace-ray launch failed");
+    return MPENV_OK;
+}
+
 int mpenv_copy_actions(mpenv_manager *m, const int32_t *src, void *stream)
 {
     if (!m || !src) return fail(MPENV_ERR_INVALID, "null argument");
@@ -708,7 +721,7 @@ int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes,
                 std::memcpy(verts_out, s.bvhVerts.data(), s.bvhVerts.size() * 12);
             *num_verts = (int32_t)s.bvhVerts.size();
         }
-        if (max_stack) *max_stack = s.maxStack;
+        if (max_stack) *max_stack = std::max(s.maxStack, s.maxStackAnyOrder);
     } catch (const std::exception &e) {
         return fail(MPENV_ERR_IO, e.what());
     }

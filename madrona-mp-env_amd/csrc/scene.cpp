@@ -331,6 +331,20 @@ void buildBVH(const std::vector<Vec3> &tri_verts, Scene &out)
         occ[oid] = std::max(k, best);
     }
     out.maxStack = std::max(1, occ[0]);
+    // Worst case over every push order (the front-to-back traversal pushes in
+    // t_near order): the first-popped child can sit on all k-1 siblings.
+    std::vector<int> occ_any(num_inner, 0);
+    for (int oid = num_inner - 1; oid >= 0; oid--) {
+        const BVHNode &n = out.nodes[oid];
+        int k = 0, deepest = 0;
+        for (int i = 0; i < 4; i++) {
+            if (n.children[i] == -1 || (n.children[i] & 0x80000000)) continue;
+            deepest = std::max(deepest, occ_any[n.children[i]]);
+            k++;
+        }
+        occ_any[oid] = k == 0 ? 0 : std::max(k, (k - 1) + deepest);
+    }
+    out.maxStackAnyOrder = std::max(1, occ_any[0]);
 }
 
 Scene loadScene(const std::string &dir, bool spawn_in_middle)

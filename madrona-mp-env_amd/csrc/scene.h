@@ -66,7 +66,8 @@ struct Scene {
     mp::AABB rootAABB;
     int32_t numLeaves = 0;
     int32_t maxDepth = 0;      // deepest inner-node level (root = 1)
-    int32_t maxStack = 0;      // bound on traversal stack occupancy
+    int32_t maxStack = 0;      // bound on traversal stack occupancy (reference order)
+    int32_t maxStackAnyOrder = 0; // bound for any child push order
 
     std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
     uint32_t numDefaultASpawns = 0, numDefaultBSpawns = 0;

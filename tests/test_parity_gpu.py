@@ -196,7 +196,7 @@ def test_kernel_timing_hooks():
     launches = (C.c_int32 * 16)()
     n = e.lib.mpenv_kernel_timings(e.h, 16, names, ms, launches)
     got = {names[i].decode(): (ms[i], launches[i]) for i in range(n)}
-    assert set(got) >= {"k_sim", "k_vis", "k_obs", "k_lidar"}
+    assert set(got) >= {"k_move", "k_sim", "k_vis", "k_obs", "k_lidar"}
     assert all(v[1] == 5 and v[0] > 0 for v in got.values())
 
 
@@ -259,3 +259,61 @@ def test_gpu_stream_step_buffers_abi():
         for (io, nm, ename), b in zip(names, bufs):
             if io == 1:
                 np.testing.assert_array_equal(b.cpu().numpy(), o.get(ename), err_msg=f"{nm} @ {s}")
+
+
+def _edge_aimed_rays(verts, n_origins, seed):
+    """Rays aimed exactly at every triangle vertex and edge midpoint (shared
+    edges/vertices are where two triangles tie) from random origins."""
+    rng = np.random.default_rng(seed)
+    tris = verts.reshape(-1, 3, 3).astype(np.float64)
+    targets = np.concatenate([tris.reshape(-1, 3),
+                              0.5 * (tris[:, 0] + tris[:, 1]), 0.5 * (tris[:, 1] + tris[:, 2]),
+                              0.5 * (tris[:, 2] + tris[:, 0])])
+    o = rng.uniform([-1500, -1500, -50], [1500, 1500, 300], (n_origins, 3))
+    oo = np.repeat(o, len(targets), axis=0)
+    tt = np.tile(targets, (n_origins, 1))
+    d = tt - oo
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return oo.astype(np.float32), d.astype(np.float32)
+
+
+def test_bvh_traversal_matches_oracle_on_edge_cases():
+    """GPU closest-hit traversal (inlined and out-of-line) vs the oracle's
+    restatement of MeshBVH::traceRay, on random rays and on rays aimed
+    exactly at shared edges/vertices (where triangles tie)."""
+    import ctypes as C
+    import torch
+
+    lib = T.lib_mpenv()
+    lib.mpenv_debug_trace_rays.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]
+    e = T.Engine(1, 1)
+    o = T.Oracle(1, 1)
+    nodes, verts, _ = T.scene_bvh()
+    rng = np.random.default_rng(11)
+    ro = rng.uniform([-2000, -2000, -150], [2000, 2000, 600], (200000, 3)).astype(np.float32)
+    rd = rng.normal(size=(200000, 3))
+    rd = (rd / np.linalg.norm(rd, axis=1, keepdims=True)).astype(np.float32)
+    eo, ed = _edge_aimed_rays(verts, 40, 12)
+    ro = np.concatenate([ro, eo])
+    rd = np.concatenate([rd, ed])
+    n = len(ro)
+    od = torch.from_numpy(ro).cuda()
+    dd = torch.from_numpy(rd).cuda()
+    res = []
+    for mode in (0, 1):
+        t = torch.zeros(n, dtype=torch.float32, device="cuda")
+        h = torch.zeros(n, dtype=torch.int32, device="cuda")
+        assert lib.mpenv_debug_trace_rays(e.h, od.data_ptr(), dd.data_ptr(), n, mode, t.data_ptr(),
+                                          h.data_ptr(), None) == 0
+        res.append((t.cpu().numpy(), h.cpu().numpy()))
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    # oracle (reference order on the CPU) on a subset incl. all edge-aimed rays
+    idx = np.concatenate([np.arange(0, 200000, 97), np.arange(200000, n)])
+    for i in idx:
+        tt = C.c_float(0)
+        hit = o.lib.oracle_trace_ray(o.h, T.fptr(ro[i]), T.fptr(rd[i]), C.byref(tt))
+        assert hit == res[1][1][i], i
+        if hit:
+            assert tt.value == res[1][0][i], (i, tt.value, res[1][0][i])
