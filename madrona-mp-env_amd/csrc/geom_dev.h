@@ -50,29 +50,69 @@ __device__ __forceinline__ uint32_t bsPop(ByteStack &s)
 }
 
 // Stage nodes + vertices into dynamic LDS (all threads participate).
+// LDS image: nodes verbatim (64 B each), then every triangle vertex padded
+// to a float4 so a triangle is three ds_read_b128.
 __device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc)
 {
-    const int node_words = sc.numNodes * 16; // 64 B per node
+    const int node_q = sc.numNodes * 4; // uint4 per node
     const uint4 *src_n = reinterpret_cast<const uint4 *>(sc.nodes);
     uint4 *dst_n = reinterpret_cast<uint4 *>(smem);
-    for (int k = threadIdx.x; k < node_words / 4; k += blockDim.x) dst_n[k] = src_n[k];
-    const int vert_words = sc.numVerts * 3;
-    const uint32_t *src_v = reinterpret_cast<const uint32_t *>(sc.verts);
-    uint32_t *dst_v = reinterpret_cast<uint32_t *>(smem + (size_t)node_words * 4);
-    for (int k = threadIdx.x; k < vert_words; k += blockDim.x) dst_v[k] = src_v[k];
+    for (int k = threadIdx.x; k < node_q; k += blockDim.x) dst_n[k] = src_n[k];
+    const float *src_v = sc.verts;
+    float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
+    for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
+        dst_v[k] = make_float4(src_v[3 * k], src_v[3 * k + 1], src_v[3 * k + 2], 0.f);
     __syncthreads();
     LBVH b;
     b.nodes = (const MP_LDS BVHNode *)(smem);
-    b.verts = (const MP_LDS float *)(smem + (size_t)node_words * 4);
+    b.verts = (const MP_LDS float *)(smem + (size_t)node_q * 16);
     return b;
 }
 
+typedef float lf4 __attribute__((ext_vector_type(4)));
+typedef uint32_t lu4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ void loadTri(const LBVH &b, int tri, mp::Vec3 &a, mp::Vec3 &bb, mp::Vec3 &c)
 {
-    const MP_LDS float *p = b.verts + tri * 9;
-    a = mp::v3(p[0], p[1], p[2]);
-    bb = mp::v3(p[3], p[4], p[5]);
-    c = mp::v3(p[6], p[7], p[8]);
+    const MP_LDS lf4 *p = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + tri * 3;
+    const lf4 x = p[0], y = p[1], z = p[2];
+    a = mp::v3(x.x, x.y, x.z);
+    bb = mp::v3(y.x, y.y, y.z);
+    c = mp::v3(z.x, z.y, z.z);
+}
+
+// A node decoded from four ds_read_b128 (mesh_bvh.hpp:61-86 byte layout:
+// min xyz | exp xyz, internal | triSize[4] | qMin x,y,z [4] | qMax x,y,z [4]
+// | children[4] | parent).  Quantised bounds stay packed 4 per register;
+// qb() converts byte i exactly (v_cvt_f32_ubyteN).
+struct NodeR {
+    float minX, minY, minZ;
+    int expX, expY, expZ;
+    uint32_t triSize, qMinX, qMinY, qMinZ, qMaxX, qMaxY, qMaxZ;
+    int32_t child[4];
+};
+
+__device__ __forceinline__ float qb(uint32_t w, int i) { return (float)((w >> (8 * i)) & 0xffu); }
+
+__device__ __forceinline__ NodeR loadNode(const LBVH &b, uint32_t idx)
+{
+    const MP_LDS lu4 *p = reinterpret_cast<const MP_LDS lu4 *>(b.nodes + idx);
+    const lu4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    NodeR n;
+    n.minX = __uint_as_float(q0.x);
+    n.minY = __uint_as_float(q0.y);
+    n.minZ = __uint_as_float(q0.z);
+    n.expX = (int)(int8_t)(q0.w & 0xffu);
+    n.expY = (int)(int8_t)((q0.w >> 8) & 0xffu);
+    n.expZ = (int)(int8_t)((q0.w >> 16) & 0xffu);
+    n.triSize = q1.x;
+    n.qMinX = q1.y; n.qMinY = q1.z; n.qMinZ = q1.w;
+    n.qMaxX = q2.x; n.qMaxY = q2.y; n.qMaxZ = q2.z;
+    n.child[0] = (int32_t)q2.w;
+    n.child[1] = (int32_t)q3.x;
+    n.child[2] = (int32_t)q3.y;
+    n.child[3] = (int32_t)q3.z;
+    return n;
 }
 
 struct RayTxfmD {
@@ -140,7 +180,7 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
     return true;
 }
 
-__device__ __forceinline__ float expScaleD(int8_t e) { return mp::u2f((uint32_t)((int32_t)e + 127) << 23); }
+__device__ __forceinline__ float expScaleD(int e) { return mp::u2f((uint32_t)(e + 127) << 23); }
 
 // MeshBVH::traceRay (mesh_bvh.inl:110-208) over the LDS-resident BVH.
 // Returns hit flag; *t_out = closest hit t when hit.
@@ -162,7 +202,7 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     bsPush(st, 0);
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
-        const MP_LDS BVHNode &node = b.nodes[node_idx];
+        const NodeR node = loadNode(b, node_idx);
         const float dirQuantX = expScaleD(node.expX) * rayXInv;
         const float dirQuantY = expScaleD(node.expY) * rayYInv;
         const float dirQuantZ = expScaleD(node.expZ) * rayZInv;
@@ -171,14 +211,14 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
         const float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int32_t child = node.children[i];
+            const int32_t child = node.child[i];
             if (child == -1) continue;
-            float t_near_x = node.qMinX[i] * dirQuantX + originQuantX;
-            float t_near_y = node.qMinY[i] * dirQuantY + originQuantY;
-            float t_near_z = node.qMinZ[i] * dirQuantZ + originQuantZ;
-            float t_far_x = node.qMaxX[i] * dirQuantX + originQuantX;
-            float t_far_y = node.qMaxY[i] * dirQuantY + originQuantY;
-            float t_far_z = node.qMaxZ[i] * dirQuantZ + originQuantZ;
+            float t_near_x = qb(node.qMinX, i) * dirQuantX + originQuantX;
+            float t_near_y = qb(node.qMinY, i) * dirQuantY + originQuantY;
+            float t_near_z = qb(node.qMinZ, i) * dirQuantZ + originQuantZ;
+            float t_far_x = qb(node.qMaxX, i) * dirQuantX + originQuantX;
+            float t_far_y = qb(node.qMaxY, i) * dirQuantY + originQuantY;
+            float t_far_z = qb(node.qMaxZ, i) * dirQuantZ + originQuantZ;
             float t_near = fmax_(fmin_(t_near_x, t_far_x),
                                  fmax_(fmin_(t_near_y, t_far_y), fmax_(fmin_(t_near_z, t_far_z), 0.f)));
             float t_far = fmin_(fmax_(t_far_x, t_near_x),
@@ -186,11 +226,15 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
             if (t_near <= t_far) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;
-                    const int ntri = node.triSize[i];
+                    const int ntri = (int)((node.triSize >> (8 * i)) & 0xffu);
                     bool hit_tri = false;
                     float hit_t = 0.f;
                     float leaf_tmax = t_max;
+#ifdef MPENV_LAB_NO_TRI
+                    for (int k = 0; k < 0; k++) {
+#else
                     for (int k = 0; k < ntri; k++) {
+#endif
                         Vec3 a, bb, c;
                         loadTri(b, leaf + k, a, bb, c);
                         if (rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t)) {
@@ -414,8 +458,16 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     using namespace mp;
     float min_t = kFltMax;
     float tb;
+#ifdef MPENV_LAB_NO_BVH
+    bool hit = false;
+    tb = 0.f;
+#else
     bool hit = bvhTraceRayD(b, org, d, tb);
+#endif
     if (hit) min_t = tb;
+#ifdef MPENV_LAB_NO_CAPSULE
+    N = 0;
+#endif
     int ent = -1;
     // Conservative cull: every point of a Z-capsule lies within r of its
     // vertical axis, so a ray whose xy line passes farther than r from the

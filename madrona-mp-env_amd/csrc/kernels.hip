@@ -1243,7 +1243,7 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 // Step graph part 1 (sim.cpp:5299-5320 up to updateMoveStatePostFall): the
 // per-agent systems, which read no other agent's state.  Lane = agent, no
 // barriers, so sphere-cast latency overlaps across the whole grid.
-__global__ void __launch_bounds__(kBlock) k_move(DevState S, SceneDev sc)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) k_move(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const LBVH bvh = stageBVH(smem, sc);
@@ -1827,7 +1827,7 @@ const char *kernelName(int k)
     return (k >= 0 && k < kNumTimedKernels) ? names[k] : "?";
 }
 
-size_t bvhLdsBytes(const SceneDev &sc) { return (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 12; }
+size_t bvhLdsBytes(const SceneDev &sc) { return (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16; }
 
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -61,8 +62,12 @@ struct Builder {
     std::vector<Box> triBox;
     std::vector<Vec3> centroid;
     std::vector<BNode> bnodes;
+    int maxLeaf = 2;
 
-    explicit Builder(const std::vector<Vec3> &verts) : v(verts) {}
+    explicit Builder(const std::vector<Vec3> &verts) : v(verts)
+    {
+        if (const char *e = std::getenv("MPENV_BVH_LEAF")) maxLeaf = std::max(1, std::min(2, std::atoi(e)));
+    }
 
     int build(std::vector<int> tris)
     {
@@ -72,7 +77,7 @@ struct Builder {
         int id = (int)bnodes.size();
         bnodes.push_back(node);
 
-        if (tris.size() <= 2) { // maxLeafSize = numTrisPerLeaf (mesh_bvh_builder.cpp:345-346)
+        if ((int)tris.size() <= maxLeaf) { // maxLeafSize = numTrisPerLeaf (mesh_bvh_builder.cpp:345-346)
             bnodes[id].tris = tris;
             return id;
         }

@@ -1,0 +1,100 @@
+"""Kernel lab: build variants of libmpenv.so with extra -D switches and time
+their step kernels on the C3 workload (development tool; variants that
+switch parts of a kernel off give wrong results by design and are never
+used outside this tool).
+
+  python tools/kernel_lab.py build NAME [-DFOO=1 ...]   (here, cross-compiles)
+  python tools/kernel_lab.py run NAME [NAME ...]        (on the GPU box)
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "madrona-mp-env_amd")
+LAB = os.path.join(PKG, "lab")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def build(name, defines):
+    import build_native as B
+
+    out = os.path.join(LAB, name)
+    os.makedirs(out, exist_ok=True)
+    common = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{B.CSRC}",
+              f"-I{B.INCLUDE}"] + list(defines)
+    objs = []
+    for src in B.LIB_SOURCES:
+        s = os.path.join(B.CSRC, src)
+        o = os.path.join(out, src + ".o")
+        if src.endswith(".hip"):
+            cmd = [B.HIPCC, "-x", "hip", f"--offload-arch={B.ARCH}", "-c", s, "-o", o] + common
+        else:
+            cmd = [B.HIPCC, "-x", "c++", "-c", s, "-o", o] + common + ["-D__HIP_PLATFORM_AMD__",
+                                                                      "-I/opt/rocm/include"]
+        subprocess.run(cmd, check=True)
+        objs.append(o)
+    subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o",
+                    os.path.join(out, "libmpenv.so")] + objs, check=True)
+    json.dump({"defines": defines}, open(os.path.join(out, "variant.json"), "w"))
+    print("built", name, defines)
+
+
+def time_one(name, worlds=16384, team=6, warm=30, steps=100):
+    import mpenv_testlib as T
+
+    path = os.path.join(LAB, name, "libmpenv.so") if name != "main" else os.path.join(PKG, "libmpenv.so")
+    lib = C.CDLL(path)
+    lib.mpenv_create.argtypes = [C.POINTER(T.MpenvConfig), C.POINTER(C.c_void_p)]
+    lib.mpenv_last_error.restype = C.c_char_p
+    for f in ("mpenv_init", "mpenv_step"):
+        getattr(lib, f).argtypes = [C.c_void_p]
+    lib.mpenv_enable_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
+    lib.mpenv_kernel_timings.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_char_p),
+                                         C.POINTER(C.c_float), C.POINTER(C.c_int32)]
+    cfg = T.MpenvConfig(1, 0, worlds, 5, 1, 0, 2, team, 0, 0, T.SCENE.encode(), 0, None, None, None,
+                        None, 0)
+    h = C.c_void_p()
+    assert lib.mpenv_create(C.byref(cfg), C.byref(h)) == 0, lib.mpenv_last_error()
+    assert lib.mpenv_init(h) == 0
+    # 16-step action ring in device memory (hash tape, as bench.py)
+    ring = T.mpenv_tape.tape_ring(1234, 0, worlds * 2 * team, 16)
+    hip = C.CDLL("libamdhip64.so")
+    dptr = C.c_void_p()
+    assert hip.hipMalloc(C.byref(dptr), C.c_size_t(ring.nbytes)) == 0
+    assert hip.hipMemcpy(dptr, ring.ctypes.data_as(C.c_void_p), C.c_size_t(ring.nbytes), 1) == 0
+    lib.mpenv_copy_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    per = ring[0].nbytes
+
+    def step(s):
+        lib.mpenv_copy_actions(h, C.c_void_p(dptr.value + (s % 16) * per), None)
+        lib.mpenv_step(h)
+
+    for s in range(warm):
+        step(s)
+    lib.mpenv_enable_kernel_timing(h, 1)
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step(warm + s)
+    el = time.perf_counter() - t0
+    names = (C.c_char_p * 16)()
+    ms = (C.c_float * 16)()
+    ln = (C.c_int32 * 16)()
+    n = lib.mpenv_kernel_timings(h, 16, names, ms, ln)
+    res = {names[i].decode(): round(ms[i], 4) for i in range(n)}
+    print(json.dumps({"variant": name, "ms_per_step": round(1e3 * el / steps, 4), "kernels": res}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(sys.argv[2], sys.argv[3:])
+    elif sys.argv[1] == "run":
+        for name in sys.argv[2:]:
+            subprocess.run([sys.executable, __file__, "_one", name], check=True)
+    elif sys.argv[1] == "_one":
+        time_one(sys.argv[2])

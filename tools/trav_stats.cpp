@@ -4,6 +4,7 @@
 //
 //   trav_stats SCENE_DIR RAYS.f32   (RAYS: n x 6 floats, origin + direction)
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -24,6 +25,7 @@ struct Node {
 
 struct Stats {
     double pops = 0, boxes = 0, tris = 0, maxStack = 0;
+    std::vector<std::array<int, 4>> slotTris; // per popped node: tris tested in each child slot
 };
 
 static std::vector<Node> nodes;
@@ -47,6 +49,48 @@ static bool tri(const float *v, const float *o, const float *d, float tmax, floa
     return t > 0 && t < tmax;
 }
 
+struct Visit {
+    std::vector<int> nodes;
+    std::vector<int> leaves; // first triangle ids of leaves whose box passed
+};
+
+static void traceVisits(const float *o, const float *d, Visit &v)
+{
+    float inv[3];
+    for (int k = 0; k < 3; k++) inv[k] = d[k] == 0 ? 1e7f : 1.f / d[k];
+    float tmax = 3.4e38f;
+    std::vector<int> stack = { 0 };
+    while (!stack.empty()) {
+        int ni = stack.back();
+        stack.pop_back();
+        v.nodes.push_back(ni);
+        const Node &n = nodes[ni];
+        for (int i = 0; i < 4; i++) {
+            if (n.children[i] == -1) continue;
+            float sx = std::ldexp(1.f, n.expX), sy = std::ldexp(1.f, n.expY), sz = std::ldexp(1.f, n.expZ);
+            float lo[3] = { n.minX + sx * n.qMinX[i], n.minY + sy * n.qMinY[i], n.minZ + sz * n.qMinZ[i] };
+            float hi[3] = { n.minX + sx * n.qMaxX[i], n.minY + sy * n.qMaxY[i], n.minZ + sz * n.qMaxZ[i] };
+            float tn = 0, tf = tmax;
+            for (int k = 0; k < 3; k++) {
+                float a = (lo[k] - o[k]) * inv[k], b = (hi[k] - o[k]) * inv[k];
+                tn = std::max(tn, std::min(a, b));
+                tf = std::min(tf, std::max(a, b));
+            }
+            if (tn > tf) continue;
+            if (n.children[i] & 0x80000000) {
+                int leaf = n.children[i] & 0x7fffffff;
+                v.leaves.push_back(leaf * 4 + n.triSize[i]);
+                for (int k = 0; k < n.triSize[i]; k++) {
+                    float t;
+                    if (tri(&verts[(leaf + k) * 9], o, d, tmax, t)) tmax = t;
+                }
+            } else {
+                stack.push_back(n.children[i]);
+            }
+        }
+    }
+}
+
 static void trace(const float *o, const float *d, bool ftb, Stats &st)
 {
     float inv[3];
@@ -61,6 +105,7 @@ static void trace(const float *o, const float *d, bool ftb, Stats &st)
         const Node &n = nodes[ni];
         std::pair<float, int> kids[4];
         int nk = 0;
+        st.slotTris.push_back({ 0, 0, 0, 0 });
         for (int i = 0; i < 4; i++) {
             if (n.children[i] == -1) continue;
             st.boxes++;
@@ -78,6 +123,7 @@ static void trace(const float *o, const float *d, bool ftb, Stats &st)
                 int leaf = n.children[i] & 0x7fffffff;
                 for (int k = 0; k < n.triSize[i]; k++) {
                     st.tris++;
+                    st.slotTris.back()[i]++;
                     float t;
                     if (tri(&verts[(leaf + k) * 9], o, d, tmax, t)) tmax = t;
                 }
@@ -107,21 +153,57 @@ int main(int argc, char **argv)
     while (fread(buf, 4, 6, f) == 6) rays.insert(rays.end(), buf, buf + 6);
     fclose(f);
     size_t n = rays.size() / 6;
+    {
+        double un = 0, ut = 0;
+        for (size_t w0 = 0; w0 < n; w0 += 64) {
+            std::vector<char> seen_n(nodes.size(), 0);
+            std::vector<int> leafset;
+            for (size_t r = w0; r < std::min(n, w0 + 64); r++) {
+                Visit v;
+                traceVisits(&rays[6 * r], &rays[6 * r + 3], v);
+                for (int x : v.nodes) seen_n[x] = 1;
+                for (int x : v.leaves) leafset.push_back(x);
+            }
+            std::sort(leafset.begin(), leafset.end());
+            leafset.erase(std::unique(leafset.begin(), leafset.end()), leafset.end());
+            for (char c : seen_n) un += c;
+            for (int x : leafset) ut += x & 3;
+        }
+        double waves = (double)((n + 63) / 64);
+        printf("packet (64 consecutive rays): union nodes/wave %.2f, union tris/wave %.2f\n", un / waves, ut / waves);
+    }
     for (int ftb = 0; ftb < 2; ftb++) {
         Stats st;
-        double wave_pops = 0, wave_tris = 0;
+        double wave_pops = 0, wave_tris = 0, simt_slot = 0, simt_merged = 0;
         for (size_t w0 = 0; w0 < n; w0 += 64) {
             double mp = 0, mt = 0;
+            std::vector<Stats> lanes;
             for (size_t r = w0; r < std::min(n, w0 + 64); r++) {
                 Stats one;
                 trace(&rays[6 * r], &rays[6 * r + 3], ftb, one);
+                lanes.push_back(one);
                 mp = std::max(mp, one.pops);
                 mt = std::max(mt, one.tris);
                 st.pops += one.pops; st.boxes += one.boxes; st.tris += one.tris;
                 st.maxStack = std::max(st.maxStack, one.maxStack);
             }
             wave_pops += mp * 64; wave_tris += mt * 64;
+            // lockstep: iteration it runs slot i's tri loop max_lanes(slotTris[it][i]) times
+            for (int it = 0; it < (int)mp; it++) {
+                int merged = 0;
+                for (int i = 0; i < 4; i++) {
+                    int m = 0;
+                    for (auto &L : lanes)
+                        if (it < (int)L.slotTris.size()) m = std::max(m, L.slotTris[it][i]);
+                    simt_slot += m * 64;
+                }
+                for (auto &L : lanes)
+                    if (it < (int)L.slotTris.size())
+                        merged = std::max(merged, L.slotTris[it][0] + L.slotTris[it][1] + L.slotTris[it][2] + L.slotTris[it][3]);
+                simt_merged += merged * 64;
+            }
         }
+        printf("   SIMT tri executions/ray: per-slot loops %.2f, merged loop %.2f\n", simt_slot / n, simt_merged / n);
         printf("%s: rays %zu  pops/ray %.2f  boxes/ray %.2f  tris/ray %.2f  maxStack %.0f | wave-max pops/ray %.2f tris %.2f\n",
                ftb ? "front-to-back" : "reference    ", n, st.pops / n, st.boxes / n, st.tris / n, st.maxStack,
                wave_pops / n, wave_tris / n);
