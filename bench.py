@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="N>1: RCCL-gather obs/reward/done to rank 0 every step (learner mode)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--bots", choices=["none", "team1", "all"], default="none",
+                    help="A* scripted bots (AgentPolicy -1, planAStarAISystem) for team 1 / everyone "
+                         "(config C5's nav-mesh pathing); the headline C3 line uses none")
     return ap.parse_args()
 
 
@@ -146,6 +149,15 @@ def main():
     torch.cuda.synchronize()
     sim.init()
 
+    if args.bots != "none":
+        pol = torch.zeros((W, 2, ts), dtype=torch.int32)
+        if args.bots == "all":
+            pol[:] = -1
+        else:
+            pol[:, 1, :] = -1
+        sim.policy_assignment_tensor().to_torch().copy_(pol.view(-1, 1).to(dev))
+        torch.cuda.synchronize()
+
     ring = torch.from_numpy(mpenv_tape.tape_ring(TAPE_SEED, offset * N, A, RING)).to(dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
@@ -188,7 +200,7 @@ def main():
     dom_ms = timings[dom][0]
     alg = KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W
     achieved = alg / (dom_ms * 1e-3) / 1e9
-    workload = f"simple_map {ts}v{ts} x {W} worlds/GPU"
+    workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})")
     tk, traffic = load_traffic(args.traffic, workload)
     step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W
     kern_ms = sum(v[0] for v in timings.values())
@@ -214,6 +226,7 @@ def main():
             "task": "Zone",
             "sim_flags": "Default",
             "sim_control": [0, 1, 1],
+            "bots": args.bots,
             "rand_seed": 5,
             "parallelism": f"world-sharded x{world_size}" + (" + RCCL gather" if outs else ""),
         },

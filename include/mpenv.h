@@ -284,6 +284,14 @@ int mpenv_enable_kernel_timing(mpenv_manager *mgr, int32_t enable);
 int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes,
                     float *verts_out, int32_t *num_verts, int32_t *max_stack);
 
+/* Host-side navmesh (Navmesh::initFromPolygons, mgr.cpp:1301-1327) and A*
+ * next-hop table (buildAStarLookup, mgr.cpp:1155-1211) of a scene, for
+ * tests and the oracle.  Two-call pattern: pass *num_tris = 0 to query the
+ * count; with *num_tris >= T fills tri_verts [T][3][3], adj [T][3] and
+ * astar [T][T] (each optional). */
+int mpenv_scene_navmesh(const char *scene_path, float *tri_verts_out, int32_t *num_tris, int32_t *adj_out,
+                        int32_t *astar_out);
+
 const char *mpenv_last_error(void);
 int32_t mpenv_abi_version(void);
 

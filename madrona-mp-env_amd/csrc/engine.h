@@ -149,6 +149,10 @@ struct SceneDev {
     int32_t autoReset;
     uint32_t worldOffset;
     mp::RandKey initRandKey;
+    // navmesh for the scripted bots (sim.cpp:4958-5172)
+    const float *navTris;   // 9 floats per triangle (deduplicated vertices)
+    const int32_t *astar;   // [numNavTris][numNavTris] next hop
+    int32_t numNavTris;
 };
 
 // Host launchers (kernels.hip)

@@ -482,6 +482,12 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
         Vec3 tr = org - co;
         const float cr = tr.x * d.y - tr.y * d.x;
         if (cr * cr > cull_r2 * dxy2) continue;
+        // Behind the origin: the capsule's farthest point along d is at
+        // dot(axis base - org, d) + max(0, h d.z) + r (|d| = 1); if that is
+        // negative no t > 0 exists.  Same 1% radius margin.
+        const float ahead = -(tr.x * d.x + tr.y * d.y + tr.z * d.z) + fmaxD(0.f, kCapsuleSegment * d.z) +
+                            kCapsuleRadius * 1.01f;
+        if (ahead < 0.f) continue;
         float t = intersectRayZOriginCapsule(tr, d, kCapsuleRadius, kCapsuleSegment);
         if (t != 0 && t < min_t) {
             min_t = t;

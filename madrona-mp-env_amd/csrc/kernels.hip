@@ -144,6 +144,134 @@ __device__ __forceinline__ void stAim(const DevState &S, int64_t g, const AimD &
 
 // ====================================================== per-agent systems
 // sim.cpp:2057-2091 applyBotActionsSystem
+// ---- scripted bots: NavUtils (sim.cpp:4958-5037) + planAStarAISystem
+// (sim.cpp:5041-5172).  The triangle loops index the navmesh uniformly
+// across the wave, so its vertices come in as scalar loads.
+__device__ __forceinline__ Vec3 navVertD(const SceneDev &sc, int tri, int k)
+{
+    const float *p = sc.navTris + 9 * tri + 3 * k;
+    return v3(p[0], p[1], p[2]);
+}
+
+__device__ Vec3 navTriCenterD(const SceneDev &sc, int tri)
+{
+    Vec3 c = v3(0.f, 0.f, 0.f);
+    for (int k = 0; k < 3; k++) c = c + navVertD(sc, tri, k) / 3.0f;
+    return c;
+}
+
+// NearestNavTri (sim.cpp:4975-5010): first containing triangle (xy winding
+// test), else the candidate kept by the reference's distance bookkeeping.
+__device__ int nearestNavTriD(const SceneDev &sc, Vec3 pos)
+{
+    float closest = kFltMax;
+    int closest_idx = -1;
+    for (int tri = 0; tri < sc.numNavTris; tri++) {
+        bool contained = true;
+        bool gtz = false;
+        for (int k = 0; k < 3; k++) {
+            const Vec3 v1 = navVertD(sc, tri, k);
+            const Vec3 v2 = navVertD(sc, tri, k == 2 ? 0 : k + 1);
+            const Vec3 e = v2 - v1;
+            const Vec3 vp = pos - v1;
+            const Vec3 c = cross(e, vp);
+            if ((c.z > 0.0f) != gtz && k > 0) contained = false;
+            gtz = c.z > 0.0f;
+            float distsq = length2(v1 - pos);
+            if (distsq < closest) {
+                const float dir = dot(e, vp);
+                const Vec3 perp = vp * (-dir / dot(e, e)) + e;
+                distsq = dot(perp, perp);
+                if (distsq < closest) {
+                    closest = fabs_(c.z);
+                    closest_idx = tri;
+                }
+            }
+        }
+        if (contained) return tri;
+    }
+    return closest_idx;
+}
+
+// PathfindToPoint (sim.cpp:5012-5035)
+__device__ Vec3 pathfindToPointD(const SceneDev &sc, Vec3 start, Vec3 pos)
+{
+    const int start_tri = nearestNavTriD(sc, start);
+    const int goal_tri = nearestNavTriD(sc, pos);
+    if (start_tri < 0 || goal_tri < 0) return v3(0.f, 0.f, 0.f); // (asserted in the reference)
+    const int next = sc.astar[start_tri * sc.numNavTris + goal_tri];
+    if (next == -1) return v3(0.f, 0.f, 0.f);
+    if (next == goal_tri) return pos;
+    return navTriCenterD(sc, next);
+}
+
+__device__ void planAStarD(const DevState &S, const SceneDev &sc, int64_t g)
+{
+    if (S.policy[g] != -1) return; // consts::aStarPolicyID
+    const int w = (int)(g / S.N);
+    RNG rng = ldRng(S, g);
+    int move_amount = rngI32(rng, 0, 2);
+    int move_angle = rngI32(rng, 0, 2);
+    int r_yaw = rngI32(rng, 0, 5);
+    const int r_pitch = rngI32(rng, 0, 2);
+    const int reload = S.magazine[2 * g] == 0 ? 1 : 0;
+    int stand = rngI32(rng, 0, 2);
+    stRng(S, g, rng);
+    // fire if any opponent is visible (OpponentsVisibility of the last step)
+    int fire = (S.visMask[g] & ((1u << S.T) - 1u)) != 0 ? 1 : 0;
+
+    const int zi = S.curZone[w];
+    const AABB z = sc.zoneAABB[zi];
+    Vec3 center = (z.pMin + z.pMax) / 2.f; // AABB::centroid
+    const Vec3 pos = v3(S.px[g], S.py[g], 0.f);
+    center = pathfindToPointD(sc, pos, center);
+    center.z = 0.f;
+    const float yaw = S.ayaw[g];
+    const Vec3 fwd = v3(-sinf_(yaw), cosf_(yaw), 0.f);
+    const Vec3 tgt = normalize(center - pos);
+    move_amount = dot(fwd, tgt) > 0.6f ? 1 : 0;
+    r_yaw = cross(fwd, tgt).z < 0.0f ? 0 + move_amount : 4 - move_amount;
+    move_amount *= 2;
+    move_angle = 0;
+    stand = 0;
+
+    // wall avoidance from last step's forward lidar depths
+    float coll_ang = 0.f, coll_norm = 0.f;
+    const float *lid = &S.fwdLidar[g * kFwdRays * 4];
+    for (int y = 0; y < 2; y++) {
+        for (int x = 0; x < 32; x++) {
+            if (lid[(y * 32 + x) * 4] < 16.0f) {
+                coll_norm++;
+                coll_ang += x;
+            }
+        }
+    }
+    if (coll_norm > 0.f) {
+        coll_ang /= coll_norm;
+        move_amount = 1;
+        switch ((int)(coll_ang / 32.f * 8.0f)) {
+        case 0: move_angle = 2; break;
+        case 1:
+        case 2: move_angle = 3; break;
+        case 3:
+        case 4: move_angle = 4; move_amount = 2; break;
+        case 5:
+        case 6: move_angle = 5; break;
+        case 7: move_angle = 6; break;
+        }
+    }
+    if (reload) fire = 0;
+    if (fire) r_yaw = 2;
+    int32_t *out = &S.botAction[7 * g];
+    out[0] = move_amount;
+    out[1] = move_angle;
+    out[2] = r_yaw;
+    out[3] = r_pitch;
+    out[4] = fire;
+    out[5] = reload;
+    out[6] = stand;
+}
+
 __device__ void applyBotActionsD(const DevState &S, int64_t g)
 {
     if (S.policy[g] != -1) return;
@@ -1249,8 +1377,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
     const LBVH bvh = stageBVH(smem, sc);
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= S.A) return;
-    // planAStarAISystem (sim.cpp:5041-5172) acts only for AgentPolicy == -1
-    // (bots) and is not part of round 1.
+    planAStarD(S, sc, g);
     applyBotActionsD(S, g);
     pvpMovementD(S, g);
     pvpAimD(S, g);

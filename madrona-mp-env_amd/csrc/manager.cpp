@@ -272,6 +272,25 @@ static void buildSceneDev(mpenv_manager &m)
         if (!v.empty()) m.upload(p, v.data(), sizeof(Spawn) * v.size());
         return p;
     };
+    {
+        const NavMesh &nm = s.nav;
+        const size_t T = nm.numTris();
+        std::vector<float> tv(std::max<size_t>(T * 9, 1), 0.f);
+        for (size_t t = 0; t < T; t++)
+            for (int k = 0; k < 3; k++) {
+                const mp::Vec3 v = nm.verts[nm.tris[3 * t + k]];
+                tv[9 * t + 3 * k + 0] = v.x;
+                tv[9 * t + 3 * k + 1] = v.y;
+                tv[9 * t + 3 * k + 2] = v.z;
+            }
+        float *d_nav = m.alloc<float>(tv.size());
+        m.upload(d_nav, tv.data(), sizeof(float) * tv.size());
+        int32_t *d_astar = m.alloc<int32_t>(std::max<size_t>(nm.astar.size(), 1));
+        if (!nm.astar.empty()) m.upload(d_astar, nm.astar.data(), sizeof(int32_t) * nm.astar.size());
+        sc.navTris = d_nav;
+        sc.astar = d_astar;
+        sc.numNavTris = (int32_t)T;
+    }
     sc.nodes = d_nodes;
     sc.verts = d_verts;
     sc.numNodes = (int32_t)s.nodes.size();
@@ -703,6 +722,36 @@ int mpenv_kernel_timings(mpenv_manager *m, int32_t max_n, const char **names, fl
         if (launches) launches[k] = steps;
     }
     return nk;
+}
+
+// Host-side access to the navmesh and A* table (tests / oracle input).
+int mpenv_scene_navmesh(const char *scene_path, float *tri_verts_out, int32_t *num_tris, int32_t *adj_out,
+                        int32_t *astar_out)
+{
+    try {
+        Scene s = loadScene(scene_path);
+        const NavMesh &nm = s.nav;
+        const int32_t T = (int32_t)nm.numTris();
+        if (num_tris) {
+            if (*num_tris >= T) {
+                for (int32_t t = 0; t < T; t++)
+                    for (int k = 0; k < 3; k++) {
+                        const mp::Vec3 v = nm.verts[nm.tris[3 * t + k]];
+                        if (tri_verts_out) {
+                            tri_verts_out[9 * t + 3 * k + 0] = v.x;
+                            tri_verts_out[9 * t + 3 * k + 1] = v.y;
+                            tri_verts_out[9 * t + 3 * k + 2] = v.z;
+                        }
+                        if (adj_out) adj_out[3 * t + k] = nm.adj[3 * t + k];
+                    }
+                if (astar_out) std::memcpy(astar_out, nm.astar.data(), sizeof(int32_t) * nm.astar.size());
+            }
+            *num_tris = T;
+        }
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_IO, e.what());
+    }
+    return MPENV_OK;
 }
 
 // Host-side access to the scene BVH (for the parity oracle and tests).

@@ -423,6 +423,7 @@ Scene loadScene(const std::string &dir, bool spawn_in_middle)
         readPod(f, &ni, 1, path);
         s.navIndices.resize(ni);
         readPod(f, s.navIndices.data(), ni, path);
+        buildNavMesh(s, path);
     }
 
     // ---- spawns.bin (map_importer.cpp:508-543)

@@ -53,6 +53,17 @@ struct GoalRegion {
     float rewardStrength;
 };
 
+// Navigation mesh after vertex dedup + triangulation, with triangle
+// adjacency and the A* next-hop table (navmesh.cpp).
+struct NavMesh {
+    std::vector<mp::Vec3> verts;
+    std::vector<uint32_t> tris;   // 3 per triangle
+    std::vector<int32_t> adj;     // 3 per triangle (neighbour across edge k, or -1)
+    std::vector<int32_t> astar;   // [T][T] next triangle toward goal, -1 unreachable
+    bool astarFromCache = false;
+    size_t numTris() const { return tris.size() / 3; }
+};
+
 struct Scene {
     mp::AABB worldBounds;
 
@@ -80,12 +91,17 @@ struct Scene {
     std::vector<uint32_t> navIndices;
 
     std::vector<GoalRegion> goalRegions;
+
+    NavMesh nav;
 };
 
 // Loads <dir>/{collisions,navmesh,spawns,zones}.bin (bindings.cpp:56-81) and
 // builds the BVH.  Throws std::runtime_error on I/O failure (the reference
 // FATALs, map_importer.cpp:229-231).
 Scene loadScene(const std::string &scene_dir, bool spawn_in_middle = false);
+
+// Dedups, triangulates and links the navmesh and builds/reads its A* table.
+void buildNavMesh(Scene &s, const std::string &navmesh_path);
 
 // Builds the compressed 4-wide BVH over de-indexed triangles.
 void buildBVH(const std::vector<mp::Vec3> &tri_verts, Scene &out);

@@ -215,6 +215,9 @@ struct Oracle {
     float maxDist;
     float frustum[4];
     std::vector<Node> nodes;
+    std::vector<Vec3> navTris;   // 3 per triangle
+    std::vector<int32_t> astar;  // [T][T]
+    int numNavTris = 0;
     std::vector<Vec3> verts;
     std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
     uint32_t numDefaultASpawns, numDefaultBSpawns;
@@ -1067,6 +1070,117 @@ void pvpDiscreteAimSystem(Oracle &o, int w, int i)
     AimS a = computeAim(ag.aimYaw, ag.aimPitch);
     ag.aimYaw = a.yaw; ag.aimPitch = a.pitch; ag.aimRot = a.rot;
     ag.rot = qnormalize(angleAxis(ag.aimYaw, kUp));
+}
+
+// ---- NavUtils (sim.cpp:4958-5037)
+Vec3 navTriCenter(const Oracle &o, int tri)
+{
+    Vec3 c = v3(0.f, 0.f, 0.f);
+    for (int k = 0; k < 3; k++) c = c + o.navTris[3 * tri + k] / 3.0f;
+    return c;
+}
+
+// NearestNavTri (sim.cpp:4975-5010)
+int nearestNavTri(const Oracle &o, Vec3 pos)
+{
+    float closest = kFltMax;
+    int closest_idx = -1;
+    for (int tri = 0; tri < o.numNavTris; tri++) {
+        bool contained = true;
+        bool gtz = false;
+        for (int i = 0; i < 3; i++) {
+            Vec3 v1 = o.navTris[3 * tri + i];
+            Vec3 v2 = o.navTris[3 * tri + (i + 1) % 3];
+            Vec3 v3_ = v2 - v1;
+            Vec3 vp = pos - v1;
+            Vec3 c = cross(v3_, vp);
+            if ((c.z > 0.0f) != gtz && i > 0) contained = false;
+            gtz = c.z > 0.0f;
+            float distsq = length2(v1 - pos);
+            if (distsq < closest) {
+                float dir = dot(v3_, vp);
+                Vec3 perp = vp * (-dir / dot(v3_, v3_)) + v3_;
+                distsq = dot(perp, perp);
+                if (distsq < closest) {
+                    closest = fabs_(c.z);
+                    closest_idx = tri;
+                }
+            }
+        }
+        if (contained) return tri;
+    }
+    return closest_idx;
+}
+
+// PathfindToPoint (sim.cpp:5012-5035)
+Vec3 pathfindToPoint(const Oracle &o, Vec3 start, Vec3 pos)
+{
+    int start_tri = nearestNavTri(o, start);
+    int goal_tri = nearestNavTri(o, pos);
+    if (start_tri < 0 || goal_tri < 0) return v3(0.f, 0.f, 0.f); // assert in the reference
+    int next_tri = o.astar[(size_t)start_tri * o.numNavTris + goal_tri];
+    if (next_tri == -1) return v3(0.f, 0.f, 0.f);
+    if (next_tri == goal_tri) return pos;
+    return navTriCenter(o, next_tri);
+}
+
+// sim.cpp:5041-5172 planAStarAISystem
+void planAStarAISystem(Oracle &o, int w, int i)
+{
+    size_t g = o.gi(w, i);
+    if (o.policy[g] != -1) return; // consts::aStarPolicyID
+    Agent &ag = o.agent(w, i);
+    const World &wd = o.worlds[w];
+    RNG &rng = ag.rng;
+    int move_amount = rngI32(rng, 0, 2);
+    int move_angle = rngI32(rng, 0, 2);
+    int r_yaw = rngI32(rng, 0, 5);
+    int r_pitch = rngI32(rng, 0, 2);
+    int r = o.magazine[2 * g] == 0 ? 1 : 0;
+    int stand = rngI32(rng, 0, 2);
+    int f = 0;
+    for (int k = 0; k < o.N / 2; k++)
+        if (ag.canSee[k]) f = 1;
+    AABB zb = o.zoneAABBs[wd.curZone];
+    Vec3 center = (zb.pMin + zb.pMax) / 2.f; // AABB::centroid
+    Vec3 pos = v3(ag.pos.x, ag.pos.y, 0.0f);
+    center = pathfindToPoint(o, pos, center);
+    center.z = 0.0f;
+    Vec3 fwd = v3(-sinf_(ag.aimYaw), cosf_(ag.aimYaw), 0.f);
+    Vec3 tgt_dir = normalize(center - pos);
+    move_amount = dot(fwd, tgt_dir) > 0.6f ? 1 : 0;
+    r_yaw = cross(fwd, tgt_dir).z < 0.0f ? 0 + move_amount : 4 - move_amount;
+    move_amount *= 2;
+    move_angle = 0;
+    stand = 0;
+    float collision_ang = 0.0f, collision_norm = 0.0f;
+    for (int y = 0; y < 2; y++) {
+        for (int x = 0; x < 32; x++) {
+            if (o.fwdLidar[((g * 2 + y) * 32 + x) * 4] < 16.0f) {
+                collision_norm++;
+                collision_ang += x;
+            }
+        }
+    }
+    if (collision_norm > 0.0f) {
+        collision_ang /= collision_norm;
+        move_amount = 1;
+        switch ((int)(collision_ang / (float)32 * 8.0f)) {
+        case 0: move_angle = 2; break;
+        case 1:
+        case 2: move_angle = 3; break;
+        case 3:
+        case 4: move_angle = 4; move_amount = 2; break;
+        case 5:
+        case 6: move_angle = 5; break;
+        case 7: move_angle = 6; break;
+        }
+    }
+    if (r) f = 0;
+    if (f) r_yaw = 2;
+    int32_t *out = &o.botAction[7 * g];
+    out[0] = move_amount; out[1] = move_angle; out[2] = r_yaw; out[3] = r_pitch;
+    out[4] = f; out[5] = r; out[6] = stand;
 }
 
 // sim.cpp:2057-2091 applyBotActionsSystem
@@ -1969,8 +2083,7 @@ void resetAndObs(Oracle &o, int w)
 void stepWorld(Oracle &o, int w)
 {
     const int N = o.N;
-    // planAStarAISystem (sim.cpp:5041-5172) runs only for AgentPolicy == -1;
-    // bots are not implemented in round 1.
+    for (int i = 0; i < N; i++) planAStarAISystem(o, w, i);
     for (int i = 0; i < N; i++) applyBotActionsSystem(o, w, i);
     for (int i = 0; i < N; i++) pvpMovementSystem(o, w, i);
     for (int i = 0; i < N; i++) pvpContinuousAimSystem(o, w, i);
@@ -2197,6 +2310,13 @@ void *oracle_create(const oracle_config *cfg)
         for (int i = 0; i < cfg->num_bvh_verts; i++)
             o->verts[i] = v3(cfg->bvh_verts[3 * i], cfg->bvh_verts[3 * i + 1], cfg->bvh_verts[3 * i + 2]);
         if (o->simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) addMiddleSpawnCells(*o);
+        if (cfg->nav_tris && cfg->astar && cfg->num_nav_tris > 0) {
+            o->numNavTris = cfg->num_nav_tris;
+            o->navTris.resize((size_t)cfg->num_nav_tris * 3);
+            for (int i = 0; i < cfg->num_nav_tris * 3; i++)
+                o->navTris[i] = v3(cfg->nav_tris[3 * i], cfg->nav_tris[3 * i + 1], cfg->nav_tris[3 * i + 2]);
+            o->astar.assign(cfg->astar, cfg->astar + (size_t)cfg->num_nav_tris * cfg->num_nav_tris);
+        }
         // sim.cpp:5855 maxDist; 5869-5882 frustumData
         o->maxDist = length(o->worldBounds.pMax - o->worldBounds.pMin);
         {

@@ -29,6 +29,12 @@ typedef struct oracle_config {
     int32_t num_nodes;
     const float *bvh_verts;
     int32_t num_bvh_verts;
+    /* Navmesh triangles [T][3][3] and A* next-hop table [T][T] from the
+     * product's builder (mpenv_scene_navmesh; checked by tests/test_navmesh.py).
+     * Optional: without them bots (AgentPolicy == -1) are rejected. */
+    const float *nav_tris;
+    int32_t num_nav_tris;
+    const int32_t *astar;
 } oracle_config;
 
 void *oracle_create(const oracle_config *cfg);

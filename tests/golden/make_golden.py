@@ -34,6 +34,8 @@ CASES = {
                            policy="combat"),
     "6v6_mid_combat": dict(team_size=6, worlds=2, steps=300, sim_flags=1, ctrl=[0, 1, 1],
                            policy="combat"),
+    # team 1 as A* bots (AgentPolicy = -1, planAStarAISystem)
+    "3v3_bots": dict(team_size=3, worlds=3, steps=250, sim_flags=1, ctrl=[0, 1, 1], bots="team1"),
 }
 TAPE_SEED = 1234
 FINAL_TENSORS = ["SELF_OBSERVATION", "REWARD", "HP", "FWD_LIDAR"]
@@ -51,6 +53,8 @@ def rollout(sim, case, record=None):
     sim.put_ctrl(np.array(case["ctrl"], np.int32))
     A = case["worlds"] * 2 * case["team_size"]
     sim.init()
+    if case.get("bots"):
+        set_bots(sim, case)
     yield -1
     for s in range(case["steps"]):
         if case.get("policy") == "combat":
@@ -59,6 +63,20 @@ def rollout(sim, case, record=None):
             sim.set_actions(T.mpenv_tape.tape_actions(TAPE_SEED, s, 0, A))
         sim.step()
         yield s
+
+
+def set_bots(sim, case):
+    """AgentPolicy = -1 (consts::aStarPolicyID) for team 1 or everyone."""
+    W, ts = case["worlds"], case["team_size"]
+    pol = np.zeros((W, 2, ts), np.int32)
+    if case["bots"] == "all":
+        pol[:] = -1
+    else:
+        pol[:, 1, :] = -1
+    if hasattr(sim, "view"):
+        sim.view("AGENT_POLICY")[:] = pol.reshape(-1, 1)
+    else:
+        sim.put("AGENT_POLICY", pol.reshape(-1, 1))
 
 
 def make(name, case):

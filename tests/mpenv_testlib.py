@@ -58,6 +58,7 @@ class OracleConfig(C.Structure):
         ("sim_flags", C.c_uint32), ("team_size", C.c_uint32), ("world_id_offset", C.c_uint32),
         ("scene_path", C.c_char_p), ("bvh_nodes", C.c_void_p), ("num_nodes", C.c_int32),
         ("bvh_verts", C.c_void_p), ("num_bvh_verts", C.c_int32),
+        ("nav_tris", C.c_void_p), ("num_nav_tris", C.c_int32), ("astar", C.c_void_p),
     ]
 
 
@@ -95,6 +96,8 @@ def lib_mpenv():
         lib.mpenv_last_error.restype = C.c_char_p
         lib.mpenv_scene_bvh.argtypes = [C.c_char_p, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.mpenv_scene_navmesh.argtypes = [C.c_char_p, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
+                                            C.c_void_p]
         lib.mpenv_trigger_reset.argtypes = [C.c_void_p, C.c_int32]
         lib.mpenv_set_hp.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
         lib.mpenv_enable_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
@@ -140,6 +143,23 @@ def fptr(a):
     return a.ctypes.data_as(C.POINTER(C.c_float))
 
 
+def scene_navmesh(scene=SCENE):
+    """(tri_verts [T,3,3] f32, adjacency [T,3] i32, astar [T,T] i32) from the
+    product's navmesh builder."""
+    lib = lib_mpenv()
+    nt = C.c_int32(0)
+    rc = lib.mpenv_scene_navmesh(scene.encode(), None, C.byref(nt), None, None)
+    assert rc == 0, lib.mpenv_last_error()
+    T = nt.value
+    tv = np.zeros((T, 3, 3), np.float32)
+    adj = np.zeros((T, 3), np.int32)
+    astar = np.zeros((T, T), np.int32)
+    rc = lib.mpenv_scene_navmesh(scene.encode(), tv.ctypes.data, C.byref(nt), adj.ctypes.data,
+                                 astar.ctypes.data)
+    assert rc == 0, lib.mpenv_last_error()
+    return tv, adj, astar
+
+
 def scene_bvh(scene=SCENE):
     lib = lib_mpenv()
     nn, nv, ms = C.c_int32(0), C.c_int32(0), C.c_int32(0)
@@ -160,9 +180,11 @@ class Oracle:
                  world_id_offset=0, scene=SCENE):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
+        self.nav_tris, _, self.astar = scene_navmesh(scene)
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
                            world_id_offset, scene.encode(), self.nodes.ctypes.data,
-                           len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3)
+                           len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3,
+                           self.nav_tris.ctypes.data, len(self.nav_tris), self.astar.ctypes.data)
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
         self.W, self.N = num_worlds, 2 * team_size

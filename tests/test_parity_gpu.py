@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import mpenv_testlib as T
-from golden.make_golden import rollout, step_hashes
+from golden.make_golden import rollout, set_bots, step_hashes
 
 pytestmark = pytest.mark.gpu
 
@@ -53,6 +53,8 @@ LIVE = [
     (2, 16, 300, 1 | 8 | 16, [0, 0, 0], "combat"),      # NoRespawn | StaggerStarts
     (4, 8, 300, 1 | (1 << 7) | (1 << 10), [1, 0, 1], "combat"),  # RandomFlip | SimEvalMode
     (5, 8, 300, 1 | (1 << 8), [0, 1, 0], "combat"),     # StaticFlipTeams
+    (3, 16, 300, 1, [0, 1, 1], "bots_team1"),           # A* bots vs tape
+    (6, 8, 300, 0, [0, 1, 1], "bots_all"),              # everyone an A* bot
 ]
 
 
@@ -64,6 +66,8 @@ def test_engine_matches_oracle_live(ts, worlds, steps, flags, ctrl, policy):
     for sim in (e, o):
         sim.put_ctrl(ctrl)
         sim.init()
+        if policy.startswith("bots"):
+            set_bots(sim, dict(worlds=worlds, team_size=ts, bots=policy[5:]))
     _compare_all(e, o, "init")
     A = worlds * 2 * ts
     for s in range(steps):
