@@ -71,6 +71,12 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="N>1: RCCL-gather obs/reward/done to rank 0 every step (learner mode)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--share-device", action="store_true",
+                    help="debug: map every rank to GPU 0 (rehearse N>1 on a one-GPU box; no --gather)")
+    ap.add_argument("--no-isolation", action="store_true",
+                    help="skip the isolated per-kernel window (profiling runs: keep launches uniform)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="debug: no per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--bots", choices=["none", "team1", "all"], default="none",
                     help="A* scripted bots (AgentPolicy -1, planAStarAISystem) for team 1 / everyone "
                          "(config C5's nav-mesh pathing); the headline C3 line uses none")
@@ -107,14 +113,17 @@ def cpu_baseline(args, world_size):
     }
 
 
-def load_traffic(path, workload):
+VALU_PEAK = 256 * 4 * 0.5 * 2.4e9  # wave-instr/s: 256 CUs x 4 SIMD32 x 1/2 per clock x 2.4 GHz
+
+
+def load_profile(path, workload):
+    """profiles/pmc_traffic.json (tools/pmc_summary.py) if it was collected
+    on this workload: HBM bytes and VALU instructions per launch per kernel."""
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
-        return None, None
-    if d.get("workload") != workload:
-        return None, None
-    return d.get("kernel"), d.get("hbm_bytes_per_launch")
+        return {}
+    return d if d.get("workload") == workload else {}
 
 
 def main():
@@ -127,10 +136,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = 0 if args.share_device else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    gather_group = None
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # Control plane (barriers, max-over-ranks time) on gloo: the step has
+        # no data-path collective.  The optional learner gather runs on RCCL.
+        dist.init_process_group("gloo")
+        if args.gather:
+            if args.share_device:
+                raise SystemExit("--gather needs one GPU per rank")
+            gather_group = dist.new_group(backend="nccl")
 
     import madrona_mp_env as m
     from mpenv_dist import gather_to_learner
@@ -140,7 +157,7 @@ def main():
     N = 2 * ts
     A = W * N
     offset = rank * W  # weak scaling: each rank owns W global worlds
-    sim = m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=local, num_worlds=W, rand_seed=5,
+    sim = m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=gpu, num_worlds=W, rand_seed=5,
                        auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
                        team_size=ts, num_pbt_policies=0, policy_history_size=0,
                        scene_path=args.scene, world_id_offset=offset)
@@ -168,14 +185,14 @@ def main():
         sim.copy_actions(ring[s % RING].data_ptr(), sptr)
         sim.step_async(sptr)
         if outs is not None:
-            gather_to_learner(outs, dst=0)
+            gather_to_learner(outs, dst=0, group=gather_group)
 
     for s in range(args.warmup):
         one_step(s)
     torch.cuda.synchronize()
     if world_size > 1:
         dist.barrier()
-    sim.enable_kernel_timing(True)
+    sim.enable_kernel_timing(not args.no_kernel_timing)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
@@ -185,11 +202,29 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timings = sim.kernel_timings()  # {name: (avg ms, launches)}
+    if args.no_kernel_timing:
+        print(json.dumps({"value": world_size * A * args.steps / elapsed, "ms_per_step": 1e3 * elapsed / args.steps}))
+        return
     sim.enable_kernel_timing(False)
     if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # Isolation window (after the timed region, not part of `value`): each
+    # kernel alone on the GPU, one launch per step, so its duration is not
+    # shared with the overlapped world groups of the timed region.
+    groups = sim.world_groups()
+    iso = None
+    if groups > 1 and not args.no_isolation:
+        sim.set_world_groups(1)
+        sim.enable_kernel_timing(True)
+        for s in range(30):
+            one_step(args.warmup + args.steps + s)
+        torch.cuda.synchronize()
+        iso = sim.kernel_timings()
+        sim.enable_kernel_timing(False)
+        sim.set_world_groups(groups)
 
     total_agent_steps = world_size * A * args.steps
     value = total_agent_steps / elapsed
@@ -198,12 +233,16 @@ def main():
     # dominant kernel and its HBM roofline
     dom = max(timings, key=lambda k: timings[k][0])
     dom_ms = timings[dom][0]
-    alg = KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W
+    # world groups: each step launches every kernel once per group (stream)
+    lps = max(1, round(timings[dom][1] / args.steps))
+    alg = (KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W) // lps
     achieved = alg / (dom_ms * 1e-3) / 1e9
     workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})")
-    tk, traffic = load_traffic(args.traffic, workload)
+    prof = load_profile(args.traffic, workload)
+    traffic = prof.get("per_kernel", {}).get(dom)
+    valu = prof.get("valu_insts_per_launch", {}).get(dom)
     step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W
-    kern_ms = sum(v[0] for v in timings.values())
+    kern_ms = sum(v[0] for v in timings.values()) * lps
 
     result = {
         "metric": "env steps/sec x agents (whole node), simple_map 6v6 @ 16384 worlds",
@@ -238,15 +277,37 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic if tk == dom else None,
+            "traffic": traffic,
             "algorithmic_bytes_per_launch": alg,
+            "launches_per_step": lps,
+            # the ray kernels are VALU-issue bound, not HBM bound: their VALU
+            # instructions per launch (PMC, profiles/) over the live duration
+            "valu_issue": None if not valu else {
+                "insts_per_launch": valu,
+                "achieved_per_s": round(valu / (dom_ms * 1e-3), 1),
+                "peak_per_s": VALU_PEAK,
+                "frac": round(valu / (dom_ms * 1e-3) / VALU_PEAK, 4),
+            },
         },
         "kernels_ms": {k: round(v[0], 4) for k, v in timings.items()},
+        "world_groups": groups,
         "step_hbm": {
             "algorithmic_bytes_per_step": step_bytes,
             "achieved_GBps_over_kernels": round(step_bytes / (kern_ms * 1e-3) / 1e9, 2),
         },
     }
+    if iso is not None:
+        idom = max(iso, key=lambda k: iso[k][0])
+        ibytes = KERNEL_BYTES_PER_AGENT[idom] * A + KERNEL_BYTES_PER_WORLD[idom] * W
+        result["roofline_isolated"] = {
+            "note": "30 steps after the timed region with world groups = 1 (each kernel alone)",
+            "kernel": idom,
+            "achieved": round(ibytes / (iso[idom][0] * 1e-3) / 1e9, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(ibytes / (iso[idom][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "kernels_ms": {k: round(v[0], 4) for k, v in iso.items()},
+        }
     if rank == 0 and world_size == 1 and args.cpu_baseline == "auto":
         result["cpu_baseline"] = cpu_baseline(args, world_size)
     if rank == 0:

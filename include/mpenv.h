@@ -253,6 +253,13 @@ int mpenv_copy_actions(mpenv_manager *mgr, const int32_t *src_device, void *hip_
 int mpenv_debug_trace_rays(mpenv_manager *mgr, const float *o_device, const float *d_device, int32_t n,
                            int32_t mode, float *t_device, int32_t *hit_device, void *hip_stream);
 
+/* Extension: step the worlds as `groups` contiguous ranges on concurrent
+ * HIP streams (fork/join on the step stream; results identical for any
+ * split).  Default: 3 for >= 3072 worlds, else 1; env MPENV_WORLD_GROUPS
+ * overrides at creation.  Capped at 3. */
+int mpenv_set_world_groups(mpenv_manager *mgr, int32_t groups);
+int mpenv_world_groups(mpenv_manager *mgr, int32_t *groups);
+
 /* Manager::triggerReset (mgr.cpp:2484-2500) */
 int mpenv_trigger_reset(mpenv_manager *mgr, int32_t world_idx);
 /* Manager::setPvPAction (mgr.cpp:2518-2566) */

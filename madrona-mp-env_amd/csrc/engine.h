@@ -64,6 +64,7 @@ enum : int32_t {
 struct DevState {
     int32_t W, N, T;
     int64_t A;
+    int64_t dmgStride;     // row stride of dmg (all agents of the manager)
 
 #define MP_DECL_F(n) float *n;
 #define MP_DECL_I(n) int32_t *n;

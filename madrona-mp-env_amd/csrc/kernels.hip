@@ -573,7 +573,7 @@ __device__ void fireD(const DevState &S, const LBVH &bvh, int w, int i)
     if (success) {
         S.landedOn[g] = h.entity;
         if (S.hp[g0 + h.entity] <= c::kDmgPerBullet) flags |= kFlagSuccessfulKill;
-        S.dmg[(int64_t)offset * S.A + g0 + h.entity] = c::kDmgPerBullet;
+        S.dmg[(int64_t)offset * S.dmgStride + g0 + h.entity] = c::kDmgPerBullet;
     }
     S.flags[g] = flags;
 }
@@ -587,7 +587,7 @@ __device__ void applyDmgD(const DevState &S, int64_t g)
     if (rs > 0) S.respawnSteps[g] = rs - 1;
     float hp = S.hp[g];
     for (int k = 0; k < S.T; k++) {
-        const int64_t di = (int64_t)k * S.A + g;
+        const int64_t di = (int64_t)k * S.dmgStride + g;
         float d = S.dmg[di];
         if (d > 0.f) {
             was_shot += 1;
@@ -1324,7 +1324,7 @@ __global__ void __launch_bounds__(64) k_construct(DevState S, SceneDev sc, int32
         S.discreteAim[2 * g] = c::kDiscreteAimYawBuckets / 2;
         S.discreteAim[2 * g + 1] = c::kDiscreteAimPitchBuckets / 2;
         S.dyv[g] = 0.f; S.dpv[g] = 0.f;
-        for (int k = 0; k < kMaxTeamSize; k++) S.dmg[(int64_t)k * S.A + g] = 0.f;
+        for (int k = 0; k < kMaxTeamSize; k++) S.dmg[(int64_t)k * S.dmgStride + g] = 0.f;
         stRot(S, g, quat(1, 0, 0, 0));
         stAimRot(S, g, quat(1, 0, 0, 0));
         S.landedOn[g] = -1;

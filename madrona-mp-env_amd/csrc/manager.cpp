@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -107,6 +108,15 @@ struct mpenv_manager {
     int32_t *dbgAI = nullptr, *dbgWI = nullptr;
     uint32_t *dbgExplore = nullptr;
 
+    // World groups: contiguous world ranges stepped on their own streams
+    // (fork/join with events) so independent kernels overlap on the GPU.
+    int groups = 1;
+    std::vector<hipStream_t> gstreams;
+    std::vector<DevState> gS;
+    std::vector<SceneDev> gsc;
+    hipEvent_t forkEv = nullptr;
+    std::vector<hipEvent_t> joinEv;
+
     // Kernel timing
     bool timing = false;
     std::vector<hipEvent_t> eventPool;
@@ -115,7 +125,11 @@ struct mpenv_manager {
     ~mpenv_manager()
     {
         if (stream) (void)hipStreamSynchronize(stream);
+        for (hipStream_t gs : gstreams) (void)hipStreamSynchronize(gs);
         for (hipEvent_t e : eventPool) (void)hipEventDestroy(e);
+        for (hipEvent_t e : joinEv) (void)hipEventDestroy(e);
+        if (forkEv) (void)hipEventDestroy(forkEv);
+        for (hipStream_t gs : gstreams) (void)hipStreamDestroy(gs);
         for (void *p : allocations) (void)hipFree(p);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -154,20 +168,40 @@ struct mpenv_manager {
         if (timing) HIP_CHECK(hipEventRecord(nextEvent(), st));
     }
 
-    void runStep(hipStream_t st)
+    // The Step graph over one world range on one stream.  With timing on,
+    // kNumTimedKernels + 1 events bracket the kernels (one segment per
+    // range per step, contiguous in the pool).
+    void stepRange(const DevState &R, const SceneDev &rsc, hipStream_t st)
     {
         record(st);
-        if (launchMove(S, sc, st)) throw std::runtime_error("k_move launch failed");
+        if (launchMove(R, rsc, st)) throw std::runtime_error("k_move launch failed");
         record(st);
-        if (launchSimStep(S, sc, st)) throw std::runtime_error("k_sim launch failed");
+        if (launchSimStep(R, rsc, st)) throw std::runtime_error("k_sim launch failed");
         record(st);
-        if (launchVisibility(S, sc, st)) throw std::runtime_error("k_vis launch failed");
+        if (launchVisibility(R, rsc, st)) throw std::runtime_error("k_vis launch failed");
         record(st);
-        if (launchObservations(S, sc, st)) throw std::runtime_error("k_obs launch failed");
+        if (launchObservations(R, rsc, st)) throw std::runtime_error("k_obs launch failed");
         record(st);
-        if (launchLidar(S, sc, st)) throw std::runtime_error("k_lidar launch failed");
+        if (launchLidar(R, rsc, st)) throw std::runtime_error("k_lidar launch failed");
         record(st);
     }
+
+    void runStep(hipStream_t st)
+    {
+        if (groups <= 1) {
+            stepRange(S, sc, st);
+            return;
+        }
+        HIP_CHECK(hipEventRecord(forkEv, st));
+        for (int i = 0; i < groups; i++) HIP_CHECK(hipStreamWaitEvent(gstreams[i], forkEv, 0));
+        for (int i = 0; i < groups; i++) {
+            stepRange(gS[i], gsc[i], gstreams[i]);
+            HIP_CHECK(hipEventRecord(joinEv[i], gstreams[i]));
+        }
+        for (int i = 0; i < groups; i++) HIP_CHECK(hipStreamWaitEvent(st, joinEv[i], 0));
+    }
+
+    void setupGroups(int want);
 
     void runInitGraph(hipStream_t st)
     {
@@ -360,6 +394,7 @@ static void allocState(mpenv_manager &m)
 #undef MP_ALLOC_WI
 #undef MP_ALLOC_WF
     S.dmg = m.alloc<float>(A * kMaxTeamSize);
+    S.dmgStride = (int64_t)A;
     S.visMask = m.alloc<uint8_t>(A);
     S.visited = m.alloc<uint32_t>(A * kGridCells);
     S.filtLast = m.alloc<int32_t>(W * 6);
@@ -395,6 +430,100 @@ static void allocState(mpenv_manager &m)
     S.magazine = m.alloc<int32_t>(A * 2);
     S.rewardCoefs = m.alloc<float>(A * 9);
     S.trainCtrl = m.alloc<int32_t>(3);
+}
+
+// A contiguous world range [w0, w0 + nw) of the manager viewed as a complete
+// engine: every per-agent / per-world column offset to the range, W/A set
+// to its size, and the scene's world-id offset advanced so RNG keys stay
+// global.  Worlds never read each other, so step kernels launched on
+// different ranges are independent and can run on concurrent streams.
+static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_t nw, int32_t track_len,
+                       DevState &G, SceneDev &gsc)
+{
+    G = S;
+    gsc = sc;
+    const int64_t g0 = w0 * S.N;
+    G.W = (int32_t)nw;
+    G.A = nw * S.N;
+    gsc.worldOffset = sc.worldOffset + (uint32_t)w0;
+#define MP_SL_A(n) G.n = S.n + g0;
+#define MP_SL_W(n) G.n = S.n + w0;
+    MP_AGENT_F32(MP_SL_A)
+    MP_AGENT_I32(MP_SL_A)
+    MP_WORLD_I32(MP_SL_W)
+    MP_WORLD_F32(MP_SL_W)
+#undef MP_SL_A
+#undef MP_SL_W
+    G.dmg = S.dmg + g0; // stride stays S.dmgStride
+    G.visMask = S.visMask + g0;
+    G.visited = S.visited + g0 * kGridCells;
+    G.filtLast = S.filtLast + w0 * 6;
+    G.zoneStats = S.zoneStats + w0 * 25;
+    G.spawnTrack = S.spawnTrack + w0 * 3 * track_len;
+    G.crumbs = S.crumbs + w0 * kMaxCrumbs * 2;
+    G.reset = S.reset + w0;
+    G.worldCurr = S.worldCurr + w0;
+    G.matchResult = S.matchResult + w0 * 30;
+    G.exploreAction = S.exploreAction + g0 * 4;
+    G.discreteAction = S.discreteAction + g0 * 4;
+    G.aimAction = S.aimAction + g0 * 2;
+    G.discreteAim = S.discreteAim + g0 * 2;
+    G.policy = S.policy + g0;
+    G.botAction = S.botAction + g0 * 7;
+    G.reward = S.reward + g0;
+    G.done = S.done + g0;
+    G.selfObs = S.selfObs + g0 * kSelfObs;
+    G.filters = S.filters + g0;
+    G.tmObs = S.tmObs + g0 * 5 * kOtherObs;
+    G.oppObs = S.oppObs + g0 * 6 * kOtherObs;
+    G.lkObs = S.lkObs + g0 * 6 * kOtherObs;
+    G.selfPos = S.selfPos + g0 * 3;
+    G.tmPos = S.tmPos + g0 * 15;
+    G.oppPos = S.oppPos + g0 * 18;
+    G.lkPos = S.lkPos + g0 * 18;
+    G.masks = S.masks + g0 * 6;
+    G.fwdLidar = S.fwdLidar + g0 * kFwdRays * 4;
+    G.rearLidar = S.rearLidar + g0 * kRearRays * 4;
+    G.agentMap = S.agentMap + g0 * 16 * 16 * 4;
+    G.hp = S.hp + g0;
+    G.alive = S.alive + g0;
+    G.magazine = S.magazine + g0 * 2;
+    G.rewardCoefs = S.rewardCoefs + g0 * 9;
+}
+
+void mpenv_manager::setupGroups(int want)
+{
+    // release a previous split
+    for (hipStream_t gs : gstreams) {
+        HIP_CHECK(hipStreamSynchronize(gs));
+        HIP_CHECK(hipStreamDestroy(gs));
+    }
+    for (hipEvent_t e : joinEv) HIP_CHECK(hipEventDestroy(e));
+    if (forkEv) HIP_CHECK(hipEventDestroy(forkEv));
+    gstreams.clear();
+    joinEv.clear();
+    gS.clear();
+    gsc.clear();
+    forkEv = nullptr;
+    // at most 3: with the manager's own stream that is the 4 hardware queues
+    // a process gets by default (GPU_MAX_HW_QUEUES); more would share queues
+    groups = std::max(1, std::min(std::min(want, 3), S.W));
+    if (groups == 1) return;
+    HIP_CHECK(hipEventCreateWithFlags(&forkEv, hipEventDisableTiming));
+    for (int i = 0; i < groups; i++) {
+        const int64_t w0 = (int64_t)S.W * i / groups, w1 = (int64_t)S.W * (i + 1) / groups;
+        DevState G;
+        SceneDev gs;
+        sliceState(S, sc, w0, w1 - w0, sc.spawnTrackLen, G, gs);
+        gS.push_back(G);
+        gsc.push_back(gs);
+        hipStream_t st;
+        HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        gstreams.push_back(st);
+        hipEvent_t ev;
+        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        joinEv.push_back(ev);
+    }
 }
 
 extern "C" {
@@ -455,6 +584,12 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m->S.N = 2 * m->S.T;
         m->S.A = (int64_t)m->S.W * m->S.N;
         allocState(*m);
+        {
+            // World groups (concurrent streams).  MPENV_WORLD_GROUPS overrides.
+            int want = m->S.W >= 3072 ? 3 : 1;
+            if (const char *e = std::getenv("MPENV_WORLD_GROUPS")) want = std::atoi(e);
+            m->setupGroups(want);
+        }
         // TrainControl from sim flags (mgr.cpp:1397-1413)
         int32_t tc[3] = { (cfg->sim_flags & MPENV_SIMFLAG_SIM_EVAL_MODE) ? 1 : 0,
                           (cfg->sim_flags & MPENV_SIMFLAG_STAGGER_STARTS) ? 1 : 0,
@@ -598,6 +733,25 @@ int mpenv_debug_trace_rays(mpenv_manager *m, const float *o, const float *d, int
     hipStream_t st = stream ? (hipStream_t)stream : m->stream;
     if (launchTraceRays(m->sc, o, d, n, mode, t_out, hit_out, st) || hipStreamSynchronize(st) != hipSuccess)
         return fail(MPENV_ERR_HIP, "trace-ray launch failed");
+    return MPENV_OK;
+}
+
+int mpenv_set_world_groups(mpenv_manager *m, int32_t groups)
+{
+    if (!m || groups < 1) return fail(MPENV_ERR_INVALID, "bad argument");
+    try {
+        HIP_CHECK(hipStreamSynchronize(m->stream));
+        m->setupGroups(groups);
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_world_groups(mpenv_manager *m, int32_t *groups)
+{
+    if (!m || !groups) return fail(MPENV_ERR_INVALID, "bad argument");
+    *groups = m->groups;
     return MPENV_OK;
 }
 

@@ -222,6 +222,8 @@ PYBIND11_MODULE(madrona_mp_env, m)
         .def("copy_actions", [](PySimManager &s, uintptr_t src, uintptr_t stream) {
             check(mpenv_copy_actions(s.h->mgr, reinterpret_cast<const int32_t *>(src), reinterpret_cast<void *>(stream)));
         }, py::arg("src"), py::arg("stream") = 0)
+        .def("set_world_groups", [](PySimManager &s, int32_t g) { check(mpenv_set_world_groups(s.h->mgr, g)); })
+        .def("world_groups", [](PySimManager &s) { int32_t g = 0; check(mpenv_world_groups(s.h->mgr, &g)); return g; })
         .def("enable_kernel_timing", [](PySimManager &s, bool on) { check(mpenv_enable_kernel_timing(s.h->mgr, on)); })
         .def("kernel_timings", [](PySimManager &s) {
             const char *names[16];

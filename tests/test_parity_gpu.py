@@ -321,3 +321,34 @@ def test_bvh_traversal_matches_oracle_on_edge_cases():
         assert hit == res[1][1][i], i
         if hit:
             assert tt.value == res[1][0][i], (i, tt.value, res[1][0][i])
+
+
+def test_world_groups_on_streams_match_oracle(monkeypatch):
+    """Worlds split into 3 uneven groups stepped on concurrent streams
+    (MPENV_WORLD_GROUPS) give the oracle's results for worlds at the group
+    boundaries."""
+    monkeypatch.setenv("MPENV_WORLD_GROUPS", "3")
+    ts, W, steps = 2, 2050, 60
+    N = 2 * ts
+    e = T.Engine(W, ts, sim_flags=1)
+    e.put_ctrl([0, 1, 1])
+    e.init()
+    probes = [0, 682, 683, 1366, 1367, W - 2]
+    oracles = []
+    for w0 in probes:
+        o = T.Oracle(2, ts, sim_flags=1, world_id_offset=w0)
+        o.put_ctrl([0, 1, 1])
+        o.init()
+        oracles.append(o)
+    for s in range(steps):
+        e.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, W * N))
+        e.step()
+        for w0, o in zip(probes, oracles):
+            o.set_actions(T.mpenv_tape.tape_actions(1234, s, w0 * N, 2 * N))
+            o.step()
+        if s % 7 == 0 or s == steps - 1:
+            for w0, o in zip(probes, oracles):
+                for n in T.STEP_OUTPUTS:
+                    _, _, shape = e.desc(n)
+                    r0, r1 = (w0, w0 + 2) if shape[0] == W else (w0 * N, (w0 + 2) * N)
+                    T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
