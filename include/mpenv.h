@@ -108,8 +108,15 @@ enum mpenv_export_id {
     MPENV_EXPORT_DEBUG_WORLD_I32 = 67, /* [W][MPENV_DBG_WI_COUNT] */
     MPENV_EXPORT_DEBUG_WORLD_F32 = 68, /* [W][MPENV_DBG_WF_COUNT] */
     MPENV_EXPORT_DEBUG_EXPLORE = 69,   /* [A][81*81] u32 ExploreTracker.visited */
-    MPENV_EXPORT_DEBUG_CRUMBS = 70     /* [W][MPENV_MAX_CRUMBS][8] f32 breadcrumb pool */
+    MPENV_EXPORT_DEBUG_CRUMBS = 70,    /* [W][MPENV_MAX_CRUMBS][8] f32 breadcrumb pool */
+    MPENV_EXPORT_RECORD_LOG = 71,      /* [W] mpenv_step_log as i32[W][217] (record mode) */
+    MPENV_EXPORT_REPLAY_LOG = 72,      /* [W] mpenv_step_log as i32[W][217] (replay mode) */
+    MPENV_EXPORT_SNAPSHOT_WRITTEN = 73 /* [W][1] i32: snapshot written this step (event log) */
 };
+/* EVENT_LOG (36): this step's GameEvent slots as i32[W][2N+1][6] (slot 2i, 2i+1
+ * = agent i's reload / shot / kill, slot 2N = capture; type 0 = empty).
+ * PACKED_STEP_SNAPSHOT (37): i32[W][48] mpenv_packed_step_snapshot.  Both
+ * exist only when an event log directory is configured. */
 
 /* Debug-state column layouts (parity tests compare these bit-exactly). */
 enum mpenv_dbg_agent_f32 {
@@ -182,6 +189,81 @@ enum mpenv_dbg_world_f32 {
  * bounded by ~6 per agent; creations beyond capacity are
  * dropped and counted in MPENV_DBG_WI_CRUMB_OVERFLOW. */
 #define MPENV_MAX_CRUMBS 128
+
+/* ---- Record / replay / event-log wire formats ----
+ * Byte-compatible with the reference's structs (little-endian, natural
+ * alignment), so files written here and by the reference interchange. */
+
+/* AgentLogData (types.hpp:574-584): 72 bytes */
+typedef struct mpenv_agent_log {
+    float position[3];
+    float aim_yaw, aim_pitch;
+    float aim_rot[4];          /* Quat w, x, y, z */
+    float hp;
+    int32_t mag_num_bullets, mag_is_reloading;
+    int32_t cur_pose, tgt_pose, transition_remaining; /* StandState */
+    int32_t shot_agent_idx;    /* -1 = none */
+    float fired_shot_t;
+    uint8_t was_killed, successful_kill;
+    uint8_t pad_[2];
+} mpenv_agent_log;
+
+/* StepLog (types.hpp:586-589): 868 bytes, one per world per step in the
+ * record / replay file (world-major). */
+typedef struct mpenv_step_log {
+    mpenv_agent_log agents[12];
+    int32_t cur_step;
+} mpenv_step_log;
+
+/* EventType (types.hpp:614-620) */
+#define MPENV_EVENT_CAPTURE 1u
+#define MPENV_EVENT_RELOAD 2u
+#define MPENV_EVENT_KILL 4u
+#define MPENV_EVENT_PLAYER_SHOT 8u
+
+/* GameEvent (types.hpp:729-760): 24 bytes.  a/b/c16 hold the union:
+ *   Capture    {u8 zoneIDX, u8 captureTeam, u16 inZoneMask}
+ *   Reload     {u8 player,  u8 numBulletsAtReloadTime}
+ *   Kill       {u8 killer,  u8 killed}
+ *   PlayerShot {u8 attacker, u8 target}
+ * Player ids are team * 6 + offset within the team. */
+typedef struct mpenv_game_event {
+    uint32_t type;
+    uint32_t pad_;
+    uint64_t match_id;
+    uint32_t step;
+    uint8_t a, b;
+    uint16_t c16;
+} mpenv_game_event;
+
+/* PackedPlayerSnapshot (types.hpp:603-612): 14 bytes */
+typedef struct mpenv_packed_player {
+    int16_t pos[3];
+    int16_t yaw, pitch;
+    uint8_t mag_num_bullets, is_reloading, hp, flags; /* flags: 2 FiredShot, 4 Crouch, 8 Prone */
+} mpenv_packed_player;
+
+/* PackedStepSnapshot (types.hpp:622-636): 192 bytes, one per world per step
+ * in steps.bin. */
+typedef struct mpenv_packed_step_snapshot {
+    uint32_t num_events;       /* the reference stores a 0/1 "any event" flag */
+    uint32_t event_mask;
+    uint64_t match_id;
+    uint16_t step;
+    uint8_t cur_zone;
+    int8_t cur_zone_controller;
+    uint16_t zone_steps_remaining;
+    uint16_t steps_until_point;
+    mpenv_packed_player players[12];
+} mpenv_packed_step_snapshot;
+
+#ifdef __cplusplus
+static_assert(sizeof(mpenv_agent_log) == 72, "AgentLogData layout");
+static_assert(sizeof(mpenv_step_log) == 868, "StepLog layout");
+static_assert(sizeof(mpenv_game_event) == 24, "GameEvent layout");
+static_assert(sizeof(mpenv_packed_player) == 14, "PackedPlayerSnapshot layout");
+static_assert(sizeof(mpenv_packed_step_snapshot) == 192, "PackedStepSnapshot layout");
+#endif
 
 /* Tensor element types (madrona::py::TensorElementType subset) */
 #define MPENV_DTYPE_INT32 0

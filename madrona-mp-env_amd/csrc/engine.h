@@ -13,6 +13,7 @@
 
 #include <cstdint>
 
+#include "mpenv.h"
 #include "mpenv_core.h"
 #include "scene.h"
 
@@ -47,7 +48,8 @@ constexpr int kMaxBVHStack = 16; // register byte-stack capacity
     X(captured) X(earned) X(zoneSteps) X(stepsUntilPoint) X(episode) \
     X(episodeCounter) X(wRngA) X(wRngB) X(wRngCtr) X(filtAct0) X(filtAct1) \
     X(filtMatched0) X(filtMatched1) X(episodeCurr) X(numCrumbs) X(nextCrumbId) \
-    X(crumbOverflow) X(curTier) X(curSpawnIdx) X(spawnCurriculum)
+    X(crumbOverflow) X(curTier) X(curSpawnIdx) X(spawnCurriculum) \
+    X(matchValid) X(evLogged) X(evMask) X(snapWritten)
 
 #define MP_WORLD_F32(X) \
     X(teamRew0) X(teamRew1) X(goalMin0) X(goalMin1) X(goalTeam0) X(goalTeam1)
@@ -113,6 +115,13 @@ struct DevState {
     int32_t *magazine;     // [A][2]
     float *rewardCoefs;    // [A][9]
     int32_t *trainCtrl;    // [3]
+
+    // Record / replay / event logs (allocated only when enabled)
+    mpenv_step_log *recordLog;             // [W] written by the step
+    const mpenv_step_log *replayLog;       // [W] read by the step
+    mpenv_game_event *events;              // [W][evStride] slots: 2 per agent + capture
+    mpenv_packed_step_snapshot *snapshots; // [W]
+    int32_t evStride;                      // 2 * N + 1
 };
 
 struct ZOBBDev {
@@ -154,6 +163,8 @@ struct SceneDev {
     const float *navTris;   // 9 floats per triangle (deduplicated vertices)
     const int32_t *astar;   // [numNavTris][numNavTris] next hop
     int32_t numNavTris;
+    // logs (sim.cpp:4750-4843 record/replay, 23-106 + 4592-4634 events)
+    int32_t recordOn, replayOn, eventsOn;
 };
 
 // Host launchers (kernels.hip)

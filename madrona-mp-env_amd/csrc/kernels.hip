@@ -510,7 +510,29 @@ __device__ void fallD(const DevState &S, const LBVH &bvh, int64_t g)
 }
 
 // sim.cpp:1443-1615 fireSystem
-__device__ void fireD(const DevState &S, const LBVH &bvh, int w, int i)
+// ---- event log (sim.cpp:23-39 logEvent; GameEvent types.hpp:729-760)
+__device__ __forceinline__ uint64_t matchIdD(const DevState &S, const SceneDev &sc, int w)
+{
+    return ((uint64_t)(sc.worldOffset + (uint32_t)w) << 32) | (uint64_t)(uint32_t)S.episode[w];
+}
+
+__device__ __forceinline__ void putEventD(const DevState &S, const SceneDev &sc, int w, int slot, uint32_t type,
+                                          int a, int b, int c16)
+{
+    mpenv_game_event ev;
+    ev.type = type;
+    ev.pad_ = 0;
+    ev.match_id = matchIdD(S, sc, w);
+    ev.step = (uint32_t)S.curStep[w];
+    ev.a = (uint8_t)a;
+    ev.b = (uint8_t)b;
+    ev.c16 = (uint16_t)c16;
+    S.events[(int64_t)w * S.evStride + slot] = ev;
+}
+
+__device__ __forceinline__ int playerIdD(const DevState &S, int i) { return (i / S.T) * kMaxTeamSize + i % S.T; }
+
+__device__ void fireD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -525,6 +547,7 @@ __device__ void fireD(const DevState &S, const LBVH &bvh, int w, int i)
     int32_t mag0 = S.magazine[2 * g], mag1 = S.magazine[2 * g + 1];
     const int fire = S.discreteAction[4 * g + 2];
     if (fire == 2) {
+        if (sc.eventsOn) putEventD(S, sc, w, 2 * i, MPENV_EVENT_RELOAD, playerIdD(S, i), mag0, 0);
         if (mag0 == c::kMagSize) flags |= kFlagReloadedFullMag;
         mag0 = c::kMagSize;
         mag1 = c::kReloadTime;
@@ -571,8 +594,12 @@ __device__ void fireD(const DevState &S, const LBVH &bvh, int w, int i)
         if (success && S.respawnSteps[g0 + h.entity] > 0) success = false;
     }
     if (success) {
+        if (sc.eventsOn) putEventD(S, sc, w, 2 * i, MPENV_EVENT_PLAYER_SHOT, playerIdD(S, i), playerIdD(S, h.entity), 0);
         S.landedOn[g] = h.entity;
-        if (S.hp[g0 + h.entity] <= c::kDmgPerBullet) flags |= kFlagSuccessfulKill;
+        if (S.hp[g0 + h.entity] <= c::kDmgPerBullet) {
+            flags |= kFlagSuccessfulKill;
+            if (sc.eventsOn) putEventD(S, sc, w, 2 * i + 1, MPENV_EVENT_KILL, playerIdD(S, i), playerIdD(S, h.entity), 0);
+        }
         S.dmg[(int64_t)offset * S.dmgStride + g0 + h.entity] = c::kDmgPerBullet;
     }
     S.flags[g] = flags;
@@ -838,6 +865,7 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
 __device__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool triggered_reset, const int32_t *tc)
 {
     const uint32_t world_id = sc.worldOffset + (uint32_t)w;
+    S.matchValid[w] = 1; // matchID = worldID << 32 | curEpisodeIdx (sim.cpp:736-738)
     S.episodeCurr[w] = S.worldCurr[w];
     const uint32_t ep = (uint32_t)S.episode[w];
     RandKey episode_key = splitI(sc.initRandKey, ep, world_id);
@@ -1103,7 +1131,9 @@ __device__ void updateFiltersD(const DevState &S, int w, int cur_step)
 }
 
 // sim.cpp:4470-4673 zoneMatchInfoSystem
-__device__ void zoneMatchInfoD(const DevState &S, int w)
+__device__ void writeSnapshotD(const DevState &S, const SceneDev &sc, int w, bool new_captured);
+
+__device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1143,6 +1173,7 @@ __device__ void zoneMatchInfoD(const DevState &S, int w)
         if (S.contested[w]) zs[3] += 1;
         if (new_captured) zs[0] += 1;
         updateFiltersD(S, w, cur_step);
+        if (sc.eventsOn) writeSnapshotD(S, sc, w, new_captured);
     }
     if (finished) {
         if (mr[3] > mr[4]) mr[0] = 0;
@@ -1153,6 +1184,131 @@ __device__ void zoneMatchInfoD(const DevState &S, int w)
     }
     S.curStep[w] = cur_step;
     S.finished[w] = finished ? 1 : 0;
+}
+
+// Capture event + writePackedStepSnapshot (sim.cpp:4592-4634, 41-106).  The
+// reference's per-world eventLoggedInStep / eventMask accumulate from every
+// logEvent since the last snapshot; here they are folded in from this
+// step's event slots, and reset when a snapshot is written (only for a
+// valid matchID, i.e. after the first triggered reset).
+__device__ void writeSnapshotD(const DevState &S, const SceneDev &sc, int w, bool new_captured)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    const bool valid = S.matchValid[w] != 0;
+    if (valid && new_captured) {
+        const int cz = S.curZone[w];
+        AABB za = sc.zoneAABB[cz];
+        Quat to_zone = qinv(angleAxis(sc.zoneRot[cz], kUp));
+        za.pMin = rotateVec(to_zone, za.pMin);
+        za.pMax = rotateVec(to_zone, za.pMax);
+        uint32_t mask = 0;
+        const int ctrl = S.controlling[w];
+        for (int i = 0; i < N; i++) {
+            if (i / S.T != ctrl) continue;
+            Vec3 p = ldPos(S, g0 + i);
+            p.z += c::kStandHeight / 2.f;
+            if (aabbContains(za, rotateVec(to_zone, p))) mask |= 1u << i;
+        }
+        putEventD(S, sc, w, 2 * N, MPENV_EVENT_CAPTURE, cz, ctrl, (int)mask);
+    }
+    int32_t logged = S.evLogged[w], emask = S.evMask[w];
+    const mpenv_game_event *ev = &S.events[(int64_t)w * S.evStride];
+    for (int k = 0; k < S.evStride; k++) {
+        if (ev[k].type != 0) {
+            logged = 1;
+            emask |= (int32_t)ev[k].type;
+        }
+    }
+    if (!valid) {
+        S.evLogged[w] = logged;
+        S.evMask[w] = emask;
+        S.snapWritten[w] = 0;
+        return;
+    }
+    mpenv_packed_step_snapshot sn;
+    sn.num_events = (uint32_t)logged;
+    sn.event_mask = (uint32_t)emask;
+    sn.match_id = matchIdD(S, sc, w);
+    sn.step = (uint16_t)S.curStep[w];
+    sn.cur_zone = (uint8_t)S.curZone[w];
+    sn.cur_zone_controller = (int8_t)(S.captured[w] ? S.controlling[w] : -1);
+    sn.zone_steps_remaining = (uint16_t)S.zoneSteps[w];
+    sn.steps_until_point = (uint16_t)S.stepsUntilPoint[w];
+    for (int i = 0; i < kMaxAgents; i++) {
+        mpenv_packed_player &pl = sn.players[i];
+        if (i >= N) {
+            pl = mpenv_packed_player {};
+            continue;
+        }
+        const int64_t g = g0 + i;
+        // float -> i16 through i32 (in range except yaw == +pi, which wraps)
+        pl.pos[0] = (int16_t)(int32_t)S.px[g];
+        pl.pos[1] = (int16_t)(int32_t)S.py[g];
+        pl.pos[2] = (int16_t)(int32_t)S.pz[g];
+        pl.yaw = (int16_t)(int32_t)(S.ayaw[g] * 32768 / kPi);
+        pl.pitch = (int16_t)(int32_t)(S.apitch[g] * 32768 / kPi);
+        pl.mag_num_bullets = (uint8_t)(uint16_t)S.magazine[2 * g];
+        pl.is_reloading = (uint8_t)S.magazine[2 * g + 1];
+        pl.hp = (uint8_t)S.hp[g];
+        uint8_t fl = 0;
+        if (S.landedOn[g] != -1) fl |= 2;
+        if (S.curPose[g] == kCrouch) fl |= 4;
+        else if (S.curPose[g] == kProne) fl |= 8;
+        pl.flags = fl;
+    }
+    S.snapshots[w] = sn;
+    S.evLogged[w] = 0;
+    S.evMask[w] = 0;
+    S.snapWritten[w] = 1;
+}
+
+// pvpRecordSystem (sim.cpp:4750-4792): per agent lane + curStep by the world lane
+__device__ void recordAgentD(const DevState &S, int w, int i)
+{
+    const int64_t g = (int64_t)w * S.N + i;
+    mpenv_agent_log &a = S.recordLog[w].agents[i];
+    a.position[0] = S.px[g]; a.position[1] = S.py[g]; a.position[2] = S.pz[g];
+    a.aim_yaw = S.ayaw[g];
+    a.aim_pitch = S.apitch[g];
+    a.aim_rot[0] = S.aw[g]; a.aim_rot[1] = S.ax[g]; a.aim_rot[2] = S.ay[g]; a.aim_rot[3] = S.az[g];
+    a.hp = S.hp[g];
+    a.mag_num_bullets = S.magazine[2 * g];
+    a.mag_is_reloading = S.magazine[2 * g + 1];
+    a.cur_pose = S.curPose[g];
+    a.tgt_pose = S.tgtPose[g];
+    a.transition_remaining = S.transRem[g];
+    a.shot_agent_idx = S.landedOn[g];
+    a.fired_shot_t = S.firedT[g];
+    a.was_killed = (S.flags[g] & kFlagWasKilled) ? 1 : 0;
+    a.successful_kill = (S.flags[g] & kFlagSuccessfulKill) ? 1 : 0;
+    a.pad_[0] = 0;
+    a.pad_[1] = 0;
+}
+
+// pvpReplaySystem (sim.cpp:4794-4843) for one agent (shot visualisation,
+// viewer-only, is skipped)
+__device__ void replayAgentD(const DevState &S, int w, int i)
+{
+    const int64_t g = (int64_t)w * S.N + i;
+    const mpenv_agent_log &a = S.replayLog[w].agents[i];
+    S.px[g] = a.position[0]; S.py[g] = a.position[1]; S.pz[g] = a.position[2];
+    S.ayaw[g] = a.aim_yaw;
+    S.apitch[g] = a.aim_pitch;
+    S.aw[g] = a.aim_rot[0]; S.ax[g] = a.aim_rot[1]; S.ay[g] = a.aim_rot[2]; S.az[g] = a.aim_rot[3];
+    stRot(S, g, qnormalize(angleAxis(a.aim_yaw, kUp)));
+    S.hp[g] = a.hp;
+    S.magazine[2 * g] = a.mag_num_bullets;
+    S.magazine[2 * g + 1] = a.mag_is_reloading;
+    S.curPose[g] = a.cur_pose;
+    S.tgtPose[g] = a.tgt_pose;
+    S.transRem[g] = a.transition_remaining;
+    S.landedOn[g] = a.shot_agent_idx;
+    S.firedT[g] = a.fired_shot_t;
+    int32_t fl = S.flags[g] & ~(kFlagWasKilled | kFlagSuccessfulKill);
+    if (a.was_killed) fl |= kFlagWasKilled | kFlagHasDied;
+    if (a.successful_kill) fl |= kFlagSuccessfulKill;
+    S.flags[g] = fl;
 }
 
 // sim.cpp:3998-4087 distToZOBB + evaluateGoalRegionsSystem
@@ -1343,6 +1499,10 @@ __global__ void __launch_bounds__(64) k_construct(DevState S, SceneDev sc, int32
     S.worldCurr[w] = 1; // WorldCurriculum::FullMatch (sim.cpp:5959)
     const int32_t tc[3] = { tc0, tc1, tc2 };
     initWorldD(S, sc, w, true, tc);
+    S.matchValid[w] = 0; // matchID = ~0 after construction (sim.cpp:5971)
+    S.evLogged[w] = 0;
+    S.evMask[w] = 0;
+    S.snapWritten[w] = 0;
     for (int k = 0; k < 25; k++) S.zoneStats[(int64_t)w * 25 + k] = 0;
     S.filtAct0[w] = 0; S.filtAct1[w] = 0;
     S.filtMatched0[w] = -1; S.filtMatched1[w] = -1;
@@ -1378,6 +1538,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= S.A) return;
     planAStarD(S, sc, g);
+    if (sc.replayOn) return; // pvpReplayLogic replaces the gameplay systems (sim.cpp:5587-5605)
     applyBotActionsD(S, g);
     pvpMovementD(S, g);
     pvpAimD(S, g);
@@ -1403,25 +1564,44 @@ __global__ void __launch_bounds__(kSimBlock) k_sim(DevState S, SceneDev sc)
     const bool wlane = act && i == 0;
     const int64_t g = (int64_t)w * N + i;
 
-    if (act) fireD(S, bvh, w, i);
-    __syncthreads();
-    if (act) applyDmgD(S, g);
-    __syncthreads();
-    if (wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
-    __syncthreads();
-    if (act) autoHealD(S, g);
-    __syncthreads();
-    if (wlane) zoneSystemD(S, sc, w);
-    __syncthreads();
-    if (act) leaveBreadcrumbAgentD(S, w, g);
-    __syncthreads();
-    if (wlane) appendCrumbsD(S, w);
-    __syncthreads();
-    if (act) accumulateCrumbsD(S, w, i);
-    __syncthreads();
+    if (act && sc.eventsOn) { // ClearTmpNode<GameEventEntity> at step start (sim.cpp:5344)
+        mpenv_game_event *ev = &S.events[(int64_t)w * S.evStride];
+        ev[2 * i].type = 0;
+        ev[2 * i + 1].type = 0;
+        if (wlane) ev[2 * N].type = 0;
+    }
+    if (sc.replayOn) {
+        // pvpReplayLogic: pvpReplaySystem then zoneSystem
+        if (act) replayAgentD(S, w, i);
+        if (wlane) S.curStep[w] = S.replayLog[w].cur_step;
+        __syncthreads();
+        if (wlane) zoneSystemD(S, sc, w);
+        __syncthreads();
+    } else {
+        if (act) fireD(S, sc, bvh, w, i);
+        __syncthreads();
+        if (act) applyDmgD(S, g);
+        __syncthreads();
+        if (wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
+        __syncthreads();
+        if (act) autoHealD(S, g);
+        __syncthreads();
+        if (wlane) zoneSystemD(S, sc, w);
+        __syncthreads();
+        if (sc.recordOn) {
+            if (act) recordAgentD(S, w, i);
+            if (wlane) S.recordLog[w].cur_step = S.curStep[w];
+        }
+        if (act) leaveBreadcrumbAgentD(S, w, g);
+        __syncthreads();
+        if (wlane) appendCrumbsD(S, w);
+        __syncthreads();
+        if (act) accumulateCrumbsD(S, w, i);
+        __syncthreads();
+    }
     if (wlane) {
-        decayCrumbsD(S, w);
-        zoneMatchInfoD(S, w);
+        if (!sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem
+        zoneMatchInfoD(S, sc, w);
         goalRegionsD(S, sc, w);
     }
     __syncthreads();

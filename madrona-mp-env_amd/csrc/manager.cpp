@@ -117,6 +117,15 @@ struct mpenv_manager {
     hipEvent_t forkEv = nullptr;
     std::vector<hipEvent_t> joinEv;
 
+    // Record / replay / event logs (mgr.cpp:155-300: per-step file I/O
+    // around the Step graph)
+    FILE *replayFile = nullptr, *recordFile = nullptr, *eventsFile = nullptr, *stepsFile = nullptr;
+    bool replayEof = false;
+    std::vector<mpenv_step_log> hostLog;
+    std::vector<mpenv_game_event> hostEvents;
+    std::vector<mpenv_packed_step_snapshot> hostSnaps;
+    std::vector<int32_t> hostSnapWritten;
+
     // Kernel timing
     bool timing = false;
     std::vector<hipEvent_t> eventPool;
@@ -130,6 +139,8 @@ struct mpenv_manager {
         for (hipEvent_t e : joinEv) (void)hipEventDestroy(e);
         if (forkEv) (void)hipEventDestroy(forkEv);
         for (hipStream_t gs : gstreams) (void)hipStreamDestroy(gs);
+        for (FILE *f : { replayFile, recordFile, eventsFile, stepsFile })
+            if (f) std::fclose(f);
         for (void *p : allocations) (void)hipFree(p);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -186,7 +197,51 @@ struct mpenv_manager {
         record(st);
     }
 
+    // Replay: next W StepLogs from the file (a short read at EOF keeps the
+    // rest of the previous step's records, as the reference's fstream read).
+    void preStep(hipStream_t st)
+    {
+        if (!replayFile) return;
+        const size_t n = std::fread(hostLog.data(), sizeof(mpenv_step_log), hostLog.size(), replayFile);
+        if (n < hostLog.size()) replayEof = true;
+        HIP_CHECK(hipMemcpyAsync((void *)S.replayLog, hostLog.data(), sizeof(mpenv_step_log) * hostLog.size(),
+                                 hipMemcpyHostToDevice, st));
+    }
+
+    // Record: W StepLogs per step.  Events: the step's events world-major
+    // (per world: agent slots in order, then the capture) to events.bin and
+    // the written snapshots to steps.bin (writeGameEvents, mgr.cpp:104-116).
+    void postStep(hipStream_t st)
+    {
+        if (!recordFile && !eventsFile) return;
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (recordFile) {
+            HIP_CHECK(hipMemcpy(hostLog.data(), S.recordLog, sizeof(mpenv_step_log) * hostLog.size(),
+                                hipMemcpyDeviceToHost));
+            std::fwrite(hostLog.data(), sizeof(mpenv_step_log), hostLog.size(), recordFile);
+        }
+        if (eventsFile) {
+            HIP_CHECK(hipMemcpy(hostEvents.data(), S.events, sizeof(mpenv_game_event) * hostEvents.size(),
+                                hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(hostSnaps.data(), S.snapshots, sizeof(mpenv_packed_step_snapshot) * hostSnaps.size(),
+                                hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(hostSnapWritten.data(), S.snapWritten, sizeof(int32_t) * hostSnapWritten.size(),
+                                hipMemcpyDeviceToHost));
+            for (const mpenv_game_event &e : hostEvents)
+                if (e.type != 0) std::fwrite(&e, sizeof(e), 1, eventsFile);
+            for (size_t w = 0; w < hostSnaps.size(); w++)
+                if (hostSnapWritten[w]) std::fwrite(&hostSnaps[w], sizeof(hostSnaps[w]), 1, stepsFile);
+        }
+    }
+
     void runStep(hipStream_t st)
+    {
+        preStep(st);
+        launchStep(st);
+        postStep(st);
+    }
+
+    void launchStep(hipStream_t st)
     {
         if (groups <= 1) {
             stepRange(S, sc, st);
@@ -256,6 +311,21 @@ bool mpenv_manager::exportDesc(int32_t id, TensorDesc &d)
     case MPENV_EXPORT_MAGAZINE: return set(S.magazine, MPENV_DTYPE_INT32, { A, 2 });
     case MPENV_EXPORT_FILTERS_STATE: return set(S.filters, MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_REWARD_HYPER_PARAMS: return set(S.rewardCoefs, MPENV_DTYPE_FLOAT32, { A, 9 });
+    case MPENV_EXPORT_EVENT_LOG:
+        if (!S.events) return false;
+        return set(S.events, MPENV_DTYPE_INT32, { W, S.evStride, 6 });
+    case MPENV_EXPORT_PACKED_STEP_SNAPSHOT:
+        if (!S.snapshots) return false;
+        return set(S.snapshots, MPENV_DTYPE_INT32, { W, 48 });
+    case MPENV_EXPORT_RECORD_LOG:
+        if (!S.recordLog) return false;
+        return set(S.recordLog, MPENV_DTYPE_INT32, { W, 217 });
+    case MPENV_EXPORT_REPLAY_LOG:
+        if (!S.replayLog) return false;
+        return set((void *)S.replayLog, MPENV_DTYPE_INT32, { W, 217 });
+    case MPENV_EXPORT_SNAPSHOT_WRITTEN:
+        if (!S.snapshots) return false;
+        return set(S.snapWritten, MPENV_DTYPE_INT32, { W, 1 });
     case MPENV_EXPORT_SIM_CONTROL: return set(S.trainCtrl, MPENV_DTYPE_INT32, { 3 });
     case MPENV_EXPORT_DEBUG_AGENT_F32: gatherDebug(); return set(dbgAF, MPENV_DTYPE_FLOAT32, { A, MPENV_DBG_AF_COUNT });
     case MPENV_EXPORT_DEBUG_AGENT_I32: gatherDebug(); return set(dbgAI, MPENV_DTYPE_INT32, { A, MPENV_DBG_AI_COUNT });
@@ -432,6 +502,38 @@ static void allocState(mpenv_manager &m)
     S.trainCtrl = m.alloc<int32_t>(3);
 }
 
+static void openLogs(mpenv_manager &m, const mpenv_config *cfg)
+{
+    DevState &S = m.S;
+    const size_t W = (size_t)S.W;
+    S.evStride = 2 * S.N + 1;
+    if (cfg->replay_log_path) {
+        m.replayFile = std::fopen(cfg->replay_log_path, "rb");
+        if (!m.replayFile) throw std::runtime_error(std::string("cannot open replay log ") + cfg->replay_log_path);
+        S.replayLog = m.alloc<mpenv_step_log>(W);
+        m.sc.replayOn = 1;
+    }
+    if (cfg->record_log_path) {
+        m.recordFile = std::fopen(cfg->record_log_path, "wb");
+        if (!m.recordFile) throw std::runtime_error(std::string("cannot open record log ") + cfg->record_log_path);
+        S.recordLog = m.alloc<mpenv_step_log>(W);
+        m.sc.recordOn = 1;
+    }
+    if (m.replayFile || m.recordFile) m.hostLog.assign(W, mpenv_step_log {});
+    if (cfg->event_log_path) {
+        const std::string dir = cfg->event_log_path;
+        m.eventsFile = std::fopen((dir + "/events.bin").c_str(), "wb");
+        m.stepsFile = std::fopen((dir + "/steps.bin").c_str(), "wb");
+        if (!m.eventsFile || !m.stepsFile) throw std::runtime_error("cannot open event logs in " + dir);
+        S.events = m.alloc<mpenv_game_event>(W * S.evStride);
+        S.snapshots = m.alloc<mpenv_packed_step_snapshot>(W);
+        m.hostEvents.assign(W * S.evStride, mpenv_game_event {});
+        m.hostSnaps.assign(W, mpenv_packed_step_snapshot {});
+        m.hostSnapWritten.assign(W, 0);
+        m.sc.eventsOn = 1;
+    }
+}
+
 // A contiguous world range [w0, w0 + nw) of the manager viewed as a complete
 // engine: every per-agent / per-world column offset to the range, W/A set
 // to its size, and the scene's world-id offset advanced so RNG keys stay
@@ -489,6 +591,10 @@ static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_
     G.alive = S.alive + g0;
     G.magazine = S.magazine + g0 * 2;
     G.rewardCoefs = S.rewardCoefs + g0 * 9;
+    if (S.recordLog) G.recordLog = S.recordLog + w0;
+    if (S.replayLog) G.replayLog = S.replayLog + w0;
+    if (S.events) G.events = S.events + w0 * S.evStride;
+    if (S.snapshots) G.snapshots = S.snapshots + w0;
 }
 
 void mpenv_manager::setupGroups(int want)
@@ -557,9 +663,10 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
             if (cfg->sim_flags & unsupported & (1u << b)) msg += std::string(" ") + names[b];
         return fail(MPENV_ERR_UNSUPPORTED, msg);
     }
-    if (cfg->replay_log_path || cfg->record_log_path || cfg->event_log_path || cfg->curriculum_data_path ||
-        cfg->train_flank)
-        return fail(MPENV_ERR_UNSUPPORTED, "record/replay/event logs, curricula and flank rewards are not implemented");
+    if (cfg->curriculum_data_path || cfg->train_flank)
+        return fail(MPENV_ERR_UNSUPPORTED, "trajectory curricula and flank rewards are not implemented");
+    if (cfg->replay_log_path && cfg->record_log_path)
+        return fail(MPENV_ERR_UNSUPPORTED, "record and replay logs together are not supported");
 
     mpenv_manager *m = nullptr;
     try {
@@ -584,6 +691,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m->S.N = 2 * m->S.T;
         m->S.A = (int64_t)m->S.W * m->S.N;
         allocState(*m);
+        openLogs(*m, cfg);
         {
             // World groups (concurrent streams).  MPENV_WORLD_GROUPS overrides.
             int want = m->S.W >= 3072 ? 3 : 1;
@@ -825,11 +933,18 @@ int mpenv_set_uniform_agent_policy(mpenv_manager *m, int32_t policy)
     return MPENV_OK;
 }
 
+// Manager::isReplayFinished (mgr.cpp:2603-2617): the replay file hit EOF
 int mpenv_is_replay_finished(mpenv_manager *m, int32_t *finished)
 {
-    (void)m;
-    if (finished) *finished = 1;
-    return fail(MPENV_ERR_UNSUPPORTED, "replay logs are not implemented");
+    if (!m || !finished) return fail(MPENV_ERR_INVALID, "null argument");
+    if (!m->replayFile) return fail(MPENV_ERR_INVALID, "no replay log configured");
+    if (!m->replayEof) {
+        const int c = std::fgetc(m->replayFile);
+        if (c == EOF) m->replayEof = true;
+        else std::ungetc(c, m->replayFile);
+    }
+    *finished = m->replayEof ? 1 : 0;
+    return MPENV_OK;
 }
 
 int mpenv_dims(mpenv_manager *m, int32_t *num_worlds, int32_t *agents_per_world)

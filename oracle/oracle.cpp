@@ -190,6 +190,7 @@ struct World {
     int filtersLastMatchedStep[2];
     int episodeCurriculum;
     uint64_t matchID;
+    uint32_t eventLoggedInStep, eventMask; // sim.hpp:162-163
     // SpawnUsageCounter (types.hpp:95-100) lives in Oracle::spawnTrack.
     // GoalRegionsState (types.hpp:808-814)
     bool regionsActive[10];
@@ -243,6 +244,12 @@ struct Oracle {
         selfPos, teammatePos, opponentPos, lastKnownPos, masks, fwdLidar, rearLidar, agentMap, hp,
         alive, rewardCoefs;
     std::vector<float> dbgAF, dbgWF, dbgCrumbs;
+    // logs (record / replay / events), enabled by oracle_set_log_modes
+    bool recordOn = false, replayOn = false, eventsOn = false;
+    std::vector<mpenv_step_log> recordLog, replayLog;
+    std::vector<mpenv_game_event> events;        // [W][2N+1]
+    std::vector<mpenv_packed_step_snapshot> snapshots;
+    std::vector<int32_t> snapWritten;
     std::vector<int32_t> dbgAI, dbgWI;
     std::vector<uint32_t> dbgExplore;
 
@@ -1324,6 +1331,24 @@ void fallSystem(Oracle &o, int w, int i)
 }
 
 // sim.cpp:1443-1615 fireSystem
+// sim.cpp:23-39 logEvent into the step's per-world event slots (slot 2i,
+// 2i+1: agent i; slot 2N: capture)
+void logEvent(Oracle &o, int w, int slot, uint32_t type, int a, int b, int c16)
+{
+    if (!o.eventsOn) return;
+    World &wd = o.worlds[w];
+    mpenv_game_event &e = o.events[(size_t)w * (2 * o.N + 1) + slot];
+    e.type = type;
+    e.pad_ = 0;
+    e.match_id = wd.matchID;
+    e.step = (uint32_t)wd.curStep;
+    e.a = (uint8_t)a;
+    e.b = (uint8_t)b;
+    e.c16 = (uint16_t)c16;
+}
+
+int playerId(const Agent &a) { return a.team * kMaxTeamSize + a.offset; }
+
 void fireSystem(Oracle &o, int w, int i)
 {
     Agent &ag = o.agent(w, i);
@@ -1336,6 +1361,7 @@ void fireSystem(Oracle &o, int w, int i)
     int32_t *mag = &o.magazine[2 * g];
     int fire = o.discreteAction[4 * g + 2];
     if (fire == 2) {
+        logEvent(o, w, 2 * i, MPENV_EVENT_RELOAD, playerId(ag), mag[0], 0);
         if (mag[0] == kMagSize) ag.reloadedFullMag = true;
         mag[0] = kMagSize;
         mag[1] = kReloadTime;
@@ -1374,8 +1400,12 @@ void fireSystem(Oracle &o, int w, int i)
         if (success && tgt.remainingRespawnSteps > 0) success = false;
     }
     if (!success) return;
+    logEvent(o, w, 2 * i, MPENV_EVENT_PLAYER_SHOT, playerId(ag), playerId(o.agent(w, h.entity)), 0);
     ag.landedShotOn = h.entity;
-    if (o.hp[o.gi(w, h.entity)] <= kDmgPerBullet) ag.successfulKill = true;
+    if (o.hp[o.gi(w, h.entity)] <= kDmgPerBullet) {
+        ag.successfulKill = true;
+        logEvent(o, w, 2 * i + 1, MPENV_EVENT_KILL, playerId(ag), playerId(o.agent(w, h.entity)), 0);
+    }
     o.agent(w, h.entity).dmg[ag.offset] = kDmgPerBullet;
 }
 
@@ -1601,6 +1631,123 @@ void updateFiltersState(Oracle &o, int w, int cur_step)
 }
 
 // sim.cpp:4470-4673 zoneMatchInfoSystem
+// sim.cpp:4592-4634 (capture event) + 41-106 writePackedStepSnapshot.
+// eventLoggedInStep / eventMask accumulate every logEvent of the step.
+void captureAndSnapshot(Oracle &o, int w, bool new_captured)
+{
+    World &wd = o.worlds[w];
+    const size_t base = (size_t)w * (2 * o.N + 1);
+    o.snapWritten[w] = 0;
+    if (wd.matchID != ~0ull && new_captured) {
+        AABB za = o.zoneAABBs[wd.curZone];
+        Quat to_zone = qinv(angleAxis(o.zoneRot[wd.curZone], kUp));
+        za.pMin = rotateVec(to_zone, za.pMin);
+        za.pMax = rotateVec(to_zone, za.pMax);
+        uint32_t mask = 0;
+        for (int i = 0; i < o.N; i++) {
+            const Agent &ag = o.agent(w, i);
+            if (ag.team != wd.curControllingTeam) continue;
+            Vec3 p = ag.pos;
+            p.z += kStandHeight / 2.f;
+            if (aabbContains(za, rotateVec(to_zone, p))) mask |= 1u << i;
+        }
+        logEvent(o, w, 2 * o.N, MPENV_EVENT_CAPTURE, wd.curZone, wd.curControllingTeam, (int)mask);
+    }
+    for (int k = 0; k < 2 * o.N + 1; k++) {
+        if (o.events[base + k].type != 0) {
+            wd.eventLoggedInStep = 1;
+            wd.eventMask |= o.events[base + k].type;
+        }
+    }
+    if (wd.matchID == ~0ull) return;
+    mpenv_packed_step_snapshot &sn = o.snapshots[w];
+    std::memset(&sn, 0, sizeof(sn));
+    sn.num_events = wd.eventLoggedInStep;
+    sn.event_mask = wd.eventMask;
+    wd.eventLoggedInStep = 0;
+    wd.eventMask = 0;
+    sn.match_id = wd.matchID;
+    sn.step = (uint16_t)wd.curStep;
+    sn.cur_zone = (uint8_t)wd.curZone;
+    sn.cur_zone_controller = (int8_t)(wd.isCaptured ? wd.curControllingTeam : -1);
+    sn.zone_steps_remaining = (uint16_t)wd.zoneStepsRemaining;
+    sn.steps_until_point = (uint16_t)wd.stepsUntilPoint;
+    for (int i = 0; i < o.N; i++) {
+        const Agent &ag = o.agent(w, i);
+        const size_t g = o.gi(w, i);
+        mpenv_packed_player &pl = sn.players[i];
+        pl.pos[0] = (int16_t)(int32_t)ag.pos.x;
+        pl.pos[1] = (int16_t)(int32_t)ag.pos.y;
+        pl.pos[2] = (int16_t)(int32_t)ag.pos.z;
+        pl.yaw = (int16_t)(int32_t)(ag.aimYaw * 32768 / kPi);
+        pl.pitch = (int16_t)(int32_t)(ag.aimPitch * 32768 / kPi);
+        pl.mag_num_bullets = (uint8_t)(uint16_t)o.magazine[2 * g];
+        pl.is_reloading = (uint8_t)o.magazine[2 * g + 1];
+        pl.hp = (uint8_t)o.hp[g];
+        uint8_t fl = 0;
+        if (ag.landedShotOn != -1) fl |= 2;
+        if (ag.curPose == 1) fl |= 4;
+        else if (ag.curPose == 2) fl |= 8;
+        pl.flags = fl;
+    }
+    o.snapWritten[w] = 1;
+}
+
+// sim.cpp:4750-4792 pvpRecordSystem
+void pvpRecordSystem(Oracle &o, int w)
+{
+    mpenv_step_log &log = o.recordLog[w];
+    log.cur_step = o.worlds[w].curStep;
+    for (int i = 0; i < o.N; i++) {
+        const Agent &ag = o.agent(w, i);
+        const size_t g = o.gi(w, i);
+        mpenv_agent_log &a = log.agents[i];
+        a.position[0] = ag.pos.x; a.position[1] = ag.pos.y; a.position[2] = ag.pos.z;
+        a.aim_yaw = ag.aimYaw;
+        a.aim_pitch = ag.aimPitch;
+        a.aim_rot[0] = ag.aimRot.w; a.aim_rot[1] = ag.aimRot.x; a.aim_rot[2] = ag.aimRot.y; a.aim_rot[3] = ag.aimRot.z;
+        a.hp = o.hp[g];
+        a.mag_num_bullets = o.magazine[2 * g];
+        a.mag_is_reloading = o.magazine[2 * g + 1];
+        a.cur_pose = ag.curPose;
+        a.tgt_pose = ag.tgtPose;
+        a.transition_remaining = ag.transitionRemaining;
+        a.shot_agent_idx = ag.landedShotOn;
+        a.fired_shot_t = ag.firedShotT;
+        a.was_killed = ag.wasKilled ? 1 : 0;
+        a.successful_kill = ag.successfulKill ? 1 : 0;
+        a.pad_[0] = a.pad_[1] = 0;
+    }
+}
+
+// sim.cpp:4794-4843 pvpReplaySystem (viewer shot entities skipped)
+void pvpReplaySystem(Oracle &o, int w)
+{
+    const mpenv_step_log &log = o.replayLog[w];
+    o.worlds[w].curStep = log.cur_step;
+    for (int i = 0; i < o.N; i++) {
+        Agent &ag = o.agent(w, i);
+        const size_t g = o.gi(w, i);
+        const mpenv_agent_log &a = log.agents[i];
+        ag.pos = v3(a.position[0], a.position[1], a.position[2]);
+        ag.aimYaw = a.aim_yaw;
+        ag.aimPitch = a.aim_pitch;
+        ag.aimRot = quat(a.aim_rot[0], a.aim_rot[1], a.aim_rot[2], a.aim_rot[3]);
+        ag.rot = qnormalize(angleAxis(a.aim_yaw, kUp));
+        o.hp[g] = a.hp;
+        o.magazine[2 * g] = a.mag_num_bullets;
+        o.magazine[2 * g + 1] = a.mag_is_reloading;
+        ag.curPose = a.cur_pose;
+        ag.tgtPose = a.tgt_pose;
+        ag.transitionRemaining = a.transition_remaining;
+        ag.landedShotOn = a.shot_agent_idx;
+        ag.firedShotT = a.fired_shot_t;
+        ag.wasKilled = a.was_killed != 0;
+        ag.successfulKill = a.successful_kill != 0;
+        if (ag.wasKilled) ag.hasDiedDuringEpisode = true;
+    }
+}
+
 void zoneMatchInfoSystem(Oracle &o, int w)
 {
     World &wd = o.worlds[w];
@@ -1634,6 +1781,7 @@ void zoneMatchInfoSystem(Oracle &o, int w)
         if (wd.isContested) zs[3] += 1;
         if (new_captured) zs[0] += 1;
         updateFiltersState(o, w, cur_step);
+        if (o.eventsOn) captureAndSnapshot(o, w, new_captured);
     }
     if (finished) {
         if (mr[3] > mr[4]) mr[0] = 0;
@@ -2080,10 +2228,21 @@ void resetAndObs(Oracle &o, int w)
 }
 
 // sim.cpp:5342-5842 setupStepTasks, Task::Zone, default flags
+void replayTail(Oracle &o, int w);
+
 void stepWorld(Oracle &o, int w)
 {
     const int N = o.N;
+    if (o.eventsOn) // ClearTmpNode<GameEventEntity> (sim.cpp:5344)
+        for (int k = 0; k < 2 * N + 1; k++) o.events[(size_t)w * (2 * N + 1) + k].type = 0;
     for (int i = 0; i < N; i++) planAStarAISystem(o, w, i);
+    if (o.replayOn) {
+        // pvpReplayLogic (sim.cpp:5587-5605): replay + zoneSystem only
+        pvpReplaySystem(o, w);
+        zoneSystem(o, w);
+        replayTail(o, w);
+        return;
+    }
     for (int i = 0; i < N; i++) applyBotActionsSystem(o, w, i);
     for (int i = 0; i < N; i++) pvpMovementSystem(o, w, i);
     for (int i = 0; i < N; i++) pvpContinuousAimSystem(o, w, i);
@@ -2101,8 +2260,16 @@ void stepWorld(Oracle &o, int w)
     if (!(o.simFlags & MPENV_SIMFLAG_NO_RESPAWN)) spawnAgents(o, w, true);
     for (int i = 0; i < N; i++) autoHealSystem(o, w, i);
     zoneSystem(o, w);
+    if (o.recordOn) pvpRecordSystem(o, w);
     for (int i = 0; i < N; i++) leaveBreadcrumbsSystem(o, w, i);
     accumulateBreadcrumbPenalties(o, w);
+    replayTail(o, w);
+}
+
+// Systems after the gameplay / replay logic (sim.cpp:5664-5750 onward)
+void replayTail(Oracle &o, int w)
+{
+    const int N = o.N;
     zoneMatchInfoSystem(o, w);
     evaluateGoalRegionsSystem(o, w);
     for (int i = 0; i < N; i++) exploreVisitedSystem(o, w, i);
@@ -2132,6 +2299,8 @@ void constructWorld(Oracle &o, int w)
     for (int z = 0; z < kMaxZones; z++)
         for (int k = 0; k < 5; k++) wd.zoneStats[z][k] = 0;
     wd.matchID = ~0ull;
+    wd.eventLoggedInStep = 0;
+    wd.eventMask = 0;
     for (int t = 0; t < 2; t++) {
         wd.filtersActive[t] = 0;
         wd.filtersLastMatchedStep[t] = -1;
@@ -2431,6 +2600,21 @@ int oracle_export(void *h, int32_t id, void **ptr, int32_t *dtype, int32_t *ndim
     case MPENV_EXPORT_MAGAZINE: return set(o.magazine.data(), MPENV_DTYPE_INT32, { A, 2 });
     case MPENV_EXPORT_FILTERS_STATE: return set(o.filtersObs.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_REWARD_HYPER_PARAMS: return set(o.rewardCoefs.data(), MPENV_DTYPE_FLOAT32, { A, 9 });
+    case MPENV_EXPORT_EVENT_LOG:
+        if (!o.eventsOn) return -1;
+        return set(o.events.data(), MPENV_DTYPE_INT32, { W, 2 * (int64_t)o.N + 1, 6 });
+    case MPENV_EXPORT_PACKED_STEP_SNAPSHOT:
+        if (!o.eventsOn) return -1;
+        return set(o.snapshots.data(), MPENV_DTYPE_INT32, { W, 48 });
+    case MPENV_EXPORT_SNAPSHOT_WRITTEN:
+        if (!o.eventsOn) return -1;
+        return set(o.snapWritten.data(), MPENV_DTYPE_INT32, { W, 1 });
+    case MPENV_EXPORT_RECORD_LOG:
+        if (!o.recordOn) return -1;
+        return set(o.recordLog.data(), MPENV_DTYPE_INT32, { W, 217 });
+    case MPENV_EXPORT_REPLAY_LOG:
+        if (!o.replayOn) return -1;
+        return set(o.replayLog.data(), MPENV_DTYPE_INT32, { W, 217 });
     case MPENV_EXPORT_SIM_CONTROL: return set(o.trainControl, MPENV_DTYPE_INT32, { 3 });
     case MPENV_EXPORT_DEBUG_AGENT_F32: return set(o.dbgAF.data(), MPENV_DTYPE_FLOAT32, { A, MPENV_DBG_AF_COUNT });
     case MPENV_EXPORT_DEBUG_AGENT_I32: return set(o.dbgAI.data(), MPENV_DTYPE_INT32, { A, MPENV_DBG_AI_COUNT });
@@ -2462,6 +2646,22 @@ void oracle_step_worlds(void *h, int32_t w0, int32_t w1)
 }
 
 void oracle_refresh_debug(void *h) { refreshDebug(*static_cast<Oracle *>(h)); }
+
+void oracle_set_log_modes(void *h, int32_t record, int32_t replay, int32_t events)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    const size_t W = (size_t)o.W;
+    o.recordOn = record != 0;
+    o.replayOn = replay != 0;
+    o.eventsOn = events != 0;
+    if (o.recordOn) o.recordLog.assign(W, mpenv_step_log {});
+    if (o.replayOn) o.replayLog.assign(W, mpenv_step_log {});
+    if (o.eventsOn) {
+        o.events.assign(W * (2 * o.N + 1), mpenv_game_event {});
+        o.snapshots.assign(W, mpenv_packed_step_snapshot {});
+        o.snapWritten.assign(W, 0);
+    }
+}
 
 double oracle_run_threaded(void *h, int32_t nsteps, int32_t nthreads, const int32_t *ring, int32_t ring_len)
 {

@@ -49,6 +49,11 @@ void oracle_step(void *h);
 void oracle_step_worlds(void *h, int32_t w0, int32_t w1);
 /* Refresh MPENV_EXPORT_DEBUG_* buffers from internal state. */
 void oracle_refresh_debug(void *h);
+/* Record / replay / event-log modes (sim.cpp:4750-4843, 23-106): buffers
+ * exported as MPENV_EXPORT_RECORD_LOG / REPLAY_LOG / EVENT_LOG /
+ * PACKED_STEP_SNAPSHOT / SNAPSHOT_WRITTEN; in replay mode the caller fills
+ * REPLAY_LOG before each step. */
+void oracle_set_log_modes(void *h, int32_t record, int32_t replay, int32_t events);
 /* CPU baseline timing: runs nsteps steps over all worlds with nthreads
  * std::threads (static world partition, like ThreadPoolExecutor,
  * mgr.cpp:1863-1871).  Before each step the discrete/aim actions of step s

@@ -32,7 +32,8 @@ EXPORT = dict(
     REAR_LIDAR=20, AGENT_MAP=21, UNMASKED_AGENT_MAP=22, HP=23, ALIVE=24, MAGAZINE=25,
     FILTERS_STATE=38, REWARD_HYPER_PARAMS=39, SIM_CONTROL=64, DEBUG_AGENT_F32=65,
     DEBUG_AGENT_I32=66, DEBUG_WORLD_I32=67, DEBUG_WORLD_F32=68, DEBUG_EXPLORE=69,
-    DEBUG_CRUMBS=70,
+    DEBUG_CRUMBS=70, EVENT_LOG=36, PACKED_STEP_SNAPSHOT=37, RECORD_LOG=71, REPLAY_LOG=72,
+    SNAPSHOT_WRITTEN=73,
 )
 
 # Exports compared between engine and oracle after every step.
@@ -120,6 +121,7 @@ def lib_oracle():
         for fn in ("oracle_init", "oracle_step", "oracle_refresh_debug"):
             getattr(lib, fn).argtypes = [C.c_void_p]
         lib.oracle_step_worlds.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        lib.oracle_set_log_modes.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
         lib.oracle_run_threaded.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32]
         lib.oracle_run_threaded.restype = C.c_double
         fp = C.POINTER(C.c_float)
@@ -250,12 +252,14 @@ class Engine:
     """The gfx950 engine through its C ABI (include/mpenv.h)."""
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
-                 world_id_offset=0, scene=SCENE, gpu_id=0):
+                 world_id_offset=0, scene=SCENE, gpu_id=0, replay=None, record=None, events=None):
         self.lib = lib_mpenv()
         self.mem = HipMem()
         self._scene = scene.encode()
+        self._paths = [p.encode() if p else None for p in (replay, record, events)]
         cfg = MpenvConfig(1, gpu_id, num_worlds, rand_seed, int(auto_reset), sim_flags, 2,
-                          team_size, 0, 0, self._scene, 0, None, None, None, None, world_id_offset)
+                          team_size, 0, 0, self._scene, 0, self._paths[0], self._paths[1], self._paths[2],
+                          None, world_id_offset)
         h = C.c_void_p()
         rc = self.lib.mpenv_create(C.byref(cfg), C.byref(h))
         assert rc == 0, self.lib.mpenv_last_error().decode()

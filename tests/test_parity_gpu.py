@@ -6,6 +6,7 @@ the floats, because both sides compile the same IEEE-exact definitions
 the north star allows (1e-5 relative); the tests run with 0 (bit-exact) and
 only fall back to the tolerance where a test says so.
 """
+import ctypes as C
 import json
 import os
 import glob
@@ -352,3 +353,68 @@ def test_world_groups_on_streams_match_oracle(monkeypatch):
                     _, _, shape = e.desc(n)
                     r0, r1 = (w0, w0 + 2) if shape[0] == W else (w0 * N, (w0 + 2) * N)
                     T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
+
+
+def test_logs_record_and_events_match_oracle(tmp_path):
+    """record_log_path + event_log_path: the engine's StepLog file,
+    events.bin and steps.bin equal, byte for byte, what the oracle's buffers
+    give for the same run (mgr.cpp:104-116, sim.cpp:23-106, 4750-4792)."""
+    W, ts, steps = 12, 3, 250
+    rec = str(tmp_path / "rec.bin")
+    e = T.Engine(W, ts, sim_flags=1, record=rec, events=str(tmp_path))
+    o = T.Oracle(W, ts, sim_flags=1)
+    o.lib.oracle_set_log_modes(o.h, 1, 0, 1)
+    for sim in (e, o):
+        sim.put_ctrl([0, 1, 1])
+        sim.init()
+    exp_rec, exp_ev, exp_steps = [], [], []
+    for s in range(steps):
+        acts = T.combat_actions(o, s)
+        e.set_actions(acts)
+        o.set_actions(acts)
+        e.step()
+        o.step()
+        exp_rec.append(o.get("RECORD_LOG").astype("<i4").tobytes())
+        rows = o.get("EVENT_LOG").reshape(-1, 6)
+        exp_ev.append(rows[rows[:, 0] != 0].astype("<i4").tobytes())
+        sn, wr = o.get("PACKED_STEP_SNAPSHOT"), o.get("SNAPSHOT_WRITTEN").ravel()
+        exp_steps.append(sn[wr != 0].astype("<i4").tobytes())
+        if s % 25 == 0:
+            _compare_all(e, o, f"step {s}")
+    e.close()  # flushes the files
+    got_rec = open(rec, "rb").read()
+    assert got_rec == b"".join(exp_rec)
+    got_ev = open(tmp_path / "events.bin", "rb").read()
+    assert len(got_ev) > 24 * 20
+    assert got_ev == b"".join(exp_ev)
+    assert open(tmp_path / "steps.bin", "rb").read() == b"".join(exp_steps)
+
+
+def test_logs_replay_matches_oracle(tmp_path):
+    """replay_log_path: the engine replays a recorded match (pvpReplayLogic)
+    exactly as the oracle does from the same StepLogs."""
+    W, ts, steps = 8, 2, 200
+    rec = str(tmp_path / "rec.bin")
+    src = T.Engine(W, ts, sim_flags=1, record=rec)
+    src.put_ctrl([0, 1, 1])
+    src.init()
+    for s in range(steps):
+        src.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, W * 2 * ts))
+        src.step()
+    src.close()
+    logs = np.fromfile(rec, dtype=np.int32).reshape(steps, W, 217)
+    e = T.Engine(W, ts, sim_flags=1, replay=rec)
+    o = T.Oracle(W, ts, sim_flags=1)
+    o.lib.oracle_set_log_modes(o.h, 0, 1, 0)
+    for sim in (e, o):
+        sim.put_ctrl([0, 1, 1])
+        sim.init()
+    zero = np.zeros((W * 2 * ts, 6), np.int32)
+    for s in range(steps):
+        o.view("REPLAY_LOG")[:] = logs[s]
+        for sim in (e, o):
+            sim.set_actions(zero)
+            sim.step()
+        _compare_all(e, o, f"replay step {s}")
+    fin = C.c_int32(0)
+    assert e.lib.mpenv_is_replay_finished(e.h, C.byref(fin)) == 0 and fin.value == 1
