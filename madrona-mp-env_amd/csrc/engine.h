@@ -162,6 +162,7 @@ struct SceneDev {
     // navmesh for the scripted bots (sim.cpp:4958-5172)
     const float *navTris;   // 9 floats per triangle (deduplicated vertices)
     const int32_t *astar;   // [numNavTris][numNavTris] next hop
+    const float *navCdf;    // [numNavTris] running triangle areas (NavmeshSpawn)
     int32_t numNavTris;
     // logs (sim.cpp:4750-4843 record/replay, 23-106 + 4592-4634 events)
     int32_t recordOn, replayOn, eventsOn;

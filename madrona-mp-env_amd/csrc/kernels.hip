@@ -69,6 +69,7 @@ constexpr uint32_t kFlagSpawnInMiddle = 1u << 0;
 constexpr uint32_t kFlagRandomizeHP = 1u << 1;
 constexpr uint32_t kFlagHardcodedSpawns = 1u << 6;
 constexpr uint32_t kFlagEnableCurriculum = 1u << 5;
+constexpr uint32_t kFlagNavmeshSpawn = 1u << 2;
 constexpr int32_t kFlagCrumbRequest = 64; // transient (leave -> append)
 
 __device__ __forceinline__ float viewHeightD(int pose)
@@ -773,9 +774,26 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
         const int64_t g = g0 + ai;
         Vec3 spawn_pt;
         float spawn_yaw;
-        RNG rng = ldRng(S, g);
-        standardSpawnPointD(S, sc, w, ai, is_respawn, use_middle, rng, spawn_pt, spawn_yaw);
-        stRng(S, g, rng);
+        if ((sc.simFlags & kFlagHardcodedSpawns) && !is_respawn) {
+            // utils.cpp:480-650 hardcodedSpawnPoint
+            const int team = ai / S.T;
+            hardcodedSpawn((team == S.teamA[w] ? 0 : 3) + (ai - team * S.T), spawn_pt, spawn_yaw);
+        } else if (sc.simFlags & kFlagNavmeshSpawn) {
+            // utils.cpp:807-809
+            spawn_pt = navSamplePoint(sc.navTris, sc.navCdf, sc.numNavTris, rngAdvance(base));
+            spawn_yaw = rngUniform(base) * 2.f * kPi;
+        } else {
+            RNG rng = ldRng(S, g);
+            standardSpawnPointD(S, sc, w, ai, is_respawn, use_middle, rng, spawn_pt, spawn_yaw);
+            stRng(S, g, rng);
+            if ((sc.simFlags & kFlagEnableCurriculum) && S.episodeCurr[w] == 0) {
+                // utils.cpp:819-837 LearnShooting
+                const bool north = spawn_pt.y > 0.f;
+                const float x = -700.f + rngUniform(base) * 1400.f;
+                const float y = rngUniform(base) * 350.f;
+                spawn_pt = v3(x, north ? y : -y, 0.f);
+            }
+        }
         stPos(S, g, spawn_pt);
         stRot(S, g, qnormalize(angleAxis(spawn_yaw, kUp)));
         stAim(S, g, computeAimD(spawn_yaw, 0.f));

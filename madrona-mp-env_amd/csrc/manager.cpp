@@ -394,6 +394,11 @@ static void buildSceneDev(mpenv_manager &m)
         m.upload(d_nav, tv.data(), sizeof(float) * tv.size());
         int32_t *d_astar = m.alloc<int32_t>(std::max<size_t>(nm.astar.size(), 1));
         if (!nm.astar.empty()) m.upload(d_astar, nm.astar.data(), sizeof(int32_t) * nm.astar.size());
+        std::vector<float> cdf(std::max<size_t>(T, 1), 0.f);
+        mp::navAreaCDF(tv.data(), (int)T, cdf.data());
+        float *d_cdf = m.alloc<float>(cdf.size());
+        m.upload(d_cdf, cdf.data(), sizeof(float) * cdf.size());
+        sc.navCdf = d_cdf;
         sc.navTris = d_nav;
         sc.astar = d_astar;
         sc.numNavTris = (int32_t)T;
@@ -653,9 +658,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         return fail(MPENV_ERR_INVALID, "team_size must be in [1, 6]");
     if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");
     if (!cfg->scene_path) return fail(MPENV_ERR_INVALID, "scene_path is required");
-    const uint32_t unsupported = MPENV_SIMFLAG_NAVMESH_SPAWN | MPENV_SIMFLAG_ENABLE_CURRICULUM |
-                                 MPENV_SIMFLAG_HARDCODED_SPAWNS | MPENV_SIMFLAG_FULL_TEAM_POLICY |
-                                 MPENV_SIMFLAG_SUB_ZONES;
+    const uint32_t unsupported = MPENV_SIMFLAG_FULL_TEAM_POLICY | MPENV_SIMFLAG_SUB_ZONES;
     if (cfg->sim_flags & unsupported) {
         static const char *names[] = { "SpawnInMiddle", "RandomizeHPMagazine", "NavmeshSpawn", "NoRespawn",
                                        "StaggerStarts", "EnableCurriculum", "HardcodedSpawns",
@@ -666,6 +669,10 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
             if (cfg->sim_flags & unsupported & (1u << b)) msg += std::string(" ") + names[b];
         return fail(MPENV_ERR_UNSUPPORTED, msg);
     }
+    // hardcodedSpawnPoint indexes a 6-entry table with (team A ? 0 : 3) +
+    // offset (utils.cpp:545-549): larger teams read past it in the reference.
+    if ((cfg->sim_flags & MPENV_SIMFLAG_HARDCODED_SPAWNS) && cfg->team_size > 3)
+        return fail(MPENV_ERR_UNSUPPORTED, "HardcodedSpawns has spawn points for team_size <= 3 only");
     if (cfg->curriculum_data_path || cfg->train_flank)
         return fail(MPENV_ERR_UNSUPPORTED, "trajectory curricula and flank rewards are not implemented");
     if (cfg->replay_log_path && cfg->record_log_path)

@@ -472,4 +472,64 @@ MP_HD void tapeActions(uint32_t seed, uint32_t step, uint32_t agent, int32_t *di
     aim[1] = mulhi(tapeHash(seed, step, agent, 5), 7);
 }
 
+// ----------------------------------------------------------- spawn helpers
+// hardcodedSpawnPoint table (utils.cpp:503-541; hardcodedSpawnIdx is always
+// 0, sim.cpp:795-798): entries 0-2 for team A's offsets, 3-5 for the other
+// team.  The literals are doubles narrowed to float, as in the reference's
+// brace initialisers.  Pitch is 0 for every entry.
+MP_HD void hardcodedSpawn(int idx, Vec3 &pos, float &yaw)
+{
+    switch (idx) {
+    case 0: pos = v3((float)510.0, (float)179.1, -64.f); yaw = (float)-2.05; break;
+    case 1: pos = v3((float)525.8, (float)17.1, -64.f); yaw = (float)-0.80; break;
+    case 2: pos = v3((float)434.3, (float)184.7, -64.f); yaw = (float)-1.80; break;
+    case 3: pos = v3((float)1037.2, (float)449.0, -56.f); yaw = (float)2.37; break;
+    case 4: pos = v3((float)1094.3, (float)200.1, -56.f); yaw = (float)1.41; break;
+    default: pos = v3((float)1045.8, (float)416.8, -56.f); yaw = 2.37f; break;
+    }
+}
+
+// Navmesh::samplePoint(RandKey) (called at utils.cpp:808) lives in Madrona,
+// which is not vendored: parity to the reference's bitstream is unpinned and
+// the sampler is DEFINED here as area-uniform sampling over the deduplicated
+// fan-triangulated navmesh (navmesh.cpp):
+//   triangle = first t with u0 * cdf[T-1] < cdf[t], u0 = uniform(split_i(key, 0))
+//   (cdf[t] = float running sum of triangle areas 0.5 |(b-a) x (c-a)|, in order)
+//   b1, b2 = uniform(split_i(key, 1)), uniform(split_i(key, 2)); reflected
+//   into the triangle when b1 + b2 > 1; point = a + (b-a) b1 + (c-a) b2.
+// tris: 9 floats per triangle.
+MP_HD float navTriArea(const float *t)
+{
+    const Vec3 a = v3(t[0], t[1], t[2]), b = v3(t[3], t[4], t[5]), c = v3(t[6], t[7], t[8]);
+    return 0.5f * length(cross(b - a, c - a));
+}
+
+inline void navAreaCDF(const float *tris, int T, float *cdf)
+{
+    float run = 0.f;
+    for (int t = 0; t < T; t++) {
+        run += navTriArea(tris + 9 * t);
+        cdf[t] = run;
+    }
+}
+
+MP_HD Vec3 navSamplePoint(const float *tris, const float *cdf, int T, RandKey key)
+{
+    const float u = keyUniform(splitI(key, 0)) * cdf[T - 1];
+    int lo = 0, hi = T - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (u < cdf[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    float b1 = keyUniform(splitI(key, 1)), b2 = keyUniform(splitI(key, 2));
+    if (b1 + b2 > 1.f) {
+        b1 = 1.f - b1;
+        b2 = 1.f - b2;
+    }
+    const float *t = tris + 9 * lo;
+    const Vec3 a = v3(t[0], t[1], t[2]), b = v3(t[3], t[4], t[5]), c = v3(t[6], t[7], t[8]);
+    return a + (b - a) * b1 + (c - a) * b2;
+}
+
 } // namespace mp

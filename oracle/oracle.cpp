@@ -217,6 +217,7 @@ struct Oracle {
     float frustum[4];
     std::vector<Node> nodes;
     std::vector<Vec3> navTris;   // 3 per triangle
+    std::vector<float> navCdf;   // running triangle areas (navSamplePoint)
     std::vector<int32_t> astar;  // [T][T]
     int numNavTris = 0;
     std::vector<Vec3> verts;
@@ -749,7 +750,7 @@ void standardSpawnPoint(Oracle &o, int w, int ai, bool is_respawn, bool use_midd
     o.track(w, 2)[best_idx] = (uint32_t)wd.curStep;
 }
 
-// utils.cpp:734-948 spawnAgents (Zone task, default flags)
+// utils.cpp:734-948 spawnAgents (Zone task)
 void spawnAgents(Oracle &o, int w, bool is_respawn)
 {
     World &wd = o.worlds[w];
@@ -766,6 +767,9 @@ void spawnAgents(Oracle &o, int w, bool is_respawn)
     bool use_middle = false;
     if (o.simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) use_middle = rngUniform(base) < 0.5f;
     const bool randomize_hp = (o.simFlags & MPENV_SIMFLAG_RANDOMIZE_HP_MAGAZINE) != 0;
+    const bool hardcoded = (o.simFlags & MPENV_SIMFLAG_HARDCODED_SPAWNS) != 0;
+    const bool navmesh_spawn = (o.simFlags & MPENV_SIMFLAG_NAVMESH_SPAWN) != 0;
+    const bool curriculum = (o.simFlags & MPENV_SIMFLAG_ENABLE_CURRICULUM) != 0;
 
     for (int d = 0; d < num_dead; d++) {
         int ai = dead[d];
@@ -774,7 +778,24 @@ void spawnAgents(Oracle &o, int w, bool is_respawn)
         Vec3 spawn_pt;
         float spawn_yaw;
         float spawn_pitch = 0.f;
-        standardSpawnPoint(o, w, ai, is_respawn, use_middle, &spawn_pt, &spawn_yaw);
+        if (hardcoded && !is_respawn) {
+            // utils.cpp:480-650 hardcodedSpawnPoint (curriculum branch disabled)
+            hardcodedSpawn((ag.team == wd.teamA ? 0 : 3) + ag.offset, spawn_pt, spawn_yaw);
+        } else if (navmesh_spawn) {
+            // utils.cpp:807-809
+            spawn_pt = navSamplePoint(&o.navTris[0].x, o.navCdf.data(), o.numNavTris, rngAdvance(base));
+            spawn_yaw = rngUniform(base) * 2.f * kPi;
+        } else if (curriculum && wd.episodeCurriculum == 0) {
+            // utils.cpp:819-837 LearnShooting: standard point, then a random
+            // point on the spawn's side of y = 0
+            standardSpawnPoint(o, w, ai, is_respawn, use_middle, &spawn_pt, &spawn_yaw);
+            const bool north = spawn_pt.y > 0.f;
+            const float x = -700.f + rngUniform(base) * 1400.f;
+            const float y = rngUniform(base) * 350.f;
+            spawn_pt = v3(x, north ? y : -y, 0.f);
+        } else {
+            standardSpawnPoint(o, w, ai, is_respawn, use_middle, &spawn_pt, &spawn_yaw);
+        }
 
         ag.pos = spawn_pt;
         ag.rot = qnormalize(angleAxis(spawn_yaw, kUp));
@@ -2485,6 +2506,8 @@ void *oracle_create(const oracle_config *cfg)
             for (int i = 0; i < cfg->num_nav_tris * 3; i++)
                 o->navTris[i] = v3(cfg->nav_tris[3 * i], cfg->nav_tris[3 * i + 1], cfg->nav_tris[3 * i + 2]);
             o->astar.assign(cfg->astar, cfg->astar + (size_t)cfg->num_nav_tris * cfg->num_nav_tris);
+            o->navCdf.resize(cfg->num_nav_tris);
+            navAreaCDF(cfg->nav_tris, cfg->num_nav_tris, o->navCdf.data());
         }
         // sim.cpp:5855 maxDist; 5869-5882 frustumData
         o->maxDist = length(o->worldBounds.pMax - o->worldBounds.pMin);

@@ -36,6 +36,12 @@ CASES = {
                            policy="combat"),
     # team 1 as A* bots (AgentPolicy = -1, planAStarAISystem)
     "3v3_bots": dict(team_size=3, worlds=3, steps=250, sim_flags=1, ctrl=[0, 1, 1], bots="team1"),
+    # HardcodedSpawns | SpawnInMiddle | RandomizeHPMagazine, random team sides
+    "3v3_hardcoded": dict(team_size=3, worlds=3, steps=200, sim_flags=1 | 2 | (1 << 6), ctrl=[0, 1, 1],
+                          policy="combat"),
+    # NavmeshSpawn | EnableCurriculum (LearnShooting rewards)
+    "2v2_navmesh_curriculum": dict(team_size=2, worlds=4, steps=200, sim_flags=(1 << 2) | (1 << 5),
+                                   ctrl=[0, 1, 1], policy="combat"),
 }
 TAPE_SEED = 1234
 FINAL_TENSORS = ["SELF_OBSERVATION", "REWARD", "HP", "FWD_LIDAR"]

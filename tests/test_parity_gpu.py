@@ -56,6 +56,9 @@ LIVE = [
     (5, 8, 300, 1 | (1 << 8), [0, 1, 0], "combat"),     # StaticFlipTeams
     (3, 16, 300, 1, [0, 1, 1], "bots_team1"),           # A* bots vs tape
     (6, 8, 300, 0, [0, 1, 1], "bots_all"),              # everyone an A* bot
+    (3, 16, 300, 1 | (1 << 6), [0, 1, 1], "combat"),    # HardcodedSpawns
+    (6, 16, 300, 2 | (1 << 2), [0, 1, 1], "combat"),    # NavmeshSpawn
+    (2, 32, 300, 1 | (1 << 5), [0, 1, 1], "combat"),    # EnableCurriculum
 ]
 
 
@@ -110,6 +113,40 @@ def test_auto_reset_off_and_triggered_resets():
         e.step()
         o.step()
         _compare_all(e, o, f"step {s}")
+
+
+def test_curriculum_resets_match_oracle():
+    """EnableCurriculum across many episodes: the LearnShooting/FullMatch
+    draw per reset (sim.cpp:852-867), LearnShooting spawns and rewards
+    (utils.cpp:819-837, sim.cpp:3707-3732), with NavmeshSpawn on half the
+    runs taking precedence for spawns (utils.cpp:805-809)."""
+    for flags in (1 << 5, (1 << 5) | (1 << 2)):
+        ts, W = 2, 16
+        e = T.Engine(W, ts, sim_flags=flags, auto_reset=False)
+        o = T.Oracle(W, ts, sim_flags=flags, auto_reset=False)
+        for sim in (e, o):
+            sim.put_ctrl([0, 1, 1])
+            sim.init()
+        for s in range(400):
+            if s % 8 == 0:
+                for w in range(W):
+                    if (s // 8 + w) % 3 == 0:
+                        e.trigger_reset(w)
+                        o.view("RESET")[w] = 1
+            acts = T.combat_actions(o, s)
+            e.set_actions(acts)
+            o.set_actions(acts)
+            e.step()
+            o.step()
+            if s % 5 == 0:
+                _compare_all(e, o, f"flags {flags} step {s}")
+            else:
+                for n in ("SELF_OBSERVATION", "REWARD", "WORLD_CURRICULUM"):
+                    T.compare(e.get(n), o.get(n), f"{n} @ flags {flags} step {s}")
+        cur = o.get("WORLD_CURRICULUM").ravel()
+        assert 0 < cur.sum() < W or s > 0
+        e.close()
+        o.close()
 
 
 def test_headline_batch_shards_match_oracle():
