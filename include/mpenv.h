@@ -113,6 +113,25 @@ enum mpenv_export_id {
     MPENV_EXPORT_REPLAY_LOG = 72,      /* [W] mpenv_step_log as i32[W][217] (replay mode) */
     MPENV_EXPORT_SNAPSHOT_WRITTEN = 73 /* [W][1] i32: snapshot written this step (event log) */
 };
+/* FULL_TEAM_* (26-35): one row per (world, team) = [W * 2], six player slots
+ * (slots >= team_size stay zero), floats per slot (types.hpp:1048-1100):
+ *   common (24): isValid, id[6] (one-hot slot), isAlive, global xyz
+ *     (normalised, unclamped), facing yaw, pitch, velocity xyz (world frame),
+ *     stand[7] (cur S/C/P, tgt S/C/P, transition), inZone
+ *   player = common + hp/100, bullets/30, isReloading, autoheal fraction
+ *   enemy  = common + wasHit, firedShot, hasLOS[6] (per own slot), teamKnowsLocation
+ *   global (16): teamID[2], fraction of match remaining, zone: center xyz,
+ *     mine / enemy controlling, contested, captured, steps until point,
+ *     steps remaining, id[4]
+ * FULL_TEAM_FWD/REAR_LIDAR hold the agents' lidar as of the previous step
+ * (the reference copies it before pvpLidarSystem runs).  FULL_TEAM_ACTIONS
+ * and FULL_TEAM_POLICY_ASSIGNMENTS are inputs the step never reads
+ * (readFullTeamActionsPolicies is compiled out, sim.cpp:4928-4957). */
+#define MPENV_FT_COMMON_DIM 24
+#define MPENV_FT_PLAYER_DIM 28
+#define MPENV_FT_ENEMY_DIM 33
+#define MPENV_FT_GLOBAL_DIM 16
+
 /* EVENT_LOG (36): this step's GameEvent slots as i32[W][2N+1][6] (slot 2i, 2i+1
  * = agent i's reload / shot / kill, slot 2N = capture; type 0 = empty).
  * PACKED_STEP_SNAPSHOT (37): i32[W][48] mpenv_packed_step_snapshot.  Both

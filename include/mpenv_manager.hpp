@@ -191,6 +191,20 @@ public:
     Tensor magazineTensor() const { return get(MPENV_EXPORT_MAGAZINE); }
     Tensor aliveTensor() const { return get(MPENV_EXPORT_ALIVE); }
     Tensor rewardHyperParamsTensor() const { return get(MPENV_EXPORT_REWARD_HYPER_PARAMS); }
+    // FullTeamInterface (mgr.hpp:110-120)
+    Tensor fullTeamActionTensor() const { return get(MPENV_EXPORT_FULL_TEAM_ACTIONS); }
+    Tensor fullTeamGlobalObservationsTensor() const { return get(MPENV_EXPORT_FULL_TEAM_GLOBAL); }
+    Tensor fullTeamPlayerObservationsTensor() const { return get(MPENV_EXPORT_FULL_TEAM_PLAYERS); }
+    Tensor fullTeamEnemyObservationsTensor() const { return get(MPENV_EXPORT_FULL_TEAM_ENEMIES); }
+    Tensor fullTeamLastKnownEnemyObservationsTensor() const
+    {
+        return get(MPENV_EXPORT_FULL_TEAM_LAST_KNOWN_ENEMIES);
+    }
+    Tensor fullTeamFwdLidarTensor() const { return get(MPENV_EXPORT_FULL_TEAM_FWD_LIDAR); }
+    Tensor fullTeamRearLidarTensor() const { return get(MPENV_EXPORT_FULL_TEAM_REAR_LIDAR); }
+    Tensor fullTeamRewardTensor() const { return get(MPENV_EXPORT_FULL_TEAM_REWARD); }
+    Tensor fullTeamDoneTensor() const { return get(MPENV_EXPORT_FULL_TEAM_DONE); }
+    Tensor fullTeamPolicyAssignmentTensor() const { return get(MPENV_EXPORT_FULL_TEAM_POLICY_ASSIGNMENTS); }
 
     TrainInterface trainInterface() const
     {

@@ -115,6 +115,17 @@ struct DevState {
     int32_t *magazine;     // [A][2]
     float *rewardCoefs;    // [A][9]
     int32_t *trainCtrl;    // [3]
+    // FullTeamInterface columns, one row per (world, team) (types.hpp:1040-1152)
+    int32_t *ftActions;    // [W*2][6][4] (input, never read by the step)
+    float *ftGlobal;       // [W*2][16]
+    float *ftPlayers;      // [W*2][6][28]
+    float *ftEnemies;      // [W*2][6][33]
+    float *ftLastKnown;    // [W*2][6][24]
+    float *ftFwdLidar;     // [W*2][6][64][4]
+    float *ftRearLidar;    // [W*2][6][16][4]
+    float *ftReward;       // [W*2]
+    int32_t *ftDone;       // [W*2]
+    int32_t *ftPolicy;     // [W*2] (input, never read by the step)
 
     // Record / replay / event logs (allocated only when enabled)
     mpenv_step_log *recordLog;             // [W] written by the step

@@ -1653,7 +1653,20 @@ __global__ void __launch_bounds__(kSimBlock) k_sim(DevState S, SceneDev sc)
         S.done[g] = S.finished[w] ? 1 : 0;
     }
     __syncthreads();
-    if (wlane) resetSystemD(S, sc, w);
+    if (wlane) {
+        // fullTeamDoneRewardSystem (sim.cpp:4720-4747)
+        for (int t = 0; t < 2; t++) {
+            float r = 0.f;
+            bool done = true;
+            for (int j = t * S.T; j < (t + 1) * S.T; j++) {
+                r += S.reward[(int64_t)w * N + j];
+                if (!S.done[(int64_t)w * N + j]) done = false;
+            }
+            S.ftReward[(int64_t)w * 2 + t] = r;
+            S.ftDone[(int64_t)w * 2 + t] = done ? 1 : 0;
+        }
+        resetSystemD(S, sc, w);
+    }
 }
 
 // utils.cpp:169-184 inFrustum
@@ -1860,6 +1873,104 @@ __device__ __forceinline__ void storeVec(float *dst, const float *src, int n)
     for (int k = 0; k < n; k++) dst[k] = src[k];
 }
 
+// fullTeamObservationsSystem (sim.cpp:3054-3301), the part owned by agent g
+// (team, slot off): its player slot in its own team's interface, its enemy
+// and last-known slots in the other team's interface (the common block is
+// the same in both, the one-hot id is the slot), and for slot 0 the team's
+// global observation and the zeroed slots past team_size.  Positions are
+// normalised without the clamp pvpObservations applies.  The lidar copy is
+// fused into k_lidar.
+__device__ __forceinline__ Vec3 normalizedPosUnclampedD(const SceneDev &sc, Vec3 p)
+{
+    float min_x = sc.worldBounds.pMin.x, min_y = sc.worldBounds.pMin.y, min_z = sc.worldBounds.pMin.z;
+    float max_x = sc.worldBounds.pMax.x, max_y = sc.worldBounds.pMax.y, max_z = sc.worldBounds.pMax.z;
+    float xr = max_x - min_x, yr = max_y - min_y, zr = max_z - min_z;
+    return v3((p.x - min_x) / xr, (p.y - min_y) / yr, (p.z - min_z) / zr);
+}
+
+__device__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int64_t g, int team, int off)
+{
+    const int T = S.T;
+    const int64_t g0 = (int64_t)w * S.N;
+    const int64_t mine = (int64_t)w * 2 + team, theirs = (int64_t)w * 2 + (team ^ 1);
+    float *pl = &S.ftPlayers[(mine * 6 + off) * MPENV_FT_PLAYER_DIM];
+    float *en = &S.ftEnemies[(theirs * 6 + off) * MPENV_FT_ENEMY_DIM];
+    float *lk = &S.ftLastKnown[(theirs * 6 + off) * MPENV_FT_COMMON_DIM];
+    const bool alive = S.alive[g] != 0.f;
+
+    // enemy-only fields first: they decide whether the last-known slot
+    // receives the common block
+    const float fired = alive && S.firedT[g] >= 0.f ? 1.f : 0.f;
+    bool knows = fired != 0.f;
+    uint32_t los = 0;
+    if (alive) {
+        const int64_t gm0 = g0 + (team ^ 1) * T;
+        for (int m = 0; m < T; m++) los |= ((S.visMask[gm0 + m] >> off) & 1u) << m;
+        knows = knows || los != 0;
+    }
+    en[24] = alive ? (float)S.wasShot[g] : 0.f;
+    en[25] = fired;
+    for (int m = 0; m < kMaxTeamSize; m++) en[26 + m] = (los >> m) & 1u ? 1.f : 0.f;
+    en[32] = knows ? 1.f : 0.f;
+
+    // the common block, stored to all three slots as it is produced
+    auto put = [&](int k, float v) {
+        pl[k] = v;
+        en[k] = v;
+        lk[k] = knows ? v : 0.f;
+    };
+    put(0, 1.f);
+    for (int k = 0; k < kMaxTeamSize; k++) put(1 + k, k == off ? 1.f : 0.f);
+    if (alive) {
+        put(7, 1.f);
+        const Vec3 np = normalizedPosUnclampedD(sc, ldPos(S, g));
+        put(8, np.x); put(9, np.y); put(10, np.z);
+        put(11, 0.5f * ((S.ayaw[g] / kPi) + 1.f));
+        put(12, 0.5f * (S.apitch[g] / (0.25f * kPi) + 1.f));
+        put(13, S.vx[g]); put(14, S.vy[g]); put(15, S.vz[g]);
+        const int cp = S.curPose[g], tp = S.tgtPose[g];
+        put(16, cp == kStand ? 1.f : 0.f);
+        put(17, cp == kCrouch ? 1.f : 0.f);
+        put(18, cp == kProne ? 1.f : 0.f);
+        put(19, tp == kStand ? 1.f : 0.f);
+        put(20, tp == kCrouch ? 1.f : 0.f);
+        put(21, tp == kProne ? 1.f : 0.f);
+        put(22, (float)S.transRem[g] / (float)c::kPoseTransitionSpeed);
+        put(23, (S.flags[g] & kFlagInZone) ? 1.f : 0.f);
+        pl[24] = S.hp[g] / 100.f;
+        pl[25] = (float)S.magazine[2 * g] / 30;
+        pl[26] = (float)S.magazine[2 * g + 1];
+        pl[27] = float(S.autohealSteps[g]) / float(c::kOutOfCombatSteps);
+    } else {
+        for (int k = 7; k < MPENV_FT_COMMON_DIM; k++) put(k, 0.f);
+        for (int k = MPENV_FT_COMMON_DIM; k < MPENV_FT_PLAYER_DIM; k++) pl[k] = 0.f;
+    }
+
+    if (off != 0) return;
+    for (int s = T; s < kMaxTeamSize; s++) {
+        for (int k = 0; k < MPENV_FT_PLAYER_DIM; k++) S.ftPlayers[(mine * 6 + s) * MPENV_FT_PLAYER_DIM + k] = 0.f;
+        for (int k = 0; k < MPENV_FT_ENEMY_DIM; k++) S.ftEnemies[(mine * 6 + s) * MPENV_FT_ENEMY_DIM + k] = 0.f;
+        for (int k = 0; k < MPENV_FT_COMMON_DIM; k++) S.ftLastKnown[(mine * 6 + s) * MPENV_FT_COMMON_DIM + k] = 0.f;
+    }
+    float gob[MPENV_FT_GLOBAL_DIM];
+    gob[0] = team == 0 ? 0.f : 1.f;
+    gob[1] = team == 0 ? 1.f : 0.f;
+    gob[2] = float(c::kEpisodeLen - S.curStep[w]) / c::kEpisodeLen;
+    const int cz = S.curZone[w];
+    const AABB za = sc.zoneAABB[cz];
+    const Vec3 nc = normalizedPosUnclampedD(sc, (za.pMax + za.pMin) / 2.f);
+    gob[3] = nc.x; gob[4] = nc.y; gob[5] = nc.z;
+    const int ctrl = S.controlling[w];
+    gob[6] = ctrl == team ? 1.f : 0.f;
+    gob[7] = (ctrl != -1 && ctrl != team) ? 1.f : 0.f;
+    gob[8] = S.contested[w] ? 1.f : 0.f;
+    gob[9] = S.captured[w] ? 1.f : 0.f;
+    gob[10] = float(S.stepsUntilPoint[w]) / float(c::kZonePointInterval);
+    gob[11] = float(S.zoneSteps[w]) / float(c::kNumStepsPerZone);
+    for (int k = 0; k < 4; k++) gob[12 + k] = cz == k ? 1.f : 0.f;
+    storeVec(&S.ftGlobal[mine * MPENV_FT_GLOBAL_DIM], gob, MPENV_FT_GLOBAL_DIM);
+}
+
 // pvpOpponentMasksSystem (sim.cpp:2562-2614) + pvpObservationsSystem
 // (sim.cpp:2645-3052).  Lane = agent.
 __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
@@ -1873,6 +1984,8 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
     const int team = i / T, off = i - team * T;
     const uint8_t *vm = S.visMask;
     const bool self_alive = S.alive[g] != 0.f;
+
+    fullTeamSlotD(S, sc, w, g, team, off);
 
     // ---- masks
     float mask[kMaxTeamSize];
@@ -1981,6 +2094,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
         storeVec(&S.oppObs[(g * 6 + k) * kOtherObs], oob, kOtherObs);
         storeVec(&S.oppPos[(g * 6 + k) * 3], opos, 3);
     }
+
 }
 
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray; a workgroup walks
@@ -2027,6 +2141,12 @@ __global__ void __launch_bounds__(kBlock) k_lidar(DevState S, SceneDev sc)
         ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
         const float2 cs = fan[fwd ? x : 32 + x];
         Vec3 dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
+        float4 *dst = fwd ? reinterpret_cast<float4 *>(S.fwdLidar) + g * kFwdRays + kk
+                          : reinterpret_cast<float4 *>(S.rearLidar) + g * kRearRays + kk;
+        // fullTeamObservationsSystem copies the lidar before this system
+        // overwrites it (sim.cpp:5283-5310): the previous value moves into
+        // the team interface's slot.  Loaded here so the traversal hides it.
+        const float4 prev = *dst;
         WorldHit hw = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, ray_o, dir);
         float4 out;
         if (hw.hit) {
@@ -2036,8 +2156,10 @@ __global__ void __launch_bounds__(kBlock) k_lidar(DevState S, SceneDev sc)
         } else {
             out = make_float4(-1.f, 0.f, 0.f, 0.f);
         }
-        float4 *dst = fwd ? reinterpret_cast<float4 *>(S.fwdLidar) + g * kFwdRays + kk
-                          : reinterpret_cast<float4 *>(S.rearLidar) + g * kRearRays + kk;
+        const int64_t slot = ((int64_t)w * 2 + i / T) * kMaxTeamSize + (i % T);
+        float4 *tdst = fwd ? reinterpret_cast<float4 *>(S.ftFwdLidar) + slot * kFwdRays + kk
+                           : reinterpret_cast<float4 *>(S.ftRearLidar) + slot * kRearRays + kk;
+        *tdst = prev;
         *dst = out;
     }
 }

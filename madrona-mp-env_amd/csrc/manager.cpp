@@ -312,6 +312,19 @@ bool mpenv_manager::exportDesc(int32_t id, TensorDesc &d)
     case MPENV_EXPORT_HP: return set(S.hp, MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_ALIVE: return set(S.alive, MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_MAGAZINE: return set(S.magazine, MPENV_DTYPE_INT32, { A, 2 });
+    case MPENV_EXPORT_FULL_TEAM_ACTIONS: return set(S.ftActions, MPENV_DTYPE_INT32, { W * 2, 6, 4 });
+    case MPENV_EXPORT_FULL_TEAM_GLOBAL: return set(S.ftGlobal, MPENV_DTYPE_FLOAT32, { W * 2, MPENV_FT_GLOBAL_DIM });
+    case MPENV_EXPORT_FULL_TEAM_PLAYERS:
+        return set(S.ftPlayers, MPENV_DTYPE_FLOAT32, { W * 2, 6, MPENV_FT_PLAYER_DIM });
+    case MPENV_EXPORT_FULL_TEAM_ENEMIES:
+        return set(S.ftEnemies, MPENV_DTYPE_FLOAT32, { W * 2, 6, MPENV_FT_ENEMY_DIM });
+    case MPENV_EXPORT_FULL_TEAM_LAST_KNOWN_ENEMIES:
+        return set(S.ftLastKnown, MPENV_DTYPE_FLOAT32, { W * 2, 6, MPENV_FT_COMMON_DIM });
+    case MPENV_EXPORT_FULL_TEAM_FWD_LIDAR: return set(S.ftFwdLidar, MPENV_DTYPE_FLOAT32, { W * 2, 6, 2, 32, 4 });
+    case MPENV_EXPORT_FULL_TEAM_REAR_LIDAR: return set(S.ftRearLidar, MPENV_DTYPE_FLOAT32, { W * 2, 6, 2, 8, 4 });
+    case MPENV_EXPORT_FULL_TEAM_REWARD: return set(S.ftReward, MPENV_DTYPE_FLOAT32, { W * 2, 1 });
+    case MPENV_EXPORT_FULL_TEAM_DONE: return set(S.ftDone, MPENV_DTYPE_INT32, { W * 2, 1 });
+    case MPENV_EXPORT_FULL_TEAM_POLICY_ASSIGNMENTS: return set(S.ftPolicy, MPENV_DTYPE_INT32, { W * 2, 1 });
     case MPENV_EXPORT_FILTERS_STATE: return set(S.filters, MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_REWARD_HYPER_PARAMS: return set(S.rewardCoefs, MPENV_DTYPE_FLOAT32, { A, 9 });
     case MPENV_EXPORT_EVENT_LOG:
@@ -508,6 +521,16 @@ static void allocState(mpenv_manager &m)
     S.magazine = m.alloc<int32_t>(A * 2);
     S.rewardCoefs = m.alloc<float>(A * 9);
     S.trainCtrl = m.alloc<int32_t>(3);
+    S.ftActions = m.alloc<int32_t>(W * 2 * 6 * 4);
+    S.ftGlobal = m.alloc<float>(W * 2 * MPENV_FT_GLOBAL_DIM);
+    S.ftPlayers = m.alloc<float>(W * 2 * 6 * MPENV_FT_PLAYER_DIM);
+    S.ftEnemies = m.alloc<float>(W * 2 * 6 * MPENV_FT_ENEMY_DIM);
+    S.ftLastKnown = m.alloc<float>(W * 2 * 6 * MPENV_FT_COMMON_DIM);
+    S.ftFwdLidar = m.alloc<float>(W * 2 * 6 * kFwdRays * 4);
+    S.ftRearLidar = m.alloc<float>(W * 2 * 6 * kRearRays * 4);
+    S.ftReward = m.alloc<float>(W * 2);
+    S.ftDone = m.alloc<int32_t>(W * 2);
+    S.ftPolicy = m.alloc<int32_t>(W * 2);
 }
 
 static void openLogs(mpenv_manager &m, const mpenv_config *cfg)
@@ -599,6 +622,16 @@ static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_
     G.alive = S.alive + g0;
     G.magazine = S.magazine + g0 * 2;
     G.rewardCoefs = S.rewardCoefs + g0 * 9;
+    G.ftActions = S.ftActions + w0 * 2 * 6 * 4;
+    G.ftGlobal = S.ftGlobal + w0 * 2 * MPENV_FT_GLOBAL_DIM;
+    G.ftPlayers = S.ftPlayers + w0 * 2 * 6 * MPENV_FT_PLAYER_DIM;
+    G.ftEnemies = S.ftEnemies + w0 * 2 * 6 * MPENV_FT_ENEMY_DIM;
+    G.ftLastKnown = S.ftLastKnown + w0 * 2 * 6 * MPENV_FT_COMMON_DIM;
+    G.ftFwdLidar = S.ftFwdLidar + w0 * 2 * 6 * kFwdRays * 4;
+    G.ftRearLidar = S.ftRearLidar + w0 * 2 * 6 * kRearRays * 4;
+    G.ftReward = S.ftReward + w0 * 2;
+    G.ftDone = S.ftDone + w0 * 2;
+    G.ftPolicy = S.ftPolicy + w0 * 2;
     if (S.recordLog) G.recordLog = S.recordLog + w0;
     if (S.replayLog) G.replayLog = S.replayLog + w0;
     if (S.events) G.events = S.events + w0 * S.evStride;
@@ -658,7 +691,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         return fail(MPENV_ERR_INVALID, "team_size must be in [1, 6]");
     if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");
     if (!cfg->scene_path) return fail(MPENV_ERR_INVALID, "scene_path is required");
-    const uint32_t unsupported = MPENV_SIMFLAG_FULL_TEAM_POLICY | MPENV_SIMFLAG_SUB_ZONES;
+    const uint32_t unsupported = MPENV_SIMFLAG_SUB_ZONES;
     if (cfg->sim_flags & unsupported) {
         static const char *names[] = { "SpawnInMiddle", "RandomizeHPMagazine", "NavmeshSpawn", "NoRespawn",
                                        "StaggerStarts", "EnableCurriculum", "HardcodedSpawns",

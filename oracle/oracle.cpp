@@ -244,6 +244,9 @@ struct Oracle {
     std::vector<float> aimAction, reward, selfObs, filtersObs, teammateObs, opponentObs, lastKnownObs,
         selfPos, teammatePos, opponentPos, lastKnownPos, masks, fwdLidar, rearLidar, agentMap, hp,
         alive, rewardCoefs;
+    // FullTeamInterface columns, [W * 2] team interfaces (types.hpp:1040-1152)
+    std::vector<int32_t> ftActions, ftDone, ftPolicy;
+    std::vector<float> ftGlobal, ftPlayers, ftEnemies, ftLastKnown, ftFwdLidar, ftRearLidar, ftReward;
     std::vector<float> dbgAF, dbgWF, dbgCrumbs;
     // logs (record / replay / events), enabled by oracle_set_log_modes
     bool recordOn = false, replayOn = false, eventsOn = false;
@@ -2238,6 +2241,129 @@ void pvpLidar(Oracle &o, int w, int i)
     }
 }
 
+// sim.cpp:3054-3301 fullTeamObservationsSystem, for both team interfaces of
+// world w.  Unlike pvpObservations, positions are normalised without a clamp
+// and velocities are global; last-known enemies are cleared every step and
+// hold the common part of the enemy observation only while the team knows
+// the location.  The lidar copy is the agents' lidar as it stands before
+// this step's pvpLidarSystem (that system is added to the graph after this
+// one, sim.cpp:5294-5310).
+void fullTeamObservations(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    const int T = o.teamSize;
+    auto norm = [&](Vec3 p) {
+        float min_x = o.worldBounds.pMin.x, min_y = o.worldBounds.pMin.y, min_z = o.worldBounds.pMin.z;
+        float max_x = o.worldBounds.pMax.x, max_y = o.worldBounds.pMax.y, max_z = o.worldBounds.pMax.z;
+        float xr = max_x - min_x, yr = max_y - min_y, zr = max_z - min_z;
+        return v3((p.x - min_x) / xr, (p.y - min_y) / yr, (p.z - min_z) / zr);
+    };
+    for (int team = 0; team < 2; team++) {
+        const size_t ti = (size_t)w * 2 + team;
+        float *players = &o.ftPlayers[ti * 6 * MPENV_FT_PLAYER_DIM];
+        float *enemies = &o.ftEnemies[ti * 6 * MPENV_FT_ENEMY_DIM];
+        float *last = &o.ftLastKnown[ti * 6 * MPENV_FT_COMMON_DIM];
+        std::fill(players, players + 6 * MPENV_FT_PLAYER_DIM, 0.f);
+        std::fill(enemies, enemies + 6 * MPENV_FT_ENEMY_DIM, 0.f);
+        std::fill(last, last + 6 * MPENV_FT_COMMON_DIM, 0.f);
+
+        float *gob = &o.ftGlobal[ti * MPENV_FT_GLOBAL_DIM];
+        gob[0] = team == 0 ? 0.f : 1.f;
+        gob[1] = team == 0 ? 1.f : 0.f;
+        gob[2] = float(kEpisodeLen - wd.curStep) / kEpisodeLen;
+        {
+            const AABB za = o.zoneAABBs[wd.curZone];
+            Vec3 nc = norm((za.pMax + za.pMin) / 2.f);
+            float *z = &gob[3];
+            z[0] = nc.x; z[1] = nc.y; z[2] = nc.z;
+            z[3] = (wd.curControllingTeam == team) ? 1.f : 0.f;
+            z[4] = (wd.curControllingTeam != -1 && wd.curControllingTeam != team) ? 1.f : 0.f;
+            z[5] = wd.isContested ? 1.f : 0.f;
+            z[6] = wd.isCaptured ? 1.f : 0.f;
+            z[7] = float(wd.stepsUntilPoint) / float(kZonePointInterval);
+            z[8] = float(wd.zoneStepsRemaining) / float(kNumStepsPerZone);
+            for (int k = 0; k < 4; k++) z[9 + k] = wd.curZone == k ? 1.f : 0.f;
+        }
+        auto fillCommon = [&](float *ob, int j, int slot) {
+            ob[0] = 1.f;
+            ob[1 + slot] = 1.f;
+            const size_t gj = o.gi(w, j);
+            if (!o.alive[gj]) return false;
+            const Agent &a = o.agent(w, j);
+            ob[7] = 1.f;
+            Vec3 np = norm(a.pos);
+            ob[8] = np.x; ob[9] = np.y; ob[10] = np.z;
+            ob[11] = 0.5f * ((a.aimYaw / kPi) + 1.f);
+            ob[12] = 0.5f * (a.aimPitch / (0.25f * kPi) + 1.f);
+            ob[13] = a.vel.x; ob[14] = a.vel.y; ob[15] = a.vel.z;
+            ob[16] = a.curPose == kStand ? 1.f : 0.f;
+            ob[17] = a.curPose == kCrouch ? 1.f : 0.f;
+            ob[18] = a.curPose == kProne ? 1.f : 0.f;
+            ob[19] = a.tgtPose == kStand ? 1.f : 0.f;
+            ob[20] = a.tgtPose == kCrouch ? 1.f : 0.f;
+            ob[21] = a.tgtPose == kProne ? 1.f : 0.f;
+            ob[22] = (float)a.transitionRemaining / (float)kPoseTransitionSpeed;
+            ob[23] = a.inZone ? 1.f : 0.f;
+            return true;
+        };
+        for (int s = 0; s < T; s++) {
+            const int j = team * T + s;
+            float *ob = &players[s * MPENV_FT_PLAYER_DIM];
+            if (!fillCommon(ob, j, s)) continue;
+            const size_t gj = o.gi(w, j);
+            ob[24] = (float)o.hp[gj] / 100.f;
+            ob[25] = (float)o.magazine[2 * gj] / 30;
+            ob[26] = (float)o.magazine[2 * gj + 1];
+            ob[27] = float(o.agent(w, j).remainingStepsBeforeAutoheal) / float(kOutOfCombatSteps);
+        }
+        for (int s = 0; s < T; s++) {
+            const int j = (team ^ 1) * T + s;
+            float *ob = &enemies[s * MPENV_FT_ENEMY_DIM];
+            float *lk = &last[s * MPENV_FT_COMMON_DIM];
+            if (!fillCommon(ob, j, s)) {
+                std::fill(lk, lk + MPENV_FT_COMMON_DIM, 0.f);
+                continue;
+            }
+            const Agent &a = o.agent(w, j);
+            if (a.wasKilled) std::fill(lk, lk + MPENV_FT_COMMON_DIM, 0.f);
+            ob[24] = (float)a.wasShotCount;
+            ob[25] = a.firedShotT >= 0.f ? 1.f : 0.f;
+            bool knows = ob[25] != 0.f;
+            for (int m = 0; m < T; m++) {
+                if (o.agent(w, team * T + m).canSee[s]) {
+                    ob[26 + m] = 1.f;
+                    knows = true;
+                }
+            }
+            ob[32] = knows ? 1.f : 0.f;
+            if (knows) std::copy(ob, ob + MPENV_FT_COMMON_DIM, lk);
+        }
+        for (int s = 0; s < T; s++) {
+            const size_t g = o.gi(w, team * T + s);
+            const int fl = kFwdH * kFwdW * 4, rl = kRearH * kRearW * 4;
+            std::copy(&o.fwdLidar[g * fl], &o.fwdLidar[(g + 1) * fl], &o.ftFwdLidar[(ti * 6 + s) * fl]);
+            std::copy(&o.rearLidar[g * rl], &o.rearLidar[(g + 1) * rl], &o.ftRearLidar[(ti * 6 + s) * rl]);
+        }
+    }
+}
+
+// sim.cpp:4720-4747 fullTeamDoneRewardSystem
+void fullTeamDoneReward(Oracle &o, int w)
+{
+    for (int team = 0; team < 2; team++) {
+        float r = 0.f;
+        bool done = true;
+        for (int i = 0; i < o.N; i++) {
+            if (o.agent(w, i).team != team) continue;
+            const size_t g = o.gi(w, i);
+            r += o.reward[g];
+            if (!o.done[g]) done = false;
+        }
+        o.ftReward[(size_t)w * 2 + team] = r;
+        o.ftDone[(size_t)w * 2 + team] = done ? 1 : 0;
+    }
+}
+
 // sim.cpp:5174-5320 resetAndObsTasks (per world)
 void resetAndObs(Oracle &o, int w)
 {
@@ -2245,6 +2371,7 @@ void resetAndObs(Oracle &o, int w)
     for (int i = 0; i < o.N; i++) opponentsWriteVisibility(o, w, i);
     for (int i = 0; i < o.N; i++) opponentMasks(o, w, i);
     for (int i = 0; i < o.N; i++) pvpObservations(o, w, i);
+    fullTeamObservations(o, w);
     for (int i = 0; i < o.N; i++) pvpLidar(o, w, i);
 }
 
@@ -2297,6 +2424,7 @@ void replayTail(Oracle &o, int w)
     for (int i = 0; i < N; i++) zoneRewardSystem(o, w, i);
     teamAndFinalReward(o, w);
     for (int i = 0; i < N; i++) o.done[o.gi(w, i)] = o.worlds[w].isFinished ? 1 : 0;
+    fullTeamDoneReward(o, w);
     resetAndObs(o, w);
 }
 
@@ -2562,6 +2690,16 @@ void *oracle_create(const oracle_config *cfg)
         o->masks.assign(A * 6, 0.f);
         o->fwdLidar.assign(A * kFwdH * kFwdW * 4, 0.f);
         o->rearLidar.assign(A * kRearH * kRearW * 4, 0.f);
+        o->ftActions.assign(W * 2 * 6 * 4, 0);
+        o->ftGlobal.assign(W * 2 * MPENV_FT_GLOBAL_DIM, 0.f);
+        o->ftPlayers.assign(W * 2 * 6 * MPENV_FT_PLAYER_DIM, 0.f);
+        o->ftEnemies.assign(W * 2 * 6 * MPENV_FT_ENEMY_DIM, 0.f);
+        o->ftLastKnown.assign(W * 2 * 6 * MPENV_FT_COMMON_DIM, 0.f);
+        o->ftFwdLidar.assign(W * 2 * 6 * kFwdH * kFwdW * 4, 0.f);
+        o->ftRearLidar.assign(W * 2 * 6 * kRearH * kRearW * 4, 0.f);
+        o->ftReward.assign(W * 2, 0.f);
+        o->ftDone.assign(W * 2, 0);
+        o->ftPolicy.assign(W * 2, 0);
         o->agentMap.assign(A * 16 * 16 * 4, 0.f);
         o->hp.assign(A, 0.f);
         o->alive.assign(A, 0.f);
@@ -2621,6 +2759,21 @@ int oracle_export(void *h, int32_t id, void **ptr, int32_t *dtype, int32_t *ndim
     case MPENV_EXPORT_HP: return set(o.hp.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_ALIVE: return set(o.alive.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_MAGAZINE: return set(o.magazine.data(), MPENV_DTYPE_INT32, { A, 2 });
+    case MPENV_EXPORT_FULL_TEAM_ACTIONS: return set(o.ftActions.data(), MPENV_DTYPE_INT32, { W * 2, 6, 4 });
+    case MPENV_EXPORT_FULL_TEAM_GLOBAL: return set(o.ftGlobal.data(), MPENV_DTYPE_FLOAT32, { W * 2, MPENV_FT_GLOBAL_DIM });
+    case MPENV_EXPORT_FULL_TEAM_PLAYERS:
+        return set(o.ftPlayers.data(), MPENV_DTYPE_FLOAT32, { W * 2, 6, MPENV_FT_PLAYER_DIM });
+    case MPENV_EXPORT_FULL_TEAM_ENEMIES:
+        return set(o.ftEnemies.data(), MPENV_DTYPE_FLOAT32, { W * 2, 6, MPENV_FT_ENEMY_DIM });
+    case MPENV_EXPORT_FULL_TEAM_LAST_KNOWN_ENEMIES:
+        return set(o.ftLastKnown.data(), MPENV_DTYPE_FLOAT32, { W * 2, 6, MPENV_FT_COMMON_DIM });
+    case MPENV_EXPORT_FULL_TEAM_FWD_LIDAR:
+        return set(o.ftFwdLidar.data(), MPENV_DTYPE_FLOAT32, { W * 2, 6, kFwdH, kFwdW, 4 });
+    case MPENV_EXPORT_FULL_TEAM_REAR_LIDAR:
+        return set(o.ftRearLidar.data(), MPENV_DTYPE_FLOAT32, { W * 2, 6, kRearH, kRearW, 4 });
+    case MPENV_EXPORT_FULL_TEAM_REWARD: return set(o.ftReward.data(), MPENV_DTYPE_FLOAT32, { W * 2, 1 });
+    case MPENV_EXPORT_FULL_TEAM_DONE: return set(o.ftDone.data(), MPENV_DTYPE_INT32, { W * 2, 1 });
+    case MPENV_EXPORT_FULL_TEAM_POLICY_ASSIGNMENTS: return set(o.ftPolicy.data(), MPENV_DTYPE_INT32, { W * 2, 1 });
     case MPENV_EXPORT_FILTERS_STATE: return set(o.filtersObs.data(), MPENV_DTYPE_FLOAT32, { A, 1 });
     case MPENV_EXPORT_REWARD_HYPER_PARAMS: return set(o.rewardCoefs.data(), MPENV_DTYPE_FLOAT32, { A, 9 });
     case MPENV_EXPORT_EVENT_LOG:

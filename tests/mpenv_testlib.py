@@ -33,8 +33,16 @@ EXPORT = dict(
     FILTERS_STATE=38, REWARD_HYPER_PARAMS=39, SIM_CONTROL=64, DEBUG_AGENT_F32=65,
     DEBUG_AGENT_I32=66, DEBUG_WORLD_I32=67, DEBUG_WORLD_F32=68, DEBUG_EXPLORE=69,
     DEBUG_CRUMBS=70, EVENT_LOG=36, PACKED_STEP_SNAPSHOT=37, RECORD_LOG=71, REPLAY_LOG=72,
-    SNAPSHOT_WRITTEN=73,
+    SNAPSHOT_WRITTEN=73, FULL_TEAM_ACTIONS=26, FULL_TEAM_GLOBAL=27, FULL_TEAM_PLAYERS=28,
+    FULL_TEAM_ENEMIES=29, FULL_TEAM_LAST_KNOWN_ENEMIES=30, FULL_TEAM_FWD_LIDAR=31,
+    FULL_TEAM_REAR_LIDAR=32, FULL_TEAM_REWARD=33, FULL_TEAM_DONE=34, FULL_TEAM_POLICY_ASSIGNMENTS=35,
 )
+
+# FullTeamInterface outputs (fullTeamObservationsSystem, fullTeamDoneRewardSystem)
+FULL_TEAM_OUTPUTS = [
+    "FULL_TEAM_GLOBAL", "FULL_TEAM_PLAYERS", "FULL_TEAM_ENEMIES", "FULL_TEAM_LAST_KNOWN_ENEMIES",
+    "FULL_TEAM_FWD_LIDAR", "FULL_TEAM_REAR_LIDAR", "FULL_TEAM_REWARD", "FULL_TEAM_DONE",
+]
 
 # Exports compared between engine and oracle after every step.
 STEP_OUTPUTS = [
@@ -43,7 +51,7 @@ STEP_OUTPUTS = [
     "SELF_POSITION", "TEAMMATE_POSITIONS", "OPPONENT_POSITIONS", "OPPONENT_LAST_KNOWN_POSITIONS",
     "OPPONENT_MASKS", "REWARD", "DONE", "MATCH_RESULT", "REWARD_HYPER_PARAMS", "RESET",
     "WORLD_CURRICULUM", "PVP_DISCRETE_ACTION", "PVP_DISCRETE_AIM_ACTION", "PVP_AIM_ACTION",
-]
+] + FULL_TEAM_OUTPUTS
 DEBUG_OUTPUTS = ["DEBUG_AGENT_F32", "DEBUG_AGENT_I32", "DEBUG_WORLD_I32", "DEBUG_WORLD_F32",
                  "DEBUG_CRUMBS"]
 

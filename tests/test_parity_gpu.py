@@ -59,6 +59,7 @@ LIVE = [
     (3, 16, 300, 1 | (1 << 6), [0, 1, 1], "combat"),    # HardcodedSpawns
     (6, 16, 300, 2 | (1 << 2), [0, 1, 1], "combat"),    # NavmeshSpawn
     (2, 32, 300, 1 | (1 << 5), [0, 1, 1], "combat"),    # EnableCurriculum
+    (4, 8, 200, 1 | 8 | (1 << 9), [0, 1, 1], "combat"),  # FullTeamPolicy | NoRespawn
 ]
 
 
@@ -174,8 +175,8 @@ def test_headline_batch_shards_match_oracle():
             for w0, o in zip(probes, oracles):
                 for n in T.STEP_OUTPUTS:
                     ptr, dt, shape = e.desc(n)
-                    per_world = shape[0] == W
-                    r0, r1 = (w0, w0 + 3) if per_world else (w0 * N, (w0 + 3) * N)
+                    rows_per_world = shape[0] // W  # 1 (world), 2 (team interface) or N (agent)
+                    r0, r1 = w0 * rows_per_world, (w0 + 3) * rows_per_world
                     T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
     # size-independent properties over the whole batch
     hp = e.get("HP")
@@ -388,7 +389,8 @@ def test_world_groups_on_streams_match_oracle(monkeypatch):
             for w0, o in zip(probes, oracles):
                 for n in T.STEP_OUTPUTS:
                     _, _, shape = e.desc(n)
-                    r0, r1 = (w0, w0 + 2) if shape[0] == W else (w0 * N, (w0 + 2) * N)
+                    k = shape[0] // W
+                    r0, r1 = w0 * k, (w0 + 2) * k
                     T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
 
 
