@@ -1985,8 +1985,6 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
     const uint8_t *vm = S.visMask;
     const bool self_alive = S.alive[g] != 0.f;
 
-    fullTeamSlotD(S, sc, w, g, team, off);
-
     // ---- masks
     float mask[kMaxTeamSize];
     for (int k = 0; k < kMaxTeamSize; k++) {
@@ -2095,6 +2093,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
         storeVec(&S.oppPos[(g * 6 + k) * 3], opos, 3);
     }
 
+    fullTeamSlotD(S, sc, w, g, team, off);
 }
 
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray; a workgroup walks
