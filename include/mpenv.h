@@ -148,7 +148,8 @@ enum mpenv_dbg_agent_f32 {
     MPENV_DBG_AF_FIRED_T = 18,
     MPENV_DBG_AF_BC_PENALTY = 19,
     MPENV_DBG_AF_START = 20,  /* 3 */
-    MPENV_DBG_AF_COUNT = 23
+    MPENV_DBG_AF_MINDIST_SUBZONE = 23,
+    MPENV_DBG_AF_COUNT = 24
 };
 enum mpenv_dbg_agent_i32 {
     MPENV_DBG_AI_CUR_POSE = 0,
@@ -160,7 +161,7 @@ enum mpenv_dbg_agent_i32 {
     MPENV_DBG_AI_LANDED_ON = 6,     /* agent index in world, or -1 */
     MPENV_DBG_AI_RESPAWN_STEPS = 7,
     MPENV_DBG_AI_AUTOHEAL_STEPS = 8,
-    MPENV_DBG_AI_FLAGS = 9,         /* bit0 successfulKill, 1 wasKilled, 2 inZone, 3 hasDied, 4 reloadedFullMag */
+    MPENV_DBG_AI_FLAGS = 9,         /* bit0 successfulKill, 1 wasKilled, 2 inZone, 3 hasDied, 4 reloadedFullMag, 5 inSubZone */
     MPENV_DBG_AI_WAS_SHOT = 10,
     MPENV_DBG_AI_WEAPON = 11,
     MPENV_DBG_AI_BC_LAST = 12,
@@ -191,7 +192,8 @@ enum mpenv_dbg_world_i32 {
     MPENV_DBG_WI_FILTER_LAST0 = 18,
     MPENV_DBG_WI_FILTER_LAST1 = 19,
     MPENV_DBG_WI_CRUMB_OVERFLOW = 20,
-    MPENV_DBG_WI_COUNT = 21
+    MPENV_DBG_WI_SUBZONES = 21,     /* 4 bits per sub-zone k at 4k: controlling team + 1, contested << 2, captured << 3 */
+    MPENV_DBG_WI_COUNT = 22
 };
 enum mpenv_dbg_world_f32 {
     MPENV_DBG_WF_TEAM_REWARD0 = 0,

@@ -36,7 +36,7 @@ constexpr int kMaxBVHStack = 16; // register byte-stack capacity
 #define MP_AGENT_F32(X) \
     X(px) X(py) X(pz) X(vx) X(vy) X(vz) X(rw) X(rx) X(ry) X(rz) \
     X(ayaw) X(apitch) X(aw) X(ax) X(ay) X(az) X(maxVel) X(minDistZone) \
-    X(firedT) X(bcPenalty) X(sx) X(sy) X(sz) X(dyv) X(dpv)
+    X(firedT) X(bcPenalty) X(sx) X(sy) X(sz) X(dyv) X(dpv) X(minDistSub)
 
 #define MP_AGENT_I32(X) \
     X(curPose) X(tgtPose) X(transRem) X(rngA) X(rngB) X(rngCtr) X(landedOn) \
@@ -49,7 +49,7 @@ constexpr int kMaxBVHStack = 16; // register byte-stack capacity
     X(episodeCounter) X(wRngA) X(wRngB) X(wRngCtr) X(filtAct0) X(filtAct1) \
     X(filtMatched0) X(filtMatched1) X(episodeCurr) X(numCrumbs) X(nextCrumbId) \
     X(crumbOverflow) X(curTier) X(curSpawnIdx) X(spawnCurriculum) \
-    X(matchValid) X(evLogged) X(evMask) X(snapWritten)
+    X(matchValid) X(evLogged) X(evMask) X(snapWritten) X(subState)
 
 #define MP_WORLD_F32(X) \
     X(teamRew0) X(teamRew1) X(goalMin0) X(goalMin1) X(goalTeam0) X(goalTeam1)
@@ -61,6 +61,7 @@ enum : int32_t {
     kFlagInZone = 4,
     kFlagHasDied = 8,
     kFlagReloadedFullMag = 16,
+    kFlagInSubZone = 32,
 };
 
 struct DevState {
@@ -164,6 +165,7 @@ struct SceneDev {
     mp::AABB zoneAABB[kMaxZones];
     float zoneRot[kMaxZones];
     int32_t numZones;
+    ZOBBDev subZones[8];    // SubZones only (level_gen.cpp:282-326)
     GoalRegionDev goals[4];
     int32_t numGoals;
     uint32_t simFlags;

@@ -70,6 +70,7 @@ constexpr uint32_t kFlagRandomizeHP = 1u << 1;
 constexpr uint32_t kFlagHardcodedSpawns = 1u << 6;
 constexpr uint32_t kFlagEnableCurriculum = 1u << 5;
 constexpr uint32_t kFlagNavmeshSpawn = 1u << 2;
+constexpr uint32_t kFlagSubZones = 1u << 11;
 constexpr int32_t kFlagCrumbRequest = 64; // transient (leave -> append)
 
 __device__ __forceinline__ float viewHeightD(int pose)
@@ -748,6 +749,13 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
     rtrack[best_idx] = cur_step;
 }
 
+// AgentPolicy idx clamped to the 8 sub-zones (sim.cpp:1996-1997)
+__device__ __forceinline__ int subZoneIndexD(const DevState &S, int64_t g)
+{
+    const int p = S.policy[g];
+    return p < 0 ? 0 : (p > 7 ? 7 : p);
+}
+
 // utils.cpp:734-948 spawnAgents
 __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool is_respawn)
 {
@@ -822,6 +830,20 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
             setFlag(S, g, kFlagInZone, aabbContains(za, pz));
             S.minDistZone[g] = distance(spawn_pt, zone_center);
         }
+        if (sc.simFlags & kFlagSubZones) {
+            // utils.cpp:906-926: spawn_pt already carries the +standHeight/2
+            // of the zone block and receives it a second time
+            const ZOBBDev &sz = sc.subZones[subZoneIndexD(S, g)];
+            AABB za = { sz.pMin, sz.pMax };
+            Vec3 zone_center = (za.pMax + za.pMin) / 2.f;
+            Quat to_zone = qinv(angleAxis(sz.rotation, kUp));
+            za.pMin = rotateVec(to_zone, za.pMin);
+            za.pMax = rotateVec(to_zone, za.pMax);
+            Vec3 pz = rotateVec(to_zone, spawn_pt);
+            spawn_pt.z += c::kStandHeight / 2.f;
+            setFlag(S, g, kFlagInSubZone, aabbContains(za, pz));
+            S.minDistSub[g] = distance(spawn_pt, zone_center);
+        }
         S.curPose[g] = kStand; S.tgtPose[g] = kStand; S.transRem[g] = 0;
         S.maxVel[g] = c::kMaxWalkVelocity;
         S.dyv[g] = 0.f; S.dpv[g] = 0.f;
@@ -845,7 +867,7 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
         S.autohealSteps[g] = 0;
         S.wasShot[g] = 0;
         S.firedT[g] = -kFltMax;
-        S.flags[g] = S.flags[g] & kFlagInZone; // successfulKill/wasKilled/hasDied/reloadedFullMag = false
+        S.flags[g] = S.flags[g] & (kFlagInZone | kFlagInSubZone); // successfulKill/wasKilled/hasDied/reloadedFullMag = false
         S.alive[g] = 0.f;
         float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
         for (int k = 0; k < 6 * kOtherObs / 4; k++) lk[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -913,6 +935,7 @@ __device__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool tr
     S.earned[w] = 0;
     S.zoneSteps[w] = c::kNumStepsPerZone;
     S.stepsUntilPoint[w] = c::kZonePointInterval;
+    S.subState[w] = 0; // every sub-zone: controlling -1, not contested / captured (sim.cpp:815-820)
     stWRng(S, w, base);
     resetPersistentEntitiesD(S, sc, w, episode_key);
     S.filtAct0[w] = 0; S.filtAct1[w] = 0;
@@ -997,6 +1020,52 @@ __device__ void zoneSystemD(const DevState &S, const SceneDev &sc, int w)
     S.stepsUntilPoint[w] = sup;
     S.captured[w] = captured ? 1 : 0;
     S.contested[w] = contested ? 1 : 0;
+}
+
+// SubZone state packed 4 bits per sub-zone k at bit 4k: controlling team + 1,
+// contested << 2, captured << 3 (the DEBUG_WORLD_I32 layout).
+__device__ __forceinline__ int subCtrlD(uint32_t st, int k) { return (int)((st >> (4 * k)) & 3u) - 1; }
+
+// sim.cpp:1978-2041 subzoneSystem over sub-zones 0..7
+__device__ void subzoneSystemD(const DevState &S, const SceneDev &sc, int w)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    uint32_t st = (uint32_t)S.subState[w];
+    for (int k = 0; k < 8; k++) {
+        const ZOBBDev &sz = sc.subZones[k];
+        AABB za = { sz.pMin, sz.pMax };
+        Quat to_zone = qinv(angleAxis(sz.rotation, kUp));
+        za.pMin = rotateVec(to_zone, za.pMin);
+        za.pMax = rotateVec(to_zone, za.pMax);
+        int na = 0, nb = 0;
+        for (int i = 0; i < N; i++) {
+            const int64_t g = g0 + i;
+            if (subZoneIndexD(S, g) != k) continue;
+            Vec3 p = ldPos(S, g);
+            p.z += c::kStandHeight / 2.f;
+            const bool in = aabbContains(za, rotateVec(to_zone, p));
+            setFlag(S, g, kFlagInSubZone, in);
+            if (!in) continue;
+            S.minDistSub[g] = 0.f;
+            if (i / S.T == 0) na += 1;
+            else nb += 1;
+        }
+        int ctrl = subCtrlD(st, k);
+        bool captured = (st >> (4 * k + 3)) & 1u;
+        const bool contested = na > 0 && nb > 0;
+        if (contested || (na == 0 && nb == 0)) {
+            ctrl = -1;
+            captured = false;
+        } else if (na > 0 && nb == 0) {
+            if (ctrl != 0) { ctrl = 0; captured = false; }
+        } else if (na == 0 && nb > 0) {
+            if (ctrl != 1) { ctrl = 1; captured = false; }
+        }
+        const uint32_t nib = (uint32_t)(ctrl + 1) | (contested ? 4u : 0u) | (captured ? 8u : 0u);
+        st = (st & ~(0xFu << (4 * k))) | (nib << (4 * k));
+    }
+    S.subState[w] = (int32_t)st;
 }
 
 __device__ __forceinline__ float4 *crumbPtr(const DevState &S, int w) { return &S.crumbs[(int64_t)w * kMaxCrumbs * 2]; }
@@ -1398,6 +1467,56 @@ __device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
     }
 }
 
+// sim.cpp:3734-3847 subzoneRewardSystem (after the LearnShooting branch,
+// which zoneRewardD handles for both): kills pay 3, the agent's own
+// sub-zone drives the in-zone / approach / control terms, no earned-point
+// or area terms.
+__device__ void subzoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
+{
+    const int64_t g = (int64_t)w * S.N + i;
+    int32_t flags = S.flags[g];
+    const int landed = S.landedOn[g];
+    const float *rc = &S.rewardCoefs[9 * g];
+    const float shot = rc[1], explore = rc[2], in_zone = rc[3], ctrl_s = rc[5], zdist = rc[6], crumb = rc[8];
+    float r = 0.f;
+    r -= crumb * S.bcPenalty[g];
+    if (flags & kFlagReloadedFullMag) r -= 0.5f;
+    if (flags & kFlagSuccessfulKill) r += 3.f;
+    if (landed != -1) r += shot * 1.f;
+    if (flags & kFlagWasKilled) r -= 1.5f;
+    if (S.wasShot[g] > 0) r -= shot * 1.f;
+    uint32_t nn = (uint32_t)S.newCells[g];
+    S.newCells[g] = 0;
+    if (nn > 0) r += float(nn) * explore;
+    const int k = subZoneIndexD(S, g);
+    if (flags & kFlagInSubZone) {
+        r += in_zone;
+    } else {
+        const ZOBBDev &sz = sc.subZones[k];
+        Vec3 center = (sz.pMax + sz.pMin) / 2.f;
+        float dist = distance(center, ldPos(S, g));
+        float md = S.minDistSub[g];
+        if (dist < md) {
+            float scale = zdist;
+            if (!(flags & kFlagHasDied)) scale *= 10.f;
+            r += scale * (md - dist);
+            S.minDistSub[g] = dist;
+        }
+    }
+    const int ctrl = subCtrlD((uint32_t)S.subState[w], k);
+    if (ctrl != -1) {
+        if (ctrl == i / S.T) r += ctrl_s;
+        else r -= ctrl_s;
+    }
+    if (S.alive[g] == 0.f) {
+        S.flags[g] = flags & ~(kFlagSuccessfulKill | kFlagWasKilled);
+        S.landedOn[g] = -1;
+        S.wasShot[g] = 0;
+        S.firedT[g] = -kFltMax;
+    }
+    S.reward[g] = r;
+}
+
 // sim.cpp:3849-3996 zoneRewardSystem (+ learnShootingRewardSystem 3707-3732)
 __device__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
 {
@@ -1411,6 +1530,10 @@ __device__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
         else if (S.firedT[g] >= 0.f) r -= 0.05f;
         if (flags & kFlagReloadedFullMag) r -= 0.5f;
         S.reward[g] = r;
+        return;
+    }
+    if (sc.simFlags & kFlagSubZones) {
+        subzoneRewardD(S, sc, w, i);
         return;
     }
     const float *rc = &S.rewardCoefs[9 * g];
@@ -1604,7 +1727,10 @@ __global__ void __launch_bounds__(kSimBlock) k_sim(DevState S, SceneDev sc)
         __syncthreads();
         if (act) autoHealD(S, g);
         __syncthreads();
-        if (wlane) zoneSystemD(S, sc, w);
+        if (wlane) {
+            zoneSystemD(S, sc, w);
+            if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
+        }
         __syncthreads();
         if (sc.recordOn) {
             if (act) recordAgentD(S, w, i);
@@ -2205,7 +2331,7 @@ __global__ void __launch_bounds__(256) k_debug(DevState S, float *af, int32_t *a
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < S.A) {
         const int64_t g = t;
-        float *f = &af[g * 23];
+        float *f = &af[g * MPENV_DBG_AF_COUNT];
         f[0] = S.px[g]; f[1] = S.py[g]; f[2] = S.pz[g];
         f[3] = S.vx[g]; f[4] = S.vy[g]; f[5] = S.vz[g];
         f[6] = S.rw[g]; f[7] = S.rx[g]; f[8] = S.ry[g]; f[9] = S.rz[g];
@@ -2213,11 +2339,12 @@ __global__ void __launch_bounds__(256) k_debug(DevState S, float *af, int32_t *a
         f[12] = S.aw[g]; f[13] = S.ax[g]; f[14] = S.ay[g]; f[15] = S.az[g];
         f[16] = S.maxVel[g]; f[17] = S.minDistZone[g]; f[18] = S.firedT[g]; f[19] = S.bcPenalty[g];
         f[20] = S.sx[g]; f[21] = S.sy[g]; f[22] = S.sz[g];
-        int32_t *n = &ai[g * 16];
+        f[23] = S.minDistSub[g];
+        int32_t *n = &ai[g * MPENV_DBG_AI_COUNT];
         n[0] = S.curPose[g]; n[1] = S.tgtPose[g]; n[2] = S.transRem[g];
         n[3] = S.rngA[g]; n[4] = S.rngB[g]; n[5] = S.rngCtr[g];
         n[6] = S.landedOn[g]; n[7] = S.respawnSteps[g]; n[8] = S.autohealSteps[g];
-        n[9] = S.flags[g] & 31;
+        n[9] = S.flags[g] & 63;
         n[10] = S.wasShot[g]; n[11] = S.weapon[g]; n[12] = S.bcLast[g]; n[13] = S.bcSteps[g];
         n[14] = S.visMask[g];
         n[15] = S.newCells[g];
@@ -2227,14 +2354,15 @@ __global__ void __launch_bounds__(256) k_debug(DevState S, float *af, int32_t *a
     }
     if (t < S.W) {
         const int w = (int)t;
-        int32_t *n = &wi[(int64_t)w * 21];
+        int32_t *n = &wi[(int64_t)w * MPENV_DBG_WI_COUNT];
         n[0] = S.teamA[w]; n[1] = S.curStep[w]; n[2] = S.finished[w]; n[3] = S.curZone[w];
         n[4] = S.controlling[w]; n[5] = S.contested[w]; n[6] = S.captured[w]; n[7] = S.earned[w];
         n[8] = S.zoneSteps[w]; n[9] = S.stepsUntilPoint[w]; n[10] = S.episode[w]; n[11] = S.episodeCounter[w];
         n[12] = S.wRngA[w]; n[13] = S.wRngB[w]; n[14] = S.wRngCtr[w]; n[15] = S.numCrumbs[w];
         n[16] = S.filtAct0[w]; n[17] = S.filtAct1[w]; n[18] = S.filtMatched0[w]; n[19] = S.filtMatched1[w];
         n[20] = S.crumbOverflow[w];
-        float *f = &wf[(int64_t)w * 6];
+        n[21] = S.subState[w];
+        float *f = &wf[(int64_t)w * MPENV_DBG_WF_COUNT];
         f[0] = S.teamRew0[w]; f[1] = S.teamRew1[w]; f[2] = S.goalMin0[w]; f[3] = S.goalMin1[w];
         f[4] = S.goalTeam0[w]; f[5] = S.goalTeam1[w];
         float *cdst = &crumbs[(int64_t)w * kMaxCrumbs * 8];

@@ -444,6 +444,11 @@ static void buildSceneDev(mpenv_manager &m)
     sc.spawnTrackLen = (int32_t)std::max<size_t>(
         kMinSpawnTrack, std::max(s.aSpawns.size(), std::max(s.bSpawns.size(), s.commonRespawns.size())));
     sc.numZones = (int32_t)s.zoneAABBs.size();
+    if (m.cfg.sim_flags & MPENV_SIMFLAG_SUB_ZONES) {
+        // sub-zones 0 and 1 are zones 1 and 2 (level_gen.cpp:283-293)
+        if (s.zoneAABBs.size() < 3) throw std::runtime_error("SubZones needs a scene with >= 3 zones");
+        mp::subZoneTable(s.zoneAABBs.data(), s.zoneRotations.data(), sc.subZones);
+    }
     for (int z = 0; z < sc.numZones; z++) {
         sc.zoneAABB[z] = s.zoneAABBs[z];
         sc.zoneRot[z] = s.zoneRotations[z];
@@ -691,17 +696,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         return fail(MPENV_ERR_INVALID, "team_size must be in [1, 6]");
     if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");
     if (!cfg->scene_path) return fail(MPENV_ERR_INVALID, "scene_path is required");
-    const uint32_t unsupported = MPENV_SIMFLAG_SUB_ZONES;
-    if (cfg->sim_flags & unsupported) {
-        static const char *names[] = { "SpawnInMiddle", "RandomizeHPMagazine", "NavmeshSpawn", "NoRespawn",
-                                       "StaggerStarts", "EnableCurriculum", "HardcodedSpawns",
-                                       "RandomFlipTeams", "StaticFlipTeams", "FullTeamPolicy",
-                                       "SimEvalMode", "SubZones" };
-        std::string msg = "sim_flags not implemented by this build:";
-        for (int b = 0; b < 12; b++)
-            if (cfg->sim_flags & unsupported & (1u << b)) msg += std::string(" ") + names[b];
-        return fail(MPENV_ERR_UNSUPPORTED, msg);
-    }
+    if (cfg->sim_flags >> 12) return fail(MPENV_ERR_INVALID, "sim_flags has bits beyond SubZones (1 << 11)");
     // hardcodedSpawnPoint indexes a 6-entry table with (team A ? 0 : 3) +
     // offset (utils.cpp:545-549): larger teams read past it in the reference.
     if ((cfg->sim_flags & MPENV_SIMFLAG_HARDCODED_SPAWNS) && cfg->team_size > 3)

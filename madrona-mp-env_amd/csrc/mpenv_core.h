@@ -489,6 +489,22 @@ MP_HD void hardcodedSpawn(int idx, Vec3 &pos, float &yaw)
     }
 }
 
+// level_gen.cpp:282-326: sub-zones 0 and 1 are zones 1 and 2, the rest
+// fixed boxes (sub-zone 7's x range is inverted, so it never contains a
+// point).
+template <typename Z>
+inline void subZoneTable(const AABB *zones, const float *rots, Z *out)
+{
+    out[0] = { zones[1].pMin, zones[1].pMax, rots[1] };
+    out[1] = { zones[2].pMin, zones[2].pMax, rots[2] };
+    out[2] = { v3(-950.f, -500.f, 0.f), v3(-50.f, 500.f, 1000.f), 0.f };
+    out[3] = { v3(50.f, -500.f, 0.f), v3(950.f, 500.f, 1000.f), 0.f };
+    out[4] = { v3(-1000.f, -1650.f, 0.f), v3(-50.f, -600.f, 1000.f), 0.f };
+    out[5] = { v3(50.f, -1650.f, 0.f), v3(1000.f, -600.f, 1000.f), 0.f };
+    out[6] = { v3(-1000.f, 600.f, 0.f), v3(-50.f, 1650.f, 1000.f), 0.f };
+    out[7] = { v3(1000.f, 600.f, 0.f), v3(50.f, 1650.f, 1000.f), 0.f };
+}
+
 // Navmesh::samplePoint(RandKey) (called at utils.cpp:808) lives in Madrona,
 // which is not vendored: parity to the reference's bitstream is unpinned and
 // the sampler is DEFINED here as area-uniform sampling over the deduplicated

@@ -162,6 +162,9 @@ struct Agent {
     uint32_t numNewCellsVisited;
     float daimYawVel, daimPitchVel;
     bool canSee[kMaxTeamSize];
+    // CombatState sub-zone fields (types.hpp:521-522), SubZones only
+    bool inSubZone = false;
+    float minDistToSubZone = 0.f;
 };
 
 struct Crumb {
@@ -201,6 +204,9 @@ struct World {
     std::vector<Crumb> crumbs;
     uint32_t nextCrumbId;
     int crumbOverflow;
+    // SubZone entities (types.hpp:791-796), SubZones only
+    int subCtrl[8];
+    bool subContested[8], subCaptured[8];
 };
 
 struct Oracle {
@@ -218,6 +224,7 @@ struct Oracle {
     std::vector<Node> nodes;
     std::vector<Vec3> navTris;   // 3 per triangle
     std::vector<float> navCdf;   // running triangle areas (navSamplePoint)
+    struct ZOBB { Vec3 pMin, pMax; float rotation; } subZones[8]; // level_gen.cpp:282-326
     std::vector<int32_t> astar;  // [T][T]
     int numNavTris = 0;
     std::vector<Vec3> verts;
@@ -753,6 +760,12 @@ void standardSpawnPoint(Oracle &o, int w, int ai, bool is_respawn, bool use_midd
     o.track(w, 2)[best_idx] = (uint32_t)wd.curStep;
 }
 
+// AgentPolicy idx clamped to the 8 sub-zones (sim.cpp:1996-1997, 3802-3803)
+int subZoneIndex(const Oracle &o, size_t g)
+{
+    return std::clamp(o.policy[g], 0, 7);
+}
+
 // utils.cpp:734-948 spawnAgents (Zone task)
 void spawnAgents(Oracle &o, int w, bool is_respawn)
 {
@@ -831,6 +844,20 @@ void spawnAgents(Oracle &o, int w, bool is_respawn)
             spawn_pt.z += kStandHeight / 2.f;
             ag.inZone = aabbContains(zone_aabb, pos_in_zone);
             ag.minDistToZone = distance(spawn_pt, zone_center);
+        }
+        if (o.simFlags & MPENV_SIMFLAG_SUB_ZONES) {
+            // utils.cpp:906-926 (spawn_pt already carries the +standHeight/2
+            // of the zone block above and receives it a second time)
+            const Oracle::ZOBB &sz = o.subZones[subZoneIndex(o, g)];
+            AABB zone_aabb = { sz.pMin, sz.pMax };
+            Vec3 zone_center = (zone_aabb.pMax + zone_aabb.pMin) / 2.f;
+            Quat to_zone = qinv(angleAxis(sz.rotation, kUp));
+            zone_aabb.pMin = rotateVec(to_zone, zone_aabb.pMin);
+            zone_aabb.pMax = rotateVec(to_zone, zone_aabb.pMax);
+            Vec3 pos_in_zone = rotateVec(to_zone, spawn_pt);
+            spawn_pt.z += kStandHeight / 2.f;
+            ag.inSubZone = aabbContains(zone_aabb, pos_in_zone);
+            ag.minDistToSubZone = distance(spawn_pt, zone_center);
         }
 
         ag.curPose = kStand; ag.tgtPose = kStand; ag.transitionRemaining = 0;
@@ -975,6 +1002,11 @@ void initWorld(Oracle &o, int w, bool triggered_reset)
     wd.earnedPoint = false;
     wd.zoneStepsRemaining = kNumStepsPerZone;
     wd.stepsUntilPoint = kZonePointInterval;
+    for (int k = 0; k < 8; k++) { // sim.cpp:815-820
+        wd.subCtrl[k] = -1;
+        wd.subContested[k] = false;
+        wd.subCaptured[k] = false;
+    }
 
     resetPersistentEntities(o, w, episode_key);
 
@@ -1534,6 +1566,50 @@ void zoneSystem(Oracle &o, int w)
     }
 }
 
+// sim.cpp:1978-2041 subzoneSystem, for sub-zones 0..7 in entity order
+void subzoneSystem(Oracle &o, int w)
+{
+    World &wd = o.worlds[w];
+    for (int k = 0; k < 8; k++) {
+        const Oracle::ZOBB &sz = o.subZones[k];
+        AABB za = { sz.pMin, sz.pMax };
+        Quat to_zone = qinv(angleAxis(sz.rotation, kUp));
+        za.pMin = rotateVec(to_zone, za.pMin);
+        za.pMax = rotateVec(to_zone, za.pMax);
+        int na = 0, nb = 0;
+        for (int i = 0; i < o.N; i++) {
+            if (subZoneIndex(o, o.gi(w, i)) != k) continue;
+            Agent &ag = o.agent(w, i);
+            Vec3 p = ag.pos;
+            p.z += kStandHeight / 2.f;
+            Vec3 pz = rotateVec(to_zone, p);
+            if (!aabbContains(za, pz)) {
+                ag.inSubZone = false;
+                continue;
+            }
+            ag.inSubZone = true;
+            ag.minDistToSubZone = 0.f;
+            if (ag.team == 0) na += 1;
+            if (ag.team == 1) nb += 1;
+        }
+        wd.subContested[k] = na > 0 && nb > 0;
+        if (wd.subContested[k] || (na == 0 && nb == 0)) {
+            wd.subCtrl[k] = -1;
+            wd.subCaptured[k] = false;
+        } else if (na > 0 && nb == 0) {
+            if (wd.subCtrl[k] != 0) {
+                wd.subCtrl[k] = 0;
+                wd.subCaptured[k] = false;
+            }
+        } else if (na == 0 && nb > 0) {
+            if (wd.subCtrl[k] != 1) {
+                wd.subCtrl[k] = 1;
+                wd.subCaptured[k] = false;
+            }
+        }
+    }
+}
+
 // sim.cpp:4845-4889 leaveBreadcrumbsSystem
 void leaveBreadcrumbsSystem(Oracle &o, int w, int i)
 {
@@ -1894,6 +1970,59 @@ void learnShootingReward(Agent &ag, float &r)
     if (ag.landedShotOn != -1) r += 0.5f;
     else if (ag.firedShotT >= 0.f) r -= 0.05f;
     if (ag.reloadedFullMag) r -= 0.5f;
+}
+
+// sim.cpp:3734-3847 subzoneRewardSystem (replaces zoneRewardSystem when
+// SubZones is set): kills pay 3, the agent's own sub-zone drives the
+// in-zone / approach / control terms, no earned-point or area terms.
+void subzoneRewardSystem(Oracle &o, int w, int i)
+{
+    World &wd = o.worlds[w];
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    float r = 0.f;
+    if (o.worldCurriculum[w] == 0) { // LearnShooting
+        learnShootingReward(ag, r);
+        o.reward[g] = r;
+        return;
+    }
+    const float *rc = &o.rewardCoefs[9 * g];
+    const float shot = rc[1], explore = rc[2], in_zone = rc[3], ctrl = rc[5], zdist = rc[6], crumb = rc[8];
+    r -= crumb * ag.totalPenalty;
+    if (ag.reloadedFullMag) r -= 0.5f;
+    if (ag.successfulKill) r += 3.f;
+    if (ag.landedShotOn != -1) r += shot * 1.f;
+    if (ag.wasKilled) r -= 1.5f;
+    if (ag.wasShotCount > 0) r -= shot * 1.f;
+    uint32_t nn = ag.numNewCellsVisited;
+    ag.numNewCellsVisited = 0;
+    if (nn > 0) r += float(nn) * explore;
+    const int k = subZoneIndex(o, g);
+    if (ag.inSubZone) {
+        r += in_zone;
+    } else {
+        const Oracle::ZOBB &sz = o.subZones[k];
+        Vec3 center = (sz.pMax + sz.pMin) / 2.f;
+        float dist = distance(center, ag.pos);
+        if (dist < ag.minDistToSubZone) {
+            float scale = zdist;
+            if (!ag.hasDiedDuringEpisode) scale *= 10.f;
+            r += scale * (ag.minDistToSubZone - dist);
+            ag.minDistToSubZone = dist;
+        }
+    }
+    if (wd.subCtrl[k] != -1) {
+        if (wd.subCtrl[k] == ag.team) r += ctrl;
+        else r -= ctrl;
+    }
+    if (o.alive[g] == 0.f) {
+        ag.successfulKill = false;
+        ag.landedShotOn = -1;
+        ag.wasKilled = false;
+        ag.wasShotCount = 0;
+        ag.firedShotT = -kFltMax;
+    }
+    o.reward[g] = r;
 }
 
 // sim.cpp:3849-3996 zoneRewardSystem
@@ -2408,6 +2537,7 @@ void stepWorld(Oracle &o, int w)
     if (!(o.simFlags & MPENV_SIMFLAG_NO_RESPAWN)) spawnAgents(o, w, true);
     for (int i = 0; i < N; i++) autoHealSystem(o, w, i);
     zoneSystem(o, w);
+    if (o.simFlags & MPENV_SIMFLAG_SUB_ZONES) subzoneSystem(o, w);
     if (o.recordOn) pvpRecordSystem(o, w);
     for (int i = 0; i < N; i++) leaveBreadcrumbsSystem(o, w, i);
     accumulateBreadcrumbPenalties(o, w);
@@ -2421,7 +2551,10 @@ void replayTail(Oracle &o, int w)
     zoneMatchInfoSystem(o, w);
     evaluateGoalRegionsSystem(o, w);
     for (int i = 0; i < N; i++) exploreVisitedSystem(o, w, i);
-    for (int i = 0; i < N; i++) zoneRewardSystem(o, w, i);
+    for (int i = 0; i < N; i++) {
+        if (o.simFlags & MPENV_SIMFLAG_SUB_ZONES) subzoneRewardSystem(o, w, i);
+        else zoneRewardSystem(o, w, i);
+    }
     teamAndFinalReward(o, w);
     for (int i = 0; i < N; i++) o.done[o.gi(w, i)] = o.worlds[w].isFinished ? 1 : 0;
     fullTeamDoneReward(o, w);
@@ -2559,12 +2692,13 @@ void refreshDebug(Oracle &o)
         f[12] = a.aimRot.w; f[13] = a.aimRot.x; f[14] = a.aimRot.y; f[15] = a.aimRot.z;
         f[16] = a.maxVelocity; f[17] = a.minDistToZone; f[18] = a.firedShotT; f[19] = a.totalPenalty;
         f[20] = a.startPos.x; f[21] = a.startPos.y; f[22] = a.startPos.z;
+        f[23] = a.minDistToSubZone;
         int32_t *n = &o.dbgAI[g * MPENV_DBG_AI_COUNT];
         n[0] = a.curPose; n[1] = a.tgtPose; n[2] = a.transitionRemaining;
         n[3] = (int32_t)a.rng.key.a; n[4] = (int32_t)a.rng.key.b; n[5] = (int32_t)a.rng.ctr;
         n[6] = a.landedShotOn; n[7] = a.remainingRespawnSteps; n[8] = a.remainingStepsBeforeAutoheal;
         n[9] = (a.successfulKill ? 1 : 0) | (a.wasKilled ? 2 : 0) | (a.inZone ? 4 : 0) |
-               (a.hasDiedDuringEpisode ? 8 : 0) | (a.reloadedFullMag ? 16 : 0);
+               (a.hasDiedDuringEpisode ? 8 : 0) | (a.reloadedFullMag ? 16 : 0) | (a.inSubZone ? 32 : 0);
         n[10] = a.wasShotCount; n[11] = a.weaponType; n[12] = (int32_t)a.lastBreadcrumb;
         n[13] = a.stepsSinceLastNewBreadcrumb;
         int cs = 0;
@@ -2583,6 +2717,10 @@ void refreshDebug(Oracle &o)
         n[16] = (int32_t)wd.filtersActive[0]; n[17] = (int32_t)wd.filtersActive[1];
         n[18] = wd.filtersLastMatchedStep[0]; n[19] = wd.filtersLastMatchedStep[1];
         n[20] = wd.crumbOverflow;
+        uint32_t sub = 0;
+        for (int k = 0; k < 8; k++)
+            sub |= (uint32_t)((wd.subCtrl[k] + 1) | (wd.subContested[k] ? 4 : 0) | (wd.subCaptured[k] ? 8 : 0)) << (4 * k);
+        n[21] = (int32_t)sub;
         float *f = &o.dbgWF[(size_t)w * MPENV_DBG_WF_COUNT];
         f[0] = wd.teamRewards[0]; f[1] = wd.teamRewards[1];
         f[2] = wd.minDistToRegions[0]; f[3] = wd.minDistToRegions[1];
@@ -2622,6 +2760,10 @@ void *oracle_create(const oracle_config *cfg)
         o->trainControl[1] = (cfg->sim_flags & MPENV_SIMFLAG_STAGGER_STARTS) ? 1 : 0;
         o->trainControl[2] = (cfg->sim_flags & MPENV_SIMFLAG_RANDOM_FLIP_TEAMS) ? 1 : 0;
         loadScene(*o);
+        if (o->simFlags & MPENV_SIMFLAG_SUB_ZONES) {
+            if (o->zoneAABBs.size() < 3) throw std::runtime_error("SubZones needs a scene with >= 3 zones");
+            subZoneTable(o->zoneAABBs.data(), o->zoneRot.data(), o->subZones);
+        }
         o->nodes.resize(cfg->num_nodes);
         std::memcpy(o->nodes.data(), cfg->bvh_nodes, sizeof(Node) * cfg->num_nodes);
         o->verts.resize(cfg->num_bvh_verts);

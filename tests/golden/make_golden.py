@@ -39,6 +39,9 @@ CASES = {
     # HardcodedSpawns | SpawnInMiddle | RandomizeHPMagazine, random team sides
     "3v3_hardcoded": dict(team_size=3, worlds=3, steps=200, sim_flags=1 | 2 | (1 << 6), ctrl=[0, 1, 1],
                           policy="combat"),
+    # SubZones | SpawnInMiddle with policies cycling over the sub-zones
+    "3v3_subzones": dict(team_size=3, worlds=4, steps=250, sim_flags=1 | (1 << 11), ctrl=[0, 1, 1],
+                         policy="combat", bots="cycle"),
     # NavmeshSpawn | EnableCurriculum (LearnShooting rewards)
     "2v2_navmesh_curriculum": dict(team_size=2, worlds=4, steps=200, sim_flags=(1 << 2) | (1 << 5),
                                    ctrl=[0, 1, 1], policy="combat"),
@@ -72,11 +75,15 @@ def rollout(sim, case, record=None):
 
 
 def set_bots(sim, case):
-    """AgentPolicy = -1 (consts::aStarPolicyID) for team 1 or everyone."""
+    """AgentPolicy = -1 (consts::aStarPolicyID) for team 1 ("team1") or
+    everyone ("all"); "cycle" assigns (agent % 10) - 1, i.e. -1 (bot) .. 8,
+    which SubZones clamps to sub-zones 0..7."""
     W, ts = case["worlds"], case["team_size"]
     pol = np.zeros((W, 2, ts), np.int32)
     if case["bots"] == "all":
         pol[:] = -1
+    elif case["bots"] == "cycle":
+        pol = (np.arange(W * 2 * ts, dtype=np.int32) % 10) - 1
     else:
         pol[:, 1, :] = -1
     if hasattr(sim, "view"):

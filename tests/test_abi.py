@@ -69,7 +69,7 @@ def _cfg(**kw):
     (dict(task_type=1), "Zone"),
     (dict(team_size=7), "team"),
     (dict(num_worlds=0), "world"),
-    (dict(sim_flags=1 << 11), "SubZones"),
+    (dict(sim_flags=1 << 12), "sim_flags"),
     (dict(scene_path=b"/nonexistent"), ""),
 ])
 def test_create_rejects_unsupported_configs(kw, needle):

@@ -60,6 +60,8 @@ LIVE = [
     (6, 16, 300, 2 | (1 << 2), [0, 1, 1], "combat"),    # NavmeshSpawn
     (2, 32, 300, 1 | (1 << 5), [0, 1, 1], "combat"),    # EnableCurriculum
     (4, 8, 200, 1 | 8 | (1 << 9), [0, 1, 1], "combat"),  # FullTeamPolicy | NoRespawn
+    (3, 16, 300, 1 | (1 << 11), [0, 1, 1], "bots_cycle"),     # SubZones, policies -1..8
+    (6, 8, 300, 1 | 2 | (1 << 11), [0, 1, 1], "bots_cycle"),
 ]
 
 
