@@ -697,10 +697,6 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
     if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");
     if (!cfg->scene_path) return fail(MPENV_ERR_INVALID, "scene_path is required");
     if (cfg->sim_flags >> 12) return fail(MPENV_ERR_INVALID, "sim_flags has bits beyond SubZones (1 << 11)");
-    // hardcodedSpawnPoint indexes a 6-entry table with (team A ? 0 : 3) +
-    // offset (utils.cpp:545-549): larger teams read past it in the reference.
-    if ((cfg->sim_flags & MPENV_SIMFLAG_HARDCODED_SPAWNS) && cfg->team_size > 3)
-        return fail(MPENV_ERR_UNSUPPORTED, "HardcodedSpawns has spawn points for team_size <= 3 only");
     if (cfg->curriculum_data_path || cfg->train_flank)
         return fail(MPENV_ERR_UNSUPPORTED, "trajectory curricula and flank rewards are not implemented");
     if (cfg->replay_log_path && cfg->record_log_path)

@@ -474,11 +474,15 @@ MP_HD void tapeActions(uint32_t seed, uint32_t step, uint32_t agent, int32_t *di
 
 // ----------------------------------------------------------- spawn helpers
 // hardcodedSpawnPoint table (utils.cpp:503-541; hardcodedSpawnIdx is always
-// 0, sim.cpp:795-798): entries 0-2 for team A's offsets, 3-5 for the other
-// team.  The literals are doubles narrowed to float, as in the reference's
-// brace initialisers.  Pitch is 0 for every entry.
+// 0, sim.cpp:795-798): index (team A ? 0 : 3) + offset.  The literals are
+// doubles narrowed to float, as in the reference's brace initialisers; pitch
+// is 0 for every entry.  With more than 3 agents per team the reference
+// reads past the 6-entry table for the other team's offsets 3..5 (undefined
+// behaviour; jax_train.py's ZoneCaptureDefend setup does this at team size
+// 6): defined here as index - 3, i.e. they reuse that team's entries.
 MP_HD void hardcodedSpawn(int idx, Vec3 &pos, float &yaw)
 {
+    if (idx >= 6) idx -= 3;
     switch (idx) {
     case 0: pos = v3((float)510.0, (float)179.1, -64.f); yaw = (float)-2.05; break;
     case 1: pos = v3((float)525.8, (float)17.1, -64.f); yaw = (float)-0.80; break;

@@ -57,6 +57,7 @@ LIVE = [
     (3, 16, 300, 1, [0, 1, 1], "bots_team1"),           # A* bots vs tape
     (6, 8, 300, 0, [0, 1, 1], "bots_all"),              # everyone an A* bot
     (3, 16, 300, 1 | (1 << 6), [0, 1, 1], "combat"),    # HardcodedSpawns
+    (6, 8, 200, 1 | (1 << 6), [0, 1, 1], "combat"),     # HardcodedSpawns past the table
     (6, 16, 300, 2 | (1 << 2), [0, 1, 1], "combat"),    # NavmeshSpawn
     (2, 32, 300, 1 | (1 << 5), [0, 1, 1], "combat"),    # EnableCurriculum
     (4, 8, 200, 1 | 8 | (1 << 9), [0, 1, 1], "combat"),  # FullTeamPolicy | NoRespawn

@@ -135,10 +135,19 @@ def test_curriculum_tends_to_full_match_over_episodes():
     o.close()
 
 
-def test_manager_rejects_hardcoded_spawns_for_large_teams():
-    import ctypes as C
-    lib = T.lib_mpenv()
-    c = T.MpenvConfig(1, 0, 4, 5, 1, HARDCODED, 2, 4, 0, 0, T.SCENE.encode(), 0, None, None, None, None, 0)
-    h = C.c_void_p()
-    assert lib.mpenv_create(C.byref(c), C.byref(h)) != 0
-    assert "HardcodedSpawns" in lib.mpenv_last_error().decode()
+@pytest.mark.parametrize("ts", [4, 6])
+def test_hardcoded_spawns_large_teams(ts):
+    """team_size > 3: in-table indices as the reference; the other team's
+    offsets 3..5 (past the table in the reference) reuse its entries."""
+    W = 4
+    o = T.Oracle(W, ts, sim_flags=HARDCODED)
+    o.put_ctrl([0, 0, 1])
+    o.init()
+    p = positions(o).reshape(W, 2 * ts, 3)
+    team_a = o.get("DEBUG_WORLD_I32").reshape(W, -1)[:, 0]
+    for w in range(W):
+        for i in range(2 * ts):
+            team, off = divmod(i, ts)
+            idx = (0 if team == team_a[w] else 3) + off
+            np.testing.assert_array_equal(p[w, i], TABLE[idx if idx < 6 else idx - 3])
+    o.close()
