@@ -165,6 +165,7 @@ struct SceneDev {
     mp::AABB zoneAABB[kMaxZones];
     float zoneRot[kMaxZones];
     int32_t numZones;
+    int32_t task;           // MPENV_TASK_ZONE or MPENV_TASK_ZONE_CAPTURE_DEFEND
     ZOBBDev subZones[8];    // SubZones only (level_gen.cpp:282-326)
     GoalRegionDev goals[4];
     int32_t numGoals;

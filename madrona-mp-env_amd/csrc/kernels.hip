@@ -936,6 +936,7 @@ __device__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool tr
     S.zoneSteps[w] = c::kNumStepsPerZone;
     S.stepsUntilPoint[w] = c::kZonePointInterval;
     S.subState[w] = 0; // every sub-zone: controlling -1, not contested / captured (sim.cpp:815-820)
+    if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) S.curZone[w] = 3; // sim.cpp:822-825
     stWRng(S, w, base);
     resetPersistentEntitiesD(S, sc, w, episode_key);
     S.filtAct0[w] = 0; S.filtAct1[w] = 0;
@@ -1253,6 +1254,18 @@ __device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
     S.captured[w] = captured ? 1 : 0;
     S.earned[w] = earned ? 1 : 0;
     if (mr[3] >= c::kZoneWinPoints || mr[4] >= c::kZoneWinPoints) finished = true;
+    // sim.cpp:4534-4575: ZoneCaptureDefend ends on the attacker's first
+    // point, the defender's 8th, or when every attacker has died once
+    const bool zcd = sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND;
+    const int attacker = S.teamA[w] == 1 ? 1 : 0, defender = attacker ^ 1;
+    bool attackers_all_died = true;
+    if (zcd) {
+        if (mr[3 + attacker] == 1) finished = true;
+        if (mr[3 + defender] == 8) finished = true;
+        for (int i = attacker * S.T; i < (attacker + 1) * S.T; i++)
+            if (!(S.flags[g0 + i] & kFlagHasDied)) attackers_all_died = false;
+        if (attackers_all_died) finished = true;
+    }
     {
         int32_t *zs = &zs_all[S.curZone[w] * 5];
         zs[4] += 1;
@@ -1263,7 +1276,11 @@ __device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
         if (sc.eventsOn) writeSnapshotD(S, sc, w, new_captured);
     }
     if (finished) {
-        if (mr[3] > mr[4]) mr[0] = 0;
+        if (zcd) {
+            if (mr[3 + attacker] == 1) mr[0] = attacker;
+            else if (mr[3 + defender] == 8 || attackers_all_died) mr[0] = defender;
+            else mr[0] = 2;
+        } else if (mr[3] > mr[4]) mr[0] = 0;
         else if (mr[4] > mr[3]) mr[0] = 1;
         else mr[0] = 2;
         for (int k = 0; k < 25; k++) mr[5 + k] = zs_all[k];
@@ -1467,6 +1484,52 @@ __device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
     }
 }
 
+// sim.cpp:4089-4200 zoneCaptureDefendRewardSystem: goal-region progress,
+// kills and control of the zone by the agent's own team, +-20 / -5 at the
+// end of the match; no curriculum, breadcrumb or area terms.
+__device__ void zoneCaptureDefendRewardD(const DevState &S, const SceneDev &sc, int w, int i)
+{
+    const int64_t g = (int64_t)w * S.N + i;
+    const int team = i / S.T;
+    int32_t flags = S.flags[g];
+    const float *rc = &S.rewardCoefs[9 * g];
+    const float shot = rc[1], explore = rc[2], ctrl_s = rc[5], earned_s = rc[7];
+    float r = 0.f;
+    r += 0.02f * (team == 0 ? S.goalTeam0[w] : S.goalTeam1[w]);
+    if (flags & kFlagReloadedFullMag) r -= 0.01f;
+    if (flags & kFlagSuccessfulKill) r += 1.f;
+    if (S.landedOn[g] != -1) r += shot * 1.f;
+    if (flags & kFlagWasKilled) r -= 1.f;
+    if (S.wasShot[g] > 0) r -= shot * 1.f;
+    uint32_t nn = (uint32_t)S.newCells[g];
+    S.newCells[g] = 0;
+    if (nn > 0) r += float(nn) * explore;
+    if (!(flags & kFlagInZone)) {
+        AABB za = sc.zoneAABB[S.curZone[w]];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        float dist = distance(center, ldPos(S, g));
+        if (dist < S.minDistZone[g]) S.minDistZone[g] = dist;
+    }
+    const int ctrl = S.controlling[w];
+    if (ctrl != -1 && ctrl == team) {
+        r += ctrl_s;
+        if (S.earned[w]) r += earned_s;
+    }
+    if (S.finished[w]) {
+        const int win = S.matchResult[(int64_t)w * 30];
+        if (win == 2) r -= 5.f;
+        else if (win == team) r += 20.f;
+        else r -= 20.f;
+    }
+    if (S.alive[g] == 0.f) {
+        S.flags[g] = flags & ~(kFlagSuccessfulKill | kFlagWasKilled);
+        S.landedOn[g] = -1;
+        S.wasShot[g] = 0;
+        S.firedT[g] = -kFltMax;
+    }
+    S.reward[g] = r;
+}
+
 // sim.cpp:3734-3847 subzoneRewardSystem (after the LearnShooting branch,
 // which zoneRewardD handles for both): kills pay 3, the agent's own
 // sub-zone drives the in-zone / approach / control terms, no earned-point
@@ -1525,6 +1588,10 @@ __device__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
     int32_t flags = S.flags[g];
     const int landed = S.landedOn[g];
     float r = 0.f;
+    if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) {
+        zoneCaptureDefendRewardD(S, sc, w, i);
+        return;
+    }
     if (S.worldCurr[w] == 0) {
         if (landed != -1) r += 0.5f;
         else if (S.firedT[g] >= 0.f) r -= 0.05f;

@@ -444,6 +444,10 @@ static void buildSceneDev(mpenv_manager &m)
     sc.spawnTrackLen = (int32_t)std::max<size_t>(
         kMinSpawnTrack, std::max(s.aSpawns.size(), std::max(s.bSpawns.size(), s.commonRespawns.size())));
     sc.numZones = (int32_t)s.zoneAABBs.size();
+    sc.task = m.cfg.task_type;
+    // initWorld starts every ZoneCaptureDefend episode at zone 3 (sim.cpp:822-825)
+    if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND && s.zoneAABBs.size() < 4)
+        throw std::runtime_error("ZoneCaptureDefend needs a scene with >= 4 zones");
     if (m.cfg.sim_flags & MPENV_SIMFLAG_SUB_ZONES) {
         // sub-zones 0 and 1 are zones 1 and 2 (level_gen.cpp:283-293)
         if (s.zoneAABBs.size() < 3) throw std::runtime_error("SubZones needs a scene with >= 3 zones");
@@ -690,8 +694,8 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
     *out = nullptr;
     if (cfg->exec_mode != MPENV_EXEC_CUDA)
         return fail(MPENV_ERR_UNSUPPORTED, "ExecMode.CPU is not supported: this engine runs only on the GPU (HIP)");
-    if (cfg->task_type != MPENV_TASK_ZONE)
-        return fail(MPENV_ERR_UNSUPPORTED, "only Task.Zone is implemented");
+    if (cfg->task_type != MPENV_TASK_ZONE && cfg->task_type != MPENV_TASK_ZONE_CAPTURE_DEFEND)
+        return fail(MPENV_ERR_UNSUPPORTED, "only Task.Zone and Task.ZoneCaptureDefend are implemented");
     if (cfg->team_size < 1 || cfg->team_size > kMaxTeamSize)
         return fail(MPENV_ERR_INVALID, "team_size must be in [1, 6]");
     if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");

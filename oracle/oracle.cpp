@@ -216,6 +216,7 @@ struct Oracle {
     uint32_t worldOffset;
     bool autoReset;
     uint32_t simFlags;
+    int task = MPENV_TASK_ZONE; // Zone or ZoneCaptureDefend
     RandKey initRandKey;
 
     AABB worldBounds;
@@ -1007,6 +1008,7 @@ void initWorld(Oracle &o, int w, bool triggered_reset)
         wd.subContested[k] = false;
         wd.subCaptured[k] = false;
     }
+    if (o.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) wd.curZone = 3; // sim.cpp:822-825
 
     resetPersistentEntities(o, w, episode_key);
 
@@ -1874,6 +1876,20 @@ void zoneMatchInfoSystem(Oracle &o, int w)
         wd.earnedPoint = true;
     }
     if (mr[3] >= kZoneWinPoints || mr[4] >= kZoneWinPoints) finished = true;
+    // sim.cpp:4534-4575: ZoneCaptureDefend ends on the attacker's first
+    // point, the defender's 8th, or when every attacker has died once
+    const int attacker = wd.teamA == 1 ? 1 : 0, defender = attacker ^ 1;
+    bool all_died[2] = { true, true };
+    const bool zcd = o.task == MPENV_TASK_ZONE_CAPTURE_DEFEND;
+    if (zcd) {
+        if (mr[3 + attacker] == 1) finished = true;
+        if (mr[3 + defender] == 8) finished = true;
+        for (int i = 0; i < o.N; i++) {
+            const Agent &ag = o.agent(w, i);
+            if (!ag.hasDiedDuringEpisode) all_died[ag.team] = false;
+        }
+        if (all_died[attacker]) finished = true;
+    }
     {
         int *zs = wd.zoneStats[wd.curZone];
         zs[4] += 1; // numTotalActiveSteps
@@ -1884,7 +1900,11 @@ void zoneMatchInfoSystem(Oracle &o, int w)
         if (o.eventsOn) captureAndSnapshot(o, w, new_captured);
     }
     if (finished) {
-        if (mr[3] > mr[4]) mr[0] = 0;
+        if (zcd) {
+            if (mr[3 + attacker] == 1) mr[0] = attacker;
+            else if (mr[3 + defender] == 8 || all_died[attacker]) mr[0] = defender;
+            else mr[0] = 2;
+        } else if (mr[3] > mr[4]) mr[0] = 0;
         else if (mr[4] > mr[3]) mr[0] = 1;
         else mr[0] = 2;
         for (int z = 0; z < kMaxZones; z++)
@@ -2014,6 +2034,52 @@ void subzoneRewardSystem(Oracle &o, int w, int i)
     if (wd.subCtrl[k] != -1) {
         if (wd.subCtrl[k] == ag.team) r += ctrl;
         else r -= ctrl;
+    }
+    if (o.alive[g] == 0.f) {
+        ag.successfulKill = false;
+        ag.landedShotOn = -1;
+        ag.wasKilled = false;
+        ag.wasShotCount = 0;
+        ag.firedShotT = -kFltMax;
+    }
+    o.reward[g] = r;
+}
+
+// sim.cpp:4089-4200 zoneCaptureDefendRewardSystem: goal-region progress,
+// kills and control of the zone by the agent's own team, +-20 / -5 at the
+// end of the match; no curriculum, breadcrumb or area terms.
+void zoneCaptureDefendRewardSystem(Oracle &o, int w, int i)
+{
+    World &wd = o.worlds[w];
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    const float *rc = &o.rewardCoefs[9 * g];
+    const float shot = rc[1], explore = rc[2], ctrl = rc[5], earned = rc[7];
+    float r = 0.f;
+    r += 0.02f * wd.teamStepRewards[ag.team];
+    if (ag.reloadedFullMag) r -= 0.01f;
+    if (ag.successfulKill) r += 1.f;
+    if (ag.landedShotOn != -1) r += shot * 1.f;
+    if (ag.wasKilled) r -= 1.f;
+    if (ag.wasShotCount > 0) r -= shot * 1.f;
+    uint32_t nn = ag.numNewCellsVisited;
+    ag.numNewCellsVisited = 0;
+    if (nn > 0) r += float(nn) * explore;
+    if (!ag.inZone) {
+        AABB za = o.zoneAABBs[wd.curZone];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+        float dist = distance(center, ag.pos);
+        if (dist < ag.minDistToZone) ag.minDistToZone = dist;
+    }
+    if (wd.curControllingTeam != -1 && wd.curControllingTeam == ag.team) {
+        r += ctrl;
+        if (wd.earnedPoint) r += earned;
+    }
+    if (wd.isFinished) {
+        const int win = o.matchResult[(size_t)w * 30];
+        if (win == 2) r -= 5.f;
+        else if (win == ag.team) r += 20.f;
+        else r -= 20.f;
     }
     if (o.alive[g] == 0.f) {
         ag.successfulKill = false;
@@ -2552,7 +2618,8 @@ void replayTail(Oracle &o, int w)
     evaluateGoalRegionsSystem(o, w);
     for (int i = 0; i < N; i++) exploreVisitedSystem(o, w, i);
     for (int i = 0; i < N; i++) {
-        if (o.simFlags & MPENV_SIMFLAG_SUB_ZONES) subzoneRewardSystem(o, w, i);
+        if (o.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) zoneCaptureDefendRewardSystem(o, w, i);
+        else if (o.simFlags & MPENV_SIMFLAG_SUB_ZONES) subzoneRewardSystem(o, w, i);
         else zoneRewardSystem(o, w, i);
     }
     teamAndFinalReward(o, w);
@@ -2752,6 +2819,9 @@ void *oracle_create(const oracle_config *cfg)
         o->worldOffset = cfg->world_id_offset;
         o->autoReset = cfg->auto_reset != 0;
         o->simFlags = cfg->sim_flags;
+        o->task = cfg->task_type;
+        if (o->task != MPENV_TASK_ZONE && o->task != MPENV_TASK_ZONE_CAPTURE_DEFEND)
+            throw std::runtime_error("oracle: task must be Zone or ZoneCaptureDefend");
         // mgr.cpp:1736-1738
         RandKey init_key = initKey(cfg->rand_seed);
         o->initRandKey = splitI(init_key, 0);
@@ -2760,6 +2830,8 @@ void *oracle_create(const oracle_config *cfg)
         o->trainControl[1] = (cfg->sim_flags & MPENV_SIMFLAG_STAGGER_STARTS) ? 1 : 0;
         o->trainControl[2] = (cfg->sim_flags & MPENV_SIMFLAG_RANDOM_FLIP_TEAMS) ? 1 : 0;
         loadScene(*o);
+        if (o->task == MPENV_TASK_ZONE_CAPTURE_DEFEND && o->zoneAABBs.size() < 4)
+            throw std::runtime_error("ZoneCaptureDefend needs a scene with >= 4 zones");
         if (o->simFlags & MPENV_SIMFLAG_SUB_ZONES) {
             if (o->zoneAABBs.size() < 3) throw std::runtime_error("SubZones needs a scene with >= 3 zones");
             subZoneTable(o->zoneAABBs.data(), o->zoneRot.data(), o->subZones);

@@ -35,6 +35,8 @@ typedef struct oracle_config {
     const float *nav_tris;
     int32_t num_nav_tris;
     const int32_t *astar;
+    /* Task (MPENV_TASK_*): Zone or ZoneCaptureDefend. */
+    int32_t task_type;
 } oracle_config;
 
 void *oracle_create(const oracle_config *cfg);

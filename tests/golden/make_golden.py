@@ -42,11 +42,30 @@ CASES = {
     # SubZones | SpawnInMiddle with policies cycling over the sub-zones
     "3v3_subzones": dict(team_size=3, worlds=4, steps=250, sim_flags=1 | (1 << 11), ctrl=[0, 1, 1],
                          policy="combat", bots="cycle"),
+    # ZoneCaptureDefend as scripts/jax_train.py configures it (HardcodedSpawns,
+    # StaggerStarts, RandomFlipTeams), 6v6 on a four-zone scene
+    "6v6_capture_defend": dict(team_size=6, worlds=3, steps=300, sim_flags=1 | (1 << 6) | (1 << 4),
+                               ctrl=[0, 1, 1], policy="combat", task=T.TASK_ZONE_CAPTURE_DEFEND,
+                               scene="four_zones"),
     # NavmeshSpawn | EnableCurriculum (LearnShooting rewards)
     "2v2_navmesh_curriculum": dict(team_size=2, worlds=4, steps=200, sim_flags=(1 << 2) | (1 << 5),
                                    ctrl=[0, 1, 1], policy="combat"),
 }
 TAPE_SEED = 1234
+_SCENES = {}
+
+
+def make_sim(cls, case):
+    """T.Oracle or T.Engine for a case (task and scene are optional keys;
+    scene "four_zones" is simple_map plus a fourth zone, generated on first
+    use)."""
+    kw = dict(sim_flags=case["sim_flags"], task=case.get("task", T.TASK_ZONE))
+    if case.get("scene") == "four_zones":
+        if "four_zones" not in _SCENES:
+            import tempfile
+            _SCENES["four_zones"] = T.four_zone_scene(tempfile.mkdtemp(prefix="mpenv_scene_"))
+        kw["scene"] = _SCENES["four_zones"]
+    return cls(case["worlds"], case["team_size"], **kw)
 FINAL_TENSORS = ["SELF_OBSERVATION", "REWARD", "HP", "FWD_LIDAR"]
 
 
@@ -93,7 +112,7 @@ def set_bots(sim, case):
 
 
 def make(name, case):
-    o = T.Oracle(case["worlds"], case["team_size"], sim_flags=case["sim_flags"])
+    o = make_sim(T.Oracle, case)
     hashes = []
     for _ in rollout(o, case):
         hashes.append(step_hashes(o))

@@ -57,6 +57,9 @@ DEBUG_OUTPUTS = ["DEBUG_AGENT_F32", "DEBUG_AGENT_I32", "DEBUG_WORLD_I32", "DEBUG
 
 DTYPES = {0: np.int32, 1: np.float32, 2: np.uint32}
 
+# Task (sim.hpp Task enum, include/mpenv.h MPENV_TASK_*)
+TASK_TDM, TASK_ZONE, TASK_TURRET, TASK_ZONE_CAPTURE_DEFEND = 1, 2, 3, 4
+
 SIMFLAG_STAGGER_STARTS = 1 << 4
 SIMFLAG_RANDOM_FLIP_TEAMS = 1 << 7
 
@@ -68,6 +71,7 @@ class OracleConfig(C.Structure):
         ("scene_path", C.c_char_p), ("bvh_nodes", C.c_void_p), ("num_nodes", C.c_int32),
         ("bvh_verts", C.c_void_p), ("num_bvh_verts", C.c_int32),
         ("nav_tris", C.c_void_p), ("num_nav_tris", C.c_int32), ("astar", C.c_void_p),
+        ("task_type", C.c_int32),
     ]
 
 
@@ -183,18 +187,40 @@ def scene_bvh(scene=SCENE):
     return nodes, verts, ms.value
 
 
+def four_zone_scene(dst):
+    """simple_map with a fourth zone appended to zones.bin (the reference's
+    ZoneCaptureDefend starts every episode at zone 3, sim.cpp:822-825, and
+    simple_map has three): a 250 x 250 box between the hardcoded spawns.
+    Written under dst; returns the scene directory."""
+    import shutil
+    d = os.path.join(str(dst), "four_zones")
+    os.makedirs(d, exist_ok=True)
+    for f in ("collisions.bin", "navmesh.bin", "spawns.bin"):
+        shutil.copy(os.path.join(SCENE, f), d)
+    raw = open(os.path.join(SCENE, "zones.bin"), "rb").read()
+    n = int(np.frombuffer(raw[:4], np.uint32)[0])
+    boxes = np.frombuffer(raw[4:4 + 24 * n], np.float32).reshape(n, 6)
+    rots = np.frombuffer(raw[4 + 24 * n:], np.float32)[:n]
+    extra = np.array([[700.0, 250.0, -80.0, 950.0, 500.0, 300.0]], np.float32)
+    with open(os.path.join(d, "zones.bin"), "wb") as f:
+        f.write(np.uint32(n + 1).tobytes())
+        f.write(np.concatenate([boxes, extra]).tobytes())
+        f.write(np.concatenate([rots, np.zeros(1, np.float32)]).tobytes())
+    return d
+
+
 class Oracle:
     """CPU restatement of the reference step (test infrastructure)."""
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
-                 world_id_offset=0, scene=SCENE):
+                 world_id_offset=0, scene=SCENE, task=TASK_ZONE):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
         self.nav_tris, _, self.astar = scene_navmesh(scene)
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
                            world_id_offset, scene.encode(), self.nodes.ctypes.data,
                            len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3,
-                           self.nav_tris.ctypes.data, len(self.nav_tris), self.astar.ctypes.data)
+                           self.nav_tris.ctypes.data, len(self.nav_tris), self.astar.ctypes.data, task)
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
         self.W, self.N = num_worlds, 2 * team_size
@@ -260,12 +286,13 @@ class Engine:
     """The gfx950 engine through its C ABI (include/mpenv.h)."""
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
-                 world_id_offset=0, scene=SCENE, gpu_id=0, replay=None, record=None, events=None):
+                 world_id_offset=0, scene=SCENE, gpu_id=0, replay=None, record=None, events=None,
+                 task=TASK_ZONE):
         self.lib = lib_mpenv()
         self.mem = HipMem()
         self._scene = scene.encode()
         self._paths = [p.encode() if p else None for p in (replay, record, events)]
-        cfg = MpenvConfig(1, gpu_id, num_worlds, rand_seed, int(auto_reset), sim_flags, 2,
+        cfg = MpenvConfig(1, gpu_id, num_worlds, rand_seed, int(auto_reset), sim_flags, task,
                           team_size, 0, 0, self._scene, 0, self._paths[0], self._paths[1], self._paths[2],
                           None, world_id_offset)
         h = C.c_void_p()

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import mpenv_testlib as T
-from golden.make_golden import rollout, set_bots, step_hashes
+from golden.make_golden import make_sim, rollout, set_bots, step_hashes
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +33,7 @@ def _compare_all(e, o, where):
 def test_engine_matches_golden_fixture(path):
     g = json.load(open(path))
     case = g["case"]
-    e = T.Engine(case["worlds"], case["team_size"], sim_flags=case["sim_flags"])
+    e = make_sim(T.Engine, case)
     for k, s in enumerate(rollout(e, case)):
         got = step_hashes(e)
         bad = [n for n in got if got[n] != g["hashes"][k][n]]
@@ -117,6 +117,37 @@ def test_auto_reset_off_and_triggered_resets():
         e.step()
         o.step()
         _compare_all(e, o, f"step {s}")
+
+
+def test_zone_capture_defend_matches_oracle(tmp_path):
+    """Task.ZoneCaptureDefend, 6v6 as scripts/jax_train.py sets it up
+    (HardcodedSpawns | StaggerStarts, random team sides), on simple_map
+    with a fourth zone; long enough for several matches to end."""
+    scene = T.four_zone_scene(tmp_path)
+    ts, W = 6, 16
+    flags = 1 | (1 << 6) | (1 << 4)
+    e = T.Engine(W, ts, sim_flags=flags, task=T.TASK_ZONE_CAPTURE_DEFEND, scene=scene)
+    o = T.Oracle(W, ts, sim_flags=flags, task=T.TASK_ZONE_CAPTURE_DEFEND, scene=scene)
+    for sim in (e, o):
+        sim.put_ctrl([0, 1, 1])
+        sim.init()
+    _compare_all(e, o, "init")
+    ends = 0
+    for s in range(700):
+        acts = T.combat_actions(o, s)
+        e.set_actions(acts)
+        o.set_actions(acts)
+        e.step()
+        o.step()
+        ends += int(o.get("DONE").reshape(W, -1)[:, 0].sum())
+        if s % 10 == 0:
+            _compare_all(e, o, f"step {s}")
+        else:
+            for n in ("SELF_OBSERVATION", "REWARD", "DONE", "MATCH_RESULT", "DEBUG_WORLD_I32"):
+                T.compare(e.get(n), o.get(n), f"{n} @ step {s}")
+    assert ends > 0
+    e.close()
+    o.close()
 
 
 def test_curriculum_resets_match_oracle():
