@@ -278,7 +278,20 @@ typedef struct mpenv_packed_step_snapshot {
     mpenv_packed_player players[12];
 } mpenv_packed_step_snapshot;
 
+/* CurriculumSnapshot (types.hpp:816-819): 176 bytes.  A curriculum_data_path
+ * file is a bare array of them (mgr.cpp:1424-1441; size / 176 snapshots),
+ * e.g. the match state + players of steps.bin records. */
+typedef struct mpenv_curriculum_snapshot {
+    uint16_t step;
+    uint8_t cur_zone;
+    int8_t cur_zone_controller;
+    uint16_t zone_steps_remaining;
+    uint16_t steps_until_point;
+    mpenv_packed_player players[12];
+} mpenv_curriculum_snapshot;
+
 #ifdef __cplusplus
+static_assert(sizeof(mpenv_curriculum_snapshot) == 176, "CurriculumSnapshot layout");
 static_assert(sizeof(mpenv_agent_log) == 72, "AgentLogData layout");
 static_assert(sizeof(mpenv_step_log) == 868, "StepLog layout");
 static_assert(sizeof(mpenv_game_event) == 24, "GameEvent layout");

@@ -177,6 +177,9 @@ struct SceneDev {
     const float *navTris;   // 9 floats per triangle (deduplicated vertices)
     const int32_t *astar;   // [numNavTris][numNavTris] next hop
     const float *navCdf;    // [numNavTris] running triangle areas (NavmeshSpawn)
+    // TrajectoryCurriculum (level_gen.cpp:498-581), curriculum_data_path
+    const mpenv_curriculum_snapshot *curriculum;
+    int32_t numSnapshots;
     int32_t numNavTris;
     // logs (sim.cpp:4750-4843 record/replay, 23-106 + 4592-4634 events)
     int32_t recordOn, replayOn, eventsOn;

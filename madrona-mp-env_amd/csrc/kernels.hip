@@ -893,12 +893,45 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
         rc[0] = 0.f; rc[1] = 0.5f; rc[2] = 0.005f; rc[3] = 0.05f; rc[4] = 0.01f;
         rc[5] = 0.1f; rc[6] = 0.0005f; rc[7] = 1.f; rc[8] = 0.1f;
     }
-    stWRng(S, w, base);
     // GoalRegionsState (level_gen.cpp:472-485)
     S.goalMin0[w] = kFltMax;
     S.goalMin1[w] = kFltMax;
     S.goalTeam0[w] = 0.f;
     S.goalTeam1[w] = 0.f;
+
+    // level_gen.cpp:498-580: start from a recorded match state half the time
+    // (not in eval mode); the uniform is drawn whenever snapshots exist
+    if (sc.numSnapshots > 0 && rngUniform(base) < 0.5f && !S.trainCtrl[0]) {
+        const mpenv_curriculum_snapshot &sn = sc.curriculum[rngI32(base, 0, sc.numSnapshots)];
+        S.curZone[w] = sn.cur_zone;
+        if (sn.cur_zone_controller == -1) {
+            S.controlling[w] = -1;
+            S.captured[w] = 0;
+        } else {
+            S.captured[w] = 1;
+            S.controlling[w] = sn.cur_zone_controller;
+            S.stepsUntilPoint[w] = sn.steps_until_point;
+            S.zoneSteps[w] = sn.zone_steps_remaining;
+        }
+        S.curStep[w] = sn.step;
+        const int half = N / 2;
+        const int team_a = S.teamA[w];
+        for (int i = 0; i < N; i++) {
+            const int j = team_a == 0 ? i : (i < half ? half + i : i - half);
+            const int64_t g = g0 + j;
+            const mpenv_packed_player &p = sn.players[i];
+            stPos(S, g, v3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]));
+            const AimD aim = computeAimD((float)p.yaw * kPi / 32768.f, (float)p.pitch * kPi / 32768.f);
+            stAim(S, g, aim);
+            stRot(S, g, qnormalize(angleAxis(aim.yaw, kUp)));
+            S.hp[g] = (float)p.hp;
+            S.magazine[2 * g] = p.mag_num_bullets;
+            S.magazine[2 * g + 1] = p.is_reloading;
+            if (p.flags & 4) { S.curPose[g] = kCrouch; S.tgtPose[g] = kCrouch; S.transRem[g] = 0; }
+            if (p.flags & 8) { S.curPose[g] = kProne; S.tgtPose[g] = kProne; S.transRem[g] = 0; }
+        }
+    }
+    stWRng(S, w, base);
 }
 
 // sim.cpp:732-833 initWorld

@@ -445,6 +445,31 @@ static void buildSceneDev(mpenv_manager &m)
         kMinSpawnTrack, std::max(s.aSpawns.size(), std::max(s.bSpawns.size(), s.commonRespawns.size())));
     sc.numZones = (int32_t)s.zoneAABBs.size();
     sc.task = m.cfg.task_type;
+    if (m.cfg.curriculum_data_path) {
+        // mgr.cpp:1424-1441: the file is an array of CurriculumSnapshot
+        // (size / 176 of them).  Snapshots naming a zone or controller the
+        // scene does not have are rejected (the reference would index past
+        // its zone arrays).
+        FILE *f = std::fopen(m.cfg.curriculum_data_path, "rb");
+        if (!f) throw std::runtime_error(std::string("cannot open curriculum data ") + m.cfg.curriculum_data_path);
+        std::fseek(f, 0, SEEK_END);
+        const long size = std::ftell(f);
+        std::fseek(f, 0, SEEK_SET);
+        std::vector<mpenv_curriculum_snapshot> snaps((size_t)std::max<long>(size, 0) / sizeof(mpenv_curriculum_snapshot));
+        const size_t got = snaps.empty() ? 0 : std::fread(snaps.data(), sizeof(mpenv_curriculum_snapshot), snaps.size(), f);
+        std::fclose(f);
+        if (got != snaps.size()) throw std::runtime_error("short read of curriculum data");
+        for (const mpenv_curriculum_snapshot &sn : snaps) {
+            if (sn.cur_zone >= s.zoneAABBs.size() || sn.cur_zone_controller < -1 || sn.cur_zone_controller > 1)
+                throw std::runtime_error("curriculum snapshot names a zone or controller outside the scene");
+        }
+        if (!snaps.empty()) {
+            auto *d = m.alloc<mpenv_curriculum_snapshot>(snaps.size());
+            m.upload(d, snaps.data(), sizeof(mpenv_curriculum_snapshot) * snaps.size());
+            sc.curriculum = d;
+        }
+        sc.numSnapshots = (int32_t)snaps.size();
+    }
     // initWorld starts every ZoneCaptureDefend episode at zone 3 (sim.cpp:822-825)
     if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND && s.zoneAABBs.size() < 4)
         throw std::runtime_error("ZoneCaptureDefend needs a scene with >= 4 zones");
@@ -701,8 +726,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
     if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");
     if (!cfg->scene_path) return fail(MPENV_ERR_INVALID, "scene_path is required");
     if (cfg->sim_flags >> 12) return fail(MPENV_ERR_INVALID, "sim_flags has bits beyond SubZones (1 << 11)");
-    if (cfg->curriculum_data_path || cfg->train_flank)
-        return fail(MPENV_ERR_UNSUPPORTED, "trajectory curricula and flank rewards are not implemented");
+    if (cfg->train_flank) return fail(MPENV_ERR_UNSUPPORTED, "flank rewards (train_flank) are not implemented");
     if (cfg->replay_log_path && cfg->record_log_path)
         return fail(MPENV_ERR_UNSUPPORTED, "record and replay logs together are not supported");
 
@@ -730,6 +754,9 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m->S.A = (int64_t)m->S.W * m->S.N;
         allocState(*m);
         openLogs(*m, cfg);
+        // the caller's path strings are not kept past create
+        m->cfg.replay_log_path = m->cfg.record_log_path = m->cfg.event_log_path = nullptr;
+        m->cfg.curriculum_data_path = nullptr;
         {
             // World groups (concurrent streams).  MPENV_WORLD_GROUPS overrides.
             int want = m->S.W >= 3072 ? 3 : 1;

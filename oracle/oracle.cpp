@@ -225,6 +225,7 @@ struct Oracle {
     std::vector<Node> nodes;
     std::vector<Vec3> navTris;   // 3 per triangle
     std::vector<float> navCdf;   // running triangle areas (navSamplePoint)
+    std::vector<mpenv_curriculum_snapshot> curriculum; // TrajectoryCurriculum
     struct ZOBB { Vec3 pMin, pMax; float rotation; } subZones[8]; // level_gen.cpp:282-326
     std::vector<int32_t> astar;  // [T][T]
     int numNavTris = 0;
@@ -955,6 +956,40 @@ void resetPersistentEntities(Oracle &o, int w, RandKey episode_key)
     }
     wd.teamStepRewards[0] = 0.f;
     wd.teamStepRewards[1] = 0.f;
+
+    // level_gen.cpp:498-580: start from a recorded match state half the time
+    // (not in eval mode); the uniform is drawn whenever snapshots exist
+    if (!o.curriculum.empty() && rngUniform(base) < 0.5f && !o.trainControl[0]) {
+        const int idx = rngI32(base, 0, (int)o.curriculum.size());
+        const mpenv_curriculum_snapshot &sn = o.curriculum[idx];
+        wd.curZone = sn.cur_zone;
+        if (sn.cur_zone_controller == -1) {
+            wd.curControllingTeam = -1;
+            wd.isCaptured = false;
+        } else {
+            wd.isCaptured = true;
+            wd.curControllingTeam = sn.cur_zone_controller;
+            wd.stepsUntilPoint = sn.steps_until_point;
+            wd.zoneStepsRemaining = sn.zone_steps_remaining;
+        }
+        wd.curStep = sn.step;
+        const int half = o.N / 2;
+        for (int i = 0; i < o.N; i++) {
+            const int j = wd.teamA == 0 ? i : (i < half ? half + i : i - half);
+            Agent &ag = o.agent(w, j);
+            const size_t g = o.gi(w, j);
+            const mpenv_packed_player &p = sn.players[i];
+            ag.pos = v3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]);
+            AimS aim = computeAim((float)p.yaw * kPi / 32768.f, (float)p.pitch * kPi / 32768.f);
+            ag.aimYaw = aim.yaw; ag.aimPitch = aim.pitch; ag.aimRot = aim.rot;
+            ag.rot = qnormalize(angleAxis(aim.yaw, kUp));
+            o.hp[g] = (float)p.hp;
+            o.magazine[2 * g] = p.mag_num_bullets;
+            o.magazine[2 * g + 1] = p.is_reloading;
+            if (p.flags & 4) { ag.curPose = kCrouch; ag.tgtPose = kCrouch; ag.transitionRemaining = 0; }
+            if (p.flags & 8) { ag.curPose = kProne; ag.tgtPose = kProne; ag.transitionRemaining = 0; }
+        }
+    }
 }
 
 // sim.cpp:732-833 initWorld
@@ -3036,6 +3071,13 @@ void oracle_step_worlds(void *h, int32_t w0, int32_t w1)
 }
 
 void oracle_refresh_debug(void *h) { refreshDebug(*static_cast<Oracle *>(h)); }
+
+void oracle_set_curriculum(void *h, const void *snapshots, int32_t n)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    const auto *p = static_cast<const mpenv_curriculum_snapshot *>(snapshots);
+    o.curriculum.assign(p, p + (n > 0 ? n : 0));
+}
 
 void oracle_set_log_modes(void *h, int32_t record, int32_t replay, int32_t events)
 {

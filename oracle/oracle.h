@@ -56,6 +56,9 @@ void oracle_refresh_debug(void *h);
  * PACKED_STEP_SNAPSHOT / SNAPSHOT_WRITTEN; in replay mode the caller fills
  * REPLAY_LOG before each step. */
 void oracle_set_log_modes(void *h, int32_t record, int32_t replay, int32_t events);
+/* Trajectory curriculum (level_gen.cpp:498-581): n CurriculumSnapshots
+ * (include/mpenv.h mpenv_curriculum_snapshot), copied. */
+void oracle_set_curriculum(void *h, const void *snapshots, int32_t n);
 /* CPU baseline timing: runs nsteps steps over all worlds with nthreads
  * std::threads (static world partition, like ThreadPoolExecutor,
  * mgr.cpp:1863-1871).  Before each step the discrete/aim actions of step s

@@ -134,6 +134,7 @@ def lib_oracle():
             getattr(lib, fn).argtypes = [C.c_void_p]
         lib.oracle_step_worlds.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         lib.oracle_set_log_modes.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
+        lib.oracle_set_curriculum.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         lib.oracle_run_threaded.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32]
         lib.oracle_run_threaded.restype = C.c_double
         fp = C.POINTER(C.c_float)
@@ -209,11 +210,57 @@ def four_zone_scene(dst):
     return d
 
 
+CURRICULUM_SNAPSHOT = np.dtype([("step", "<u2"), ("cur_zone", "u1"), ("controller", "i1"),
+                                ("zone_steps_remaining", "<u2"), ("steps_until_point", "<u2"),
+                                ("players", [("pos", "<i2", 3), ("yaw", "<i2"), ("pitch", "<i2"),
+                                             ("mag", "u1"), ("reloading", "u1"), ("hp", "u1"),
+                                             ("flags", "u1")], 12)])
+
+
+def make_curriculum_file(path, n=64, seed=7):
+    """A curriculum_data_path file (n CurriculumSnapshots, 176 B each,
+    types.hpp:816-819).  Player positions come from a 6v6 oracle rollout so
+    they sit on the map; the rest of each snapshot is drawn at random:
+    controller -1/0/1, crouch / prone flags, hp, magazine, step."""
+    assert CURRICULUM_SNAPSHOT.itemsize == 176
+    rng = np.random.default_rng(seed)
+    o = Oracle(4, 6, sim_flags=1)
+    o.put_ctrl([0, 1, 1])
+    o.init()
+    pos = []
+    for s in range(60):
+        o.set_actions(mpenv_tape.tape_actions(99, s, 0, 4 * 12))
+        o.step()
+        if s % 4 == 3:
+            o.lib.oracle_refresh_debug(o.h)
+            pos.append(o.get("DEBUG_AGENT_F32")[:, :3].reshape(4, 12, 3).copy())
+    o.close()
+    pos = np.concatenate(pos)  # [k, 12, 3]
+    out = np.zeros(n, CURRICULUM_SNAPSHOT)
+    for k in range(n):
+        sn = out[k]
+        sn["step"] = rng.integers(0, 2900)
+        sn["cur_zone"] = rng.integers(0, 3)
+        sn["controller"] = rng.integers(-1, 2)
+        sn["zone_steps_remaining"] = rng.integers(1, 601)
+        sn["steps_until_point"] = rng.integers(1, 21)
+        pl = sn["players"]
+        pl["pos"] = np.round(pos[k % len(pos)]).astype(np.int16)
+        pl["yaw"] = rng.integers(-32768, 32768, 12)
+        pl["pitch"] = rng.integers(-6000, 6000, 12)
+        pl["mag"] = rng.integers(0, 31, 12)
+        pl["reloading"] = rng.integers(0, 3, 12)
+        pl["hp"] = rng.integers(1, 101, 12)
+        pl["flags"] = rng.choice([0, 2, 4, 8], 12)
+    out.tofile(path)
+    return path
+
+
 class Oracle:
     """CPU restatement of the reference step (test infrastructure)."""
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
-                 world_id_offset=0, scene=SCENE, task=TASK_ZONE):
+                 world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
         self.nav_tris, _, self.astar = scene_navmesh(scene)
@@ -223,6 +270,10 @@ class Oracle:
                            self.nav_tris.ctypes.data, len(self.nav_tris), self.astar.ctypes.data, task)
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
+        if curriculum:
+            data = np.fromfile(curriculum, np.uint8)
+            n = len(data) // 176
+            self.lib.oracle_set_curriculum(self.h, data.ctypes.data, n)
         self.W, self.N = num_worlds, 2 * team_size
 
     def close(self):
@@ -287,14 +338,14 @@ class Engine:
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
                  world_id_offset=0, scene=SCENE, gpu_id=0, replay=None, record=None, events=None,
-                 task=TASK_ZONE):
+                 task=TASK_ZONE, curriculum=None):
         self.lib = lib_mpenv()
         self.mem = HipMem()
         self._scene = scene.encode()
-        self._paths = [p.encode() if p else None for p in (replay, record, events)]
+        self._paths = [p.encode() if p else None for p in (replay, record, events, curriculum)]
         cfg = MpenvConfig(1, gpu_id, num_worlds, rand_seed, int(auto_reset), sim_flags, task,
                           team_size, 0, 0, self._scene, 0, self._paths[0], self._paths[1], self._paths[2],
-                          None, world_id_offset)
+                          self._paths[3], world_id_offset)
         h = C.c_void_p()
         rc = self.lib.mpenv_create(C.byref(cfg), C.byref(h))
         assert rc == 0, self.lib.mpenv_last_error().decode()

@@ -150,6 +150,38 @@ def test_zone_capture_defend_matches_oracle(tmp_path):
     o.close()
 
 
+def test_curriculum_data_matches_oracle(tmp_path):
+    """curriculum_data_path: recorded match states applied at episode
+    starts (level_gen.cpp:498-580), over many triggered resets."""
+    path = T.make_curriculum_file(str(tmp_path / "curriculum.bin"), n=48)
+    for ts in (6, 3):
+        W = 16
+        e = T.Engine(W, ts, sim_flags=1, curriculum=path)
+        o = T.Oracle(W, ts, sim_flags=1, curriculum=path)
+        for sim in (e, o):
+            sim.put_ctrl([0, 1, 1])
+            sim.init()
+        _compare_all(e, o, f"ts {ts} init")
+        for s in range(200):
+            if s % 10 == 0:
+                for w in range(W):
+                    if (s // 10 + w) % 4 == 0:
+                        e.trigger_reset(w)
+                        o.view("RESET")[w] = 1
+            acts = T.combat_actions(o, s)
+            e.set_actions(acts)
+            o.set_actions(acts)
+            e.step()
+            o.step()
+            if s % 5 == 0:
+                _compare_all(e, o, f"ts {ts} step {s}")
+            else:
+                for n in ("SELF_OBSERVATION", "REWARD", "HP", "DEBUG_WORLD_I32"):
+                    T.compare(e.get(n), o.get(n), f"{n} @ ts {ts} step {s}")
+        e.close()
+        o.close()
+
+
 def test_curriculum_resets_match_oracle():
     """EnableCurriculum across many episodes: the LearnShooting/FullMatch
     draw per reset (sim.cpp:852-867), LearnShooting spawns and rewards
