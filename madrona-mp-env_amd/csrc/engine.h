@@ -166,6 +166,7 @@ struct SceneDev {
     float zoneRot[kMaxZones];
     int32_t numZones;
     int32_t task;           // MPENV_TASK_ZONE or MPENV_TASK_ZONE_CAPTURE_DEFEND
+    int32_t flank;          // RewardMode::Flank (train_flank)
     ZOBBDev subZones[8];    // SubZones only (level_gen.cpp:282-326)
     GoalRegionDev goals[4];
     int32_t numGoals;

@@ -1792,6 +1792,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
 // by workgroup barriers.
 constexpr int kSimBlock = 128;
 
+__device__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
+
 __global__ void __launch_bounds__(kSimBlock) k_sim(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1851,7 +1853,8 @@ __global__ void __launch_bounds__(kSimBlock) k_sim(DevState S, SceneDev sc)
     __syncthreads();
     if (act) {
         exploreVisitedD(S, w, g);
-        zoneRewardD(S, sc, w, i);
+        if (sc.flank && sc.task == MPENV_TASK_ZONE) flankRewardD(S, sc, bvh, w, i);
+        else zoneRewardD(S, sc, w, i);
     }
     __syncthreads();
     if (wlane) {
@@ -1925,6 +1928,73 @@ __device__ __forceinline__ Vec3 visSamplePointD(const DevState &S, int64_t gt, V
     if (p == 2) pt = pt - delta_right;
     if (p == 3) pt = pt + delta_right;
     return pt;
+}
+
+// utils.cpp:169-271 isAgentVisible for one (viewer, target) pair, lane-wise
+// (the flank reward's checks; k_vis batches the opponent checks instead).
+__device__ bool isAgentVisibleD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, Vec3 org,
+                                Quat aim_rot, int target)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    const Quat inv_rot = qinv(aim_rot);
+    const Vec3 delta_right = rotateVec(aim_rot, kRight) * 0.9f * c::kAgentRadius;
+    for (int p = 0; p < 4; p++) {
+        Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
+        Vec3 view = rotateVec(inv_rot, to_test);
+        if (view.y <= 0.f) continue;
+        if (!inFrustumD(sc, view)) continue;
+        const float len = length(to_test);
+        if (len < c::kAgentRadius) continue;
+        to_test = to_test / len;
+        WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, org, to_test);
+        if (h.hit && h.entity == target) return true;
+    }
+    return false;
+}
+
+// sim.cpp:4202-4278 flankRewardSystem (Task.Zone with train_flank): small
+// bonuses for teammates out of sight or >= 100 units away and for each
+// opponent that cannot see the agent (judged with the agent's own aim),
+// hits / kills from behind the target, exploration.  CombatState is taken
+// by value there, so nothing is cleared.
+__device__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
+{
+    const int T = S.T, N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    const int64_t g = g0 + i;
+    const int team = i / T, off = i - team * T;
+    const Vec3 pos = ldPos(S, g);
+    const Quat aim_rot = ldAimRot(S, g);
+    float r = 0.f;
+    Vec3 vis = pos;
+    vis.z += viewHeightD(S.curPose[g]);
+    const float flank_dist = 100.f;
+    float mates = 0.f;
+    for (int k = 0; k < T - 1; k++) {
+        const int j = team * T + (k < off ? k : k + 1);
+        const Vec3 dir = ldPos(S, g0 + j) - pos;
+        const bool seen = isAgentVisibleD(S, sc, bvh, w, vis, aim_rot, j);
+        if (length2(dir) >= flank_dist * flank_dist || !seen) mates += 0.001f;
+    }
+    r += mates;
+    float opps = 0.f;
+    for (int k = 0; k < T; k++) {
+        const int64_t go = g0 + (team ^ 1) * T + k;
+        Vec3 op_pos = ldPos(S, go);
+        op_pos.z += viewHeightD(S.curPose[go]);
+        if (!isAgentVisibleD(S, sc, bvh, w, op_pos, aim_rot, i)) opps += 0.001f;
+    }
+    r += opps;
+    const int landed = S.landedOn[g];
+    if (landed != -1) {
+        const float yaw_diff = fabs_(S.ayaw[g0 + landed] - S.ayaw[g]);
+        if (yaw_diff > kPi) r += (S.flags[g] & kFlagSuccessfulKill) ? 1.f : 0.2f;
+    }
+    uint32_t nn = (uint32_t)S.newCells[g];
+    S.newCells[g] = 0;
+    if (nn > 0) r += float(nn) * S.rewardCoefs[9 * g + 2];
+    S.reward[g] = r;
 }
 
 __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)

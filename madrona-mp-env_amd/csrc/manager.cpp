@@ -445,6 +445,7 @@ static void buildSceneDev(mpenv_manager &m)
         kMinSpawnTrack, std::max(s.aSpawns.size(), std::max(s.bSpawns.size(), s.commonRespawns.size())));
     sc.numZones = (int32_t)s.zoneAABBs.size();
     sc.task = m.cfg.task_type;
+    sc.flank = m.cfg.train_flank ? 1 : 0; // RewardMode::Flank applies to Task.Zone (sim.cpp:5733-5748)
     if (m.cfg.curriculum_data_path) {
         // mgr.cpp:1424-1441: the file is an array of CurriculumSnapshot
         // (size / 176 of them).  Snapshots naming a zone or controller the
@@ -726,7 +727,6 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
     if (cfg->num_worlds == 0) return fail(MPENV_ERR_INVALID, "num_worlds must be > 0");
     if (!cfg->scene_path) return fail(MPENV_ERR_INVALID, "scene_path is required");
     if (cfg->sim_flags >> 12) return fail(MPENV_ERR_INVALID, "sim_flags has bits beyond SubZones (1 << 11)");
-    if (cfg->train_flank) return fail(MPENV_ERR_UNSUPPORTED, "flank rewards (train_flank) are not implemented");
     if (cfg->replay_log_path && cfg->record_log_path)
         return fail(MPENV_ERR_UNSUPPORTED, "record and replay logs together are not supported");
 

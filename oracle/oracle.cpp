@@ -217,6 +217,7 @@ struct Oracle {
     bool autoReset;
     uint32_t simFlags;
     int task = MPENV_TASK_ZONE; // Zone or ZoneCaptureDefend
+    bool flank = false;         // RewardMode::Flank
     RandKey initRandKey;
 
     AABB worldBounds;
@@ -2126,6 +2127,46 @@ void zoneCaptureDefendRewardSystem(Oracle &o, int w, int i)
     o.reward[g] = r;
 }
 
+// sim.cpp:4202-4278 flankRewardSystem (Task.Zone with train_flank): small
+// bonuses for teammates out of sight or >= 100 units away and for each
+// opponent that cannot see the agent (judged with the agent's own aim),
+// hits / kills from behind the target (|yaw difference| > pi), exploration.
+// CombatState is taken by value there, so nothing is cleared.
+void flankRewardSystem(Oracle &o, int w, int i)
+{
+    Agent &ag = o.agent(w, i);
+    size_t g = o.gi(w, i);
+    const float explore = o.rewardCoefs[9 * g + 2];
+    float r = 0.f;
+    Vec3 vis = ag.pos;
+    vis.z += viewHeight(ag.curPose);
+    const float flank_dist = 100.f;
+    float mates = 0.f;
+    for (int k = 0; k < o.teamSize - 1; k++) {
+        const int j = ag.team * o.teamSize + (k < ag.offset ? k : k + 1);
+        Vec3 dir = o.agent(w, j).pos - ag.pos;
+        const bool seen = isAgentVisible(o, w, vis, ag.aimRot, j);
+        if (length2(dir) >= flank_dist * flank_dist || !seen) mates += 0.001f;
+    }
+    r += mates;
+    float opps = 0.f;
+    for (int k = 0; k < o.teamSize; k++) {
+        const Agent &op = o.agent(w, (ag.team ^ 1) * o.teamSize + k);
+        Vec3 op_pos = op.pos;
+        op_pos.z += viewHeight(op.curPose);
+        if (!isAgentVisible(o, w, op_pos, ag.aimRot, i)) opps += 0.001f;
+    }
+    r += opps;
+    if (ag.landedShotOn != -1) {
+        const float yaw_diff = fabs_(o.agent(w, ag.landedShotOn).aimYaw - ag.aimYaw);
+        if (yaw_diff > kPi) r += ag.successfulKill ? 1.f : 0.2f;
+    }
+    uint32_t nn = ag.numNewCellsVisited;
+    ag.numNewCellsVisited = 0;
+    if (nn > 0) r += float(nn) * explore;
+    o.reward[g] = r;
+}
+
 // sim.cpp:3849-3996 zoneRewardSystem
 void zoneRewardSystem(Oracle &o, int w, int i)
 {
@@ -2654,6 +2695,7 @@ void replayTail(Oracle &o, int w)
     for (int i = 0; i < N; i++) exploreVisitedSystem(o, w, i);
     for (int i = 0; i < N; i++) {
         if (o.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) zoneCaptureDefendRewardSystem(o, w, i);
+        else if (o.flank) flankRewardSystem(o, w, i);
         else if (o.simFlags & MPENV_SIMFLAG_SUB_ZONES) subzoneRewardSystem(o, w, i);
         else zoneRewardSystem(o, w, i);
     }
@@ -2855,6 +2897,7 @@ void *oracle_create(const oracle_config *cfg)
         o->autoReset = cfg->auto_reset != 0;
         o->simFlags = cfg->sim_flags;
         o->task = cfg->task_type;
+        o->flank = cfg->train_flank != 0;
         if (o->task != MPENV_TASK_ZONE && o->task != MPENV_TASK_ZONE_CAPTURE_DEFEND)
             throw std::runtime_error("oracle: task must be Zone or ZoneCaptureDefend");
         // mgr.cpp:1736-1738

@@ -37,6 +37,8 @@ typedef struct oracle_config {
     const int32_t *astar;
     /* Task (MPENV_TASK_*): Zone or ZoneCaptureDefend. */
     int32_t task_type;
+    /* RewardMode::Flank (train_flank, mgr.cpp:1746-1750) */
+    int32_t train_flank;
 } oracle_config;
 
 void *oracle_create(const oracle_config *cfg);

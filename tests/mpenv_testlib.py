@@ -71,7 +71,7 @@ class OracleConfig(C.Structure):
         ("scene_path", C.c_char_p), ("bvh_nodes", C.c_void_p), ("num_nodes", C.c_int32),
         ("bvh_verts", C.c_void_p), ("num_bvh_verts", C.c_int32),
         ("nav_tris", C.c_void_p), ("num_nav_tris", C.c_int32), ("astar", C.c_void_p),
-        ("task_type", C.c_int32),
+        ("task_type", C.c_int32), ("train_flank", C.c_int32),
     ]
 
 
@@ -260,14 +260,15 @@ class Oracle:
     """CPU restatement of the reference step (test infrastructure)."""
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
-                 world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None):
+                 world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None, flank=False):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
         self.nav_tris, _, self.astar = scene_navmesh(scene)
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
                            world_id_offset, scene.encode(), self.nodes.ctypes.data,
                            len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3,
-                           self.nav_tris.ctypes.data, len(self.nav_tris), self.astar.ctypes.data, task)
+                           self.nav_tris.ctypes.data, len(self.nav_tris), self.astar.ctypes.data, task,
+                           int(flank))
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
         if curriculum:
@@ -338,13 +339,13 @@ class Engine:
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
                  world_id_offset=0, scene=SCENE, gpu_id=0, replay=None, record=None, events=None,
-                 task=TASK_ZONE, curriculum=None):
+                 task=TASK_ZONE, curriculum=None, flank=False):
         self.lib = lib_mpenv()
         self.mem = HipMem()
         self._scene = scene.encode()
         self._paths = [p.encode() if p else None for p in (replay, record, events, curriculum)]
         cfg = MpenvConfig(1, gpu_id, num_worlds, rand_seed, int(auto_reset), sim_flags, task,
-                          team_size, 0, 0, self._scene, 0, self._paths[0], self._paths[1], self._paths[2],
+                          team_size, 0, 0, self._scene, int(flank), self._paths[0], self._paths[1], self._paths[2],
                           self._paths[3], world_id_offset)
         h = C.c_void_p()
         rc = self.lib.mpenv_create(C.byref(cfg), C.byref(h))

@@ -182,6 +182,31 @@ def test_curriculum_data_matches_oracle(tmp_path):
         o.close()
 
 
+def test_flank_reward_matches_oracle():
+    """train_flank: flankRewardSystem's visibility checks run per agent in
+    k_sim (sim.cpp:4202-4278)."""
+    for ts in (2, 6):
+        W = 16
+        e = T.Engine(W, ts, sim_flags=1, flank=True)
+        o = T.Oracle(W, ts, sim_flags=1, flank=True)
+        for sim in (e, o):
+            sim.put_ctrl([0, 1, 1])
+            sim.init()
+        for s in range(200):
+            acts = T.combat_actions(o, s)
+            e.set_actions(acts)
+            o.set_actions(acts)
+            e.step()
+            o.step()
+            if s % 10 == 0:
+                _compare_all(e, o, f"ts {ts} step {s}")
+            else:
+                for n in ("REWARD", "DEBUG_AGENT_I32"):
+                    T.compare(e.get(n), o.get(n), f"{n} @ ts {ts} step {s}")
+        e.close()
+        o.close()
+
+
 def test_curriculum_resets_match_oracle():
     """EnableCurriculum across many episodes: the LearnShooting/FullMatch
     draw per reset (sim.cpp:852-867), LearnShooting spawns and rewards
