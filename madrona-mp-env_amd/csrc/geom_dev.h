@@ -195,6 +195,12 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     const float rayYInv = copysign_(ray_d.y == 0 ? 1 / diveps : 1 / ray_d.y, ray_d.y);
     const float rayZInv = copysign_(ray_d.z == 0 ? 1 / diveps : 1 / ray_d.z, ray_d.z);
 
+    // Slab selection by ray direction sign: fma(q, dq, oq) is monotonic in q
+    // and dq != 0, so per axis min(t(qMin), t(qMax)) is t(qMin) when dq > 0
+    // and t(qMax) otherwise -- the reference's six fminf/fmaxf give the same
+    // values (mesh_bvh.inl:165-183).
+    const bool negX = rayXInv < 0.f, negY = rayYInv < 0.f, negZ = rayZInv < 0.f;
+
     float t_max = kFltMax;
     bool ray_hit = false;
     ByteStack st;
@@ -209,20 +215,22 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
         const float originQuantX = (node.minX - ray_o.x) * rayXInv;
         const float originQuantY = (node.minY - ray_o.y) * rayYInv;
         const float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
+        const uint32_t nearX = negX ? node.qMaxX : node.qMinX, farX = negX ? node.qMinX : node.qMaxX;
+        const uint32_t nearY = negY ? node.qMaxY : node.qMinY, farY = negY ? node.qMinY : node.qMaxY;
+        const uint32_t nearZ = negZ ? node.qMaxZ : node.qMinZ, farZ = negZ ? node.qMinZ : node.qMaxZ;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int32_t child = node.child[i];
             if (child == -1) continue;
-            float t_near_x = qb(node.qMinX, i) * dirQuantX + originQuantX;
-            float t_near_y = qb(node.qMinY, i) * dirQuantY + originQuantY;
-            float t_near_z = qb(node.qMinZ, i) * dirQuantZ + originQuantZ;
-            float t_far_x = qb(node.qMaxX, i) * dirQuantX + originQuantX;
-            float t_far_y = qb(node.qMaxY, i) * dirQuantY + originQuantY;
-            float t_far_z = qb(node.qMaxZ, i) * dirQuantZ + originQuantZ;
-            float t_near = fmax_(fmin_(t_near_x, t_far_x),
-                                 fmax_(fmin_(t_near_y, t_far_y), fmax_(fmin_(t_near_z, t_far_z), 0.f)));
-            float t_far = fmin_(fmax_(t_far_x, t_near_x),
-                                fmin_(fmax_(t_far_y, t_near_y), fmin_(fmax_(t_far_z, t_near_z), t_max)));
+            // fused like the reference's NVRTC build (--fmad=true)
+            const float t_near_x = fma_(qb(nearX, i), dirQuantX, originQuantX);
+            const float t_near_y = fma_(qb(nearY, i), dirQuantY, originQuantY);
+            const float t_near_z = fma_(qb(nearZ, i), dirQuantZ, originQuantZ);
+            const float t_far_x = fma_(qb(farX, i), dirQuantX, originQuantX);
+            const float t_far_y = fma_(qb(farY, i), dirQuantY, originQuantY);
+            const float t_far_z = fma_(qb(farZ, i), dirQuantZ, originQuantZ);
+            const float t_near = fmax_(fmax_(t_near_x, t_near_y), fmax_(t_near_z, 0.f));
+            const float t_far = fmin_(fmin_(t_far_x, t_far_y), fmin_(t_far_z, t_max));
             if (t_near <= t_far) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;

@@ -364,12 +364,14 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
         float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
         for (int i = 0; i < 4; i++) {
             if (node.children[i] == -1) continue;
-            float t_near_x = node.qMinX[i] * dirQuantX + originQuantX;
-            float t_near_y = node.qMinY[i] * dirQuantY + originQuantY;
-            float t_near_z = node.qMinZ[i] * dirQuantZ + originQuantZ;
-            float t_far_x = node.qMaxX[i] * dirQuantX + originQuantX;
-            float t_far_y = node.qMaxY[i] * dirQuantY + originQuantY;
-            float t_far_z = node.qMaxZ[i] * dirQuantZ + originQuantZ;
+            // q * dirQuant + originQuant, fused: the reference's GPU build is
+            // compiled with NVRTC's default --fmad=true, which contracts it
+            float t_near_x = fma_((float)node.qMinX[i], dirQuantX, originQuantX);
+            float t_near_y = fma_((float)node.qMinY[i], dirQuantY, originQuantY);
+            float t_near_z = fma_((float)node.qMinZ[i], dirQuantZ, originQuantZ);
+            float t_far_x = fma_((float)node.qMaxX[i], dirQuantX, originQuantX);
+            float t_far_y = fma_((float)node.qMaxY[i], dirQuantY, originQuantY);
+            float t_far_z = fma_((float)node.qMaxZ[i], dirQuantZ, originQuantZ);
             float t_near = fmax_(fmin_(t_near_x, t_far_x),
                                  fmax_(fmin_(t_near_y, t_far_y), fmax_(fmin_(t_near_z, t_far_z), 0.f)));
             float t_far = fmin_(fmax_(t_far_x, t_near_x),
