@@ -408,23 +408,55 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
     Vec3 closest = v3(0.f, 0.f, 0.f);
     const float t_max0 = kFltMax;
     float hit_t = t_max0;
+#ifdef MPENV_LAB_NO_SPHERE
+    if (ray_o.x != 12345.f) {
+        SphereHit h0;
+        h0.t = t_max0;
+        h0.n = closest;
+        return h0;
+    }
+#endif
+    // sphereCastNodeCheck (mesh_bvh.inl:817-855) with the slab ends chosen
+    // once per cast from the sign of inv_d: per axis b_min is the child's
+    // (min - r) or (max + r) end, exactly as the per-child selects pick it;
+    // the running t_min / t_max updates `i > t ? i : t` are maxNum / minNum
+    // (a NaN slab from 0 * inf leaves them unchanged either way, and a -0 / +0
+    // tie does not change the final t_min < t_max).
+    const bool negX = __builtin_signbit(inv_d.x), negY = __builtin_signbit(inv_d.y),
+               negZ = __builtin_signbit(inv_d.z);
+    const float nrX = negX ? r : -r, nrY = negY ? r : -r, nrZ = negZ ? r : -r;
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
     bsPush(st, 0);
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
         const MP_LDS BVHNode &node = b.nodes[node_idx];
+        const MP_LDS uint32_t *qw = reinterpret_cast<const MP_LDS uint32_t *>(&node.triSize[0]);
+        // qw: [0] triSize, [1..3] qMin x/y/z, [4..6] qMax x/y/z
         const float sx = expScaleD(node.expX), sy = expScaleD(node.expY), sz = expScaleD(node.expZ);
+        const uint32_t nearX = qw[negX ? 4 : 1], farX = qw[negX ? 1 : 4];
+        const uint32_t nearY = qw[negY ? 5 : 2], farY = qw[negY ? 2 : 5];
+        const uint32_t nearZ = qw[negZ ? 6 : 3], farZ = qw[negZ ? 3 : 6];
+        const uint32_t tri_size = qw[0];
+#pragma unroll 1
         for (int i = 0; i < 4; i++) {
             const int32_t child = node.children[i];
             if (child == -1) continue;
-            AABB cb;
-            cb.pMin = v3(node.minX + sx * node.qMinX[i], node.minY + sy * node.qMinY[i], node.minZ + sz * node.qMinZ[i]);
-            cb.pMax = v3(node.minX + sx * node.qMaxX[i], node.minY + sy * node.qMaxY[i], node.minZ + sz * node.qMaxZ[i]);
-            if (sphereNodeCheckD(ray_o, inv_d, hit_t, r, cb)) {
+            const float bnx = (node.minX + sx * qb(nearX, i)) + nrX;
+            const float bny = (node.minY + sy * qb(nearY, i)) + nrY;
+            const float bnz = (node.minZ + sz * qb(nearZ, i)) + nrZ;
+            const float bfx = (node.minX + sx * qb(farX, i)) - nrX;
+            const float bfy = (node.minY + sy * qb(farY, i)) - nrY;
+            const float bfz = (node.minZ + sz * qb(farZ, i)) - nrZ;
+            const float i_min_x = (bnx - ray_o.x) * inv_d.x, i_max_x = (bfx - ray_o.x) * inv_d.x;
+            const float i_min_y = (bny - ray_o.y) * inv_d.y, i_max_y = (bfy - ray_o.y) * inv_d.y;
+            const float i_min_z = (bnz - ray_o.z) * inv_d.z, i_max_z = (bfz - ray_o.z) * inv_d.z;
+            const float t_lo = fmax_(fmax_(fmax_(0.f, i_min_x), i_min_y), i_min_z);
+            const float t_hi = fmin_(fmin_(fmin_(hit_t, i_max_x), i_max_y), i_max_z);
+            if (t_lo < t_hi) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;
-                    const int ntri = node.triSize[i];
+                    const int ntri = (int)((tri_size >> (8 * i)) & 0xffu);
                     Vec3 leaf_n = v3(0.f, 0.f, 0.f);
                     float leaf_t = hit_t;
                     for (int k = 0; k < ntri; k++) {
