@@ -206,6 +206,93 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
     bsPush(st, 0);
+#ifdef MPENV_TRAV_FLAT
+    while (st.n > 0) {
+        const uint32_t node_idx = bsPop(st);
+        const NodeR node = loadNode(b, node_idx);
+        const float dirQuantX = expScaleD(node.expX) * rayXInv;
+        const float dirQuantY = expScaleD(node.expY) * rayYInv;
+        const float dirQuantZ = expScaleD(node.expZ) * rayZInv;
+        const float originQuantX = (node.minX - ray_o.x) * rayXInv;
+        const float originQuantY = (node.minY - ray_o.y) * rayYInv;
+        const float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
+        const uint32_t nearX = negX ? node.qMaxX : node.qMinX, farX = negX ? node.qMinX : node.qMaxX;
+        const uint32_t nearY = negY ? node.qMaxY : node.qMinY, farY = negY ? node.qMinY : node.qMaxY;
+        const uint32_t nearZ = negZ ? node.qMaxZ : node.qMinZ, farZ = negZ ? node.qMinZ : node.qMaxZ;
+        // Slab intervals of the four children without the t_max clamp (the
+        // clamp is applied when the child's turn comes, with the t_max the
+        // reference would hold then: leaves of lower slots may have shrunk it).
+        float tn0, tn1, tn2, tn3, tf0, tf1, tf2, tf3;
+        uint32_t leafBits = 0, intBits = 0;
+#define MP_SLAB(i, TN, TF)                                                                    \
+    {                                                                                         \
+        const float t_near_x = fma_(qb(nearX, i), dirQuantX, originQuantX);                  \
+        const float t_near_y = fma_(qb(nearY, i), dirQuantY, originQuantY);                  \
+        const float t_near_z = fma_(qb(nearZ, i), dirQuantZ, originQuantZ);                  \
+        const float t_far_x = fma_(qb(farX, i), dirQuantX, originQuantX);                    \
+        const float t_far_y = fma_(qb(farY, i), dirQuantY, originQuantY);                    \
+        const float t_far_z = fma_(qb(farZ, i), dirQuantZ, originQuantZ);                    \
+        TN = fmax_(fmax_(t_near_x, t_near_y), fmax_(t_near_z, 0.f));                        \
+        TF = fmin_(fmin_(t_far_x, t_far_y), t_far_z);                                        \
+        const int32_t child = node.child[i];                                                 \
+        if (child != -1 && TN <= fmin_(TF, t_max)) {                                         \
+            if (child & 0x80000000) leafBits |= 1u << i;                                     \
+            else intBits |= 1u << i;                                                         \
+        }                                                                                     \
+    }
+        MP_SLAB(0, tn0, tf0)
+        MP_SLAB(1, tn1, tf1)
+        MP_SLAB(2, tn2, tf2)
+        MP_SLAB(3, tn3, tf3)
+#undef MP_SLAB
+        // register selects (a dynamically indexed array would live in scratch)
+        auto pickF = [&](int k, float v0, float v1, float v2, float v3) {
+            return k == 0 ? v0 : (k == 1 ? v1 : (k == 2 ? v2 : v3));
+        };
+        auto pickI = [&](int k) {
+            return k == 0 ? node.child[0] : (k == 1 ? node.child[1] : (k == 2 ? node.child[2] : node.child[3]));
+        };
+        auto passes = [&](int k) {
+            return pickF(k, tn0, tn1, tn2, tn3) <= fmin_(pickF(k, tf0, tf1, tf2, tf3), t_max);
+        };
+        // Leaf triangles, one per iteration, lanes sharing the test whatever
+        // slot their leaf sits in (the per-slot unrolled form runs the test
+        // once per slot any lane needs).  Internal children below the leaf's
+        // slot are pushed first, in slot order, as the reference does.
+        int cur = 0, end = 0;
+        for (;;) {
+            if (cur == end) {
+                if (leafBits == 0) break;
+                const int j = __builtin_ctz(leafBits);
+                leafBits &= leafBits - 1;
+                uint32_t below = intBits & ((1u << j) - 1u);
+                intBits &= ~below;
+                while (below) {
+                    const int k = __builtin_ctz(below);
+                    below &= below - 1;
+                    if (passes(k)) bsPush(st, (uint32_t)pickI(k));
+                }
+                if (!passes(j)) continue;
+                cur = pickI(j) & 0x7fffffff;
+                end = cur + (int)((node.triSize >> (8 * j)) & 0xffu);
+                if (cur == end) continue;
+            }
+            Vec3 a, bb, c;
+            loadTri(b, cur, a, bb, c);
+            float hit_t;
+            if (rayTri(a, bb, c, tx, ray_o, t_max, hit_t)) {
+                ray_hit = true;
+                t_max = hit_t;
+            }
+            cur++;
+        }
+        while (intBits) {
+            const int k = __builtin_ctz(intBits);
+            intBits &= intBits - 1;
+            if (passes(k)) bsPush(st, (uint32_t)pickI(k));
+        }
+    }
+#else
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
         const NodeR node = loadNode(b, node_idx);
@@ -260,6 +347,7 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
             }
         }
     }
+#endif
     t_out = t_max;
     return ray_hit;
 }

@@ -74,20 +74,52 @@ def time_one(name, worlds=16384, team=6, warm=30, steps=100):
         lib.mpenv_copy_actions(h, C.c_void_p(dptr.value + (s % 16) * per), None)
         lib.mpenv_step(h)
 
+    lib.mpenv_set_world_groups.argtypes = [C.c_void_p, C.c_int32]
     for s in range(warm):
         step(s)
-    lib.mpenv_enable_kernel_timing(h, 1)
+    # step time with the default world groups, no timing hooks
+    hip.hipDeviceSynchronize()
     t0 = time.perf_counter()
     for s in range(steps):
         step(warm + s)
+    hip.hipDeviceSynchronize()
+    el_groups = time.perf_counter() - t0
+    # per-kernel times with one group (kernels alone on the GPU)
+    lib.mpenv_set_world_groups(h, 1)
+    for s in range(5):
+        step(warm + steps + s)
+    lib.mpenv_enable_kernel_timing(h, 1)
+    hip.hipDeviceSynchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step(warm + steps + 5 + s)
+    hip.hipDeviceSynchronize()
     el = time.perf_counter() - t0
     names = (C.c_char_p * 16)()
     ms = (C.c_float * 16)()
     ln = (C.c_int32 * 16)()
     n = lib.mpenv_kernel_timings(h, 16, names, ms, ln)
     res = {names[i].decode(): round(ms[i], 4) for i in range(n)}
-    print(json.dumps({"variant": name, "ms_per_step": round(1e3 * el / steps, 4), "kernels": res}),
-          flush=True)
+    # Output digest: variants that keep the arithmetic must agree bit-for-bit.
+    import hashlib
+
+    lib.mpenv_export_tensor.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+    hip.hipDeviceSynchronize()
+    dig = hashlib.sha1()
+    for eid in (6, 10, 12, 13, 18, 19, 20, 23, 24, 65, 66, 67):
+        p, dt, nd, gid = C.c_void_p(), C.c_int32(), C.c_int32(), C.c_int32()
+        dims = (C.c_int64 * 8)()
+        assert lib.mpenv_export_tensor(h, eid, C.byref(p), C.byref(dt), C.byref(nd), dims, C.byref(gid)) == 0
+        nbytes = 4
+        for i in range(nd.value):
+            nbytes *= dims[i]
+        buf = (C.c_char * nbytes)()
+        assert hip.hipMemcpy(buf, p, C.c_size_t(nbytes), 2) == 0
+        dig.update(bytes(buf))
+    print(json.dumps({"variant": name, "ms_per_step": round(1e3 * el_groups / steps, 4),
+                      "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
+                      "digest": dig.hexdigest()[:16]}), flush=True)
 
 
 if __name__ == "__main__":
