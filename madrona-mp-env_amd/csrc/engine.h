@@ -152,6 +152,11 @@ struct GoalRegionDev {
 struct SceneDev {
     const BVHNode *nodes;
     const float *verts;     // 3 floats per vertex, 3 vertices per triangle
+    // Per triangle, ray-independent terms of sphereCastTriangle
+    // (mesh_bvh.inl:885-1127): unit normal xyz, |normal|, |e01|^2, |e02|^2,
+    // |e12|^2, 0 -- computed on the host with the same mpenv_core.h
+    // expressions the traversal would evaluate (bit-identical).
+    const float *triPre;
     int32_t numNodes;
     int32_t numVerts;
     mp::AABB worldBounds;
@@ -197,6 +202,7 @@ enum KernelId { kKMove = 0, kKSim = 1, kKVis = 2, kKObs = 3, kKLidar = 4, kNumTi
 
 const char *kernelName(int k);
 size_t bvhLdsBytes(const SceneDev &sc);
+size_t bvhLdsBytesSphere(const SceneDev &sc); // + triPre (sphere-casting kernels)
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t ctor_train_ctrl[3], void *stream);
 int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream);

@@ -25,6 +25,7 @@ namespace mpenv {
 struct LBVH {
     const MP_LDS BVHNode *nodes;
     const MP_LDS float *verts;
+    const MP_LDS float *pre; // sphere-casting kernels only (stageBVHSphere)
 };
 
 // Byte stack: push shifts left by 8 across a 128-bit register pair.
@@ -66,6 +67,21 @@ __device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc)
     LBVH b;
     b.nodes = (const MP_LDS BVHNode *)(smem);
     b.verts = (const MP_LDS float *)(smem + (size_t)node_q * 16);
+    b.pre = nullptr;
+    return b;
+}
+
+// stageBVH plus the per-triangle sphere-cast constants (SceneDev::triPre,
+// two float4 per triangle) after the vertices.
+__device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
+{
+    const size_t pre_off = (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16;
+    const int pre_q = (sc.numVerts / 3) * 2;
+    const float4 *src_p = reinterpret_cast<const float4 *>(sc.triPre);
+    float4 *dst_p = reinterpret_cast<float4 *>(smem + pre_off);
+    for (int k = threadIdx.x; k < pre_q; k += blockDim.x) dst_p[k] = src_p[k];
+    LBVH b = stageBVH(smem, sc); // ends with __syncthreads
+    b.pre = (const MP_LDS float *)(smem + pre_off);
     return b;
 }
 
@@ -206,93 +222,6 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
     bsPush(st, 0);
-#ifdef MPENV_TRAV_FLAT
-    while (st.n > 0) {
-        const uint32_t node_idx = bsPop(st);
-        const NodeR node = loadNode(b, node_idx);
-        const float dirQuantX = expScaleD(node.expX) * rayXInv;
-        const float dirQuantY = expScaleD(node.expY) * rayYInv;
-        const float dirQuantZ = expScaleD(node.expZ) * rayZInv;
-        const float originQuantX = (node.minX - ray_o.x) * rayXInv;
-        const float originQuantY = (node.minY - ray_o.y) * rayYInv;
-        const float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
-        const uint32_t nearX = negX ? node.qMaxX : node.qMinX, farX = negX ? node.qMinX : node.qMaxX;
-        const uint32_t nearY = negY ? node.qMaxY : node.qMinY, farY = negY ? node.qMinY : node.qMaxY;
-        const uint32_t nearZ = negZ ? node.qMaxZ : node.qMinZ, farZ = negZ ? node.qMinZ : node.qMaxZ;
-        // Slab intervals of the four children without the t_max clamp (the
-        // clamp is applied when the child's turn comes, with the t_max the
-        // reference would hold then: leaves of lower slots may have shrunk it).
-        float tn0, tn1, tn2, tn3, tf0, tf1, tf2, tf3;
-        uint32_t leafBits = 0, intBits = 0;
-#define MP_SLAB(i, TN, TF)                                                                    \
-    {                                                                                         \
-        const float t_near_x = fma_(qb(nearX, i), dirQuantX, originQuantX);                  \
-        const float t_near_y = fma_(qb(nearY, i), dirQuantY, originQuantY);                  \
-        const float t_near_z = fma_(qb(nearZ, i), dirQuantZ, originQuantZ);                  \
-        const float t_far_x = fma_(qb(farX, i), dirQuantX, originQuantX);                    \
-        const float t_far_y = fma_(qb(farY, i), dirQuantY, originQuantY);                    \
-        const float t_far_z = fma_(qb(farZ, i), dirQuantZ, originQuantZ);                    \
-        TN = fmax_(fmax_(t_near_x, t_near_y), fmax_(t_near_z, 0.f));                        \
-        TF = fmin_(fmin_(t_far_x, t_far_y), t_far_z);                                        \
-        const int32_t child = node.child[i];                                                 \
-        if (child != -1 && TN <= fmin_(TF, t_max)) {                                         \
-            if (child & 0x80000000) leafBits |= 1u << i;                                     \
-            else intBits |= 1u << i;                                                         \
-        }                                                                                     \
-    }
-        MP_SLAB(0, tn0, tf0)
-        MP_SLAB(1, tn1, tf1)
-        MP_SLAB(2, tn2, tf2)
-        MP_SLAB(3, tn3, tf3)
-#undef MP_SLAB
-        // register selects (a dynamically indexed array would live in scratch)
-        auto pickF = [&](int k, float v0, float v1, float v2, float v3) {
-            return k == 0 ? v0 : (k == 1 ? v1 : (k == 2 ? v2 : v3));
-        };
-        auto pickI = [&](int k) {
-            return k == 0 ? node.child[0] : (k == 1 ? node.child[1] : (k == 2 ? node.child[2] : node.child[3]));
-        };
-        auto passes = [&](int k) {
-            return pickF(k, tn0, tn1, tn2, tn3) <= fmin_(pickF(k, tf0, tf1, tf2, tf3), t_max);
-        };
-        // Leaf triangles, one per iteration, lanes sharing the test whatever
-        // slot their leaf sits in (the per-slot unrolled form runs the test
-        // once per slot any lane needs).  Internal children below the leaf's
-        // slot are pushed first, in slot order, as the reference does.
-        int cur = 0, end = 0;
-        for (;;) {
-            if (cur == end) {
-                if (leafBits == 0) break;
-                const int j = __builtin_ctz(leafBits);
-                leafBits &= leafBits - 1;
-                uint32_t below = intBits & ((1u << j) - 1u);
-                intBits &= ~below;
-                while (below) {
-                    const int k = __builtin_ctz(below);
-                    below &= below - 1;
-                    if (passes(k)) bsPush(st, (uint32_t)pickI(k));
-                }
-                if (!passes(j)) continue;
-                cur = pickI(j) & 0x7fffffff;
-                end = cur + (int)((node.triSize >> (8 * j)) & 0xffu);
-                if (cur == end) continue;
-            }
-            Vec3 a, bb, c;
-            loadTri(b, cur, a, bb, c);
-            float hit_t;
-            if (rayTri(a, bb, c, tx, ray_o, t_max, hit_t)) {
-                ray_hit = true;
-                t_max = hit_t;
-            }
-            cur++;
-        }
-        while (intBits) {
-            const int k = __builtin_ctz(intBits);
-            intBits &= intBits - 1;
-            if (passes(k)) bsPush(st, (uint32_t)pickI(k));
-        }
-    }
-#else
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
         const NodeR node = loadNode(b, node_idx);
@@ -347,7 +276,6 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
             }
         }
     }
-#endif
     t_out = t_max;
     return ray_hit;
 }
@@ -390,15 +318,16 @@ __device__ __forceinline__ bool sphereNodeCheckD(mp::Vec3 o, mp::Vec3 inv_d, flo
 }
 
 // mesh_bvh.inl:885-1127 (same quirks as the oracle restatement)
-__device__ __forceinline__ float sphereTriD(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, mp::Vec3 ray_o, mp::Vec3 ray_d,
-                                            float t_max, float r, mp::Vec3 &out_n)
+// pre: unit normal, |normal|, squared edge lengths (SceneDev::triPre) --
+// the ray-independent subexpressions, same bits as computing them here.
+__device__ __forceinline__ float sphereTriD(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, float4 pre0, float4 pre1,
+                                            mp::Vec3 ray_o, mp::Vec3 ray_d, float t_max, float r, mp::Vec3 &out_n)
 {
     using namespace mp;
     const Vec3 e01 = tb - ta, e02 = tc - ta, e12 = tc - tb;
     const Vec3 v0 = ta - ray_o, v1 = tb - ray_o, v2 = tc - ray_o;
-    Vec3 nu = computeTriangleGeoNormal(e01, e02, e12);
-    float n_len = length(nu);
-    Vec3 n = nu / n_len;
+    const float n_len = pre0.w;
+    const Vec3 n = v3(pre0.x, pre0.y, pre0.z);
     const float n_dot_d = dot(n, ray_d);
     const float r2 = r * r;
 
@@ -437,6 +366,7 @@ __device__ __forceinline__ float sphereTriD(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 t
     {
         const Vec3 axes[3] = { e01, e02, e12 };
         const Vec3 bases[3] = { v0, v0, v1 };
+        const float alen2[3] = { pre1.x, pre1.y, pre1.z };
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             Vec3 axis = axes[k];
@@ -445,7 +375,7 @@ __device__ __forceinline__ float sphereTriD(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 t
             const float d_dot_a = dot(ray_d, axis);
             const float e_dot_a = s_dot_a + d_dot_a;
             if (s_dot_a < 0.0f && e_dot_a < 0.0f) continue;
-            const float a_len2 = length2(axis);
+            const float a_len2 = alen2[k];
             if (s_dot_a > a_len2 && e_dot_a > a_len2) continue;
             float a = a_len2 * d_len2 - d_dot_a * d_dot_a;
             if (fabs_(a) < edge_eps) continue;
@@ -550,7 +480,10 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
                     for (int k = 0; k < ntri; k++) {
                         Vec3 a, bb, c;
                         loadTri(b, leaf + k, a, bb, c);
-                        leaf_t = sphereTriD(a, bb, c, ray_o, ray_d, leaf_t, r, leaf_n);
+                        const MP_LDS lf4 *pp = reinterpret_cast<const MP_LDS lf4 *>(b.pre) + 2 * (leaf + k);
+                        const lf4 p0 = pp[0], p1 = pp[1];
+                        leaf_t = sphereTriD(a, bb, c, make_float4(p0.x, p0.y, p0.z, p0.w),
+                                            make_float4(p1.x, p1.y, p1.z, p1.w), ray_o, ray_d, leaf_t, r, leaf_n);
                     }
                     if (leaf_t < hit_t) {
                         hit_t = leaf_t;

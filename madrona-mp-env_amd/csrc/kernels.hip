@@ -1772,10 +1772,13 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 // Step graph part 1 (sim.cpp:5299-5320 up to updateMoveStatePostFall): the
 // per-agent systems, which read no other agent's state.  Lane = agent, no
 // barriers, so sphere-cast latency overlaps across the whole grid.
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) k_move(DevState S, SceneDev sc)
+#ifndef MPENV_MOVE_WPE
+#define MPENV_MOVE_WPE 3
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPENV_MOVE_WPE))) k_move(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const LBVH bvh = stageBVH(smem, sc);
+    const LBVH bvh = stageBVHSphere(smem, sc);
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= S.A) return;
     planAStarD(S, sc, g);
@@ -2597,6 +2600,7 @@ const char *kernelName(int k)
 }
 
 size_t bvhLdsBytes(const SceneDev &sc) { return (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16; }
+size_t bvhLdsBytesSphere(const SceneDev &sc) { return bvhLdsBytes(sc) + (size_t)(sc.numVerts / 3) * 32; }
 
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
@@ -2618,7 +2622,7 @@ int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream)
 
 int launchMove(const DevState &s, const SceneDev &sc, void *stream)
 {
-    hipLaunchKernelGGL(k_move, dim3((unsigned)((s.A + kBlock - 1) / kBlock)), dim3(kBlock), bvhLdsBytes(sc),
+    hipLaunchKernelGGL(k_move, dim3((unsigned)((s.A + kBlock - 1) / kBlock)), dim3(kBlock), bvhLdsBytesSphere(sc),
                        (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }

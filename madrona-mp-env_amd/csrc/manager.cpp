@@ -416,6 +416,24 @@ static void buildSceneDev(mpenv_manager &m)
         sc.astar = d_astar;
         sc.numNavTris = (int32_t)T;
     }
+    {
+        // sphere-cast triangle constants (geom_dev.h sphereTriD)
+        const size_t nt = s.bvhVerts.size() / 3;
+        std::vector<float> pre(std::max<size_t>(nt, 1) * 8, 0.f);
+        for (size_t t = 0; t < nt; t++) {
+            const mp::Vec3 a = s.bvhVerts[3 * t], b = s.bvhVerts[3 * t + 1], c = s.bvhVerts[3 * t + 2];
+            const mp::Vec3 e01 = b - a, e02 = c - a, e12 = c - b;
+            const mp::Vec3 nu = mp::computeTriangleGeoNormal(e01, e02, e12);
+            const float n_len = mp::length(nu);
+            const mp::Vec3 n = nu / n_len;
+            float *o = &pre[8 * t];
+            o[0] = n.x; o[1] = n.y; o[2] = n.z; o[3] = n_len;
+            o[4] = mp::length2(e01); o[5] = mp::length2(e02); o[6] = mp::length2(e12); o[7] = 0.f;
+        }
+        float *d_pre = m.alloc<float>(pre.size());
+        m.upload(d_pre, pre.data(), sizeof(float) * pre.size());
+        sc.triPre = d_pre;
+    }
     sc.nodes = d_nodes;
     sc.verts = d_verts;
     sc.numNodes = (int32_t)s.nodes.size();
