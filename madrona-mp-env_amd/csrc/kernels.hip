@@ -2463,12 +2463,6 @@ __global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, Scen
         ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
         const float2 cs = fan[fwd ? x : 32 + x];
         Vec3 dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
-        float4 *dst = fwd ? reinterpret_cast<float4 *>(S.fwdLidar) + (int64_t)g * kFwdRays + kk
-                          : reinterpret_cast<float4 *>(S.rearLidar) + (int64_t)g * kRearRays + kk;
-        // fullTeamObservationsSystem copies the lidar before this system
-        // overwrites it (sim.cpp:5283-5310): the previous value moves into
-        // the team interface's slot.  Loaded here so the traversal hides it.
-        const float4 prev = *dst;
         WorldHit hw = traceWorldD(bvh, S.px, S.py, S.pz, g0, (int)N, ray_o, dir);
         const bool second = i >= T; // team of the casting agent
         float4 out;
@@ -2479,9 +2473,17 @@ __global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, Scen
         } else {
             out = make_float4(-1.f, 0.f, 0.f, 0.f);
         }
+        // Addresses formed after the traversal (nothing but the ray lives
+        // across it, so 64 VGPRs hold the loop without scratch spills).
+        float4 *dst = fwd ? reinterpret_cast<float4 *>(S.fwdLidar) + (int64_t)g * kFwdRays + kk
+                          : reinterpret_cast<float4 *>(S.rearLidar) + (int64_t)g * kRearRays + kk;
         const int64_t slot = ((int64_t)w * 2 + (second ? 1 : 0)) * kMaxTeamSize + (second ? i - T : i);
         float4 *tdst = fwd ? reinterpret_cast<float4 *>(S.ftFwdLidar) + slot * kFwdRays + kk
                            : reinterpret_cast<float4 *>(S.ftRearLidar) + slot * kRearRays + kk;
+        // fullTeamObservationsSystem copies the lidar before this system
+        // overwrites it (sim.cpp:5283-5310): the previous value moves into
+        // the team interface's slot.
+        const float4 prev = *dst;
         *tdst = prev;
         *dst = out;
     }
