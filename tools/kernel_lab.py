@@ -44,7 +44,7 @@ def build(name, defines):
     print("built", name, defines)
 
 
-def time_one(name, worlds=16384, team=6, warm=30, steps=100):
+def time_one(name, worlds=16384, team=6, warm=30, steps=100, label=None):
     import mpenv_testlib as T
 
     path = os.path.join(LAB, name, "libmpenv.so") if name != "main" else os.path.join(PKG, "libmpenv.so")
@@ -117,7 +117,7 @@ def time_one(name, worlds=16384, team=6, warm=30, steps=100):
         buf = (C.c_char * nbytes)()
         assert hip.hipMemcpy(buf, p, C.c_size_t(nbytes), 2) == 0
         dig.update(bytes(buf))
-    print(json.dumps({"variant": name, "ms_per_step": round(1e3 * el_groups / steps, 4),
+    print(json.dumps({"variant": label or name, "ms_per_step": round(1e3 * el_groups / steps, 4),
                       "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
                       "digest": dig.hexdigest()[:16]}), flush=True)
 
@@ -126,7 +126,13 @@ if __name__ == "__main__":
     if sys.argv[1] == "build":
         build(sys.argv[2], sys.argv[3:])
     elif sys.argv[1] == "run":
-        for name in sys.argv[2:]:
-            subprocess.run([sys.executable, __file__, "_one", name], check=True)
+        for spec in sys.argv[2:]:
+            # NAME[@ENV=VAL,ENV=VAL]: a variant library plus runtime settings
+            name, _, envs = spec.partition("@")
+            env = dict(os.environ)
+            for kv in filter(None, envs.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
+            subprocess.run([sys.executable, __file__, "_one", name, spec], check=True, env=env)
     elif sys.argv[1] == "_one":
-        time_one(sys.argv[2])
+        time_one(sys.argv[2], label=sys.argv[3] if len(sys.argv) > 3 else None)
