@@ -309,6 +309,18 @@ def main():
             "frac": round(ibytes / (iso[idom][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "kernels_ms": {k: round(v[0], 4) for k, v in iso.items()},
         }
+        # the bound that applies to the ray kernels: VALU issue.  The PMC
+        # count is per launch of the profiled (default-groups) run, so one
+        # step's instructions are that x launches per step.
+        ivalu = prof.get("valu_insts_per_launch", {}).get(idom)
+        if ivalu:
+            per_step = ivalu * lps
+            result["roofline_isolated"]["valu_issue"] = {
+                "insts_per_step": per_step,
+                "achieved_per_s": round(per_step / (iso[idom][0] * 1e-3), 1),
+                "peak_per_s": VALU_PEAK,
+                "frac": round(per_step / (iso[idom][0] * 1e-3) / VALU_PEAK, 4),
+            }
     if rank == 0 and world_size == 1 and args.cpu_baseline == "auto":
         result["cpu_baseline"] = cpu_baseline(args, world_size)
     if rank == 0:

@@ -66,6 +66,7 @@ enum : int32_t {
 
 struct DevState {
     int32_t W, N, T;
+    uint32_t nMagic;       // ceil(2^32 / N): g / N = umulhi(g, nMagic) for g < 2^32 / N^2
     int64_t A;
     int64_t dmgStride;     // row stride of dmg (all agents of the manager)
 

@@ -2441,17 +2441,22 @@ __global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, Scen
     const uint32_t N = (uint32_t)S.N, T = (uint32_t)S.T;
     const uint32_t A = (uint32_t)S.A;
     const uint32_t ntasks = (uint32_t)lidarTasks(S.A);
-    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int it = 0; it < kLidarIters; it++) {
         const uint32_t task = (blockIdx.x * kLidarIters + it) * kLidarWaves + wave; // wave-uniform
         if (task >= ntasks) break;
+        // Lane id read inside the loop (volatile: not hoisted), so the
+        // lane-derived offsets are formed per task instead of living as
+        // loop invariants across the traversal, which at 64 VGPRs the
+        // compiler would spill to scratch.
+        uint32_t lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         const uint32_t unit = task / 5u, sub = task - unit * 5u;
         const bool fwd = sub < 4u;
         const uint32_t g = unit * 4u + (fwd ? sub : (lane >> 4));
         if (g >= A) continue;
         const uint32_t kk = fwd ? lane : (lane & 15u); // ray slot within the forward / rear fan
-        const uint32_t w = g / N;
+        const uint32_t w = __umulhi(g, S.nMagic); // g / N (engine.h)
         const uint32_t i = g - w * N;
         const int64_t g0 = (int64_t)w * N;
         const uint32_t h = fwd ? (kk >> 5) : (kk >> 3), x = fwd ? (kk & 31u) : (kk & 7u);

@@ -770,6 +770,9 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m->S.T = (int32_t)cfg->team_size;
         m->S.N = 2 * m->S.T;
         m->S.A = (int64_t)m->S.W * m->S.N;
+        m->S.nMagic = (uint32_t)((0x100000000ull + (uint64_t)m->S.N - 1) / (uint64_t)m->S.N);
+        if ((uint64_t)m->S.A * (uint64_t)m->S.N * (uint64_t)m->S.N >= 0x100000000ull)
+            throw std::runtime_error("mpenv: num_worlds too large for one device (agent index division)");
         allocState(*m);
         openLogs(*m, cfg);
         // the caller's path strings are not kept past create
