@@ -2277,10 +2277,45 @@ __device__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int6
 
 // pvpOpponentMasksSystem (sim.cpp:2562-2614) + pvpObservationsSystem
 // (sim.cpp:2645-3052).  Lane = agent.
+//
+// Teammate / opponent observation rows ([A][slots][32] f32, 128 B each) leave
+// through LDS: written straight from the lane, one store instruction would
+// put a 16-byte piece into each of 64 rows (64 partial lines for the L2 to
+// merge); transposed per wave, each instruction writes 8 whole rows.
+constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
+
+__device__ __forceinline__ void storeRowsWave(float *arr, int slots, int k, const float *row, int64_t gw0, int64_t A,
+                                              float *buf, int lane)
+{
+    float4 *mine = reinterpret_cast<float4 *>(buf + lane * kObsRowPad);
+#pragma unroll
+    for (int q = 0; q < kOtherObs / 4; q++)
+        mine[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+    // the wave's own LDS writes, then reads of other lanes' rows: a
+    // wavefront-scope fence emits nothing and does not keep the compiler
+    // from moving LDS accesses across it, so drain the LDS counter behind a
+    // compiler memory barrier instead
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the wave's m live lanes (a tail wave's lanes past A have returned)
+    // share its m rows x 8 chunks
+    const int m = (int)(A - gw0 < 64 ? A - gw0 : 64);
+#pragma unroll
+    for (int j = 0; j < kOtherObs / 4; j++) {
+        const int c = lane + j * m, r = c >> 3, col = c & 7;
+        reinterpret_cast<float4 *>(arr + ((gw0 + r) * slots + k) * kOtherObs)[col] =
+            reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // reads done before the next rows land
+}
+
 __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
 {
+    __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsRowPad];
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= S.A) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t gw0 = g - lane; // first agent of the wave
+    float *wbuf = rowBuf[threadIdx.x >> 6];
+    if (g >= S.A) return; // the tail wave's lanes past A (storeRowsWave counts the live ones)
     const int T = S.T, N = S.N;
     const int w = (int)(g / N);
     const int i = (int)(g - (int64_t)w * N);
@@ -2305,6 +2340,11 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
         if (S.firedT[go] >= 0) mask[k] = 1.f;
     }
     storeVec(&S.masks[g * 6], mask, 6);
+    // mask[k] == 1 as bits for the opponent loop: reading the float array
+    // there was miscompiled (hipcc, ROCm 7.2) once the row export went
+    // through LDS -- wrong last-known updates on the 2v2 navmesh golden case.
+    uint32_t knowsBits = 0;
+    for (int k = 0; k < kMaxTeamSize; k++) knowsBits |= (mask[k] == 1.f ? 1u : 0u) << k;
 
     // ---- observations
     const int cur_step = S.curStep[w];
@@ -2359,7 +2399,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
                 fillCombatD(S, gj, &tob[28]);
             }
         }
-        storeVec(&S.tmObs[(g * 5 + k) * kOtherObs], tob, kOtherObs);
+        storeRowsWave(S.tmObs, 5, k, tob, gw0, S.A, wbuf, lane);
         storeVec(&S.tmPos[(g * 5 + k) * 3], tpos, 3);
     }
 
@@ -2385,7 +2425,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
                 oob[28] = (float)S.wasShot[gj];
                 oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
                 oob[30] = ((vm[g] >> k) & 1) ? 1.f : 0.f;
-                const bool knows = mask[k] == 1.f;
+                const bool knows = (knowsBits >> k) & 1u;
                 oob[31] = knows ? 1.f : 0.f;
                 if (knows) {
                     storeVec(lk, oob, kOtherObs);
@@ -2393,7 +2433,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
                 }
             }
         }
-        storeVec(&S.oppObs[(g * 6 + k) * kOtherObs], oob, kOtherObs);
+        storeRowsWave(S.oppObs, 6, k, oob, gw0, S.A, wbuf, lane);
         storeVec(&S.oppPos[(g * 6 + k) * 3], opos, 3);
     }
 
