@@ -1797,8 +1797,9 @@ constexpr int kSimBlock = 128;
 
 __device__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
 
-// 4 waves/SIMD (128 VGPRs; the spills sit in the reset / spawn paths):
-// k_sim alone 0.196 -> 0.139 ms, and all of its waves resident at C3.
+// 4 waves/SIMD (128 VGPRs, at the price of ~420 B/lane of scratch spills):
+// k_sim alone 0.196 -> 0.139 ms -- every wave of a C3 launch resident,
+// which hides the per-world phases' latency better than the spills cost.
 #ifndef MPENV_SIM_WPE
 #define MPENV_SIM_WPE 4
 #endif
