@@ -46,6 +46,11 @@ def test_engine_matches_golden_fixture(path):
 LIVE = [
     # team_size, worlds, steps, sim_flags, ctrl, policy
     (1, 64, 300, 0, [0, 1, 1], "tape"),
+    # agent counts that are not a multiple of 4 / 64: k_lidar's 4-agent wave
+    # units and k_obs's per-wave row transpose end in a partial unit
+    (3, 7, 120, 0, [0, 1, 1], "tape"),
+    (1, 3, 120, 1, [0, 1, 1], "combat"),
+    (5, 13, 120, 1, [0, 1, 1], "combat"),
     (2, 32, 300, 0, [0, 1, 1], "tape"),
     (3, 16, 300, 0, [0, 1, 1], "tape"),
     (6, 16, 300, 0, [0, 1, 1], "tape"),
