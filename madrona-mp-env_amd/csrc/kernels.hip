@@ -2454,8 +2454,10 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
 // Against 64 consecutive rays of the flat [agent][80] order (which straddle
 // two agents in 4 of 5 waves) this cuts the wave-lockstep node iterations by
 // ~12% and triangle tests by ~19% (tools/trav_stats.cpp on recorded rays);
-// every lane's arithmetic is unchanged.  A block's 4 waves take kLidarIters
-// consecutive task quads.
+// every lane's arithmetic is unchanged.  A block's 4 waves take `iters`
+// consecutive task quads: up to kLidarIters (amortises the BVH staging) on
+// big batches, fewer on small ones so the grid still spreads over the CUs
+// (at 64 worlds 1v1 a fixed 8 put the whole lidar on 5 CUs).
 constexpr int kLidarIters = 8;
 constexpr int kLidarWaves = kBlock / 64;
 
@@ -2468,7 +2470,7 @@ __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A +
 #endif
 #define MP_LIDAR_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_LIDAR_WPE)))
 
-__global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, SceneDev sc)
+__global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, SceneDev sc, int iters)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // Ray-fan directions (sim.cpp:3324-3506): theta depends only on the ray
@@ -2489,8 +2491,8 @@ __global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, Scen
     const uint32_t A = (uint32_t)S.A;
     const uint32_t ntasks = (uint32_t)lidarTasks(S.A);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int it = 0; it < kLidarIters; it++) {
-        const uint32_t task = (blockIdx.x * kLidarIters + it) * kLidarWaves + wave; // wave-uniform
+    for (int it = 0; it < iters; it++) {
+        const uint32_t task = (blockIdx.x * iters + it) * kLidarWaves + wave; // wave-uniform
         if (task >= ntasks) break;
         // Lane id read inside the loop (volatile: not hoisted), so the
         // lane-derived offsets are formed per task instead of living as
@@ -2676,7 +2678,12 @@ int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream)
 
 int launchMove(const DevState &s, const SceneDev &sc, void *stream)
 {
-    hipLaunchKernelGGL(k_move, dim3((unsigned)((s.A + kBlock - 1) / kBlock)), dim3(kBlock), bvhLdsBytesSphere(sc),
+    // Small batches: one-wave blocks, so the few waves spread over CUs
+    // instead of sharing a CU's SIMDs (k_move is latency-bound: 5-7
+    // dependent sphere casts per lane).  Big batches keep 256-thread blocks
+    // (the 24 KB LDS image per block would otherwise cap occupancy).
+    const int bs = s.A < (int64_t)kBlock * 256 ? 64 : kBlock;
+    hipLaunchKernelGGL(k_move, dim3((unsigned)((s.A + bs - 1) / bs)), dim3(bs), bvhLdsBytesSphere(sc),
                        (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }
@@ -2706,9 +2713,12 @@ int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
 
 int launchLidar(const DevState &s, const SceneDev &sc, void *stream)
 {
-    const int64_t per_block = (int64_t)kLidarWaves * kLidarIters;
-    const int blocks = (int)((lidarTasks(s.A) + per_block - 1) / per_block);
-    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
+    // ~1024 blocks before the iterations grow past 1
+    const int64_t tasks = lidarTasks(s.A);
+    const int iters = (int)std::max<int64_t>(1, std::min<int64_t>(kLidarIters, tasks / (kLidarWaves * 1024)));
+    const int64_t per_block = (int64_t)kLidarWaves * iters;
+    const int blocks = (int)((tasks + per_block - 1) / per_block);
+    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc, iters);
     return check(hipGetLastError());
 }
 
