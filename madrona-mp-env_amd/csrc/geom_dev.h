@@ -26,7 +26,13 @@ struct LBVH {
     const MP_LDS BVHNode *nodes;
     const MP_LDS float *verts;
     const MP_LDS float *pre; // sphere-casting kernels only (stageBVHSphere)
+    const MP_LDS float *snodes; // sphere-cast node image (stageBVHSphere), else null
 };
+
+__device__ __forceinline__ float expScaleD(int e) { return mp::u2f((uint32_t)(e + 127) << 23); }
+
+constexpr float kSphereR = 15.f;  // consts::agentRadius: the radius of every k_move sphere cast
+constexpr int kSNodeFloats = 32;  // sphere-cast node image: loR[3][4], hiR[3][4], children[4], triSize[4]
 
 // Byte stack: push shifts left by 8 across a 128-bit register pair.
 struct ByteStack {
@@ -68,6 +74,7 @@ __device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc)
     b.nodes = (const MP_LDS BVHNode *)(smem);
     b.verts = (const MP_LDS float *)(smem + (size_t)node_q * 16);
     b.pre = nullptr;
+    b.snodes = nullptr;
     return b;
 }
 
@@ -80,8 +87,35 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
     const float4 *src_p = reinterpret_cast<const float4 *>(sc.triPre);
     float4 *dst_p = reinterpret_cast<float4 *>(smem + pre_off);
     for (int k = threadIdx.x; k < pre_q; k += blockDim.x) dst_p[k] = src_p[k];
+    // Sphere-cast node image (kSNodeFloats per node): per axis a, the
+    // children's dequantised slab ends already widened by the cast radius,
+    // loR[a][i] = (min_a + 2^e_a * qMin_a[i]) - r and
+    // hiR[a][i] = (min_a + 2^e_a * qMax_a[i]) + r -- the very expressions
+    // sphereCastNodeCheck evaluates per child (mesh_bvh.inl:817-855) -- then
+    // the children and triangle counts.  Built for radius kSphereR (every
+    // k_move cast uses the agent radius).
+    const size_t sn_off = pre_off + (size_t)(sc.numVerts / 3) * 32;
+    float *sn = reinterpret_cast<float *>(smem + sn_off);
+    for (int k = threadIdx.x; k < sc.numNodes * 4; k += blockDim.x) {
+        const int n = k >> 2, i = k & 3;
+        const BVHNode &nd = sc.nodes[n];
+        float *o = sn + (size_t)n * kSNodeFloats;
+        const float mins[3] = { nd.minX, nd.minY, nd.minZ };
+        const int exps[3] = { nd.expX, nd.expY, nd.expZ };
+        const uint8_t *qmn[3] = { nd.qMinX, nd.qMinY, nd.qMinZ };
+        const uint8_t *qmx[3] = { nd.qMaxX, nd.qMaxY, nd.qMaxZ };
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const float sc_a = expScaleD(exps[a]);
+            o[a * 4 + i] = (mins[a] + sc_a * (float)qmn[a][i]) - kSphereR;
+            o[12 + a * 4 + i] = (mins[a] + sc_a * (float)qmx[a][i]) + kSphereR;
+        }
+        o[24 + i] = __int_as_float(nd.children[i]);
+        o[28 + i] = __uint_as_float((uint32_t)nd.triSize[i]);
+    }
     LBVH b = stageBVH(smem, sc); // ends with __syncthreads
     b.pre = (const MP_LDS float *)(smem + pre_off);
+    b.snodes = (const MP_LDS float *)(smem + sn_off);
     return b;
 }
 
@@ -196,7 +230,6 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
     return true;
 }
 
-__device__ __forceinline__ float expScaleD(int e) { return mp::u2f((uint32_t)(e + 127) << 23); }
 
 // MeshBVH::traceRay (mesh_bvh.inl:110-208) over the LDS-resident BVH.
 // Returns hit flag; *t_out = closest hit t when hit.
@@ -418,7 +451,8 @@ struct SphereHit {
     mp::Vec3 n; // valid only when t < FLT_MAX (the reference writes the normal only on a hit)
 };
 
-// MeshBVH::sphereCast (mesh_bvh.inl:743-815).
+// MeshBVH::sphereCast (mesh_bvh.inl:743-815).  r must be kSphereR: the
+// node image of stageBVHSphere carries slab ends widened by that radius.
 __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r)
 {
     using namespace mp;
@@ -442,39 +476,30 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
     // tie does not change the final t_min < t_max).
     const bool negX = __builtin_signbit(inv_d.x), negY = __builtin_signbit(inv_d.y),
                negZ = __builtin_signbit(inv_d.z);
-    const float nrX = negX ? r : -r, nrY = negY ? r : -r, nrZ = negZ ? r : -r;
+    // near / far ends per axis: loR or hiR of the pre-widened node image
+    // (stageBVHSphere), picked once per cast from the sign of inv_d
+    const int nX = negX ? 12 : 0, fX = negX ? 0 : 12;
+    const int nY = negY ? 16 : 4, fY = negY ? 4 : 16;
+    const int nZ = negZ ? 20 : 8, fZ = negZ ? 8 : 20;
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
     bsPush(st, 0);
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
-        const MP_LDS BVHNode &node = b.nodes[node_idx];
-        const MP_LDS uint32_t *qw = reinterpret_cast<const MP_LDS uint32_t *>(&node.triSize[0]);
-        // qw: [0] triSize, [1..3] qMin x/y/z, [4..6] qMax x/y/z
-        const float sx = expScaleD(node.expX), sy = expScaleD(node.expY), sz = expScaleD(node.expZ);
-        const uint32_t nearX = qw[negX ? 4 : 1], farX = qw[negX ? 1 : 4];
-        const uint32_t nearY = qw[negY ? 5 : 2], farY = qw[negY ? 2 : 5];
-        const uint32_t nearZ = qw[negZ ? 6 : 3], farZ = qw[negZ ? 3 : 6];
-        const uint32_t tri_size = qw[0];
+        const MP_LDS float *nd = b.snodes + node_idx * kSNodeFloats;
 #pragma unroll 1
         for (int i = 0; i < 4; i++) {
-            const int32_t child = node.children[i];
+            const int32_t child = __float_as_int(nd[24 + i]);
             if (child == -1) continue;
-            const float bnx = (node.minX + sx * qb(nearX, i)) + nrX;
-            const float bny = (node.minY + sy * qb(nearY, i)) + nrY;
-            const float bnz = (node.minZ + sz * qb(nearZ, i)) + nrZ;
-            const float bfx = (node.minX + sx * qb(farX, i)) - nrX;
-            const float bfy = (node.minY + sy * qb(farY, i)) - nrY;
-            const float bfz = (node.minZ + sz * qb(farZ, i)) - nrZ;
-            const float i_min_x = (bnx - ray_o.x) * inv_d.x, i_max_x = (bfx - ray_o.x) * inv_d.x;
-            const float i_min_y = (bny - ray_o.y) * inv_d.y, i_max_y = (bfy - ray_o.y) * inv_d.y;
-            const float i_min_z = (bnz - ray_o.z) * inv_d.z, i_max_z = (bfz - ray_o.z) * inv_d.z;
+            const float i_min_x = (nd[nX + i] - ray_o.x) * inv_d.x, i_max_x = (nd[fX + i] - ray_o.x) * inv_d.x;
+            const float i_min_y = (nd[nY + i] - ray_o.y) * inv_d.y, i_max_y = (nd[fY + i] - ray_o.y) * inv_d.y;
+            const float i_min_z = (nd[nZ + i] - ray_o.z) * inv_d.z, i_max_z = (nd[fZ + i] - ray_o.z) * inv_d.z;
             const float t_lo = fmax_(fmax_(fmax_(0.f, i_min_x), i_min_y), i_min_z);
             const float t_hi = fmin_(fmin_(fmin_(hit_t, i_max_x), i_max_y), i_max_z);
             if (t_lo < t_hi) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;
-                    const int ntri = (int)((tri_size >> (8 * i)) & 0xffu);
+                    const int ntri = (int)__float_as_uint(nd[28 + i]);
                     Vec3 leaf_n = v3(0.f, 0.f, 0.f);
                     float leaf_t = hit_t;
                     for (int k = 0; k < ntri; k++) {

@@ -2656,7 +2656,12 @@ const char *kernelName(int k)
 }
 
 size_t bvhLdsBytes(const SceneDev &sc) { return (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16; }
-size_t bvhLdsBytesSphere(const SceneDev &sc) { return bvhLdsBytes(sc) + (size_t)(sc.numVerts / 3) * 32; }
+static_assert(c::kAgentRadius == kSphereR, "k_move sphere casts use the agent radius (stageBVHSphere)");
+
+size_t bvhLdsBytesSphere(const SceneDev &sc)
+{
+    return bvhLdsBytes(sc) + (size_t)(sc.numVerts / 3) * 32 + (size_t)sc.numNodes * kSNodeFloats * 4;
+}
 
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
@@ -2678,11 +2683,11 @@ int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream)
 
 int launchMove(const DevState &s, const SceneDev &sc, void *stream)
 {
-    // Small batches: one-wave blocks, so the few waves spread over CUs
+    // Small batches (< 64 full blocks): one-wave blocks, so the few waves spread over CUs
     // instead of sharing a CU's SIMDs (k_move is latency-bound: 5-7
     // dependent sphere casts per lane).  Big batches keep 256-thread blocks
     // (the 24 KB LDS image per block would otherwise cap occupancy).
-    const int bs = s.A < (int64_t)kBlock * 256 ? 64 : kBlock;
+    const int bs = s.A < (int64_t)kBlock * 64 ? 64 : kBlock;
     hipLaunchKernelGGL(k_move, dim3((unsigned)((s.A + bs - 1) / bs)), dim3(bs), bvhLdsBytesSphere(sc),
                        (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
