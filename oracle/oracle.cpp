@@ -27,6 +27,13 @@
 // reference always reads 2, mesh_bvh.inl:867); ExploreTracker cells outside
 // the initialised quadrant start at 0; uninitialised locals (the first
 // slope-cast normal, sim.cpp:927) start at zero.
+//
+// Parity unpinned against the reference's own output bitstream: the
+// reference cannot be built here (Madrona, Embree, meshoptimizer absent) and
+// holds no tests or golden vectors for this path.  The restatement is pinned
+// instead to the reference's scene data fixtures (data/simple_map/*.bin),
+// closed-form ray / sphere-cast hits on that geometry, BVH-vs-brute-force
+// equality and the Threefry-2x32-20 known-answer vectors.
 #include "oracle.h"
 
 #include <algorithm>
