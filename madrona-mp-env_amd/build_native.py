@@ -38,8 +38,9 @@ def _stale(out, deps):
 
 
 def _run(cmd):
-    print("[build]", " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    # stderr: callers such as bench.py own stdout (one JSON line)
+    print("[build]", " ".join(cmd), file=sys.stderr, flush=True)
+    subprocess.run(cmd, check=True, stdout=sys.stderr)
 
 
 def build_lib(force=False):
