@@ -233,7 +233,11 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
 
 // MeshBVH::traceRay (mesh_bvh.inl:110-208) over the LDS-resident BVH.
 // Returns hit flag; *t_out = closest hit t when hit.
-__device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out)
+// t_max0 < FLT_MAX: only hits up to about t_max0 are sought (boxes entered
+// beyond it are pruned from the start); see visibleRayD for when that gives
+// the reference's answer.
+__device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
+                                             float t_max0 = mp::kFltMax)
 {
     using namespace mp;
     const float diveps = 0.0000001f;
@@ -250,7 +254,7 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     // values (mesh_bvh.inl:165-183).
     const bool negX = rayXInv < 0.f, negY = rayYInv < 0.f, negZ = rayZInv < 0.f;
 
-    float t_max = kFltMax;
+    float t_max = t_max0;
     bool ray_hit = false;
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
@@ -586,6 +590,55 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     h.t = min_t;
     h.entity = ent;
     return h;
+}
+
+// traceRayAgainstWorld(org, d).entity == target (utils.cpp:10-72, as
+// isAgentVisible uses it, utils.cpp:218) without the full closest-hit
+// search: the answer only depends on hits nearer than the target capsule's
+// t_c.  (1) t_c == 0 (missed / inside) -> the target can never be the
+// entity.  (2) The BVH search starts with t_max = t_c * 1.001: every
+// triangle with t <= 1.001 t_c is still found (its boxes are entered before
+// that bound; slab rounding is ~1e-7 relative) so the nearest hit is exact
+// whenever it can matter, and any other result is > t_c, which decides the
+// capsule loop exactly as the true nearest hit (also > t_c) would.
+// (3) The capsule loop then runs as in traceWorldD.
+__device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restrict__ px,
+                                            const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
+                                            int N, mp::Vec3 org, mp::Vec3 d, int target)
+{
+    using namespace mp;
+    Vec3 ct = v3(px[g0 + target], py[g0 + target], pz[g0 + target]);
+    ct.z += kCapsuleRadius;
+    const float t_c = intersectRayZOriginCapsule(org - ct, d, kCapsuleRadius, kCapsuleSegment);
+    if (t_c == 0) return false;
+    float min_t = kFltMax;
+    float tb;
+    if (bvhTraceRayD(b, org, d, tb, t_c * 1.001f)) min_t = tb;
+    int ent = -1;
+    const float dxy2 = d.x * d.x + d.y * d.y;
+    const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
+    for (int j = 0; j < N; j++) {
+        float t;
+        if (j == target) {
+            t = t_c;
+        } else {
+            Vec3 co = v3(px[g0 + j], py[g0 + j], pz[g0 + j]);
+            co.z += kCapsuleRadius;
+            const Vec3 tr = org - co;
+            // the conservative culls of traceWorldD (skip only exact misses)
+            const float cr = tr.x * d.y - tr.y * d.x;
+            if (cr * cr > cull_r2 * dxy2) continue;
+            const float ahead = -(tr.x * d.x + tr.y * d.y + tr.z * d.z) + fmaxD(0.f, kCapsuleSegment * d.z) +
+                                kCapsuleRadius * 1.01f;
+            if (ahead < 0.f) continue;
+            t = intersectRayZOriginCapsule(tr, d, kCapsuleRadius, kCapsuleSegment);
+        }
+        if (t != 0 && t < min_t) {
+            min_t = t;
+            ent = j;
+        }
+    }
+    return ent == target;
 }
 
 } // namespace mpenv

@@ -1957,8 +1957,7 @@ __device__ bool isAgentVisibleD(const DevState &S, const SceneDev &sc, const LBV
         const float len = length(to_test);
         if (len < c::kAgentRadius) continue;
         to_test = to_test / len;
-        WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, org, to_test);
-        if (h.hit && h.entity == target) return true;
+        if (visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target)) return true;
     }
     return false;
 }
@@ -2083,8 +2082,8 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
         const float len = length(to_test);
         to_test = to_test / len;
-        WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, org, to_test);
-        if (h.hit && h.entity == target) atomicOr(&masks[(int)(g - agent0)], 1u << k);
+        if (visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target))
+            atomicOr(&masks[(int)(g - agent0)], 1u << k);
     }
     __syncthreads();
 
