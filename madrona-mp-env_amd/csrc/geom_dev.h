@@ -575,9 +575,14 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
         // Behind the origin: the capsule's farthest point along d is at
         // dot(axis base - org, d) + max(0, h d.z) + r (|d| = 1); if that is
         // negative no t > 0 exists.  Same 1% radius margin.
-        const float ahead = -(tr.x * d.x + tr.y * d.y + tr.z * d.z) + fmaxD(0.f, kCapsuleSegment * d.z) +
-                            kCapsuleRadius * 1.01f;
+        const float along = -(tr.x * d.x + tr.y * d.y + tr.z * d.z);
+        const float ahead = along + fmaxD(0.f, kCapsuleSegment * d.z) + kCapsuleRadius * 1.01f;
         if (ahead < 0.f) continue;
+        // Beyond the nearest hit so far: every capsule point lies at least
+        // dot(axis base - org, d) + min(0, h d.z) - r along d, so an entering
+        // t can be no smaller (same 1% radius margin); the exact test could
+        // not pass `t < min_t`.
+        if (along + fminD(0.f, kCapsuleSegment * d.z) - kCapsuleRadius * 1.01f > min_t) continue;
         float t = intersectRayZOriginCapsule(tr, d, kCapsuleRadius, kCapsuleSegment);
         if (t != 0 && t < min_t) {
             min_t = t;
@@ -628,9 +633,10 @@ __device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restri
             // the conservative culls of traceWorldD (skip only exact misses)
             const float cr = tr.x * d.y - tr.y * d.x;
             if (cr * cr > cull_r2 * dxy2) continue;
-            const float ahead = -(tr.x * d.x + tr.y * d.y + tr.z * d.z) + fmaxD(0.f, kCapsuleSegment * d.z) +
-                                kCapsuleRadius * 1.01f;
+            const float along = -(tr.x * d.x + tr.y * d.y + tr.z * d.z);
+            const float ahead = along + fmaxD(0.f, kCapsuleSegment * d.z) + kCapsuleRadius * 1.01f;
             if (ahead < 0.f) continue;
+            if (along + fminD(0.f, kCapsuleSegment * d.z) - kCapsuleRadius * 1.01f > min_t) continue;
             t = intersectRayZOriginCapsule(tr, d, kCapsuleRadius, kCapsuleSegment);
         }
         if (t != 0 && t < min_t) {
