@@ -188,6 +188,9 @@ struct SceneDev {
     const mpenv_curriculum_snapshot *curriculum;
     int32_t numSnapshots;
     int32_t numNavTris;
+    // NearestNavTri of each zone's centroid (computed once at scene upload
+    // by k_zone_goals with the same device function planAStarD would run)
+    int32_t zoneGoalTri[kMaxZones];
     // logs (sim.cpp:4750-4843 record/replay, 23-106 + 4592-4634 events)
     int32_t recordOn, replayOn, eventsOn;
 };
@@ -212,6 +215,8 @@ int launchSimStep(const DevState &s, const SceneDev &sc, void *stream);
 int launchVisibility(const DevState &s, const SceneDev &sc, void *stream);
 int launchObservations(const DevState &s, const SceneDev &sc, void *stream);
 int launchLidar(const DevState &s, const SceneDev &sc, void *stream);
+// synchronous on `stream`, at scene upload; dev_scratch holds kMaxZones ints
+int computeZoneGoalTris(const SceneDev &sc, int32_t *dev_scratch, int32_t *host_out, void *stream);
 int launchTraceRays(const SceneDev &sc, const float *o, const float *d, int n, int mode, float *t, int32_t *hit,
                     void *stream);
 int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, float *wf, uint32_t *explore,

@@ -195,11 +195,21 @@ __device__ int nearestNavTriD(const SceneDev &sc, Vec3 pos)
     return closest_idx;
 }
 
-// PathfindToPoint (sim.cpp:5012-5035)
-__device__ Vec3 pathfindToPointD(const SceneDev &sc, Vec3 start, Vec3 pos)
+// The bots' goal is always a zone centroid: its NearestNavTri is computed
+// once per zone at scene upload (same function, same input).
+__global__ void k_zone_goals(SceneDev sc, int32_t *out)
+{
+    const int zi = threadIdx.x;
+    if (zi >= sc.numZones) return;
+    const AABB z = sc.zoneAABB[zi];
+    const Vec3 center = (z.pMin + z.pMax) / 2.f; // as planAStarD forms it
+    out[zi] = nearestNavTriD(sc, center);
+}
+
+// PathfindToPoint (sim.cpp:5012-5035); goal_tri = NearestNavTri(pos)
+__device__ Vec3 pathfindToPointD(const SceneDev &sc, Vec3 start, Vec3 pos, int goal_tri)
 {
     const int start_tri = nearestNavTriD(sc, start);
-    const int goal_tri = nearestNavTriD(sc, pos);
     if (start_tri < 0 || goal_tri < 0) return v3(0.f, 0.f, 0.f); // (asserted in the reference)
     const int next = sc.astar[start_tri * sc.numNavTris + goal_tri];
     if (next == -1) return v3(0.f, 0.f, 0.f);
@@ -226,7 +236,7 @@ __device__ void planAStarD(const DevState &S, const SceneDev &sc, int64_t g)
     const AABB z = sc.zoneAABB[zi];
     Vec3 center = (z.pMin + z.pMax) / 2.f; // AABB::centroid
     const Vec3 pos = v3(S.px[g], S.py[g], 0.f);
-    center = pathfindToPointD(sc, pos, center);
+    center = pathfindToPointD(sc, pos, center, sc.zoneGoalTri[zi]);
     center.z = 0.f;
     const float yaw = S.ayaw[g];
     const Vec3 fwd = v3(-sinf_(yaw), cosf_(yaw), 0.f);
@@ -2713,6 +2723,16 @@ int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
     const int blocks = (int)((s.A + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
+}
+
+int computeZoneGoalTris(const SceneDev &sc, int32_t *dev_scratch, int32_t *host_out, void *stream)
+{
+    hipLaunchKernelGGL(k_zone_goals, dim3(1), dim3(64), 0, (hipStream_t)stream, sc, dev_scratch);
+    int rc = check(hipGetLastError());
+    if (!rc) rc = check(hipMemcpyAsync(host_out, dev_scratch, sizeof(int32_t) * sc.numZones, hipMemcpyDeviceToHost,
+                                       (hipStream_t)stream));
+    if (!rc) rc = check(hipStreamSynchronize((hipStream_t)stream));
+    return rc;
 }
 
 int launchLidar(const DevState &s, const SceneDev &sc, void *stream)

@@ -501,6 +501,9 @@ static void buildSceneDev(mpenv_manager &m)
         sc.zoneAABB[z] = s.zoneAABBs[z];
         sc.zoneRot[z] = s.zoneRotations[z];
     }
+    for (int z = 0; z < kMaxZones; z++) sc.zoneGoalTri[z] = -1;
+    if (sc.numNavTris > 0 && computeZoneGoalTris(sc, m.alloc<int32_t>(kMaxZones), sc.zoneGoalTri, m.stream))
+        throw std::runtime_error("zone goal triangle kernel failed");
     sc.numGoals = (int32_t)s.goalRegions.size();
     for (int gi = 0; gi < sc.numGoals && gi < 4; gi++) {
         const GoalRegion &g = s.goalRegions[gi];
