@@ -2467,7 +2467,10 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
 // consecutive task quads: up to kLidarIters (amortises the BVH staging) on
 // big batches, fewer on small ones so the grid still spreads over the CUs
 // (at 64 worlds 1v1 a fixed 8 put the whole lidar on 5 CUs).
-constexpr int kLidarIters = 8;
+#ifndef MPENV_LIDAR_ITERS
+#define MPENV_LIDAR_ITERS 4 // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 ms (k_lidar alone, C3)
+#endif
+constexpr int kLidarIters = MPENV_LIDAR_ITERS;
 constexpr int kLidarWaves = kBlock / 64;
 
 __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A + 3) / 4) * 5; }
