@@ -66,55 +66,80 @@ def parse():
     ap.add_argument("--worlds", type=int, default=16384, help="worlds per GPU")
     ap.add_argument("--team-size", type=int, default=6)
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "simple_map"))
+    ap.add_argument("--world-groups", type=int, default=1,
+                    help="world ranges stepped on concurrent streams (engine option; 1 = one stream, "
+                         "so per-kernel times are exclusive and match rocprof)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline timed budget")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPUs this process may use")
     ap.add_argument("--gather", action="store_true",
-                    help="N>1: RCCL-gather obs/reward/done to rank 0 every step (learner mode)")
+                    help="N>1: learner exchange -- every trainInterface output gathered to rank 0 each "
+                         "step over RCCL, overlapped with the next step (double-buffered)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--share-device", action="store_true",
                     help="debug: map every rank to GPU 0 (rehearse N>1 on a one-GPU box; no --gather)")
-    ap.add_argument("--no-isolation", action="store_true",
-                    help="skip the isolated per-kernel window (profiling runs: keep launches uniform)")
-    ap.add_argument("--no-kernel-timing", action="store_true",
-                    help="debug: no per-kernel HIP events in the timed region (no roofline)")
+    ap.add_argument("--no-profile-pass", action="store_true",
+                    help="skip the second (kernel-timing + workload-counter) pass")
     ap.add_argument("--bots", choices=["none", "team1", "all"], default="none",
                     help="A* scripted bots (AgentPolicy -1, planAStarAISystem) for team 1 / everyone "
                          "(config C5's nav-mesh pathing); the headline C3 line uses none")
     return ap.parse_args()
 
 
-def cpu_baseline(args, world_size):
+def cpu_share():
+    """CPUs this process may use: affinity, capped by a cgroup v2 CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(args):
     """Oracle (test infrastructure, a restatement of the reference's CPU
-    executor) on a bounded sample: 32 worlds per thread, 10 untimed steps,
-    then 5-step chunks until --cpu-seconds elapse."""
+    executor, whose ThreadPoolExecutor partitions worlds over threads,
+    mgr.cpp:1863-1871) on the same batch as the GPU line: every world of the
+    configuration, one std::thread per usable CPU, steps until
+    --cpu-seconds elapse (at least 2 after 1 untimed)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import mpenv_testlib as T
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    W = 32 * threads
+    threads = args.cpu_threads or cpu_share()
+    W = args.worlds
     N = 2 * args.team_size
+    A = W * N
     o = T.Oracle(W, args.team_size, scene=args.scene)
     o.put_ctrl([0, 1, 1])
     o.init()
-    ring = np.ascontiguousarray(T.mpenv_tape.tape_ring(TAPE_SEED, 0, W * N, 16))
-    o.lib.oracle_run_threaded(o.h, 10, threads, ring.ctypes.data, 16)
+    ring_len = 8
+    ring = np.ascontiguousarray(T.mpenv_tape.tape_ring(TAPE_SEED, 0, A, ring_len))
+    row = A * 6 * 4
+    o.lib.oracle_run_threaded(o.h, 1, threads, ring.ctypes.data, 1)
     secs, steps = 0.0, 0
-    while secs < args.cpu_seconds and steps < 400:
-        secs += o.lib.oracle_run_threaded(o.h, 5, threads, ring.ctypes.data, 16)
-        steps += 5
+    while (secs < args.cpu_seconds or steps < 2) and steps < 1000:
+        s = 1 + steps
+        secs += o.lib.oracle_run_threaded(o.h, 1, threads, ring.ctypes.data + (s % ring_len) * row, 1)
+        steps += 1
     o.close()
     return {
-        "value": W * N * steps / secs,
+        "value": A * steps / secs,
         "unit": "agent-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{W} worlds {args.team_size}v{args.team_size} simple_map, {steps} steps after 10 "
-                  f"warmup, {threads} std::threads static world partition, {secs:.1f} s",
+        "host_cpus": os.cpu_count(),
+        "sample": f"the GPU line's batch ({W} worlds {args.team_size}v{args.team_size} simple_map), "
+                  f"{steps} steps after 1 untimed, {threads} std::threads (static world partition; "
+                  f"{threads} = CPUs usable by this process, of {os.cpu_count()} on the host), {secs:.1f} s",
     }
 
 
 VALU_PEAK = 256 * 4 * 0.5 * 2.4e9  # wave-instr/s: 256 CUs x 4 SIMD32 x 1/2 per clock x 2.4 GHz
+# What bounds each kernel (DESIGN.md §4): the ray kernels issue VALU
+# instructions over divergent traversals; k_obs streams observation rows.
+KERNEL_BOUND = {"k_move": "valu", "k_sim": "latency", "k_vis": "valu", "k_obs": "hbm", "k_lidar": "valu"}
 
 
 def load_profile(path, workload):
@@ -151,7 +176,7 @@ def main():
             gather_group = dist.new_group(backend="nccl")
 
     import madrona_mp_env as m
-    from mpenv_dist import gather_to_learner
+    from mpenv_dist import LearnerGather
     import mpenv_tape
 
     W, ts = args.worlds, args.team_size
@@ -162,91 +187,90 @@ def main():
                        auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
                        team_size=ts, num_pbt_policies=0, policy_history_size=0,
                        scene_path=args.scene, world_id_offset=offset)
+    sim.set_world_groups(args.world_groups)
+    groups = sim.world_groups()
     ctrl = sim.sim_control_tensor().to_torch()
-    ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=dev).view_as(ctrl))
-    torch.cuda.synchronize()
-    sim.init()
 
-    if args.bots != "none":
-        pol = torch.zeros((W, 2, ts), dtype=torch.int32)
-        if args.bots == "all":
-            pol[:] = -1
-        else:
-            pol[:, 1, :] = -1
-        sim.policy_assignment_tensor().to_torch().copy_(pol.view(-1, 1).to(dev))
+    def start_episode():
+        # Manager::init -- a forced reset of every world (simCtrl [0, 1, 1]:
+        # random start step and team sides, scripts/jax_train.py:377)
+        ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=dev).view_as(ctrl))
+        torch.cuda.synchronize()
+        sim.init()
+        if args.bots != "none":
+            pol = torch.zeros((W, 2, ts), dtype=torch.int32)
+            if args.bots == "all":
+                pol[:] = -1
+            else:
+                pol[:, 1, :] = -1
+            sim.policy_assignment_tensor().to_torch().copy_(pol.view(-1, 1).to(dev))
         torch.cuda.synchronize()
 
+    start_episode()
     ring = torch.from_numpy(mpenv_tape.tape_ring(TAPE_SEED, offset * N, A, RING)).to(dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    outs = [sim.self_observation_tensor().to_torch(), sim.reward_tensor().to_torch(),
-            sim.done_tensor().to_torch()] if args.gather and world_size > 1 else None
+    learner = LearnerGather(sim, dst=0, group=gather_group) if args.gather and world_size > 1 else None
 
     def one_step(s):
         sim.copy_actions(ring[s % RING].data_ptr(), sptr)
         sim.step_async(sptr)
-        if outs is not None:
-            gather_to_learner(outs, dst=0, group=gather_group)
+        if learner is not None:
+            learner.submit(sptr)
 
+    # ---- timed pass: W warmup steps, then K steps, no events or counters
     for s in range(args.warmup):
         one_step(s)
     torch.cuda.synchronize()
     if world_size > 1:
         dist.barrier()
-    sim.enable_kernel_timing(not args.no_kernel_timing)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
         one_step(args.warmup + s)
+    if learner is not None:
+        learner.drain()
     torch.cuda.synchronize()
     if world_size > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timings = sim.kernel_timings()  # {name: (avg ms, launches)}
-    if args.no_kernel_timing:
-        print(json.dumps({"value": world_size * A * args.steps / elapsed, "ms_per_step": 1e3 * elapsed / args.steps}))
-        return
-    sim.enable_kernel_timing(False)
     if world_size > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    # Isolation window (after the timed region, not part of `value`): each
-    # kernel alone on the GPU, one launch per step, so its duration is not
-    # shared with the overlapped world groups of the timed region.
-    groups = sim.world_groups()
-    iso = None
-    if groups > 1 and not args.no_isolation:
-        sim.set_world_groups(1)
-        sim.enable_kernel_timing(True)
-        for s in range(30):
-            one_step(args.warmup + args.steps + s)
-        torch.cuda.synchronize()
-        iso = sim.kernel_timings()
-        sim.enable_kernel_timing(False)
-        sim.set_world_groups(groups)
-
     total_agent_steps = world_size * A * args.steps
     value = total_agent_steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
-    # dominant kernel and its HBM roofline
-    dom = max(timings, key=lambda k: timings[k][0])
-    dom_ms = timings[dom][0]
-    # world groups: each step launches every kernel once per group (stream)
-    lps = max(1, round(timings[dom][1] / args.steps))
-    alg = (KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W) // lps
-    achieved = alg / (dom_ms * 1e-3) / 1e9
-    workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})")
-    prof = load_profile(args.traffic, workload)
-    traffic = prof.get("per_kernel", {}).get(dom)
-    valu = prof.get("valu_insts_per_launch", {}).get(dom)
-    step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W
-    kern_ms = sum(v[0] for v in timings.values()) * lps
+    # ---- profile pass (not part of `value`): the same episode window again
+    # (Manager::init, W warmup steps, K steps) with one world group, so
+    # every kernel runs alone and its HIP-event duration is exclusive, plus
+    # the kernels' workload counters.
+    prof_pass = None
+    if not args.no_profile_pass:
+        if learner is not None:
+            learner.drain()
+        sim.set_world_groups(1)
+        start_episode()
+        for s in range(args.warmup):
+            one_step(s)
+        torch.cuda.synchronize()
+        sim.enable_kernel_timing(True)
+        sim.enable_stats(True)
+        for s in range(args.steps):
+            one_step(args.warmup + s)
+        torch.cuda.synchronize()
+        timings = sim.kernel_timings()  # {name: (avg ms, launches)}
+        counts = sim.read_stats()
+        sim.enable_kernel_timing(False)
+        sim.enable_stats(False)
+        sim.set_world_groups(groups)
+        prof_pass = (timings, counts)
 
+    workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})")
     result = {
-        "metric": "env steps/sec x agents (whole node), simple_map 6v6 @ 16384 worlds",
+        "metric": f"env steps/sec x agents (whole node), simple_map {ts}v{ts} @ {W} worlds"
+                  + ("" if world_size == 1 else f"/GPU x {world_size} GPUs"),
         "value": round(value, 1),
         "unit": "agent-steps/s",
         "n_gpus": world_size,
@@ -268,63 +292,71 @@ def main():
             "sim_control": [0, 1, 1],
             "bots": args.bots,
             "rand_seed": 5,
-            "parallelism": f"world-sharded x{world_size}" + (" + RCCL gather" if outs else ""),
+            "world_groups": groups,
+            "parallelism": f"world-sharded x{world_size}" + (" + RCCL learner gather" if learner else ""),
         },
         "world_steps_per_s": round(value / N, 1),
-        "roofline": {
-            "bound": "hbm",
+    }
+    if prof_pass is not None:
+        timings, counts = prof_pass
+        steps = args.steps
+        dom = max(timings, key=lambda k: timings[k][0])
+        dom_ms = timings[dom][0]
+        alg = KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W
+        achieved = alg / (dom_ms * 1e-3) / 1e9
+        prof = load_profile(args.traffic, workload)
+        traffic = prof.get("per_kernel", {}).get(dom)
+        valu = prof.get("valu_insts_per_launch", {}).get(dom)
+        step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W
+        kern_ms = sum(v[0] for v in timings.values())
+        result["roofline"] = {
+            "bound": KERNEL_BOUND[dom],
             "kernel": dom,
+            "note": "profile pass (same episode window, one world group): exclusive HIP-event time per launch",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
             "algorithmic_bytes_per_launch": alg,
-            "launches_per_step": lps,
-            # the ray kernels are VALU-issue bound, not HBM bound: their VALU
-            # instructions per launch (PMC, profiles/) over the live duration
+            "launch_ms": round(dom_ms, 4),
+            # the limiter of the ray kernels: VALU issue (PMC instructions
+            # per launch from profiles/, same workload) over the launch time
             "valu_issue": None if not valu else {
                 "insts_per_launch": valu,
                 "achieved_per_s": round(valu / (dom_ms * 1e-3), 1),
                 "peak_per_s": VALU_PEAK,
                 "frac": round(valu / (dom_ms * 1e-3) / VALU_PEAK, 4),
+                "lane_efficiency": prof.get("lane_efficiency", {}).get(dom),
             },
-        },
-        "kernels_ms": {k: round(v[0], 4) for k, v in timings.items()},
-        "world_groups": groups,
-        "step_hbm": {
-            "algorithmic_bytes_per_step": step_bytes,
-            "achieved_GBps_over_kernels": round(step_bytes / (kern_ms * 1e-3) / 1e9, 2),
-        },
-    }
-    if iso is not None:
-        idom = max(iso, key=lambda k: iso[k][0])
-        ibytes = KERNEL_BYTES_PER_AGENT[idom] * A + KERNEL_BYTES_PER_WORLD[idom] * W
-        result["roofline_isolated"] = {
-            "note": "30 steps after the timed region with world groups = 1 (each kernel alone)",
-            "kernel": idom,
-            "achieved": round(ibytes / (iso[idom][0] * 1e-3) / 1e9, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(ibytes / (iso[idom][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-            "kernels_ms": {k: round(v[0], 4) for k, v in iso.items()},
         }
-        # the bound that applies to the ray kernels: VALU issue.  The PMC
-        # count is per launch of the profiled (default-groups) run, so one
-        # step's instructions are that x launches per step.
-        ivalu = prof.get("valu_insts_per_launch", {}).get(idom)
-        if ivalu:
-            per_step = ivalu * lps
-            result["roofline_isolated"]["valu_issue"] = {
-                "insts_per_step": per_step,
-                "achieved_per_s": round(per_step / (iso[idom][0] * 1e-3), 1),
-                "peak_per_s": VALU_PEAK,
-                "frac": round(per_step / (iso[idom][0] * 1e-3) / VALU_PEAK, 4),
-            }
+        result["kernels_ms"] = {k: round(v[0], 4) for k, v in timings.items()}
+        result["step_hbm"] = {
+            "algorithmic_bytes_per_step": step_bytes,
+            "kernel_ms_per_step": round(kern_ms, 4),
+            "achieved_GBps_over_kernels": round(step_bytes / (kern_ms * 1e-3) / 1e9, 2),
+        }
+        lidar_rays = 80 * A * steps
+        rays = lidar_rays + counts["los_rays"] + counts["shot_rays"]
+        result["workload"] = {
+            "note": f"per step, averaged over the profile pass's {steps} steps",
+            "alive_agents": round(counts["alive_agents"] / steps, 1),
+            "alive_frac": round(counts["alive_agents"] / steps / A, 4),
+            "los_pairs": round(counts["los_pairs"] / steps, 1),
+            "los_rays": round(counts["los_rays"] / steps, 1),
+            "los_seen": round(counts["los_seen"] / steps, 1),
+            "lidar_rays": 80 * A,
+            "shot_rays": round(counts["shot_rays"] / steps, 1),
+            "sphere_casts": round(counts["sphere_casts"] / steps, 1),
+            "rays_per_s": round(rays / steps / (ms_per_step * 1e-3), 1),
+            "bvh_queries_per_s": round((rays + counts["sphere_casts"]) / steps / (ms_per_step * 1e-3), 1),
+        }
     if rank == 0 and world_size == 1 and args.cpu_baseline == "auto":
-        result["cpu_baseline"] = cpu_baseline(args, world_size)
+        result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if learner is not None:
+        learner.close()
     if world_size > 1:
         dist.destroy_process_group()
 

@@ -401,6 +401,15 @@ int mpenv_kernel_timings(mpenv_manager *mgr, int32_t max_n, const char **names,
                          float *avg_ms, int32_t *launches);
 int mpenv_enable_kernel_timing(mpenv_manager *mgr, int32_t enable);
 
+/* Measurement hook (no reference counterpart): per-step workload counters
+ * accumulated by the step kernels while enabled (enabling zeroes them):
+ * [0] alive agents at k_move, [1] (viewer, opponent) pairs both alive,
+ * [2] visibility rays traced, [3] visibility rays that saw their target,
+ * [4] sphere casts, [5] shot rays.  read_stats copies min(n, 8) counters
+ * and returns the number of counters (8). */
+int mpenv_enable_stats(mpenv_manager *mgr, int32_t enable);
+int mpenv_read_stats(mpenv_manager *mgr, uint64_t *out, int32_t n);
+
 /* Scene BVH as the engine builds it (map_importer.cpp:364-419 replacement):
  * 64-byte nodes and float3 vertices (3 per triangle).  Call with null
  * outputs to query sizes.  Used by the parity oracle and tests. */

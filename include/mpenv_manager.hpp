@@ -8,7 +8,8 @@
 //   * Errors throw std::runtime_error (the reference FATALs / asserts).
 //   * ExecMode::CPU, the viewer (VizState, vizStep), getWorldContext and
 //     the ExploreAction/CoarsePvPAction setters are out of scope
-//     and throw; full-team tensors and replay are not implemented.
+//     and throw.  Full-team tensors, record/replay and event logs are
+//     implemented (fullTeam*Tensor getters, Config log paths).
 //   * gpuStreamInit/Step take the HIP stream as void*.
 #pragma once
 

@@ -110,7 +110,10 @@ def build_oracle(force=False):
     return ORACLE_LIB
 
 
-def build_all(force=False):
+def build_all(force=True):
+    """Every artefact, recompiled from source by default (build() must never
+    ship binaries it did not compile); force=False is the incremental mode
+    the test harness uses when a build already ran in this tree."""
     build_lib(force)
     build_ext(force)
     build_headless(force)
@@ -118,4 +121,4 @@ def build_all(force=False):
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    build_all(force="--incremental" not in sys.argv)

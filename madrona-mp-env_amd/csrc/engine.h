@@ -135,6 +135,21 @@ struct DevState {
     mpenv_game_event *events;              // [W][evStride] slots: 2 per agent + capture
     mpenv_packed_step_snapshot *snapshots; // [W]
     int32_t evStride;                      // 2 * N + 1
+
+    // Workload counters (mpenv_enable_stats), null when off: see StatId.
+    unsigned long long *stats;
+};
+
+// Per-step workload counters accumulated by the kernels in stats mode
+// (bench.py's workload window; never on in the timed region).
+enum StatId {
+    kStatAliveAgents = 0, // agents alive when k_move runs
+    kStatLosPairs = 1,    // (viewer, opponent) pairs with both alive
+    kStatLosRays = 2,     // visibility rays traced after the view/frustum tests
+    kStatLosSeen = 3,     // of those, rays that found their target
+    kStatSphereCasts = 4, // MeshBVH::sphereCast calls (k_move)
+    kStatShots = 5,       // fireSystem rays (k_sim)
+    kNumStats = 8,
 };
 
 struct ZOBBDev {

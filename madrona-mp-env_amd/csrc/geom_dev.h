@@ -27,12 +27,13 @@ struct LBVH {
     const MP_LDS float *verts;
     const MP_LDS float *pre; // sphere-casting kernels only (stageBVHSphere)
     const MP_LDS float *snodes; // sphere-cast node image (stageBVHSphere), else null
+    unsigned long long *stats;  // workload counters (DevState::stats), null = off
 };
 
 __device__ __forceinline__ float expScaleD(int e) { return mp::u2f((uint32_t)(e + 127) << 23); }
 
 constexpr float kSphereR = 15.f;  // consts::agentRadius: the radius of every k_move sphere cast
-constexpr int kSNodeFloats = 32;  // sphere-cast node image: loR[3][4], hiR[3][4], children[4], triSize[4]
+constexpr int kSNodeFloats = 32;  // sphere-cast node image: loR[3][4], hiR[3][4], children[4], leaf tri count[4]
 
 // Byte stack: push shifts left by 8 across a 128-bit register pair.
 struct ByteStack {
@@ -75,6 +76,7 @@ __device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc)
     b.verts = (const MP_LDS float *)(smem + (size_t)node_q * 16);
     b.pre = nullptr;
     b.snodes = nullptr;
+    b.stats = nullptr;
     return b;
 }
 
@@ -111,7 +113,18 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
             o[12 + a * 4 + i] = (mins[a] + sc_a * (float)qmx[a][i]) + kSphereR;
         }
         o[24 + i] = __int_as_float(nd.children[i]);
-        o[28 + i] = __uint_as_float((uint32_t)nd.triSize[i]);
+        // Triangles sphereCastLeaf tests: always numTrisPerLeaf = 2 in leaf
+        // order, whatever triSize says (mesh_bvh.inl:867-880;
+        // fetchLeafTriangle never reports a missing triangle, 556-576), so a
+        // 1-triangle leaf also tests the next leaf's first triangle.  Only
+        // the last triangle's overrun past the vertex array is defined here
+        // (not tested).
+        int cnt = 0;
+        if (nd.children[i] != -1 && (nd.children[i] & 0x80000000)) {
+            const int leaf = nd.children[i] & 0x7fffffff;
+            cnt = min(2, sc.numVerts / 3 - leaf);
+        }
+        o[28 + i] = __uint_as_float((uint32_t)cnt);
     }
     LBVH b = stageBVH(smem, sc); // ends with __syncthreads
     b.pre = (const MP_LDS float *)(smem + pre_off);
@@ -524,6 +537,7 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
             }
         }
     }
+    if (b.stats) atomicAdd(b.stats + kStatSphereCasts, 1ull);
     SphereHit h;
     h.t = hit_t;
     h.n = closest;

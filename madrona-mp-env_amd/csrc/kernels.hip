@@ -595,6 +595,7 @@ __device__ void fireD(const DevState &S, const SceneDev &sc, const LBVH &bvh, in
     Vec3 fire_dir = rotateVec(a.rot, kFwd);
 
     WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, fire_from, fire_dir);
+    if (S.stats) atomicAdd(S.stats + kStatShots, 1ull);
     S.firedT[g] = h.hit ? h.t : kFltMax;
     bool success = h.hit;
     const int team = i / S.T, offset = i - team * S.T;
@@ -1788,9 +1789,11 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPENV_MOVE_WPE))) k_move(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const LBVH bvh = stageBVHSphere(smem, sc);
+    LBVH bvh = stageBVHSphere(smem, sc);
+    bvh.stats = S.stats;
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= S.A) return;
+    if (S.stats && S.alive[g] != 0.f) atomicAdd(S.stats + kStatAliveAgents, 1ull);
     planAStarD(S, sc, g);
     if (sc.replayOn) return; // pvpReplayLogic replaces the gameplay systems (sim.cpp:5587-5605)
     applyBotActionsD(S, g);
@@ -2064,6 +2067,11 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
             }
         }
         const int nc = __popc(cand);
+        if (S.stats && valid && S.alive[g] != 0.f) {
+            const int64_t gt2 = (g / N) * N + (((int)(g % N) / T) ^ 1) * T + k;
+            if (S.alive[gt2] != 0.f) atomicAdd(S.stats + kStatLosPairs, 1ull);
+            if (nc) atomicAdd(S.stats + kStatLosRays, (unsigned long long)nc);
+        }
         if (nc) {
             uint32_t slot = atomicAdd(&nrays, (uint32_t)nc);
             const uint16_t lane_id = (uint16_t)(threadIdx.x << 2);
@@ -2092,8 +2100,10 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
         const float len = length(to_test);
         to_test = to_test / len;
-        if (visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target))
+        if (visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target)) {
             atomicOr(&masks[(int)(g - agent0)], 1u << k);
+            if (S.stats) atomicAdd(S.stats + kStatLosSeen, 1ull);
+        }
     }
     __syncthreads();
 

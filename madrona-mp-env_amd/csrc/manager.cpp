@@ -126,6 +126,9 @@ struct mpenv_manager {
     std::vector<mpenv_packed_step_snapshot> hostSnaps;
     std::vector<int32_t> hostSnapWritten;
 
+    // Workload counters (DevState::stats, kNumStats u64), allocated on first use
+    unsigned long long *statsBuf = nullptr;
+
     // Kernel timing
     bool timing = false;
     std::vector<hipEvent_t> eventPool;
@@ -759,6 +762,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         if (cfg->gpu_id < 0 || cfg->gpu_id >= ndev) return fail(MPENV_ERR_INVALID, "gpu_id out of range");
         HIP_CHECK(hipSetDevice(cfg->gpu_id));
         m = new mpenv_manager();
+        m->S.stats = nullptr;
         m->cfg = *cfg;
         m->scenePath = cfg->scene_path;
         m->cfg.scene_path = m->scenePath.c_str();
@@ -1050,6 +1054,40 @@ int mpenv_enable_kernel_timing(mpenv_manager *m, int32_t enable)
     m->timing = enable != 0;
     m->eventsUsed = 0;
     return MPENV_OK;
+}
+
+int mpenv_enable_stats(mpenv_manager *m, int32_t enable)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null manager");
+    try {
+        HIP_CHECK(hipStreamSynchronize(m->stream));
+        for (hipStream_t gs : m->gstreams) HIP_CHECK(hipStreamSynchronize(gs));
+        if (enable && !m->statsBuf) m->statsBuf = m->alloc<unsigned long long>(kNumStats);
+        if (enable) HIP_CHECK(hipMemsetAsync(m->statsBuf, 0, sizeof(unsigned long long) * kNumStats, m->stream));
+        HIP_CHECK(hipStreamSynchronize(m->stream));
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    unsigned long long *p = enable ? m->statsBuf : nullptr;
+    m->S.stats = p;
+    for (DevState &G : m->gS) G.stats = p;
+    return MPENV_OK;
+}
+
+int mpenv_read_stats(mpenv_manager *m, uint64_t *out, int32_t n)
+{
+    if (!m || !out) return fail(MPENV_ERR_INVALID, "null argument");
+    std::vector<unsigned long long> h(kNumStats, 0ull);
+    try {
+        HIP_CHECK(hipDeviceSynchronize());
+        if (m->statsBuf)
+            HIP_CHECK(hipMemcpy(h.data(), m->statsBuf, sizeof(unsigned long long) * kNumStats,
+                                hipMemcpyDeviceToHost));
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    for (int k = 0; k < n && k < kNumStats; k++) out[k] = h[k];
+    return kNumStats;
 }
 
 int mpenv_kernel_timings(mpenv_manager *m, int32_t max_n, const char **names, float *avg_ms, int32_t *launches)

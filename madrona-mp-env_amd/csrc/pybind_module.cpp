@@ -225,6 +225,17 @@ PYBIND11_MODULE(madrona_mp_env, m)
         .def("set_world_groups", [](PySimManager &s, int32_t g) { check(mpenv_set_world_groups(s.h->mgr, g)); })
         .def("world_groups", [](PySimManager &s) { int32_t g = 0; check(mpenv_world_groups(s.h->mgr, &g)); return g; })
         .def("enable_kernel_timing", [](PySimManager &s, bool on) { check(mpenv_enable_kernel_timing(s.h->mgr, on)); })
+        .def("enable_stats", [](PySimManager &s, bool on) { check(mpenv_enable_stats(s.h->mgr, on)); })
+        .def("read_stats", [](PySimManager &s) {
+            uint64_t v[8] = {};
+            int n = mpenv_read_stats(s.h->mgr, v, 8);
+            if (n < 0) check(n);
+            static const char *names[6] = { "alive_agents", "los_pairs", "los_rays", "los_seen",
+                                            "sphere_casts", "shot_rays" };
+            py::dict d;
+            for (int k = 0; k < 6; k++) d[py::str(names[k])] = v[k];
+            return d;
+        })
         .def("kernel_timings", [](PySimManager &s) {
             const char *names[16];
             float ms[16];

@@ -394,14 +394,20 @@ Scene loadScene(const std::string &dir, bool spawn_in_middle)
 
         // filterMeshes: drop BulletsOnly (flag value 1) triangles.
         for (uint64_t m = 0; m < num_meshes; m++) {
-            uint32_t voff = mesh_info[4 * m + 0];
-            uint32_t toff = mesh_info[4 * m + 2];
-            uint32_t nt = mesh_info[4 * m + 3];
-            for (uint32_t i = 0; i < nt; i++) {
+            const uint64_t voff = mesh_info[4 * m + 0], nv = mesh_info[4 * m + 1];
+            const uint64_t toff = mesh_info[4 * m + 2], nt = mesh_info[4 * m + 3];
+            if (voff + nv > total_verts || toff + nt > total_tris)
+                throw std::runtime_error(path + ": mesh " + std::to_string(m) +
+                                         " range outside the vertex/triangle arrays (truncated or malformed file)");
+            for (uint64_t i = 0; i < nt; i++) {
                 uint32_t mat = tri_mats[toff + i];
                 if (mat < mat_flags.size() && mat_flags[mat] == 1u) continue;
                 for (int k = 0; k < 3; k++) {
-                    s.triVerts.push_back(verts[voff + idx[3 * (toff + i) + k]]);
+                    const uint64_t vi = idx[3 * (toff + i) + k];
+                    if (vi >= nv)
+                        throw std::runtime_error(path + ": mesh " + std::to_string(m) +
+                                                 " vertex index out of range (truncated or malformed file)");
+                    s.triVerts.push_back(verts[voff + vi]);
                 }
             }
         }

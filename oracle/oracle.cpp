@@ -23,8 +23,9 @@
 // (utils.cpp:899-903), dead agents still casting lidar and dropping
 // breadcrumbs.  Deliberate, documented definitions: breadcrumb penalties
 // accumulate in creation order (the reference uses an order-dependent float
-// atomic, sim.cpp:4915); sphereCastLeaf tests triSize triangles (the
-// reference always reads 2, mesh_bvh.inl:867); ExploreTracker cells outside
+// atomic, sim.cpp:4915); sphereCastLeaf reads two consecutive triangles
+// per leaf as the reference does (mesh_bvh.inl:867-880) and skips only the
+// read past the last triangle (undefined there); ExploreTracker cells outside
 // the initialised quadrant start at 0; uninitialised locals (the first
 // slope-cast normal, sim.cpp:927) start at zero.
 //
@@ -37,10 +38,12 @@
 #include "oracle.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -235,7 +238,8 @@ struct Oracle {
     std::vector<float> navCdf;   // running triangle areas (navSamplePoint)
     std::vector<mpenv_curriculum_snapshot> curriculum; // TrajectoryCurriculum
     struct ZOBB { Vec3 pMin, pMax; float rotation; } subZones[8]; // level_gen.cpp:282-326
-    std::vector<int32_t> astar;  // [T][T]
+    std::vector<int32_t> astar;  // [T][T] (buildAStarLookup, built by the oracle)
+    std::vector<int32_t> navAdj; // [T][3]
     int numNavTris = 0;
     std::vector<Vec3> verts;
     std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
@@ -526,8 +530,14 @@ float sphereCastTriangle(Vec3 ta, Vec3 tb, Vec3 tc, Vec3 ray_o, Vec3 ray_d, floa
     return hit_t;
 }
 
-// mesh_bvh.inl:743-815 (MeshBVH::sphereCast) + 857-883 (sphereCastLeaf,
-// testing triSize triangles: see file header).
+// mesh_bvh.inl:743-815 (MeshBVH::sphereCast) + 857-883 (sphereCastLeaf:
+// two consecutive triangles per leaf, see file header).
+// Analysis counters (oracle_cast_stats): casts, casts ending at t = 0, and
+// the leaf read rule (2 = the reference's two consecutive triangles,
+// 1 = only triSize triangles, the round-1 definition kept for comparison).
+std::atomic<uint64_t> g_casts { 0 }, g_zeroCasts { 0 };
+int g_leafReadTwo = 1;
+
 float bvhSphereCast(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float r, Vec3 *out_n,
                     float t_max = kFltMax)
 {
@@ -555,7 +565,13 @@ float bvhSphereCast(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float r, Vec3 *out_
                     int32_t leaf_idx = node.children[i] & ~0x80000000;
                     Vec3 leaf_n = v3(0.f, 0.f, 0.f);
                     float leaf_t = hit_t;
-                    for (int k = 0; k < node.triSize[i]; k++) {
+                    // numTrisPerLeaf (= 2) triangles in leaf order regardless
+                    // of triSize (mesh_bvh.inl:867-880, fetchLeafTriangle
+                    // 556-576 always succeeds); the last triangle's overrun
+                    // past the vertex array is defined as "not tested".
+                    const int num_tris = (int)(o.verts.size() / 3);
+                    const int nread = g_leafReadTwo ? 2 : node.triSize[i];
+                    for (int k = 0; k < nread && leaf_idx + k < num_tris; k++) {
                         Vec3 a = o.verts[(leaf_idx + k) * 3 + 0];
                         Vec3 b = o.verts[(leaf_idx + k) * 3 + 1];
                         Vec3 c = o.verts[(leaf_idx + k) * 3 + 2];
@@ -572,6 +588,8 @@ float bvhSphereCast(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float r, Vec3 *out_
         }
     }
     if (hit_t < t_max) *out_n = closest;
+    g_casts.fetch_add(1, std::memory_order_relaxed);
+    if (hit_t == 0.f) g_zeroCasts.fetch_add(1, std::memory_order_relaxed);
     return hit_t;
 }
 
@@ -2789,6 +2807,229 @@ void addMiddleSpawnCells(Oracle &o)
     }
 }
 
+// ------------------------------------------------------------ navmesh
+// The oracle builds the bots' navmesh and A* next-hop table itself from
+// navmesh.bin, independently of the product's csrc/navmesh.cpp, so a
+// misreading of buildAStarLookup on either side shows up as a table
+// mismatch (tests/test_navmesh.py compares the two byte for byte).
+struct NavBuild {
+    std::vector<Vec3> verts;     // deduplicated
+    std::vector<uint32_t> tri;   // 3 per triangle
+    std::vector<int32_t> adj;    // 3 per triangle
+};
+
+// map_importer.cpp:421-506 importNavmesh (the world-bounds filter is
+// `#if 0`'d, so every face is kept), then mgr.cpp:1301-1318: vertices with
+// bit-identical positions share the index of their first occurrence
+// (meshopt_generateVertexRemap), then Navmesh::initFromPolygons (Madrona,
+// not vendored; defined as in DESIGN.md §2 #8: polygon (v0..vn-1) fans into
+// (v0, vk, vk+1); the neighbour across edge k of triangle t is the lowest
+// numbered other triangle holding the same undirected edge, else -1).
+NavBuild navFromFile(const std::string &path)
+{
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("oracle: cannot open navmesh.bin");
+    auto u32 = [&f]() {
+        uint32_t v = 0;
+        if (!f.read(reinterpret_cast<char *>(&v), 4)) throw std::runtime_error("oracle: navmesh.bin truncated");
+        return v;
+    };
+    const uint32_t nv = u32();
+    std::vector<float> raw((size_t)nv * 3);
+    if (!f.read(reinterpret_cast<char *>(raw.data()), raw.size() * 4))
+        throw std::runtime_error("oracle: navmesh.bin truncated");
+    const uint32_t nf = u32();
+    std::vector<uint32_t> counts(nf);
+    for (auto &c : counts) c = u32();
+    const uint32_t ni = u32();
+    std::vector<uint32_t> idx(ni);
+    for (auto &i : idx) i = u32();
+
+    NavBuild nb;
+    std::vector<uint32_t> remap(nv);
+    for (uint32_t i = 0; i < nv; i++) {
+        uint32_t found = UINT32_MAX;
+        for (uint32_t j = 0; j < (uint32_t)nb.verts.size(); j++) {
+            if (std::memcmp(&raw[3 * (size_t)i], &nb.verts[j], 12) == 0) {
+                found = j;
+                break;
+            }
+        }
+        if (found == UINT32_MAX) {
+            found = (uint32_t)nb.verts.size();
+            nb.verts.push_back(v3(raw[3 * (size_t)i], raw[3 * (size_t)i + 1], raw[3 * (size_t)i + 2]));
+        }
+        remap[i] = found;
+    }
+    size_t start = 0;
+    for (uint32_t fc : counts) {
+        if (start + fc > idx.size()) throw std::runtime_error("oracle: navmesh.bin face out of range");
+        for (uint32_t k = 2; k < fc; k++) {
+            const uint32_t a = idx[start], b = idx[start + k - 1], c = idx[start + k];
+            if (a >= nv || b >= nv || c >= nv) throw std::runtime_error("oracle: navmesh.bin index out of range");
+            nb.tri.push_back(remap[a]);
+            nb.tri.push_back(remap[b]);
+            nb.tri.push_back(remap[c]);
+        }
+        start += fc;
+    }
+    const int T = (int)(nb.tri.size() / 3);
+    nb.adj.assign((size_t)T * 3, -1);
+    for (int t = 0; t < T; t++) {
+        for (int e = 0; e < 3; e++) {
+            const uint32_t p = nb.tri[3 * t + e], q = nb.tri[3 * t + (e + 1) % 3];
+            for (int u = 0; u < T && nb.adj[3 * t + e] == -1; u++) {
+                if (u == t) continue;
+                for (int e2 = 0; e2 < 3; e2++) {
+                    const uint32_t p2 = nb.tri[3 * u + e2], q2 = nb.tri[3 * u + (e2 + 1) % 3];
+                    if ((p2 == p && q2 == q) || (p2 == q && q2 == p)) {
+                        nb.adj[3 * t + e] = u;
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    return nb;
+}
+
+// mgr.cpp:948-1153 NavUtils, restated as text.
+struct NavAStar {
+    const NavBuild &nm;
+    int numTris;
+    // NavUtils::Node (mgr.cpp:953-967)
+    struct NodeS {
+        int idx, cameFrom;
+        float startDist, score;
+    };
+    std::vector<NodeS> state;
+    // EarlyOutData (mgr.cpp:1001-1053)
+    int earlyOutForDir[9];
+    float totalDistance = 0.f, reasonableDistance2 = 0.f;
+    bool enabled = false;
+
+    explicit NavAStar(const NavBuild &m) : nm(m), numTris((int)(m.tri.size() / 3)), state(numTris) {}
+
+    // mgr.cpp:969-977: center += v / 3 per vertex, in order
+    Vec3 centerOfTri(int t) const
+    {
+        Vec3 c = v3(0.f, 0.f, 0.f);
+        for (int i = 0; i < 3; i++) c = c + nm.verts[nm.tri[t * 3 + i]] / 3.0f;
+        return c;
+    }
+
+    // mgr.cpp:1008-1037
+    void init()
+    {
+        const int reasonableNavTriCount = 400;
+        if (numTris <= reasonableNavTriCount) {
+            enabled = false;
+            return;
+        }
+        enabled = true;
+        Vec3 mins = v3(kFltMax, kFltMax, kFltMax), maxs = v3(-kFltMax, -kFltMax, -kFltMax);
+        for (const Vec3 &v : nm.verts) {
+            mins = v3(fminD(mins.x, v.x), fminD(mins.y, v.y), fminD(mins.z, v.z));
+            maxs = v3(fmaxD(maxs.x, v.x), fmaxD(maxs.y, v.y), fmaxD(maxs.z, v.z));
+        }
+        const float d = length(maxs - mins);
+        totalDistance = d;
+        reasonableDistance2 = d * (float)reasonableNavTriCount / (float)numTris;
+        reasonableDistance2 *= reasonableDistance2;
+    }
+
+    // mgr.cpp:1041-1051
+    int getEarlyOutPath(Vec3 start, Vec3 target) const
+    {
+        if (!enabled) return -1;
+        if (length2(start - target) < reasonableDistance2) return -1;
+        Vec3 dir = normalize(target - start);
+        int dx = (int)(dir.x * 1.9f), dy = (int)(dir.y * 1.9f);
+        return earlyOutForDir[(dx + 1) + (dy + 1) * 3];
+    }
+
+    // mgr.cpp:1055-1114: the open set is a std::set ordered by each
+    // triangle's *current* score (mutated while it sits in the set).
+    int pathfindToTri(int startTri, int posTri)
+    {
+        const Vec3 start = centerOfTri(startTri), pos = centerOfTri(posTri);
+        const int early = getEarlyOutPath(start, pos);
+        if (early != -1) return early;
+        for (int t = 0; t < numTris; t++) state[t] = NodeS { t, -1, kFltMax, kFltMax };
+        state[startTri].startDist = 0.0f;
+        auto sortHeap = [this](const int &l, const int &r) { return state[l].score < state[r].score; };
+        std::set<int, decltype(sortHeap)> heap(sortHeap);
+        heap.insert(startTri);
+        while (!heap.empty()) {
+            const int thisTri = *heap.begin();
+            if (thisTri == posTri) {
+                int goal = thisTri;
+                while (goal != startTri && goal != -1) {
+                    if (state[goal].cameFrom == startTri) return goal;
+                    goal = state[goal].cameFrom;
+                }
+                return posTri;
+            }
+            heap.erase(heap.begin());
+            const Vec3 center = thisTri == startTri ? start : centerOfTri(thisTri);
+            for (int i = 0; i < 3; i++) {
+                const int neighbor = nm.adj[thisTri * 3 + i];
+                if (neighbor == -1) continue;
+                const Vec3 neighpos = centerOfTri(neighbor);
+                const float score = state[thisTri].startDist + length(center - neighpos);
+                if (score < state[neighbor].startDist) {
+                    state[neighbor].cameFrom = thisTri;
+                    state[neighbor].startDist = score;
+                    state[neighbor].score = score + length(neighpos - pos);
+                    heap.insert(neighbor);
+                }
+            }
+        }
+        return -1;
+    }
+
+    // mgr.cpp:1116-1150
+    void prepareForStartTri(int startTri)
+    {
+        if (!enabled) return;
+        enabled = false;
+        for (int dirX = -1; dirX <= 1; dirX++) {
+            for (int dirY = -1; dirY <= 1; dirY++) {
+                if (dirX == 0 && dirY == 0) continue;
+                const Vec3 dir = normalize(v3((float)dirX, (float)dirY, 0.0f));
+                const Vec3 start = centerOfTri(startTri);
+                const Vec3 end = start + dir * totalDistance * 2.0f;
+                float bestDist = kFltMax;
+                int bestTri = -1;
+                for (int t = 0; t < numTris; t++) {
+                    const float d = length(centerOfTri(t) - end);
+                    if (d < bestDist) {
+                        bestDist = d;
+                        bestTri = t;
+                    }
+                }
+                earlyOutForDir[(dirX + 1) + (dirY + 1) * 3] = pathfindToTri(startTri, bestTri);
+            }
+        }
+        enabled = true;
+    }
+};
+
+// mgr.cpp:1155-1211 buildAStarLookup (the .astar disk cache is not read:
+// the oracle always computes the table it checks the product against).
+std::vector<int32_t> buildAStarLookup(const NavBuild &nm)
+{
+    NavAStar as(nm);
+    as.init();
+    const int T = as.numTris;
+    std::vector<int32_t> tbl((size_t)T * T);
+    for (int s = 0; s < T; s++) {
+        as.prepareForStartTri(s);
+        for (int g = 0; g < T; g++) tbl[(size_t)s * T + g] = as.pathfindToTri(s, g);
+    }
+    return tbl;
+}
+
 // map_importer.cpp:508-567 (spawns, zones) and 223-256 (world bounds)
 void loadScene(Oracle &o)
 {
@@ -2929,14 +3170,23 @@ void *oracle_create(const oracle_config *cfg)
         for (int i = 0; i < cfg->num_bvh_verts; i++)
             o->verts[i] = v3(cfg->bvh_verts[3 * i], cfg->bvh_verts[3 * i + 1], cfg->bvh_verts[3 * i + 2]);
         if (o->simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) addMiddleSpawnCells(*o);
-        if (cfg->nav_tris && cfg->astar && cfg->num_nav_tris > 0) {
-            o->numNavTris = cfg->num_nav_tris;
-            o->navTris.resize((size_t)cfg->num_nav_tris * 3);
-            for (int i = 0; i < cfg->num_nav_tris * 3; i++)
-                o->navTris[i] = v3(cfg->nav_tris[3 * i], cfg->nav_tris[3 * i + 1], cfg->nav_tris[3 * i + 2]);
-            o->astar.assign(cfg->astar, cfg->astar + (size_t)cfg->num_nav_tris * cfg->num_nav_tris);
-            o->navCdf.resize(cfg->num_nav_tris);
-            navAreaCDF(cfg->nav_tris, cfg->num_nav_tris, o->navCdf.data());
+        {
+            // bots' navmesh and A* table, built here from navmesh.bin
+            NavBuild nb = navFromFile(o->scenePath + "/navmesh.bin");
+            const int T = (int)(nb.tri.size() / 3);
+            o->numNavTris = T;
+            o->navTris.resize((size_t)T * 3);
+            std::vector<float> flat((size_t)T * 9);
+            for (int i = 0; i < T * 3; i++) {
+                o->navTris[i] = nb.verts[nb.tri[i]];
+                flat[3 * i] = o->navTris[i].x;
+                flat[3 * i + 1] = o->navTris[i].y;
+                flat[3 * i + 2] = o->navTris[i].z;
+            }
+            o->navAdj = nb.adj;
+            o->astar = buildAStarLookup(nb);
+            o->navCdf.resize(T);
+            if (T > 0) navAreaCDF(flat.data(), T, o->navCdf.data());
         }
         // sim.cpp:5855 maxDist; 5869-5882 frustumData
         o->maxDist = length(o->worldBounds.pMax - o->worldBounds.pMin);
@@ -3171,6 +3421,35 @@ double oracle_run_threaded(void *h, int32_t nsteps, int32_t nthreads, const int3
     for (auto &th : pool) th.join();
     auto t1 = std::chrono::steady_clock::now();
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+void oracle_cast_stats(int32_t leaf_read_two, uint64_t *out2)
+{
+    if (out2) {
+        out2[0] = g_casts.load();
+        out2[1] = g_zeroCasts.load();
+    }
+    if (leaf_read_two >= 0) {
+        g_leafReadTwo = leaf_read_two;
+        g_casts = 0;
+        g_zeroCasts = 0;
+    }
+}
+
+int oracle_navmesh(void *h, float *tris_out, int32_t *adj_out, int32_t *astar_out, int32_t *num_tris)
+{
+    const Oracle &o = *static_cast<Oracle *>(h);
+    const int T = o.numNavTris;
+    if (num_tris) *num_tris = T;
+    if (tris_out)
+        for (int i = 0; i < T * 3; i++) {
+            tris_out[3 * i] = o.navTris[i].x;
+            tris_out[3 * i + 1] = o.navTris[i].y;
+            tris_out[3 * i + 2] = o.navTris[i].z;
+        }
+    if (adj_out) std::copy(o.navAdj.begin(), o.navAdj.end(), adj_out);
+    if (astar_out) std::copy(o.astar.begin(), o.astar.end(), astar_out);
+    return 0;
 }
 
 int oracle_trace_ray(void *h, const float *org, const float *d, float *t_out)

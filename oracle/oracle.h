@@ -29,12 +29,6 @@ typedef struct oracle_config {
     int32_t num_nodes;
     const float *bvh_verts;
     int32_t num_bvh_verts;
-    /* Navmesh triangles [T][3][3] and A* next-hop table [T][T] from the
-     * product's builder (mpenv_scene_navmesh; checked by tests/test_navmesh.py).
-     * Optional: without them bots (AgentPolicy == -1) are rejected. */
-    const float *nav_tris;
-    int32_t num_nav_tris;
-    const int32_t *astar;
     /* Task (MPENV_TASK_*): Zone or ZoneCaptureDefend. */
     int32_t task_type;
     /* RewardMode::Flank (train_flank, mgr.cpp:1746-1750) */
@@ -68,6 +62,18 @@ void oracle_set_curriculum(void *h, const void *snapshots, int32_t n);
  * 4 discrete + 2 aim).  Returns wall seconds. */
 double oracle_run_threaded(void *h, int32_t nsteps, int32_t nthreads,
                            const int32_t *ring, int32_t ring_len);
+
+/* The oracle's own navmesh (scene_path/navmesh.bin: dedup, fan
+ * triangulation, adjacency) and buildAStarLookup table (mgr.cpp:946-1211),
+ * built at oracle_create independently of the product's builder:
+ * tris [T][3][3], adjacency [T][3], next hop [T][T]; any pointer may be null. */
+int oracle_navmesh(void *h, float *tris_out, int32_t *adj_out, int32_t *astar_out, int32_t *num_tris);
+
+/* Analysis only: out2 = {sphere casts, casts that ended at
+ * t = 0} since the last reset; leaf_read_two >= 0 then resets the counters
+ * and sets the sphereCastLeaf read rule (1 = two consecutive triangles, the
+ * reference's; 0 = triSize triangles, for comparison). -1 only reads. */
+void oracle_cast_stats(int32_t leaf_read_two, uint64_t *out2);
 
 /* Geometry hooks for known-answer tests (mesh_bvh.inl restatement). */
 int oracle_trace_ray(void *h, const float *o, const float *d, float *t_out);

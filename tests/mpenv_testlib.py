@@ -70,7 +70,6 @@ class OracleConfig(C.Structure):
         ("sim_flags", C.c_uint32), ("team_size", C.c_uint32), ("world_id_offset", C.c_uint32),
         ("scene_path", C.c_char_p), ("bvh_nodes", C.c_void_p), ("num_nodes", C.c_int32),
         ("bvh_verts", C.c_void_p), ("num_bvh_verts", C.c_int32),
-        ("nav_tris", C.c_void_p), ("num_nav_tris", C.c_int32), ("astar", C.c_void_p),
         ("task_type", C.c_int32), ("train_flank", C.c_int32),
     ]
 
@@ -91,7 +90,7 @@ _libs = {}
 
 
 def ensure_built():
-    build_native.build_all()
+    build_native.build_all(force=False)
 
 
 def lib_mpenv():
@@ -112,6 +111,7 @@ def lib_mpenv():
         lib.mpenv_scene_navmesh.argtypes = [C.c_char_p, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
                                             C.c_void_p]
         lib.mpenv_trigger_reset.argtypes = [C.c_void_p, C.c_int32]
+        lib.mpenv_copy_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mpenv_set_hp.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
         lib.mpenv_enable_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
         lib.mpenv_kernel_timings.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_char_p),
@@ -144,6 +144,8 @@ def lib_oracle():
         lib.oracle_sphere_cast.restype = C.c_float
         lib.oracle_sphere_cast_brute.argtypes = [C.c_void_p, fp, fp, C.c_float]
         lib.oracle_sphere_cast_brute.restype = C.c_float
+        lib.oracle_navmesh.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.POINTER(C.c_int32)]
         lib.oracle_eval_math.argtypes = [C.c_int32, fp, fp, fp, C.c_int32]
         lib.oracle_threefry.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)]
         lib.oracle_tape_actions.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32,
@@ -263,11 +265,9 @@ class Oracle:
                  world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None, flank=False):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
-        self.nav_tris, _, self.astar = scene_navmesh(scene)
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
                            world_id_offset, scene.encode(), self.nodes.ctypes.data,
-                           len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3,
-                           self.nav_tris.ctypes.data, len(self.nav_tris), self.astar.ctypes.data, task,
+                           len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3, task,
                            int(flank))
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
@@ -302,6 +302,17 @@ class Oracle:
             self.lib.oracle_refresh_debug(self.h)
         return self.view(name).copy()
 
+    def navmesh(self):
+        """The oracle's own (tri_verts [T,3,3], adjacency [T,3], astar [T,T])."""
+        nt = C.c_int32(0)
+        self.lib.oracle_navmesh(self.h, None, None, None, C.byref(nt))
+        T = nt.value
+        tv = np.zeros((T, 3, 3), np.float32)
+        adj = np.zeros((T, 3), np.int32)
+        astar = np.zeros((T, T), np.int32)
+        self.lib.oracle_navmesh(self.h, tv.ctypes.data, adj.ctypes.data, astar.ctypes.data, C.byref(nt))
+        return tv, adj, astar
+
     def put_ctrl(self, ctrl):
         self.view("SIM_CONTROL")[:] = np.asarray(ctrl, np.int32).reshape(self.view("SIM_CONTROL").shape)
 
@@ -323,6 +334,19 @@ class HipMem:
         self.hip = C.CDLL("libamdhip64.so")
         self.hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         self.hip.hipDeviceSynchronize.argtypes = []
+        self.hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        self.hip.hipFree.argtypes = [C.c_void_p]
+
+    def upload(self, arr):
+        """A device copy of arr (caller frees with free())."""
+        arr = np.ascontiguousarray(arr)
+        p = C.c_void_p()
+        assert self.hip.hipMalloc(C.byref(p), arr.nbytes) == 0, "hipMalloc failed"
+        self.h2d(p.value, arr)
+        return p.value
+
+    def free(self, ptr):
+        self.hip.hipFree(ptr)
 
     def d2h(self, ptr, nbytes, out):
         rc = self.hip.hipMemcpy(out.ctypes.data, ptr, nbytes, 2)
@@ -382,6 +406,16 @@ class Engine:
         out = np.empty((r1 - r0,) + tuple(shape[1:]), dtype=dt)
         self.mem.d2h(ptr + r0 * row, out.nbytes, out)
         return out
+
+    def put_rows(self, name, r0, arr):
+        """Overwrite rows [r0, r0 + len(arr)) of the leading dimension."""
+        ptr, dt, shape = self.desc(name)
+        row = int(np.prod(shape[1:])) * 4
+        self.mem.h2d(ptr + r0 * row, np.ascontiguousarray(arr, dtype=dt))
+
+    def copy_actions(self, dev_ptr):
+        """Step inputs from device memory [A][6] i32 (gpuStreamStep's copy)."""
+        assert self.lib.mpenv_copy_actions(self.h, dev_ptr, None) == 0, self.lib.mpenv_last_error().decode()
 
     def trigger_reset(self, w):
         assert self.lib.mpenv_trigger_reset(self.h, w) == 0

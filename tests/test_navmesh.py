@@ -102,6 +102,18 @@ def test_astar_table_hash_pinned(nav):
 ASTAR_SHA = "a48eb31bcb62a317"
 
 
+def test_oracle_builds_the_same_navmesh_and_astar_table(nav):
+    """The oracle restates navmesh.bin import + dedup + fan + adjacency and
+    buildAStarLookup (mgr.cpp:946-1211) on its own; the product's tables
+    must match it byte for byte."""
+    o = T.Oracle(1, 1)
+    tv, adj, astar = o.navmesh()
+    o.close()
+    assert tv.tobytes() == np.ascontiguousarray(nav[0]).tobytes()
+    assert adj.tobytes() == np.ascontiguousarray(nav[1]).tobytes()
+    assert astar.tobytes() == np.ascontiguousarray(nav[2]).tobytes()
+
+
 def test_oracle_bot_rollout_runs():
     """Team 1 as A* bots (AgentPolicy = -1) in the oracle: bots act (fire,
     move) and the rollout stays finite."""

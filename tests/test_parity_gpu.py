@@ -246,40 +246,108 @@ def test_curriculum_resets_match_oracle():
         o.close()
 
 
-def test_headline_batch_shards_match_oracle():
-    """C3 size (6v6 x 16384 worlds): slices of the engine's batch against
-    oracle runs of the same global worlds (world_id_offset) — bit-exact."""
-    ts, W, steps = 6, 16384, 40
+LONG = [
+    # team_size, worlds (the configuration's full batch), steps, probe world offsets
+    (6, 16384, 3100, [0, 4097, 12345, 16384 - 3]),   # C3, the headline batch
+    (3, 4096, 3100, [0, 1001, 2050, 4096 - 3]),      # C2
+]
+
+
+@pytest.mark.parametrize("ts,W,steps,probes", LONG, ids=["C3_6v6x16384", "C2_3v3x4096"])
+def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
+    """A full configuration batch (C3 / C2 size) stepped past one whole
+    episode (3,000 steps, consts.hpp episodeLen) against oracle runs of
+    3-world slices of the same global worlds (world_id_offset), bit-exact on
+    every STEP_OUTPUT and the internal state every 50 steps.
+
+    Actions: the bench's hash tape (ring of 64 steps resident in HBM, copied
+    by gpuStreamStep's input copy) with team slot 1 of every even world an A*
+    bot (AgentPolicy -1, planAStarAISystem), which walks to the zone and
+    holds it.  That drives the zone systems through their natural events
+    (sim.cpp:1892-1976 rotation after 600 controlled steps, 4470-4673 a point
+    every 20 controlled steps and the 3,000-step end).  A 125-point win needs
+    2,500 controlled steps, which the bots reach too rarely, so at steps
+    1000 and 2000 the learner-visible episode_results buffer
+    (pbt.episode_results = MATCH_RESULT, mgr.cpp:2252-2260, read and
+    accumulated in place by zoneMatchInfoSystem) is raised to 124 points per
+    team in the probed worlds, identically on both sides: the next point
+    earned ends the match by the 125-point rule (sim.cpp:4529-4532)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     N = 2 * ts
+    RING = 64
+    PW = 3  # worlds per probe slice
     e = T.Engine(W, ts)
     e.put_ctrl([0, 1, 1])
     e.init()
-    probes = [0, 4097, 12345, W - 3]
+    pol = np.zeros((W, 2, ts), np.int32)
+    pol[0::2, 1, :] = -1
+    e.put("AGENT_POLICY", pol.reshape(-1, 1))
+    ring = np.stack([T.mpenv_tape.tape_actions(1234, k, 0, W * N) for k in range(RING)])
+    dev_ring = e.mem.upload(ring)
     oracles = []
     for w0 in probes:
-        o = T.Oracle(3, ts, world_id_offset=w0)
+        o = T.Oracle(PW, ts, world_id_offset=w0)
         o.put_ctrl([0, 1, 1])
         o.init()
+        o.view("AGENT_POLICY")[:] = pol[w0:w0 + PW].reshape(-1, 1)
         oracles.append(o)
-    for s in range(steps):
-        e.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, W * N))
-        e.step()
+    names = T.STEP_OUTPUTS + ["DEBUG_AGENT_I32", "DEBUG_WORLD_I32", "DEBUG_AGENT_F32"]
+
+    def compare(s):
         for w0, o in zip(probes, oracles):
-            o.set_actions(T.mpenv_tape.tape_actions(1234, s, w0 * N, 3 * N))
-            o.step()
-        if s % 13 == 0 or s == steps - 1:
-            for w0, o in zip(probes, oracles):
-                for n in T.STEP_OUTPUTS:
-                    ptr, dt, shape = e.desc(n)
-                    rows_per_world = shape[0] // W  # 1 (world), 2 (team interface) or N (agent)
-                    r0, r1 = w0 * rows_per_world, (w0 + 3) * rows_per_world
-                    T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
+            for n in names:
+                _, _, shape = e.desc(n)
+                rpw = shape[0] // W  # rows per world: 1 (world), 2 (team interface) or N (agent)
+                T.compare(e.get_rows(n, w0 * rpw, (w0 + PW) * rpw), o.get(n), f"{n} worlds {w0}.. @ {s}")
+
+    ev = dict(rotations=0, points=0, wins=0, episode_ends=0, kills=0)
+    prev = [o.get("DEBUG_WORLD_I32").copy() for o in oracles]
+    prev_kills = [np.zeros(PW, np.int32) for _ in oracles]
+
+    def ostep(k, s):
+        o, w0 = oracles[k], probes[k]
+        o.set_actions(ring[s % RING, w0 * N:(w0 + PW) * N])
+        o.step()
+
+    compare("init")
+    with ThreadPoolExecutor(len(oracles)) as pool:
+        for s in range(steps):
+            if s in (1000, 2000):
+                for w0, o in zip(probes, oracles):
+                    mr = o.view("MATCH_RESULT")
+                    mr[:, 3] = np.maximum(mr[:, 3], 124)
+                    mr[:, 4] = np.maximum(mr[:, 4], 124)
+                    e.put_rows("MATCH_RESULT", w0, mr)
+            e.copy_actions(dev_ring + (s % RING) * W * N * 6 * 4)
+            e.step()
+            list(pool.map(lambda k: ostep(k, s), range(len(oracles))))
+            for k, o in enumerate(oracles):
+                o.lib.oracle_refresh_debug(o.h)
+                wi = o.view("DEBUG_WORLD_I32")
+                done = o.view("DONE").reshape(PW, N)[:, 0] == 1
+                mr = o.view("MATCH_RESULT")
+                ev["rotations"] += int(((wi[:, 3] != prev[k][:, 3]) & (wi[:, 1] == prev[k][:, 1] + 1)).sum())
+                ev["points"] += int(wi[:, 7].sum())
+                ev["wins"] += int((done & (np.maximum(mr[:, 3], mr[:, 4]) >= 125)).sum())
+                ev["episode_ends"] += int(done.sum())
+                kills = mr[:, 1] + mr[:, 2]
+                ev["kills"] += int(np.where(wi[:, 1] == prev[k][:, 1] + 1, np.maximum(kills - prev_kills[k], 0), 0).sum())
+                prev_kills[k] = kills.copy()
+                prev[k] = wi.copy()
+            if s % 50 == 49 or s == steps - 1:
+                compare(f"step {s}")
+    e.mem.free(dev_ring)
+    print(f"\n{ts}v{ts} x {W}, {steps} steps, {len(probes)} x {PW} probed worlds: {ev}")
+    # every zone/match event fired in the probed worlds
+    assert ev["rotations"] > 0 and ev["points"] > 0 and ev["wins"] > 0, ev
+    assert ev["episode_ends"] >= len(probes) * PW, ev  # every world passed a 3,000-step end or a win
     # size-independent properties over the whole batch
     hp = e.get("HP")
     assert np.isfinite(e.get("SELF_OBSERVATION")).all()
     assert ((hp >= 0) & (hp <= 100)).all()
-    lid = e.get("FWD_LIDAR")
-    assert np.isfinite(lid).all()
+    assert np.isfinite(e.get("FWD_LIDAR")).all()
+    e.close()
 
 
 def test_python_module_zero_copy_and_stream_step():

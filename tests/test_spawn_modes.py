@@ -61,7 +61,7 @@ def test_navmesh_spawns_lie_on_the_navmesh():
     o.put_ctrl([0, 0, 0])
     o.init()
     p = positions(o)
-    tris = o.nav_tris.reshape(-1, 3, 3)
+    tris = o.navmesh()[0]
     hit = []
     for pt in p:
         on = [t for t in range(len(tris)) if _in_triangle(pt, tris[t])]

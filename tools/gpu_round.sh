@@ -1,4 +1,8 @@
+# GPU round check (run under gpurun): GPU tests, default bench, then the driver's short window.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
-timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && cat gpurun_out/bench.json
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_short.json 2> gpurun_out/bench_short.err && \
+cat gpurun_out/bench.json gpurun_out/bench_short.json
