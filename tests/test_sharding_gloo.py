@@ -17,7 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import mpenv_testlib as T
-from mpenv_dist import shard_worlds, gather_to_learner
+from mpenv_dist import LearnerGather, shard_worlds, gather_to_learner
 
 TOTAL_WORLDS, TEAM, STEPS = 6, 2, 60
 OUTS = ["SELF_OBSERVATION", "FWD_LIDAR", "REWARD", "DONE", "HP", "MATCH_RESULT"]
@@ -76,3 +76,69 @@ def test_two_rank_shards_equal_single_run(tmp_path):
     full = _run(T.Oracle(TOTAL_WORLDS, TEAM), 0, TOTAL_WORLDS * 2 * TEAM)
     for k, name in enumerate(OUTS):
         np.testing.assert_array_equal(got[f"arr_{k}"], full[k].numpy(), err_msg=name)
+
+
+# trainInterface outputs (mgr.cpp:2383-2431, csrc/manager.cpp TIEntry) ->
+# oracle export names; agent_map / unmasked_agent_map are not shipped.
+TRAIN_OUTPUTS = {
+    "fwd_lidar": "FWD_LIDAR", "rear_lidar": "REAR_LIDAR", "hp": "HP", "magazine": "MAGAZINE",
+    "alive": "ALIVE", "self": "SELF_OBSERVATION", "filters_state": "FILTERS_STATE",
+    "teammates": "TEAMMATE_OBSERVATIONS", "opponents": "OPPONENT_OBSERVATIONS",
+    "opponents_last_known": "OPPONENT_LAST_KNOWN_OBSERVATIONS", "self_pos": "SELF_POSITION",
+    "teammate_positions": "TEAMMATE_POSITIONS", "opponent_positions": "OPPONENT_POSITIONS",
+    "opponent_last_known_positions": "OPPONENT_LAST_KNOWN_POSITIONS", "opponent_masks": "OPPONENT_MASKS",
+    "reward_coefs": "REWARD_HYPER_PARAMS", "rewards": "REWARD", "dones": "DONE",
+    "pbt.episode_results": "MATCH_RESULT",
+}
+LG_STEPS = 40
+
+
+def _lg_worker(rank, world_size, port, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        off, cnt = shard_worlds(TOTAL_WORLDS, rank, world_size)
+        N = 2 * TEAM
+        o = T.Oracle(cnt, TEAM, world_id_offset=off)
+        o.put_ctrl([0, 1, 1])
+        o.init()
+        # zero-copy views of the rank's live outputs, as train_interface() hands out
+        src = {n: torch.from_numpy(o.view(e)) for n, e in TRAIN_OUTPUTS.items()}
+        lg = LearnerGather(src, dst=0)
+        slots = {}
+        for s in range(LG_STEPS):
+            o.set_actions(T.mpenv_tape.tape_actions(1234, s, off * N, cnt * N))
+            o.step()
+            slots[s] = lg.submit()
+        lg.drain()
+        if rank == 0:
+            out = {}
+            for s in (LG_STEPS - 2, LG_STEPS - 1):  # both ring slots hold a completed step
+                for n, t in lg.outputs(slots[s]).items():
+                    out[f"{s}:{n}"] = t.reshape((-1,) + tuple(t.shape[2:])).numpy().copy()
+            np.savez(result_path, **out)
+        lg.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_learner_gather_ships_every_train_output_in_global_order(tmp_path):
+    """LearnerGather (C4's learner exchange): every trainInterface output of
+    both ranks lands on rank 0 in one flat double-buffered gather per step;
+    the two ring slots hold the last two steps, and flattening the rank axis
+    gives the single-run tensors in global world order."""
+    path = str(tmp_path / "lg.npz")
+    mp.spawn(_lg_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    got = np.load(path)
+    o = T.Oracle(TOTAL_WORLDS, TEAM)
+    o.put_ctrl([0, 1, 1])
+    o.init()
+    A = TOTAL_WORLDS * 2 * TEAM
+    for s in range(LG_STEPS):
+        o.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, A))
+        o.step()
+        if s >= LG_STEPS - 2:
+            for n, e in TRAIN_OUTPUTS.items():
+                np.testing.assert_array_equal(got[f"{s}:{n}"], o.get(e), err_msg=f"{n} @ {s}")
+    assert len(TRAIN_OUTPUTS) == 19  # 21 outputs minus the two never-written agent maps
