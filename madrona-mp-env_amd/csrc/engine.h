@@ -167,6 +167,7 @@ struct GoalRegionDev {
 // Read-only scene + task constants, passed by value as a kernel argument.
 struct SceneDev {
     const BVHNode *nodes;
+    const BVHNode *octNodes; // [8][numNodes] octant node images (scene.h octantNodeImages)
     const float *verts;     // 3 floats per vertex, 3 vertices per triangle
     // Per triangle, ray-independent terms of sphereCastTriangle
     // (mesh_bvh.inl:885-1127): unit normal xyz, |normal|, |e01|^2, |e02|^2,
@@ -222,6 +223,7 @@ enum KernelId { kKMove = 0, kKSim = 1, kKVis = 2, kKObs = 3, kKLidar = 4, kNumTi
 const char *kernelName(int k);
 size_t bvhLdsBytes(const SceneDev &sc);
 size_t bvhLdsBytesSphere(const SceneDev &sc); // + triPre (sphere-casting kernels)
+size_t bvhLdsBytesOct(const SceneDev &sc);    // octant node images + vertices (k_lidar)
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t ctor_train_ctrl[3], void *stream);
 int launchResetOnly(const DevState &s, const SceneDev &sc, void *stream);

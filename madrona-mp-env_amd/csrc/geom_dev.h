@@ -132,6 +132,34 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
     return b;
 }
 
+// k_lidar's LDS image: the 8 octant node images (scene.h octantNodeImages,
+// 8 x numNodes x 64 B) then the vertices as float4.  The traversal of a ray
+// reads image (d.x < 0) | (d.y < 0) << 1 | (d.z < 0) << 2.
+__device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
+{
+    const int node_q = sc.numNodes * 4 * 8;
+    const uint4 *src_n = reinterpret_cast<const uint4 *>(sc.octNodes);
+    uint4 *dst_n = reinterpret_cast<uint4 *>(smem);
+    for (int k = threadIdx.x; k < node_q; k += blockDim.x) dst_n[k] = src_n[k];
+    const float *src_v = sc.verts;
+    float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
+    for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
+        dst_v[k] = make_float4(src_v[3 * k], src_v[3 * k + 1], src_v[3 * k + 2], 0.f);
+    __syncthreads();
+    LBVH b;
+    b.nodes = (const MP_LDS BVHNode *)(smem);
+    b.verts = (const MP_LDS float *)(smem + (size_t)node_q * 16);
+    b.pre = nullptr;
+    b.snodes = nullptr;
+    b.stats = nullptr;
+    return b;
+}
+
+__device__ __forceinline__ int rayOctant(mp::Vec3 d)
+{
+    return (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
+}
+
 typedef float lf4 __attribute__((ext_vector_type(4)));
 typedef uint32_t lu4 __attribute__((ext_vector_type(4)));
 

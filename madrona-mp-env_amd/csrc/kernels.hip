@@ -2481,7 +2481,14 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
 #define MPENV_LIDAR_ITERS 4 // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 ms (k_lidar alone, C3)
 #endif
 constexpr int kLidarIters = MPENV_LIDAR_ITERS;
-constexpr int kLidarWaves = kBlock / 64;
+// 1024-thread blocks: the 8 octant node images + vertices (43 KB on
+// simple_map) are staged once per 16 waves, so 2 blocks per CU (8 waves per
+// SIMD) fit the 160 KB of LDS.
+#ifndef MPENV_LIDAR_BLOCK
+#define MPENV_LIDAR_BLOCK 1024
+#endif
+constexpr int kLidarBlock = MPENV_LIDAR_BLOCK;
+constexpr int kLidarWaves = kLidarBlock / 64;
 
 __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A + 3) / 4) * 5; }
 
@@ -2492,7 +2499,7 @@ __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A +
 #endif
 #define MP_LIDAR_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_LIDAR_WPE)))
 
-__global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, SceneDev sc, int iters)
+__global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S, SceneDev sc, int iters)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // Ray-fan directions (sim.cpp:3324-3506): theta depends only on the ray
@@ -2508,7 +2515,7 @@ __global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, Scen
         const float theta = range * (float(x) / float(width - 1)) + offset;
         fan[threadIdx.x] = make_float2(-cosf_(theta), sinf_(theta));
     }
-    const LBVH bvh = stageBVH(smem, sc); // ends with __syncthreads
+    const LBVH bvh = stageBVHOct(smem, sc); // ends with __syncthreads
     const uint32_t N = (uint32_t)S.N, T = (uint32_t)S.T;
     const uint32_t A = (uint32_t)S.A;
     const uint32_t ntasks = (uint32_t)lidarTasks(S.A);
@@ -2539,7 +2546,11 @@ __global__ void __launch_bounds__(kBlock) MP_LIDAR_ATTR k_lidar(DevState S, Scen
         ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
         const float2 cs = fan[fwd ? x : 32 + x];
         Vec3 dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
-        WorldHit hw = traceWorldD(bvh, S.px, S.py, S.pz, g0, (int)N, ray_o, dir);
+        // the ray's octant image: same nodes and leaves, near-first slot
+        // order (scene.h octantNodeImages); the oracle visits the same order
+        LBVH ob = bvh;
+        ob.nodes = bvh.nodes + rayOctant(dir) * sc.numNodes;
+        WorldHit hw = traceWorldD(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir);
         const bool second = i >= T; // team of the casting agent
         float4 out;
         if (hw.hit) {
@@ -2686,6 +2697,11 @@ size_t bvhLdsBytesSphere(const SceneDev &sc)
 }
 
 
+size_t bvhLdsBytesOct(const SceneDev &sc)
+{
+    return (size_t)sc.numNodes * 64 * 8 + (size_t)sc.numVerts * 16;
+}
+
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
@@ -2755,7 +2771,8 @@ int launchLidar(const DevState &s, const SceneDev &sc, void *stream)
     const int iters = (int)std::max<int64_t>(1, std::min<int64_t>(kLidarIters, tasks / (kLidarWaves * 1024)));
     const int64_t per_block = (int64_t)kLidarWaves * iters;
     const int blocks = (int)((tasks + per_block - 1) / per_block);
-    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc, iters);
+    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(kLidarBlock), bvhLdsBytesOct(sc), (hipStream_t)stream, s, sc,
+                       iters);
     return check(hipGetLastError());
 }
 

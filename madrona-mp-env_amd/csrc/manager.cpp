@@ -388,6 +388,12 @@ static void buildSceneDev(mpenv_manager &m)
 
     BVHNode *d_nodes = m.alloc<BVHNode>(s.nodes.size());
     m.upload(d_nodes, s.nodes.data(), sizeof(BVHNode) * s.nodes.size());
+    {
+        const std::vector<BVHNode> oct = octantNodeImages(s.nodes);
+        BVHNode *d_oct = m.alloc<BVHNode>(oct.size());
+        m.upload(d_oct, oct.data(), sizeof(BVHNode) * oct.size());
+        sc.octNodes = d_oct;
+    }
     float *d_verts = m.alloc<float>(s.bvhVerts.size() * 3);
     m.upload(d_verts, s.bvhVerts.data(), sizeof(float) * 3 * s.bvhVerts.size());
     auto upSpawns = [&](const std::vector<Spawn> &v) {

@@ -352,6 +352,49 @@ void buildBVH(const std::vector<Vec3> &tri_verts, Scene &out)
     out.maxStackAnyOrder = std::max(1, occ_any[0]);
 }
 
+std::vector<BVHNode> octantNodeImages(const std::vector<BVHNode> &nodes)
+{
+    const size_t n = nodes.size();
+    std::vector<BVHNode> out(8 * n);
+    for (int oct = 0; oct < 8; oct++) {
+        const double sgn[3] = { (oct & 1) ? -1.0 : 1.0, (oct & 2) ? -1.0 : 1.0, (oct & 4) ? -1.0 : 1.0 };
+        for (size_t ni = 0; ni < n; ni++) {
+            const BVHNode &nd = nodes[ni];
+            const int8_t ex[3] = { nd.expX, nd.expY, nd.expZ };
+            const float mn[3] = { nd.minX, nd.minY, nd.minZ };
+            const uint8_t *qlo[3] = { nd.qMinX, nd.qMinY, nd.qMinZ };
+            const uint8_t *qhi[3] = { nd.qMaxX, nd.qMaxY, nd.qMaxZ };
+            double key[4];
+            for (int i = 0; i < 4; i++) {
+                key[i] = 0.0;
+                for (int a = 0; a < 3; a++)
+                    key[i] += sgn[a] * ((double)mn[a] + std::ldexp(0.5 * ((double)qlo[a][i] + (double)qhi[a][i]), ex[a]));
+            }
+            std::vector<int> leaves, inner, empty;
+            for (int i = 0; i < 4; i++) {
+                if (nd.children[i] == -1) empty.push_back(i);
+                else if (nd.children[i] & 0x80000000) leaves.push_back(i);
+                else inner.push_back(i);
+            }
+            std::stable_sort(leaves.begin(), leaves.end(), [&](int a, int b) { return key[a] < key[b]; });
+            std::stable_sort(inner.begin(), inner.end(), [&](int a, int b) { return key[a] > key[b]; });
+            std::vector<int> ord = leaves;
+            ord.insert(ord.end(), inner.begin(), inner.end());
+            ord.insert(ord.end(), empty.begin(), empty.end());
+            BVHNode p = nd;
+            for (int k = 0; k < 4; k++) {
+                const int i = ord[k];
+                p.triSize[k] = nd.triSize[i];
+                p.qMinX[k] = nd.qMinX[i]; p.qMinY[k] = nd.qMinY[i]; p.qMinZ[k] = nd.qMinZ[i];
+                p.qMaxX[k] = nd.qMaxX[i]; p.qMaxY[k] = nd.qMaxY[i]; p.qMaxZ[k] = nd.qMaxZ[i];
+                p.children[k] = nd.children[i];
+            }
+            out[oct * n + ni] = p;
+        }
+    }
+    return out;
+}
+
 Scene loadScene(const std::string &dir, bool spawn_in_middle)
 {
     Scene s;

@@ -106,4 +106,16 @@ void buildNavMesh(Scene &s, const std::string &navmesh_path);
 // Builds the compressed 4-wide BVH over de-indexed triangles.
 void buildBVH(const std::vector<mp::Vec3> &tri_verts, Scene &out);
 
+// Octant node images for closest-hit rays (k_lidar): 8 copies of the node
+// array, copy o for rays whose direction signs are o (bit 0 x < 0, bit 1
+// y < 0, bit 2 z < 0).  In each copy a node's child slots are permuted --
+// leaf children first, nearest first, then internal children farthest
+// first, then empty slots -- where "near" orders the child boxes' centres
+// by their projection on the octant's diagonal (computed in double, ties
+// by slot).  The reference's traversal loop over such a copy (slots in
+// order, internal children pushed on a LIFO stack) therefore tests a
+// node's leaves near-to-far and pops its nearest internal child first.
+// Node indices, bounds and leaves are unchanged; only slot order differs.
+std::vector<BVHNode> octantNodeImages(const std::vector<BVHNode> &nodes);
+
 } // namespace mpenv

@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -240,6 +241,10 @@ struct Oracle {
     struct ZOBB { Vec3 pMin, pMax; float rotation; } subZones[8]; // level_gen.cpp:282-326
     std::vector<int32_t> astar;  // [T][T] (buildAStarLookup, built by the oracle)
     std::vector<int32_t> navAdj; // [T][3]
+    // Lidar child visit order (cfg.lidar_octant_order): per ray octant and
+    // node, the slot visited k-th (octantOrder()).
+    bool lidarOctant = false;
+    std::vector<int8_t> octOrder; // [8][numNodes][4]
     int numNavTris = 0;
     std::vector<Vec3> verts;
     std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
@@ -351,8 +356,12 @@ bool rayTriangleIntersection(Vec3 ta, Vec3 tb, Vec3 tc, const RayTxfm &tx, Vec3 
 float expScale(int8_t e) { return u2f((uint32_t)((int32_t)e + 127) << 23); }
 
 // mesh_bvh.inl:110-208 (MeshBVH::traceRay) + 360-431 (traceRayLeaf)
-bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_max = kFltMax)
+bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_max = kFltMax, bool octant = false)
 {
+    // octant: visit each node's child slots in the order octantOrder()
+    // defines for the ray's direction signs (the lidar's documented child
+    // order); otherwise slot order, as mesh_bvh.inl:160-204.
+    const int oct = (ray_d.x < 0.f ? 1 : 0) | (ray_d.y < 0.f ? 2 : 0) | (ray_d.z < 0.f ? 4 : 0);
     const float diveps = 0.0000001f;
     Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
     RayTxfm tx = computeRayIsectTxfm(ray_d, inv_d);
@@ -373,7 +382,8 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
         float originQuantX = (node.minX - ray_o.x) * rayXInv;
         float originQuantY = (node.minY - ray_o.y) * rayYInv;
         float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
-        for (int i = 0; i < 4; i++) {
+        for (int slot = 0; slot < 4; slot++) {
+            const int i = octant ? o.octOrder[((size_t)oct * o.nodes.size() + node_idx) * 4 + slot] : slot;
             if (node.children[i] == -1) continue;
             // q * dirQuant + originQuant, fused: the reference's GPU build is
             // compiled with NVRTC's default --fmad=true, which contracts it
@@ -601,11 +611,11 @@ struct HitResult {
 };
 
 // utils.cpp:10-72 traceRayAgainstWorld
-HitResult traceRayAgainstWorld(const Oracle &o, int w, Vec3 org, Vec3 d)
+HitResult traceRayAgainstWorld(const Oracle &o, int w, Vec3 org, Vec3 d, bool octant = false)
 {
     float min_hit_t = kFltMax;
     float t_bvh;
-    bool hit = bvhTraceRay(o, org, d, &t_bvh);
+    bool hit = bvhTraceRay(o, org, d, &t_bvh, kFltMax, octant);
     if (hit) min_hit_t = t_bvh;
     int hit_entity = -1;
     for (int j = 0; j < o.N; j++) {
@@ -2508,7 +2518,7 @@ void pvpLidar(Oracle &o, int w, int i)
         float x = -cosf_(theta);
         float y = sinf_(theta);
         Vec3 dir = normalize(x * right + y * fwd);
-        HitResult h = traceRayAgainstWorld(o, w, ray_o, dir);
+        HitResult h = traceRayAgainstWorld(o, w, ray_o, dir, o.lidarOctant);
         if (h.hit) {
             bool wall = h.entity == -1;
             bool tm = !wall && o.agent(w, h.entity).team == ag.team;
@@ -2805,6 +2815,53 @@ void addMiddleSpawnCells(Oracle &o)
             (x >= dim / 2 ? o.bSpawns : o.aSpawns).push_back(sp);
         }
     }
+}
+
+// ------------------------------------------------------- lidar child order
+// The documented lidar child order ("child visit order"): for
+// a ray whose direction signs are octant `oct` (bit 0 x < 0, bit 1 y < 0,
+// bit 2 z < 0), a node's leaf children first, by ascending key, then its
+// internal children by descending key, then empty slots; key = the child
+// box centre projected on the octant diagonal, sum over axes a of
+// s_a * (min_a + 2^exp_a * (qMin_a + qMax_a) / 2), in double; ties keep slot
+// order.  With the LIFO stack this tests leaves near-to-far and pops the
+// nearest internal child first.  The reference visits slots in order
+// (mesh_bvh.inl:160-204) on an Embree tree whose slot order is unpinned;
+// closest hits agree with slot order up to exact ties between distinct
+// coplanar triangles (tools/lidar_order_check.py).
+std::vector<int8_t> octantOrder(const std::vector<Node> &nodes)
+{
+    const size_t n = nodes.size();
+    std::vector<int8_t> ord(8 * n * 4);
+    for (int oct = 0; oct < 8; oct++) {
+        const double s[3] = { (oct & 1) ? -1.0 : 1.0, (oct & 2) ? -1.0 : 1.0, (oct & 4) ? -1.0 : 1.0 };
+        for (size_t ni = 0; ni < n; ni++) {
+            const Node &nd = nodes[ni];
+            double key[4];
+            for (int i = 0; i < 4; i++) {
+                const double cx = (double)nd.minX + std::ldexp(0.5 * ((double)nd.qMinX[i] + (double)nd.qMaxX[i]), nd.expX);
+                const double cy = (double)nd.minY + std::ldexp(0.5 * ((double)nd.qMinY[i] + (double)nd.qMaxY[i]), nd.expY);
+                const double cz = (double)nd.minZ + std::ldexp(0.5 * ((double)nd.qMinZ[i] + (double)nd.qMaxZ[i]), nd.expZ);
+                key[i] = 0.0;
+                key[i] += s[0] * cx;
+                key[i] += s[1] * cy;
+                key[i] += s[2] * cz;
+            }
+            // class: 0 leaf, 1 internal, 2 empty; insertion sort (stable)
+            int slots[4] = { 0, 1, 2, 3 };
+            auto cls = [&](int i) { return nd.children[i] == -1 ? 2 : (nd.children[i] & 0x80000000) ? 0 : 1; };
+            auto before = [&](int a, int b) {
+                if (cls(a) != cls(b)) return cls(a) < cls(b);
+                if (cls(a) == 0) return key[a] < key[b];
+                if (cls(a) == 1) return key[a] > key[b];
+                return false;
+            };
+            for (int k = 1; k < 4; k++)
+                for (int j = k; j > 0 && before(slots[j], slots[j - 1]); j--) std::swap(slots[j], slots[j - 1]);
+            for (int k = 0; k < 4; k++) ord[((size_t)oct * n + ni) * 4 + k] = (int8_t)slots[k];
+        }
+    }
+    return ord;
 }
 
 // ------------------------------------------------------------ navmesh
@@ -3170,6 +3227,8 @@ void *oracle_create(const oracle_config *cfg)
         for (int i = 0; i < cfg->num_bvh_verts; i++)
             o->verts[i] = v3(cfg->bvh_verts[3 * i], cfg->bvh_verts[3 * i + 1], cfg->bvh_verts[3 * i + 2]);
         if (o->simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) addMiddleSpawnCells(*o);
+        o->lidarOctant = cfg->lidar_octant_order != 0;
+        o->octOrder = octantOrder(o->nodes);
         {
             // bots' navmesh and A* table, built here from navmesh.bin
             NavBuild nb = navFromFile(o->scenePath + "/navmesh.bin");

@@ -33,6 +33,10 @@ typedef struct oracle_config {
     int32_t task_type;
     /* RewardMode::Flank (train_flank, mgr.cpp:1746-1750) */
     int32_t train_flank;
+    /* Lidar child visit order: 0 = slot order (mesh_bvh.inl:160-204 as
+     * written), 1 = the octant order the product's k_lidar uses (DESIGN.md
+     * §2); closest hits differ only at exact coplanar ties. */
+    int32_t lidar_octant_order;
 } oracle_config;
 
 void *oracle_create(const oracle_config *cfg);

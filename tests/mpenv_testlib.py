@@ -70,7 +70,7 @@ class OracleConfig(C.Structure):
         ("sim_flags", C.c_uint32), ("team_size", C.c_uint32), ("world_id_offset", C.c_uint32),
         ("scene_path", C.c_char_p), ("bvh_nodes", C.c_void_p), ("num_nodes", C.c_int32),
         ("bvh_verts", C.c_void_p), ("num_bvh_verts", C.c_int32),
-        ("task_type", C.c_int32), ("train_flank", C.c_int32),
+        ("task_type", C.c_int32), ("train_flank", C.c_int32), ("lidar_octant_order", C.c_int32),
     ]
 
 
@@ -262,13 +262,14 @@ class Oracle:
     """CPU restatement of the reference step (test infrastructure)."""
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
-                 world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None, flank=False):
+                 world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None, flank=False,
+                 lidar_order="octant"):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
                            world_id_offset, scene.encode(), self.nodes.ctypes.data,
                            len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3, task,
-                           int(flank))
+                           int(flank), 1 if lidar_order == "octant" else 0)
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
         if curriculum:

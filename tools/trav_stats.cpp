@@ -91,8 +91,40 @@ static void traceVisits(const float *o, const float *d, Visit &v)
     }
 }
 
-static void trace(const float *o, const float *d, bool ftb, Stats &st)
+// Octant-ordered mode: per node, a static child order for each ray-direction
+// octant (children sorted by their box centre projected on the octant's
+// diagonal), so the nearer side is visited first without a per-ray sort.
+static std::vector<std::array<std::array<int, 4>, 8>> octOrder;
+
+static void buildOctOrder()
 {
+    octOrder.resize(nodes.size());
+    for (size_t ni = 0; ni < nodes.size(); ni++) {
+        const Node &n = nodes[ni];
+        float c[4][3];
+        for (int i = 0; i < 4; i++) {
+            float sx = std::ldexp(1.f, n.expX), sy = std::ldexp(1.f, n.expY), sz = std::ldexp(1.f, n.expZ);
+            c[i][0] = n.minX + sx * 0.5f * (n.qMinX[i] + n.qMaxX[i]);
+            c[i][1] = n.minY + sy * 0.5f * (n.qMinY[i] + n.qMaxY[i]);
+            c[i][2] = n.minZ + sz * 0.5f * (n.qMinZ[i] + n.qMaxZ[i]);
+        }
+        for (int oct = 0; oct < 8; oct++) {
+            float sgn[3] = { (oct & 1) ? -1.f : 1.f, (oct & 2) ? -1.f : 1.f, (oct & 4) ? -1.f : 1.f };
+            std::array<int, 4> ord = { 0, 1, 2, 3 };
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                float ka = c[a][0] * sgn[0] + c[a][1] * sgn[1] + c[a][2] * sgn[2];
+                float kb = c[b][0] * sgn[0] + c[b][1] * sgn[1] + c[b][2] * sgn[2];
+                return ka < kb;
+            });
+            octOrder[ni][oct] = ord;
+        }
+    }
+}
+
+static void trace(const float *o, const float *d, int mode, Stats &st)
+{
+    const bool ftb = mode == 1;
+    const int oct = (d[0] < 0 ? 1 : 0) | (d[1] < 0 ? 2 : 0) | (d[2] < 0 ? 4 : 0);
     float inv[3];
     for (int k = 0; k < 3; k++) inv[k] = d[k] == 0 ? 1e7f : 1.f / d[k];
     float tmax = 3.4e38f;
@@ -106,7 +138,8 @@ static void trace(const float *o, const float *d, bool ftb, Stats &st)
         std::pair<float, int> kids[4];
         int nk = 0;
         st.slotTris.push_back({ 0, 0, 0, 0 });
-        for (int i = 0; i < 4; i++) {
+        for (int ii = 0; ii < 4; ii++) {
+            const int i = mode == 2 ? octOrder[ni][oct][ii] : mode == 3 ? octOrder[ni][oct][3 - ii] : ii;
             if (n.children[i] == -1) continue;
             st.boxes++;
             float sx = std::ldexp(1.f, n.expX), sy = std::ldexp(1.f, n.expY), sz = std::ldexp(1.f, n.expZ);
@@ -132,6 +165,7 @@ static void trace(const float *o, const float *d, bool ftb, Stats &st)
             }
         }
         if (ftb) std::sort(kids, kids + nk, [](auto a, auto b) { return a.first > b.first; });
+        if (mode == 2) std::reverse(kids, kids + nk); // nearest (first in order) popped first
         for (int k = 0; k < nk; k++) stack.push_back(kids[k].second);
     }
 }
@@ -172,7 +206,8 @@ int main(int argc, char **argv)
         double waves = (double)((n + 63) / 64);
         printf("packet (64 consecutive rays): union nodes/wave %.2f, union tris/wave %.2f\n", un / waves, ut / waves);
     }
-    for (int ftb = 0; ftb < 2; ftb++) {
+    buildOctOrder();
+    for (int ftb = 0; ftb < 4; ftb++) {
         Stats st;
         double wave_pops = 0, wave_tris = 0, simt_slot = 0, simt_merged = 0;
         for (size_t w0 = 0; w0 < n; w0 += 64) {
@@ -205,7 +240,7 @@ int main(int argc, char **argv)
         }
         printf("   SIMT tri executions/ray: per-slot loops %.2f, merged loop %.2f\n", simt_slot / n, simt_merged / n);
         printf("%s: rays %zu  pops/ray %.2f  boxes/ray %.2f  tris/ray %.2f  maxStack %.0f | wave-max pops/ray %.2f tris %.2f\n",
-               ftb ? "front-to-back" : "reference    ", n, st.pops / n, st.boxes / n, st.tris / n, st.maxStack,
+               ftb == 1 ? "front-to-back" : ftb == 2 ? "octant order " : ftb == 3 ? "octant rev 1L" : "reference    ", n, st.pops / n, st.boxes / n, st.tris / n, st.maxStack,
                wave_pops / n, wave_tris / n);
     }
     return 0;
