@@ -277,8 +277,12 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
 // t_max0 < FLT_MAX: only hits up to about t_max0 are sought (boxes entered
 // beyond it are pruned from the start); see visibleRayD for when that gives
 // the reference's answer.
-__device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
-                                             float t_max0 = mp::kFltMax)
+// kExit: stop as soon as a hit at t <= exit_at is found (t_out is then
+// that hit, not necessarily the closest; callers that only compare the
+// closest hit with exit_at get the same answer).
+template <bool kExit>
+__device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
+                                             float t_max0, float exit_at)
 {
     using namespace mp;
     const float diveps = 0.0000001f;
@@ -347,6 +351,12 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
                     if (hit_tri) {
                         ray_hit = true;
                         t_max = hit_t;
+                        if constexpr (kExit) {
+                            if (hit_t <= exit_at) {
+                                t_out = hit_t;
+                                return true;
+                            }
+                        }
                     }
                 } else {
                     bsPush(st, (uint32_t)child);
@@ -356,6 +366,12 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     }
     t_out = t_max;
     return ray_hit;
+}
+
+__device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
+                                             float t_max0 = mp::kFltMax)
+{
+    return bvhTraceRayT<false>(b, ray_o, ray_d, t_out, t_max0, 0.f);
 }
 
 // Out-of-line traversal for the ray-query test hook.
@@ -660,7 +676,13 @@ __device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restri
     if (t_c == 0) return false;
     float min_t = kFltMax;
     float tb;
-    if (bvhTraceRayD(b, org, d, tb, t_c * 1.001f)) min_t = tb;
+    // Any triangle hit at t <= t_c already decides the query: the closest
+    // hit is then <= t_c, and the target only wins with t_c < closest
+    // (utils.cpp:57-69 `t < min_hit_t`), so the search stops there.
+    if (bvhTraceRayT<true>(b, org, d, tb, t_c * 1.001f, t_c)) {
+        if (tb <= t_c) return false;
+        min_t = tb;
+    }
     int ent = -1;
     const float dxy2 = d.x * d.x + d.y * d.y;
     const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);

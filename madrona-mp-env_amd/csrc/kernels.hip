@@ -2072,8 +2072,21 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
             if (S.alive[gt2] != 0.f) atomicAdd(S.stats + kStatLosPairs, 1ull);
             if (nc) atomicAdd(S.stats + kStatLosRays, (unsigned long long)nc);
         }
+        // Ray-slot reservation: the wave's exclusive prefix sum of its
+        // lanes' candidate counts (4 ballots of one bit each, mbcnt), one
+        // LDS atomic per wave for the base.
+        uint32_t before = 0, wtotal = 0;
+#pragma unroll
+        for (int bit = 0; bit < 3; bit++) {
+            const uint64_t m = __ballot((nc >> bit) & 1);
+            before += (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bit;
+            wtotal += (uint32_t)__popcll(m) << bit;
+        }
+        uint32_t base = 0;
+        if (wl == 0 && wtotal) base = atomicAdd(&nrays, wtotal);
+        base = __shfl(base, 0);
         if (nc) {
-            uint32_t slot = atomicAdd(&nrays, (uint32_t)nc);
+            uint32_t slot = base + before;
             const uint16_t lane_id = (uint16_t)(threadIdx.x << 2);
             for (int p = 0; p < 4; p++)
                 if (cand & (1u << p)) rays[slot++] = (uint16_t)(lane_id | p);
