@@ -164,8 +164,22 @@ struct GoalRegionDev {
     float rewardStrength;
 };
 
+// Zone / sub-zone / goal tables in global memory.  Device code indexes them
+// with per-world values (the current zone, a sub-zone id): indexing the
+// by-value kernel-argument arrays of SceneDev dynamically makes the compiler
+// copy the whole argument struct into registers (k_sim's zoneSystem alone
+// needed ~200 VGPRs that way).
+struct SceneTables {
+    mp::AABB zoneAABB[kMaxZones];
+    float zoneRot[kMaxZones];
+    ZOBBDev subZones[8];
+    GoalRegionDev goals[4];
+    int32_t zoneGoalTri[kMaxZones];
+};
+
 // Read-only scene + task constants, passed by value as a kernel argument.
 struct SceneDev {
+    const SceneTables *tab; // device copy of the arrays below (set after scene upload)
     const BVHNode *nodes;
     const BVHNode *octNodes; // [8][numNodes] octant node images (scene.h octantNodeImages)
     const float *verts;     // 3 floats per vertex, 3 vertices per triangle

@@ -30,6 +30,18 @@ struct LBVH {
     unsigned long long *stats;  // workload counters (DevState::stats), null = off
 };
 
+// Workload counter add, one atomic per wave: the active lanes' values
+// (each < 16) summed by bit-plane ballots, added by the first active lane.
+__device__ __forceinline__ void statAdd(unsigned long long *p, uint32_t v)
+{
+    const uint64_t act = __ballot(1);
+    uint32_t total = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) total += (uint32_t)__popcll(__ballot((v >> b) & 1u)) << b;
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    if (below == 0 && total) atomicAdd(p, (unsigned long long)total);
+}
+
 __device__ __forceinline__ float expScaleD(int e) { return mp::u2f((uint32_t)(e + 127) << 23); }
 
 constexpr float kSphereR = 15.f;  // consts::agentRadius: the radius of every k_move sphere cast
@@ -272,6 +284,59 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
 }
 
 
+// rayTri with the vertex components read in the ray's (kx, ky, kz) order
+// straight from LDS (per-lane byte offsets ko = 4 * k) instead of selected
+// from full vertices: comp(ta - org, k) == ta[k] - org[k] exactly, so
+// every value equals rayTri's bit for bit.  orgP = (org[kx], org[ky],
+// org[kz]).
+struct RayPermD {
+    uint32_t kox, koy, koz; // byte offsets of the permuted components
+    float ox, oy, oz;       // origin in permuted order
+};
+
+__device__ __forceinline__ bool rayTriPermD(const LBVH &b, int tri, const RayTxfmD &tx, const RayPermD &rp,
+                                            float t_max, float &out_t)
+{
+    using namespace mp;
+    const MP_LDS char *base = reinterpret_cast<const MP_LDS char *>(b.verts) + tri * 48;
+    auto ld = [&](int v, uint32_t ko) { return *reinterpret_cast<const MP_LDS float *>(base + v * 16 + ko); };
+    const float Akx = ld(0, rp.kox) - rp.ox, Aky = ld(0, rp.koy) - rp.oy, Az_ = ld(0, rp.koz) - rp.oz;
+    const float Bkx = ld(1, rp.kox) - rp.ox, Bky = ld(1, rp.koy) - rp.oy, Bz_ = ld(1, rp.koz) - rp.oz;
+    const float Ckx = ld(2, rp.kox) - rp.ox, Cky = ld(2, rp.koy) - rp.oy, Cz_ = ld(2, rp.koz) - rp.oz;
+    const float Ax = fma_(-tx.Sx, Az_, Akx);
+    const float Ay = fma_(-tx.Sy, Az_, Aky);
+    const float Bx = fma_(-tx.Sx, Bz_, Bkx);
+    const float By = fma_(-tx.Sy, Bz_, Bky);
+    const float Cx = fma_(-tx.Sx, Cz_, Ckx);
+    const float Cy = fma_(-tx.Sy, Cz_, Cky);
+    float U = fma_(Cx, By, -(Cy * Bx));
+    float V = fma_(Ax, Cy, -(Ay * Cx));
+    float W = fma_(Bx, Ay, -(By * Ax));
+    if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        double CxBy = (double)Cx * (double)By;
+        double CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        double AxCy = (double)Ax * (double)Cy;
+        double AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        double BxAy = (double)Bx * (double)Ay;
+        double ByAx = (double)By * (double)Ax;
+        W = (float)(BxAy - ByAx);
+        if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
+    }
+    float det = U + V + W;
+    if (det == 0.f) return false;
+    const float Az = tx.Sz * Az_;
+    const float Bz = tx.Sz * Bz_;
+    const float Cz = tx.Sz * Cz_;
+    const float T = fma_(U, Az, fma_(V, Bz, W * Cz));
+    if (T < 0.0f || T > t_max * det) return false;
+    const float rcpDet = 1.0f / det;
+    out_t = T * rcpDet;
+    return true;
+}
+
 // MeshBVH::traceRay (mesh_bvh.inl:110-208) over the LDS-resident BVH.
 // Returns hit flag; *t_out = closest hit t when hit.
 // t_max0 < FLT_MAX: only hits up to about t_max0 are sought (boxes entered
@@ -280,7 +345,7 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
 // kExit: stop as soon as a hit at t <= exit_at is found (t_out is then
 // that hit, not necessarily the closest; callers that only compare the
 // closest hit with exit_at get the same answer).
-template <bool kExit>
+template <bool kExit, bool kPerm = false>
 __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
                                              float t_max0, float exit_at)
 {
@@ -298,6 +363,11 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
     // and t(qMax) otherwise -- the reference's six fminf/fmaxf give the same
     // values (mesh_bvh.inl:165-183).
     const bool negX = rayXInv < 0.f, negY = rayYInv < 0.f, negZ = rayZInv < 0.f;
+    RayPermD rp;
+    if constexpr (kPerm) {
+        rp.kox = 4u * (uint32_t)tx.kx; rp.koy = 4u * (uint32_t)tx.ky; rp.koz = 4u * (uint32_t)tx.kz;
+        rp.ox = comp(ray_o, tx.kx); rp.oy = comp(ray_o, tx.ky); rp.oz = comp(ray_o, tx.kz);
+    }
 
     float t_max = t_max0;
     bool ray_hit = false;
@@ -341,9 +411,15 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
 #else
                     for (int k = 0; k < ntri; k++) {
 #endif
-                        Vec3 a, bb, c;
-                        loadTri(b, leaf + k, a, bb, c);
-                        if (rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t)) {
+                        bool h;
+                        if constexpr (kPerm) {
+                            h = rayTriPermD(b, leaf + k, tx, rp, leaf_tmax, hit_t);
+                        } else {
+                            Vec3 a, bb, c;
+                            loadTri(b, leaf + k, a, bb, c);
+                            h = rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t);
+                        }
+                        if (h) {
                             hit_tri = true;
                             leaf_tmax = hit_t;
                         }
@@ -581,7 +657,7 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
             }
         }
     }
-    if (b.stats) atomicAdd(b.stats + kStatSphereCasts, 1ull);
+    if (b.stats) statAdd(b.stats + kStatSphereCasts, 1u);
     SphereHit h;
     h.t = hit_t;
     h.n = closest;
@@ -599,6 +675,7 @@ struct WorldHit {
 
 // traceRayAgainstWorld (utils.cpp:10-72): BVH then the world's N capsules.
 // Capsule bases are read from the SoA position columns (cached).
+template <bool kPerm = false>
 __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__restrict__ px,
                                                 const float *__restrict__ py, const float *__restrict__ pz,
                                                 int64_t g0, int N, mp::Vec3 org, mp::Vec3 d)
@@ -610,7 +687,7 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     bool hit = false;
     tb = 0.f;
 #else
-    bool hit = bvhTraceRayD(b, org, d, tb);
+    bool hit = bvhTraceRayT<false, kPerm>(b, org, d, tb, mp::kFltMax, 0.f);
 #endif
     if (hit) min_t = tb;
 #ifdef MPENV_LAB_NO_CAPSULE

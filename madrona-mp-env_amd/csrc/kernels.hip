@@ -233,10 +233,10 @@ __device__ void planAStarD(const DevState &S, const SceneDev &sc, int64_t g)
     int fire = (S.visMask[g] & ((1u << S.T) - 1u)) != 0 ? 1 : 0;
 
     const int zi = S.curZone[w];
-    const AABB z = sc.zoneAABB[zi];
+    const AABB z = sc.tab->zoneAABB[zi];
     Vec3 center = (z.pMin + z.pMax) / 2.f; // AABB::centroid
     const Vec3 pos = v3(S.px[g], S.py[g], 0.f);
-    center = pathfindToPointD(sc, pos, center, sc.zoneGoalTri[zi]);
+    center = pathfindToPointD(sc, pos, center, sc.tab->zoneGoalTri[zi]);
     center.z = 0.f;
     const float yaw = S.ayaw[g];
     const Vec3 fwd = v3(-sinf_(yaw), cosf_(yaw), 0.f);
@@ -595,7 +595,7 @@ __device__ void fireD(const DevState &S, const SceneDev &sc, const LBVH &bvh, in
     Vec3 fire_dir = rotateVec(a.rot, kFwd);
 
     WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, fire_from, fire_dir);
-    if (S.stats) atomicAdd(S.stats + kStatShots, 1ull);
+    if (S.stats) statAdd(S.stats + kStatShots, 1u);
     S.firedT[g] = h.hit ? h.t : kFltMax;
     bool success = h.hit;
     const int team = i / S.T, offset = i - team * S.T;
@@ -724,7 +724,7 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
     options = sc.commonRespawns;
     uint32_t *rtrack = track + 2 * sc.spawnTrackLen;
     const int cz = S.curZone[w];
-    AABB za = sc.zoneAABB[cz];
+    AABB za = sc.tab->zoneAABB[cz];
     Vec3 zone_center = 0.5f * (za.pMin + za.pMax);
     float best_score = kFltMax;
     int best_idx = -1;
@@ -737,6 +737,7 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
         if (elapsed < 3.f) score += elapsed_weight * (3.f - elapsed);
         Spawn sp = options[s];
         Vec3 spawn_pt = 0.5f * (sp.region.pMin + sp.region.pMax);
+        #pragma unroll 1
         for (int j = 0; j < N; j++) {
             if (j == ai) continue;
             if (S.alive[g0 + j] == 0.f) continue;
@@ -773,6 +774,7 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
     int num_dead = 0;
+    #pragma unroll 1
     for (int i = 0; i < N; i++)
         if (S.alive[g0 + i] == 0.f) num_dead++;
     if (num_dead == 0) return;
@@ -785,9 +787,11 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
 
     // Dead set fixed before the loop (utils.cpp:767-780).
     uint32_t dead_mask = 0;
+    #pragma unroll 1
     for (int i = 0; i < N; i++)
         if (S.alive[g0 + i] == 0.f) dead_mask |= 1u << i;
 
+    #pragma unroll 1
     for (int ai = 0; ai < N; ai++) {
         if (!(dead_mask & (1u << ai))) continue;
         const int64_t g = g0 + ai;
@@ -831,9 +835,9 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
         S.respawnSteps[g] = is_respawn ? 0 : c::kRespawnInvincibleSteps;
         S.autohealSteps[g] = 0;
         {
-            AABB za = sc.zoneAABB[cz];
+            AABB za = sc.tab->zoneAABB[cz];
             Vec3 zone_center = (za.pMax + za.pMin) / 2.f;
-            Quat to_zone = qinv(angleAxis(sc.zoneRot[cz], kUp));
+            Quat to_zone = qinv(angleAxis(sc.tab->zoneRot[cz], kUp));
             za.pMin = rotateVec(to_zone, za.pMin);
             za.pMax = rotateVec(to_zone, za.pMax);
             Vec3 pz = rotateVec(to_zone, spawn_pt);
@@ -844,7 +848,7 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
         if (sc.simFlags & kFlagSubZones) {
             // utils.cpp:906-926: spawn_pt already carries the +standHeight/2
             // of the zone block and receives it a second time
-            const ZOBBDev &sz = sc.subZones[subZoneIndexD(S, g)];
+            const ZOBBDev &sz = sc.tab->subZones[subZoneIndexD(S, g)];
             AABB za = { sz.pMin, sz.pMax };
             Vec3 zone_center = (za.pMax + za.pMin) / 2.f;
             Quat to_zone = qinv(angleAxis(sz.rotation, kUp));
@@ -868,6 +872,7 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
+    #pragma unroll 1
     for (int i = 0; i < N; i++) {
         const int64_t g = g0 + i;
         stPos(S, g, v3(kFltMax, kFltMax, kFltMax));
@@ -892,6 +897,7 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
     spawnAgentsD(S, sc, w, false);
 
     RNG base = ldWRng(S, w);
+    #pragma unroll 1
     for (int i = 0; i < N; i++) {
         const int64_t g = g0 + i;
         S.sx[g] = S.px[g]; S.sy[g] = S.py[g]; S.sz[g] = S.pz[g];
@@ -927,6 +933,7 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
         S.curStep[w] = sn.step;
         const int half = N / 2;
         const int team_a = S.teamA[w];
+        #pragma unroll 1
         for (int i = 0; i < N; i++) {
             const int j = team_a == 0 ? i : (i < half ? half + i : i - half);
             const int64_t g = g0 + j;
@@ -1029,15 +1036,17 @@ __device__ void zoneSystemD(const DevState &S, const SceneDev &sc, int w)
         captured = false;
         zsr = c::kNumStepsPerZone;
         sup = c::kZonePointInterval;
-        AABB za = sc.zoneAABB[cz];
+        AABB za = sc.tab->zoneAABB[cz];
         Vec3 center = (za.pMax + za.pMin) / 2.f;
+#pragma unroll 1
         for (int i = 0; i < N; i++) S.minDistZone[g0 + i] = distance(ldPos(S, g0 + i), center);
     }
-    AABB za = sc.zoneAABB[cz];
-    Quat to_zone = qinv(angleAxis(sc.zoneRot[cz], kUp));
+    AABB za = sc.tab->zoneAABB[cz];
+    Quat to_zone = qinv(angleAxis(sc.tab->zoneRot[cz], kUp));
     za.pMin = rotateVec(to_zone, za.pMin);
     za.pMax = rotateVec(to_zone, za.pMax);
     int na = 0, nb = 0;
+#pragma unroll 1
     for (int i = 0; i < N; i++) {
         Vec3 p = ldPos(S, g0 + i);
         p.z += c::kStandHeight / 2.f;
@@ -1078,12 +1087,13 @@ __device__ void subzoneSystemD(const DevState &S, const SceneDev &sc, int w)
     const int64_t g0 = (int64_t)w * N;
     uint32_t st = (uint32_t)S.subState[w];
     for (int k = 0; k < 8; k++) {
-        const ZOBBDev &sz = sc.subZones[k];
+        const ZOBBDev &sz = sc.tab->subZones[k];
         AABB za = { sz.pMin, sz.pMax };
         Quat to_zone = qinv(angleAxis(sz.rotation, kUp));
         za.pMin = rotateVec(to_zone, za.pMin);
         za.pMax = rotateVec(to_zone, za.pMax);
         int na = 0, nb = 0;
+        #pragma unroll 1
         for (int i = 0; i < N; i++) {
             const int64_t g = g0 + i;
             if (subZoneIndexD(S, g) != k) continue;
@@ -1156,6 +1166,7 @@ __device__ void appendCrumbsD(const DevState &S, int w)
     float4 *cr = crumbPtr(S, w);
     int n = S.numCrumbs[w];
     int next_id = S.nextCrumbId[w];
+    #pragma unroll 1
     for (int i = 0; i < N; i++) {
         const int64_t g = g0 + i;
         int32_t f = S.flags[g];
@@ -1231,6 +1242,7 @@ __device__ void updateFiltersD(const DevState &S, int w, int cur_step)
             }
         }
         if (fi == 2) {
+            #pragma unroll 1
             for (int p = 0; p < N; p++) {
                 const int lo = S.landedOn[g0 + p];
                 if (lo == -1) continue;
@@ -1243,6 +1255,7 @@ __device__ void updateFiltersD(const DevState &S, int w, int cur_step)
             }
         } else {
             int cnt[2] = { 0, 0 };
+            #pragma unroll 1
             for (int p = 0; p < N; p++) {
                 Vec3 pos = ldPos(S, g0 + p);
                 if (pos.x < fmin_x[fi] || pos.y < fmin_y[fi] || pos.x > fmax_x[fi] || pos.y > fmax_y[fi]) continue;
@@ -1277,6 +1290,7 @@ __device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
     if (cur_step == 1) {
         mr[0] = -1; mr[1] = 0; mr[2] = 0; mr[3] = 0; mr[4] = 0;
     }
+    #pragma unroll 1
     for (int i = 0; i < N; i++) {
         if (S.flags[g0 + i] & kFlagWasKilled) mr[1 + ((i / S.T) ^ 1)] += 1;
     }
@@ -1346,12 +1360,13 @@ __device__ void writeSnapshotD(const DevState &S, const SceneDev &sc, int w, boo
     const bool valid = S.matchValid[w] != 0;
     if (valid && new_captured) {
         const int cz = S.curZone[w];
-        AABB za = sc.zoneAABB[cz];
-        Quat to_zone = qinv(angleAxis(sc.zoneRot[cz], kUp));
+        AABB za = sc.tab->zoneAABB[cz];
+        Quat to_zone = qinv(angleAxis(sc.tab->zoneRot[cz], kUp));
         za.pMin = rotateVec(to_zone, za.pMin);
         za.pMax = rotateVec(to_zone, za.pMax);
         uint32_t mask = 0;
         const int ctrl = S.controlling[w];
+        #pragma unroll 1
         for (int i = 0; i < N; i++) {
             if (i / S.T != ctrl) continue;
             Vec3 p = ldPos(S, g0 + i);
@@ -1483,11 +1498,12 @@ __device__ void goalRegionsD(const DevState &S, const SceneDev &sc, int w)
     float mins[2] = { S.goalMin0[w], S.goalMin1[w] };
     const int attacker = S.teamA[w];
     for (int r = 0; r < sc.numGoals && r < 2; r++) {
-        const GoalRegionDev &gr = sc.goals[r];
+        const GoalRegionDev &gr = sc.tab->goals[r];
         const int region_team = gr.attackerTeam ? attacker : (attacker ^ 1);
         float max_min = -kFltMax;
         for (int s = 0; s < gr.numSub; s++) {
             float min_d = kFltMax;
+            #pragma unroll 1
             for (int i = 0; i < N; i++) {
                 if (i / S.T != region_team) continue;
                 float d = distToZOBBD(gr.sub[s], ldPos(S, g0 + i));
@@ -1549,7 +1565,7 @@ __device__ void zoneCaptureDefendRewardD(const DevState &S, const SceneDev &sc, 
     S.newCells[g] = 0;
     if (nn > 0) r += float(nn) * explore;
     if (!(flags & kFlagInZone)) {
-        AABB za = sc.zoneAABB[S.curZone[w]];
+        AABB za = sc.tab->zoneAABB[S.curZone[w]];
         Vec3 center = (za.pMax + za.pMin) / 2.f;
         float dist = distance(center, ldPos(S, g));
         if (dist < S.minDistZone[g]) S.minDistZone[g] = dist;
@@ -1599,7 +1615,7 @@ __device__ void subzoneRewardD(const DevState &S, const SceneDev &sc, int w, int
     if (flags & kFlagInSubZone) {
         r += in_zone;
     } else {
-        const ZOBBDev &sz = sc.subZones[k];
+        const ZOBBDev &sz = sc.tab->subZones[k];
         Vec3 center = (sz.pMax + sz.pMin) / 2.f;
         float dist = distance(center, ldPos(S, g));
         float md = S.minDistSub[g];
@@ -1664,7 +1680,7 @@ __device__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
     if (flags & kFlagInZone) {
         r += in_zone;
     } else {
-        AABB za = sc.zoneAABB[S.curZone[w]];
+        AABB za = sc.tab->zoneAABB[S.curZone[w]];
         Vec3 center = (za.pMax + za.pMin) / 2.f;
         float dist = distance(center, pos);
         float md = S.minDistZone[g];
@@ -1725,6 +1741,7 @@ __global__ void __launch_bounds__(64) k_construct(DevState S, SceneDev sc, int32
     if (w >= S.W) return;
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
+    #pragma unroll 1
     for (int i = 0; i < N; i++) {
         const int64_t g = g0 + i;
         S.policy[g] = 0;
@@ -1793,7 +1810,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPE
     bvh.stats = S.stats;
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= S.A) return;
-    if (S.stats && S.alive[g] != 0.f) atomicAdd(S.stats + kStatAliveAgents, 1ull);
+    if (S.stats) statAdd(S.stats + kStatAliveAgents, S.alive[g] != 0.f ? 1u : 0u);
     planAStarD(S, sc, g);
     if (sc.replayOn) return; // pvpReplayLogic replaces the gameplay systems (sim.cpp:5587-5605)
     applyBotActionsD(S, g);
@@ -1807,6 +1824,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPE
 // holds floor(kSimBlock / N) whole worlds, lane = agent, phases separated
 // by workgroup barriers.
 constexpr int kSimBlock = 128;
+// kernel_lab only: skip k_sim phases to time them (wrong results by design)
+#ifndef MPENV_LAB_SIM_SKIP
+#define MPENV_LAB_SIM_SKIP 0
+#endif
 
 __device__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
 
@@ -1844,15 +1865,15 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR k_sim(DevState S, Scene
         if (wlane) zoneSystemD(S, sc, w);
         __syncthreads();
     } else {
-        if (act) fireD(S, sc, bvh, w, i);
+        if (!(MPENV_LAB_SIM_SKIP & 1) && act) fireD(S, sc, bvh, w, i);
         __syncthreads();
-        if (act) applyDmgD(S, g);
+        if (!(MPENV_LAB_SIM_SKIP & 2048) && act) applyDmgD(S, g);
         __syncthreads();
-        if (wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
+        if (!(MPENV_LAB_SIM_SKIP & 2) && wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
         __syncthreads();
         if (act) autoHealD(S, g);
         __syncthreads();
-        if (wlane) {
+        if (!(MPENV_LAB_SIM_SKIP & 4) && wlane) {
             zoneSystemD(S, sc, w);
             if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
         }
@@ -1861,29 +1882,30 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR k_sim(DevState S, Scene
             if (act) recordAgentD(S, w, i);
             if (wlane) S.recordLog[w].cur_step = S.curStep[w];
         }
-        if (act) leaveBreadcrumbAgentD(S, w, g);
+        if (!(MPENV_LAB_SIM_SKIP & 256) && act) leaveBreadcrumbAgentD(S, w, g);
         __syncthreads();
-        if (wlane) appendCrumbsD(S, w);
+        if (!(MPENV_LAB_SIM_SKIP & 256) && wlane) appendCrumbsD(S, w);
         __syncthreads();
-        if (act) accumulateCrumbsD(S, w, i);
+        if (!(MPENV_LAB_SIM_SKIP & 512) && act) accumulateCrumbsD(S, w, i);
         __syncthreads();
     }
     if (wlane) {
-        if (!sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem
-        zoneMatchInfoD(S, sc, w);
-        goalRegionsD(S, sc, w);
+        if (!(MPENV_LAB_SIM_SKIP & 256) && !sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem
+        if (!(MPENV_LAB_SIM_SKIP & 8)) zoneMatchInfoD(S, sc, w);
+        if (!(MPENV_LAB_SIM_SKIP & 16)) goalRegionsD(S, sc, w);
     }
     __syncthreads();
     if (act) {
-        exploreVisitedD(S, w, g);
+        if (!(MPENV_LAB_SIM_SKIP & 1024)) exploreVisitedD(S, w, g);
         if (sc.flank && sc.task == MPENV_TASK_ZONE) flankRewardD(S, sc, bvh, w, i);
-        else zoneRewardD(S, sc, w, i);
+        else if (!(MPENV_LAB_SIM_SKIP & 64)) zoneRewardD(S, sc, w, i);
     }
     __syncthreads();
     if (wlane) {
         // pvpTeamRewardSystem (sim.cpp:4292-4313)
         float tr[2] = { 0.f, 0.f };
         int ts[2] = { 0, 0 };
+        #pragma unroll 1
         for (int j = 0; j < N; j++) {
             int t = j / S.T;
             tr[t] += S.reward[(int64_t)w * N + j];
@@ -1917,7 +1939,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR k_sim(DevState S, Scene
             S.ftReward[(int64_t)w * 2 + t] = r;
             S.ftDone[(int64_t)w * 2 + t] = done ? 1 : 0;
         }
-        resetSystemD(S, sc, w);
+        if (!(MPENV_LAB_SIM_SKIP & 128)) resetSystemD(S, sc, w);
     }
 }
 
@@ -2067,10 +2089,14 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
             }
         }
         const int nc = __popc(cand);
-        if (S.stats && valid && S.alive[g] != 0.f) {
-            const int64_t gt2 = (g / N) * N + (((int)(g % N) / T) ^ 1) * T + k;
-            if (S.alive[gt2] != 0.f) atomicAdd(S.stats + kStatLosPairs, 1ull);
-            if (nc) atomicAdd(S.stats + kStatLosRays, (unsigned long long)nc);
+        if (S.stats) {
+            uint32_t pair = 0;
+            if (valid && S.alive[g] != 0.f) {
+                const int64_t gt2 = (g / N) * N + (((int)(g % N) / T) ^ 1) * T + k;
+                pair = S.alive[gt2] != 0.f ? 1u : 0u;
+            }
+            statAdd(S.stats + kStatLosPairs, pair);
+            statAdd(S.stats + kStatLosRays, (uint32_t)nc);
         }
         // Ray-slot reservation: the wave's exclusive prefix sum of its
         // lanes' candidate counts (4 ballots of one bit each, mbcnt), one
@@ -2113,10 +2139,9 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
         const float len = length(to_test);
         to_test = to_test / len;
-        if (visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target)) {
-            atomicOr(&masks[(int)(g - agent0)], 1u << k);
-            if (S.stats) atomicAdd(S.stats + kStatLosSeen, 1ull);
-        }
+        const bool seen = visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target);
+        if (seen) atomicOr(&masks[(int)(g - agent0)], 1u << k);
+        if (S.stats) statAdd(S.stats + kStatLosSeen, seen ? 1u : 0u);
     }
     __syncthreads();
 
@@ -2300,7 +2325,7 @@ __device__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int6
     gob[1] = team == 0 ? 1.f : 0.f;
     gob[2] = float(c::kEpisodeLen - S.curStep[w]) / c::kEpisodeLen;
     const int cz = S.curZone[w];
-    const AABB za = sc.zoneAABB[cz];
+    const AABB za = sc.tab->zoneAABB[cz];
     const Vec3 nc = normalizedPosUnclampedD(sc, (za.pMax + za.pMin) / 2.f);
     gob[3] = nc.x; gob[4] = nc.y; gob[5] = nc.z;
     const int ctrl = S.controlling[w];
@@ -2323,6 +2348,13 @@ __device__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int6
 // merge); transposed per wave, each instruction writes 8 whole rows.
 constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
 
+__device__ __forceinline__ void waveSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ void storeRowsWave(float *arr, int slots, int k, const float *row, int64_t gw0, int64_t A,
                                               float *buf, int lane)
 {
@@ -2330,11 +2362,14 @@ __device__ __forceinline__ void storeRowsWave(float *arr, int slots, int k, cons
 #pragma unroll
     for (int q = 0; q < kOtherObs / 4; q++)
         mine[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
-    // the wave's own LDS writes, then reads of other lanes' rows: a
-    // wavefront-scope fence emits nothing and does not keep the compiler
-    // from moving LDS accesses across it, so drain the LDS counter behind a
-    // compiler memory barrier instead
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // Cross-lane exchange through LDS inside one wave: the wave's DS
+    // instructions execute in issue order, so the hardware needs no wait;
+    // what must be ordered is the compiler's view.  A wavefront-scope
+    // release/acquire fence pair around a wave barrier makes the other
+    // lanes' row writes visible to this lane's reads (and, below, the reads
+    // complete before the next rows overwrite the buffer) without a
+    // data race in the source.
+    waveSync();
     // the wave's m live lanes (a tail wave's lanes past A have returned)
     // share its m rows x 8 chunks
     const int m = (int)(A - gw0 < 64 ? A - gw0 : 64);
@@ -2344,10 +2379,18 @@ __device__ __forceinline__ void storeRowsWave(float *arr, int slots, int k, cons
         reinterpret_cast<float4 *>(arr + ((gw0 + r) * slots + k) * kOtherObs)[col] =
             reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col];
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // reads done before the next rows land
+    waveSync(); // reads done before the next rows land
 }
 
-__global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
+#ifndef MPENV_OBS_NOUNROLL
+#define MPENV_OBS_NOUNROLL 0
+#endif
+#ifdef MPENV_OBS_WPE
+#define MP_OBS_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_OBS_WPE)))
+#else
+#define MP_OBS_ATTR
+#endif
+__global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev sc)
 {
     __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsRowPad];
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2379,9 +2422,13 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
         if (S.firedT[go] >= 0) mask[k] = 1.f;
     }
     storeVec(&S.masks[g * 6], mask, 6);
-    // mask[k] == 1 as bits for the opponent loop: reading the float array
-    // there was miscompiled (hipcc, ROCm 7.2) once the row export went
-    // through LDS -- wrong last-known updates on the 2v2 navmesh golden case.
+    // teamKnowsLocation (mask[k] == 1) as bits for the opponent loop.
+    // Reading the float array there instead gives wrong last-known updates
+    // on the 2v2_navmesh_curriculum golden case at init (agents 4, 6, 9
+    // and 10 see knows(1) = 0 while their stored mask[1] is 1), with the
+    // row exchange synchronised either by s_waitcnt or by the wave barrier
+    // and wavefront fences below -- so the LDS exchange is not the cause;
+    // the bits form passes under both ("k_obs mask read").
     uint32_t knowsBits = 0;
     for (int k = 0; k < kMaxTeamSize; k++) knowsBits |= (mask[k] == 1.f ? 1u : 0u) << k;
 
@@ -2405,7 +2452,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
         fillCombatD(S, g, &ob[23]);
         float *zo = &ob[27];
         const int cz = S.curZone[w];
-        AABB za = sc.zoneAABB[cz];
+        AABB za = sc.tab->zoneAABB[cz];
         Vec3 center = (za.pMax + za.pMin) / 2.f;
         Vec3 nc = normalizedPosD(sc, center);
         zo[0] = nc.x; zo[1] = nc.y; zo[2] = nc.z;
@@ -2426,6 +2473,9 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
     storeVec(&S.selfPos[g * 3], pos3, 3);
 
     // teammates
+#if MPENV_OBS_NOUNROLL
+#pragma unroll 1
+#endif
     for (int k = 0; k < kMaxTeamSize - 1; k++) {
         float tob[kOtherObs];
         float tpos[3];
@@ -2443,6 +2493,9 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
     }
 
     // opponents (+ last known)
+#if MPENV_OBS_NOUNROLL
+#pragma unroll 1
+#endif
     for (int k = 0; k < kMaxTeamSize; k++) {
         float oob[kOtherObs];
         float opos[3];
@@ -2464,7 +2517,7 @@ __global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
                 oob[28] = (float)S.wasShot[gj];
                 oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
                 oob[30] = ((vm[g] >> k) & 1) ? 1.f : 0.f;
-                const bool knows = (knowsBits >> k) & 1u;
+                const bool knows = (knowsBits >> k) & 1u; // teamKnowsLocation (sim.cpp:2995-3003)
                 oob[31] = knows ? 1.f : 0.f;
                 if (knows) {
                     storeVec(lk, oob, kOtherObs);
@@ -2563,7 +2616,10 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // order (scene.h octantNodeImages); the oracle visits the same order
         LBVH ob = bvh;
         ob.nodes = bvh.nodes + rayOctant(dir) * sc.numNodes;
-        WorldHit hw = traceWorldD(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir);
+#ifndef MPENV_LIDAR_PERM
+#define MPENV_LIDAR_PERM 0
+#endif
+        WorldHit hw = traceWorldD<MPENV_LIDAR_PERM != 0>(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir);
         const bool second = i >= T; // team of the casting agent
         float4 out;
         if (hw.hit) {

@@ -526,6 +526,17 @@ static void buildSceneDev(mpenv_manager &m)
         d.attackerTeam = g.attackerTeam;
         d.rewardStrength = g.rewardStrength;
     }
+    {
+        SceneTables t;
+        std::memcpy(t.zoneAABB, sc.zoneAABB, sizeof(t.zoneAABB));
+        std::memcpy(t.zoneRot, sc.zoneRot, sizeof(t.zoneRot));
+        std::memcpy(t.subZones, sc.subZones, sizeof(t.subZones));
+        std::memcpy(t.goals, sc.goals, sizeof(t.goals));
+        std::memcpy(t.zoneGoalTri, sc.zoneGoalTri, sizeof(t.zoneGoalTri));
+        SceneTables *d_tab = m.alloc<SceneTables>(1);
+        m.upload(d_tab, &t, sizeof(t));
+        sc.tab = d_tab;
+    }
     sc.simFlags = m.cfg.sim_flags;
     sc.autoReset = m.cfg.auto_reset;
     sc.worldOffset = m.cfg.world_id_offset;

@@ -96,7 +96,8 @@ def ensure_built():
 def lib_mpenv():
     if "mpenv" not in _libs:
         ensure_built()
-        lib = C.CDLL(build_native.LIB)
+        # MPENV_LIB: a kernel_lab variant of the library (development only)
+        lib = C.CDLL(os.environ.get("MPENV_LIB", build_native.LIB))
         lib.mpenv_create.argtypes = [C.POINTER(MpenvConfig), C.POINTER(C.c_void_p)]
         lib.mpenv_destroy.argtypes = [C.c_void_p]
         for fn in ("mpenv_init", "mpenv_step"):

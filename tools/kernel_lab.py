@@ -44,7 +44,7 @@ def build(name, defines):
     print("built", name, defines)
 
 
-def time_one(name, worlds=16384, team=6, warm=30, steps=100, label=None):
+def time_one(name, worlds=16384, team=6, warm=100, steps=200, label=None):
     import mpenv_testlib as T
 
     path = os.path.join(LAB, name, "libmpenv.so") if name != "main" else os.path.join(PKG, "libmpenv.so")
@@ -60,6 +60,15 @@ def time_one(name, worlds=16384, team=6, warm=30, steps=100, label=None):
                         None, 0)
     h = C.c_void_p()
     assert lib.mpenv_create(C.byref(cfg), C.byref(h)) == 0, lib.mpenv_last_error()
+    # simCtrl [0, 1, 1] as bench.py (random start step and team sides)
+    lib.mpenv_export_tensor.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+    hip0 = C.CDLL("libamdhip64.so")
+    p, dt, nd, gid = C.c_void_p(), C.c_int32(), C.c_int32(), C.c_int32()
+    dims = (C.c_int64 * 8)()
+    assert lib.mpenv_export_tensor(h, 64, C.byref(p), C.byref(dt), C.byref(nd), dims, C.byref(gid)) == 0
+    ctrl = (C.c_int32 * 3)(0, 1, 1)
+    assert hip0.hipMemcpy(p, ctrl, C.c_size_t(12), 1) == 0
     assert lib.mpenv_init(h) == 0
     # 16-step action ring in device memory (hash tape, as bench.py)
     ring = T.mpenv_tape.tape_ring(1234, 0, worlds * 2 * team, 16)
