@@ -1803,12 +1803,18 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 #ifndef MPENV_MOVE_WPE
 #define MPENV_MOVE_WPE 3
 #endif
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPENV_MOVE_WPE))) k_move(DevState S, SceneDev sc)
+// apw: agents per wave (64, or fewer on small batches: a wave runs the
+// longest of its lanes' sphere-cast chains, so when the batch leaves SIMDs
+// idle, fewer agents per wave shorten every wave; launchMove picks it).
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPENV_MOVE_WPE))) k_move(DevState S, SceneDev sc, int apw)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LBVH bvh = stageBVHSphere(smem, sc);
     bvh.stats = S.stats;
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (lane >= apw) return;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t g = wave * apw + lane;
     if (g >= S.A) return;
     if (S.stats) statAdd(S.stats + kStatAliveAgents, S.alive[g] != 0.f ? 1u : 0u);
     planAStarD(S, sc, g);
@@ -2794,9 +2800,18 @@ int launchMove(const DevState &s, const SceneDev &sc, void *stream)
     // instead of sharing a CU's SIMDs (k_move is latency-bound: 5-7
     // dependent sphere casts per lane).  Big batches keep 256-thread blocks
     // (the 24 KB LDS image per block would otherwise cap occupancy).
-    const int bs = s.A < (int64_t)kBlock * 64 ? 64 : kBlock;
-    hipLaunchKernelGGL(k_move, dim3((unsigned)((s.A + bs - 1) / bs)), dim3(bs), bvhLdsBytesSphere(sc),
-                       (hipStream_t)stream, s, sc);
+    // Agents per wave: 64 once the batch fills ~1.5 waves per SIMD (1,536
+    // waves on 256 CUs), else the power of two (>= 8) that gets closest.
+#ifndef MPENV_MOVE_TARGET_WAVES
+#define MPENV_MOVE_TARGET_WAVES 1536
+#endif
+    int apw = 64;
+    while (apw > 8 && (s.A + apw - 1) / apw < MPENV_MOVE_TARGET_WAVES) apw >>= 1;
+    const int64_t waves = (s.A + apw - 1) / apw;
+    const int bs = waves < 64 * 4 ? 64 : kBlock;
+    const int64_t threads = waves * 64;
+    hipLaunchKernelGGL(k_move, dim3((unsigned)((threads + bs - 1) / bs)), dim3(bs), bvhLdsBytesSphere(sc),
+                       (hipStream_t)stream, s, sc, apw);
     return check(hipGetLastError());
 }
 

@@ -11,9 +11,9 @@ run() { # name, timeout, args...
     timeout -k 10 $t "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "FAILED $name"; exit 1; }
     cat $OUT/$name.json
 }
-run c3_no_kernel_timing 240 python -u bench.py --cpu-baseline off --no-profile-pass
+run c3_groups1 240 python -u bench.py --cpu-baseline off --world-groups 1
 run c2_3v3_4096 240 python -u bench.py --worlds 4096 --team-size 3 --cpu-baseline off
 run c1_1v1_64 240 python -u bench.py --worlds 64 --team-size 1 --steps 300 --warmup 30
 run c5_bots_team1 240 python -u bench.py --bots team1 --cpu-baseline off
 run c3_share2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29517 bench.py --gpus 2 --share-device --steps 300 --warmup 30
+    --master-port 29517 bench.py --gpus 2 --share-device --steps 300 --warmup 30 --cpu-baseline off

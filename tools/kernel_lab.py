@@ -44,7 +44,8 @@ def build(name, defines):
     print("built", name, defines)
 
 
-def time_one(name, worlds=16384, team=6, warm=100, steps=200, label=None):
+def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.environ.get("LAB_TEAM", 6)),
+             warm=100, steps=200, label=None):
     import mpenv_testlib as T
 
     path = os.path.join(LAB, name, "libmpenv.so") if name != "main" else os.path.join(PKG, "libmpenv.so")
