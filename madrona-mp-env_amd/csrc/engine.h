@@ -136,6 +136,9 @@ struct DevState {
     mpenv_packed_step_snapshot *snapshots; // [W]
     int32_t evStride;                      // 2 * N + 1
 
+    // Per agent: combat RNG key + first draw keys of a coming reset (k_sim)
+    mp::RandKey *resetKeys; // [A][11]
+
     // Workload counters (mpenv_enable_stats), null when off: see StatId.
     unsigned long long *stats;
 };

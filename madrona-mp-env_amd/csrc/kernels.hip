@@ -544,7 +544,7 @@ __device__ __forceinline__ void putEventD(const DevState &S, const SceneDev &sc,
 
 __device__ __forceinline__ int playerIdD(const DevState &S, int i) { return (i / S.T) * kMaxTeamSize + i % S.T; }
 
-__device__ void fireD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
+__device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -665,9 +665,22 @@ __device__ void autoHealD(const DevState &S, int64_t g)
 
 // ====================================================== spawning / reset
 // utils.cpp:273-479 standardSpawnPoint (Zone task)
-__device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w, int ai, bool is_respawn,
-                                    bool use_middle, RNG &rng, Vec3 &out_pt, float &out_yaw)
+// Draw keys of an agent's fresh combat RNG (counters 0 .. kPreDraws-1),
+// computed by the agent's own lane before a world reset so the world lane
+// does not evaluate them one after another (k_sim, resetPreD).
+constexpr int kPreDraws = 10;
+
+__device__ __forceinline__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w, int ai, bool is_respawn,
+                                    bool use_middle, RNG &rng, Vec3 &out_pt, float &out_yaw,
+                                    const RandKey *pre = nullptr)
 {
+    // rng's draws, from `pre` while the counter is inside it (same keys
+    // splitI(rng.key, ctr) the RNG would produce)
+    auto adv = [&]() {
+        const RandKey k = (pre && rng.ctr < (uint32_t)kPreDraws) ? pre[rng.ctr] : splitI(rng.key, rng.ctr);
+        rng.ctr += 1;
+        return k;
+    };
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
     const int team = ai / S.T;
@@ -677,10 +690,10 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
     const Spawn *options;
     auto spawnAgent = [&](int idx) {
         Spawn s = options[idx];
-        float x_rnd = rngUniform(rng);
-        float y_rnd = rngUniform(rng);
-        float z_rnd = rngUniform(rng);
-        float yaw_rnd = rngUniform(rng);
+        float x_rnd = keyUniform(adv());
+        float y_rnd = keyUniform(adv());
+        float z_rnd = keyUniform(adv());
+        float yaw_rnd = keyUniform(adv());
         float x_min = s.region.pMin.x, x_diff = s.region.pMax.x - x_min;
         float y_min = s.region.pMin.y, y_diff = s.region.pMax.y - y_min;
         float z_min = s.region.pMin.z, z_diff = s.region.pMax.z - z_min;
@@ -710,12 +723,12 @@ __device__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w
         }
         int init_idx = -1;
         for (int k = 0; k < 5; k++) {
-            int idx = rngI32(rng, 0, num_spawns);
+            int idx = keyI32(adv(), 0, num_spawns);
             if (tracker[idx] == cur_step) continue;
             init_idx = idx;
             break;
         }
-        if (init_idx == -1) init_idx = rngI32(rng, 0, num_spawns);
+        if (init_idx == -1) init_idx = keyI32(adv(), 0, num_spawns);
         spawnAgent(init_idx);
         tracker[init_idx] = cur_step;
         return;
@@ -769,7 +782,8 @@ __device__ __forceinline__ int subZoneIndexD(const DevState &S, int64_t g)
 }
 
 // utils.cpp:734-948 spawnAgents
-__device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool is_respawn)
+__device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool is_respawn,
+                                             const RandKey *pre = nullptr)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -779,7 +793,9 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
         if (S.alive[g0 + i] == 0.f) num_dead++;
     if (num_dead == 0) return;
     RNG base = ldWRng(S, w);
-    (void)rngI32(base, 0, 0); // episodes[sampleI32(0, numEpisodes = 0)]
+    // episodes[sampleI32(0, numEpisodes = 0)]: an empty range, the value is
+    // 0 whatever the key -- only the counter advances
+    base.ctr += 1;
     bool use_middle = false;
     if (sc.simFlags & kFlagSpawnInMiddle) use_middle = rngUniform(base) < 0.5f;
     const bool randomize_hp = (sc.simFlags & kFlagRandomizeHP) != 0;
@@ -807,7 +823,8 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
             spawn_yaw = rngUniform(base) * 2.f * kPi;
         } else {
             RNG rng = ldRng(S, g);
-            standardSpawnPointD(S, sc, w, ai, is_respawn, use_middle, rng, spawn_pt, spawn_yaw);
+            standardSpawnPointD(S, sc, w, ai, is_respawn, use_middle, rng, spawn_pt, spawn_yaw,
+                                pre ? pre + ai * (kPreDraws + 1) + 1 : nullptr);
             stRng(S, g, rng);
             if ((sc.simFlags & kFlagEnableCurriculum) && S.episodeCurr[w] == 0) {
                 // utils.cpp:819-837 LearnShooting
@@ -821,7 +838,10 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
         stRot(S, g, qnormalize(angleAxis(spawn_yaw, kUp)));
         stAim(S, g, computeAimD(spawn_yaw, 0.f));
         stVel(S, g, v3(0.f, 0.f, 0.f));
-        S.weapon[g] = rngI32(base, 0, c::kNumWeaponTypes);
+        // sampleI32(0, numWeaponTypes = 1) is 0 whatever the key: advance only
+        static_assert(c::kNumWeaponTypes == 1, "weapon draw shortcut assumes one weapon type");
+        base.ctr += 1;
+        S.weapon[g] = 0;
         if (randomize_hp) {
             int tenth = rngI32(base, 1, 11);
             S.hp[g] = float(tenth * 10);
@@ -868,12 +888,37 @@ __device__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool 
 }
 
 // level_gen.cpp:330-582 resetPersistentEntities
-__device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, int w, RandKey episode_key)
+// resetPersistentEntities, agent i's own part (level_gen.cpp:330-370):
+// position, combat RNG split_i(episodeKey, i + 1), combat flags, last-known
+// observations, breadcrumb state.
+__device__ __forceinline__ void resetAgentD(const DevState &S, int64_t g, RandKey agent_key)
+{
+    stPos(S, g, v3(kFltMax, kFltMax, kFltMax));
+    stRng(S, g, makeRNG(agent_key));
+    S.landedOn[g] = -1;
+    S.respawnSteps[g] = 0;
+    S.autohealSteps[g] = 0;
+    S.wasShot[g] = 0;
+    S.firedT[g] = -kFltMax;
+    S.flags[g] = S.flags[g] & (kFlagInZone | kFlagInSubZone);
+    S.alive[g] = 0.f;
+    float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
+    for (int k = 0; k < 6 * kOtherObs / 4; k++) lk[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < 18; k++) S.lkPos[g * 18 + k] = -1000.f;
+    S.bcPenalty[g] = 0.f;
+    S.bcLast[g] = -1;
+    S.bcSteps[g] = 0;
+}
+
+// pre != nullptr: every agent's resetAgentD already ran on its own lane and
+// pre holds, per agent, its RNG key then kPreDraws draw keys (resetPreD).
+__device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, int w, RandKey episode_key,
+                                         const RandKey *pre = nullptr)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
     #pragma unroll 1
-    for (int i = 0; i < N; i++) {
+    for (int i = 0; i < N && !pre; i++) {
         const int64_t g = g0 + i;
         stPos(S, g, v3(kFltMax, kFltMax, kFltMax));
         RNG r = makeRNG(splitI(episode_key, (uint32_t)(i + 1)));
@@ -892,9 +937,11 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
         S.bcLast[g] = -1;
         S.bcSteps[g] = 0;
     }
-    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
-    for (int k = 0; k < 3 * sc.spawnTrackLen; k++) track[k] = 0xFFFFFFFFu;
-    spawnAgentsD(S, sc, w, false);
+    if (!pre) {
+        uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
+        for (int k = 0; k < 3 * sc.spawnTrackLen; k++) track[k] = 0xFFFFFFFFu;
+    }
+    spawnAgentsD(S, sc, w, false, pre);
 
     RNG base = ldWRng(S, w);
     #pragma unroll 1
@@ -953,7 +1000,8 @@ __device__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, 
 }
 
 // sim.cpp:732-833 initWorld
-__device__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool triggered_reset, const int32_t *tc)
+__device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool triggered_reset, const int32_t *tc,
+                           const RandKey *pre = nullptr)
 {
     const uint32_t world_id = sc.worldOffset + (uint32_t)w;
     S.matchValid[w] = 1; // matchID = worldID << 32 | curEpisodeIdx (sim.cpp:736-738)
@@ -989,18 +1037,39 @@ __device__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool tr
     S.subState[w] = 0; // every sub-zone: controlling -1, not contested / captured (sim.cpp:815-820)
     if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) S.curZone[w] = 3; // sim.cpp:822-825
     stWRng(S, w, base);
-    resetPersistentEntitiesD(S, sc, w, episode_key);
+    resetPersistentEntitiesD(S, sc, w, episode_key, pre);
     S.filtAct0[w] = 0; S.filtAct1[w] = 0;
     S.filtMatched0[w] = 0; S.filtMatched1[w] = 0;
 }
 
 // sim.cpp:835-872 resetSystem
-__device__ void resetSystemD(const DevState &S, const SceneDev &sc, int w)
+__device__ __forceinline__ bool resetDueD(const DevState &S, const SceneDev &sc, int w)
+{
+    return S.reset[w] != 0 || (sc.autoReset && S.finished[w]);
+}
+
+// The per-agent half of a coming world reset, on the agent's own lane
+// (k_sim, before resetSystemD): the episode key initWorld will derive, the
+// agent's combat RNG key split_i(episodeKey, i + 1) and its first kPreDraws
+// draw keys into pre[0], pre[1..], the agent's resetPersistentEntities
+// stores, and its share of the spawn-usage tracker reset.
+__device__ __forceinline__ void resetPreD(const DevState &S, const SceneDev &sc, int w, int i, RandKey *pre)
+{
+    const uint32_t world_id = sc.worldOffset + (uint32_t)w;
+    const uint32_t ep = (uint32_t)S.episodeCounter[w]; // the episode resetSystemD is about to start
+    const RandKey episode_key = splitI(sc.initRandKey, ep, world_id);
+    const RandKey key = splitI(episode_key, (uint32_t)(i + 1));
+    pre[0] = key;
+    for (int c = 0; c < kPreDraws; c++) pre[1 + c] = splitI(key, (uint32_t)c);
+    resetAgentD(S, (int64_t)w * S.N + i, key);
+    uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
+    for (int k = i; k < 3 * sc.spawnTrackLen; k += S.N) track[k] = 0xFFFFFFFFu;
+}
+
+__device__ __forceinline__ void resetSystemD(const DevState &S, const SceneDev &sc, int w, const RandKey *pre = nullptr)
 {
     const int32_t force = S.reset[w];
-    int32_t should = force;
-    if (sc.autoReset && S.finished[w]) should = 1;
-    if (should == 0) return;
+    if (!resetDueD(S, sc, w)) return;
     S.reset[w] = 0;
     const int32_t ep = S.episodeCounter[w];
     S.episode[w] = ep;
@@ -1015,7 +1084,7 @@ __device__ void resetSystemD(const DevState &S, const SceneDev &sc, int w)
             S.worldCurr[w] = 1;
         }
     }
-    initWorldD(S, sc, w, force == 1, S.trainCtrl);
+    initWorldD(S, sc, w, force == 1, S.trainCtrl, pre);
 }
 
 // ====================================================== per-world systems
@@ -1225,15 +1294,43 @@ __device__ void decayCrumbsD(const DevState &S, int w)
     S.numCrumbs[w] = m;
 }
 
-// sim.cpp:128-291 updateFiltersState
-__device__ void updateFiltersD(const DevState &S, int w, int cur_step)
+// Filter boxes of updateFiltersState (sim.cpp:128-291): x/y ranges of the
+// three hard-coded analytics filters.
+__constant__ const int16_t kFiltMinX[3] = { -1272, 852, -32768 }, kFiltMinY[3] = { -866, -851, -32768 };
+__constant__ const int16_t kFiltMaxX[3] = { -825, 1280, 32767 }, kFiltMaxY[3] = { 696, 593, 32767 };
+
+__device__ __forceinline__ bool inFilterBoxD(Vec3 p, int fi)
+{
+    return !(p.x < kFiltMinX[fi] || p.y < kFiltMinY[fi] || p.x > kFiltMaxX[fi] || p.y > kFiltMaxY[fi]);
+}
+
+// What zoneMatchInfoSystem + updateFiltersState read per agent, computed by
+// the agent's own lane (all in parallel) and handed to the world lane
+// through LDS: bit 0 wasKilled, 1 hasDiedDuringEpisode, 2 / 3 inside filter
+// box 0 / 1, 4 a landed shot with shooter and target inside filter box 2.
+enum : uint32_t { kMbKilled = 1, kMbDied = 2, kMbF0 = 4, kMbF1 = 8, kMbF2 = 16 };
+
+__device__ __forceinline__ uint32_t matchAgentBitsD(const DevState &S, int w, int i)
+{
+    const int64_t g0 = (int64_t)w * S.N, g = g0 + i;
+    const int32_t f = S.flags[g];
+    uint32_t b = 0;
+    if (f & kFlagWasKilled) b |= kMbKilled;
+    if (f & kFlagHasDied) b |= kMbDied;
+    const Vec3 p = ldPos(S, g);
+    if (inFilterBoxD(p, 0)) b |= kMbF0;
+    if (inFilterBoxD(p, 1)) b |= kMbF1;
+    const int lo = S.landedOn[g];
+    if (lo != -1 && inFilterBoxD(p, 2) && inFilterBoxD(ldPos(S, g0 + lo), 2)) b |= kMbF2;
+    return b;
+}
+
+// sim.cpp:128-291 updateFiltersState from the world's agent bits
+__device__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const uint8_t *mb)
 {
     const int N = S.N;
-    const int64_t g0 = (int64_t)w * N;
     int32_t *last = &S.filtLast[(int64_t)w * 6]; // [team][filter]
     uint32_t act[2] = { (uint32_t)S.filtAct0[w], (uint32_t)S.filtAct1[w] };
-    const int16_t fmin_x[3] = { -1272, 852, -32768 }, fmin_y[3] = { -866, -851, -32768 };
-    const int16_t fmax_x[3] = { -825, 1280, 32767 }, fmax_y[3] = { 696, 593, 32767 };
     const int min_num[2] = { 5, 1 };
     for (int fi = 0; fi < 3; fi++) {
         for (int t = 0; t < 2; t++) {
@@ -1244,23 +1341,17 @@ __device__ void updateFiltersD(const DevState &S, int w, int cur_step)
         if (fi == 2) {
             #pragma unroll 1
             for (int p = 0; p < N; p++) {
-                const int lo = S.landedOn[g0 + p];
-                if (lo == -1) continue;
+                if (!(mb[p] & kMbF2)) continue;
                 const int team = p / S.T;
-                Vec3 ap = ldPos(S, g0 + p), tp = ldPos(S, g0 + lo);
-                if (ap.x < fmin_x[fi] || ap.y < fmin_y[fi] || ap.x > fmax_x[fi] || ap.y > fmax_y[fi] ||
-                    tp.x < fmin_x[fi] || tp.y < fmin_y[fi] || tp.x > fmax_x[fi] || tp.y > fmax_y[fi]) continue;
                 act[team] |= 1u << fi;
                 last[team * 3 + fi] = cur_step;
             }
         } else {
+            const uint32_t bit = fi == 0 ? kMbF0 : kMbF1;
             int cnt[2] = { 0, 0 };
             #pragma unroll 1
-            for (int p = 0; p < N; p++) {
-                Vec3 pos = ldPos(S, g0 + p);
-                if (pos.x < fmin_x[fi] || pos.y < fmin_y[fi] || pos.x > fmax_x[fi] || pos.y > fmax_y[fi]) continue;
-                cnt[p / S.T] += 1;
-            }
+            for (int p = 0; p < N; p++)
+                if (mb[p] & bit) cnt[p / S.T] += 1;
             for (int t = 0; t < 2; t++) {
                 if (cnt[t] >= min_num[fi]) {
                     act[t] |= 1u << fi;
@@ -1278,7 +1369,7 @@ __device__ void updateFiltersD(const DevState &S, int w, int cur_step)
 // sim.cpp:4470-4673 zoneMatchInfoSystem
 __device__ void writeSnapshotD(const DevState &S, const SceneDev &sc, int w, bool new_captured);
 
-__device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
+__device__ __forceinline__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w, const uint8_t *mb)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1292,7 +1383,7 @@ __device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
     }
     #pragma unroll 1
     for (int i = 0; i < N; i++) {
-        if (S.flags[g0 + i] & kFlagWasKilled) mr[1 + ((i / S.T) ^ 1)] += 1;
+        if (mb[i] & kMbKilled) mr[1 + ((i / S.T) ^ 1)] += 1;
     }
     bool earned = false;
     bool new_captured = false;
@@ -1321,7 +1412,7 @@ __device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
         if (mr[3 + attacker] == 1) finished = true;
         if (mr[3 + defender] == 8) finished = true;
         for (int i = attacker * S.T; i < (attacker + 1) * S.T; i++)
-            if (!(S.flags[g0 + i] & kFlagHasDied)) attackers_all_died = false;
+            if (!(mb[i] & kMbDied)) attackers_all_died = false;
         if (attackers_all_died) finished = true;
     }
     {
@@ -1330,7 +1421,7 @@ __device__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w)
         if (captured && ctrl >= 0) zs[1 + ctrl] += 1;
         if (S.contested[w]) zs[3] += 1;
         if (new_captured) zs[0] += 1;
-        updateFiltersD(S, w, cur_step);
+        updateFiltersBitsD(S, w, cur_step, mb);
         if (sc.eventsOn) writeSnapshotD(S, sc, w, new_captured);
     }
     if (finished) {
@@ -1490,7 +1581,7 @@ __device__ float distToZOBBD(const ZOBBDev &z, Vec3 pos)
     return sqrt_(sq);
 }
 
-__device__ void goalRegionsD(const DevState &S, const SceneDev &sc, int w)
+__device__ __forceinline__ void goalRegionsD(const DevState &S, const SceneDev &sc, int w)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1641,7 +1732,7 @@ __device__ void subzoneRewardD(const DevState &S, const SceneDev &sc, int w, int
 }
 
 // sim.cpp:3849-3996 zoneRewardSystem (+ learnShootingRewardSystem 3707-3732)
-__device__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
+__device__ __forceinline__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
 {
     const int64_t g0 = (int64_t)w * S.N;
     const int64_t g = g0 + i;
@@ -1835,7 +1926,7 @@ constexpr int kSimBlock = 128;
 #define MPENV_LAB_SIM_SKIP 0
 #endif
 
-__device__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
+__device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
 
 // 4 waves/SIMD (128 VGPRs, at the price of ~420 B/lane of scratch spills):
 // k_sim alone 0.196 -> 0.139 ms -- every wave of a C3 launch resident,
@@ -1844,7 +1935,9 @@ __device__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &
 #define MPENV_SIM_WPE 4
 #endif
 #define MP_SIM_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_SIM_WPE)))
-__global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR k_sim(DevState S, SceneDev sc)
+// flatten: every phase inlined (an outlined call needs a stack frame in
+// scratch for the whole kernel and spills around the call).
+__global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)) k_sim(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const LBVH bvh = stageBVH(smem, sc);
@@ -1895,9 +1988,14 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR k_sim(DevState S, Scene
         if (!(MPENV_LAB_SIM_SKIP & 512) && act) accumulateCrumbsD(S, w, i);
         __syncthreads();
     }
+    // zoneMatchInfoSystem's per-agent reads, one lane per agent (the world
+    // lane would otherwise walk them serially)
+    __shared__ uint8_t matchBits[kSimBlock];
+    if (act) matchBits[threadIdx.x] = (uint8_t)matchAgentBitsD(S, w, i);
+    __syncthreads();
     if (wlane) {
         if (!(MPENV_LAB_SIM_SKIP & 256) && !sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem
-        if (!(MPENV_LAB_SIM_SKIP & 8)) zoneMatchInfoD(S, sc, w);
+        if (!(MPENV_LAB_SIM_SKIP & 8)) zoneMatchInfoD(S, sc, w, &matchBits[wl * N]);
         if (!(MPENV_LAB_SIM_SKIP & 16)) goalRegionsD(S, sc, w);
     }
     __syncthreads();
@@ -1932,6 +2030,9 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR k_sim(DevState S, Scene
         S.reward[g] = my * (1.f - spirit) + team_r * spirit;
         S.done[g] = S.finished[w] ? 1 : 0;
     }
+    // resets: the agents' own parts in parallel, then the world lane
+    RandKey *pre = S.resetKeys + ((int64_t)w * N) * (kPreDraws + 1);
+    if (act && resetDueD(S, sc, w)) resetPreD(S, sc, w, i, pre + i * (kPreDraws + 1));
     __syncthreads();
     if (wlane) {
         // fullTeamDoneRewardSystem (sim.cpp:4720-4747)
@@ -1945,7 +2046,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR k_sim(DevState S, Scene
             S.ftReward[(int64_t)w * 2 + t] = r;
             S.ftDone[(int64_t)w * 2 + t] = done ? 1 : 0;
         }
-        if (!(MPENV_LAB_SIM_SKIP & 128)) resetSystemD(S, sc, w);
+        if (!(MPENV_LAB_SIM_SKIP & 128)) resetSystemD(S, sc, w, pre);
     }
 }
 
@@ -1983,7 +2084,7 @@ __device__ __forceinline__ Vec3 visSamplePointD(const DevState &S, int64_t gt, V
 
 // utils.cpp:169-271 isAgentVisible for one (viewer, target) pair, lane-wise
 // (the flank reward's checks; k_vis batches the opponent checks instead).
-__device__ bool isAgentVisibleD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, Vec3 org,
+__device__ __forceinline__ bool isAgentVisibleD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, Vec3 org,
                                 Quat aim_rot, int target)
 {
     const int N = S.N;
@@ -2008,7 +2109,7 @@ __device__ bool isAgentVisibleD(const DevState &S, const SceneDev &sc, const LBV
 // opponent that cannot see the agent (judged with the agent's own aim),
 // hits / kills from behind the target, exploration.  CombatState is taken
 // by value there, so nothing is cleared.
-__device__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
+__device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
 {
     const int T = S.T, N = S.N;
     const int64_t g0 = (int64_t)w * N;

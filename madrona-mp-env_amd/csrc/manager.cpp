@@ -566,6 +566,7 @@ static void allocState(mpenv_manager &m)
     S.visited = m.alloc<uint32_t>(A * kGridCells);
     S.filtLast = m.alloc<int32_t>(W * 6);
     S.zoneStats = m.alloc<int32_t>(W * 25);
+    S.resetKeys = m.alloc<mp::RandKey>(A * 11);
     S.spawnTrack = m.alloc<uint32_t>(W * 3 * (size_t)m.sc.spawnTrackLen);
     S.crumbs = m.alloc<float4>(W * kMaxCrumbs * 2);
     S.reset = m.alloc<int32_t>(W);
@@ -667,6 +668,7 @@ static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_
     G.visMask = S.visMask + g0;
     G.visited = S.visited + g0 * kGridCells;
     G.filtLast = S.filtLast + w0 * 6;
+    G.resetKeys = S.resetKeys + g0 * 11;
     G.zoneStats = S.zoneStats + w0 * 25;
     G.spawnTrack = S.spawnTrack + w0 * 3 * track_len;
     G.crumbs = S.crumbs + w0 * kMaxCrumbs * 2;
