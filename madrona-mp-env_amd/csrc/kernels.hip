@@ -1276,20 +1276,33 @@ __device__ void accumulateCrumbsD(const DevState &S, int w, int i)
     S.bcPenalty[g] = total;
 }
 
+// In chunks of 4 crumbs loaded before any is written back: the world lane
+// waits for one round of loads per chunk instead of per crumb, and the
+// compaction only ever writes to slots at or below the chunk being read.
 __device__ void decayCrumbsD(const DevState &S, int w)
 {
     float4 *cr = crumbPtr(S, w);
     const int n = S.numCrumbs[w];
     int m = 0;
-    for (int k = 0; k < n; k++) {
-        float4 p = cr[2 * k];
-        float4 meta = cr[2 * k + 1];
+    auto keep = [&](float4 p, float4 meta, int k) {
+        if (k >= n) return;
         p.w -= 0.025f;
         if (!(p.w <= 0.f)) {
             cr[2 * m] = p;
             cr[2 * m + 1] = meta;
             m += 1;
         }
+    };
+    #pragma unroll 1
+    for (int k0 = 0; k0 < n; k0 += 4) {
+        // past the end: re-read the last crumb (unused)
+        const int k1 = min(k0 + 1, n - 1), k2 = min(k0 + 2, n - 1), k3 = min(k0 + 3, n - 1);
+        const float4 p0 = cr[2 * k0], m0 = cr[2 * k0 + 1], p1 = cr[2 * k1], m1 = cr[2 * k1 + 1];
+        const float4 p2 = cr[2 * k2], m2 = cr[2 * k2 + 1], p3 = cr[2 * k3], m3 = cr[2 * k3 + 1];
+        keep(p0, m0, k0);
+        keep(p1, m1, k0 + 1);
+        keep(p2, m2, k0 + 2);
+        keep(p3, m3, k0 + 3);
     }
     S.numCrumbs[w] = m;
 }
