@@ -226,6 +226,13 @@ struct SceneDev {
     int32_t zoneGoalTri[kMaxZones];
     // logs (sim.cpp:4750-4843 record/replay, 23-106 + 4592-4634 events)
     int32_t recordOn, replayOn, eventsOn;
+    // Sphere-cast vertex-quirk grid (k_move): bit per qgCell x qgCell cell
+    // of the xy plane, set where some BVH vertex lies within
+    // agentRadius + 2 of the cell (scene.h quirkGrid); a cast from o can only
+    // meet the testVert quirk when the cell of 2o is set.
+    const uint32_t *quirkGrid;
+    float qgMinX, qgMinY, qgInvCell;
+    int32_t qgW, qgH;
 };
 
 // Host launchers (kernels.hip)

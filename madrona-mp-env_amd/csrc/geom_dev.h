@@ -590,12 +590,15 @@ struct SphereHit {
 
 // MeshBVH::sphereCast (mesh_bvh.inl:743-815).  r must be kSphereR: the
 // node image of stageBVHSphere carries slab ends widened by that radius.
-__device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r)
+// t_max0: MeshBVH::sphereCast's own t_max argument (mesh_bvh.inl:743-747):
+// the search starts with hit_t = t_max0 and returns it when nothing is
+// nearer.
+__device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r,
+                                                 float t_max0 = mp::kFltMax)
 {
     using namespace mp;
     Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
     Vec3 closest = v3(0.f, 0.f, 0.f);
-    const float t_max0 = kFltMax;
     float hit_t = t_max0;
 #ifdef MPENV_LAB_NO_SPHERE
     if (ray_o.x != 12345.f) {

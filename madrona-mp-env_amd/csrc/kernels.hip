@@ -392,8 +392,46 @@ __device__ __forceinline__ Vec3 rotate2DD(Vec3 dir, float radians) // sim.cpp:87
     return v3(cc * dir.x - s * dir.y, s * dir.x + cc * dir.y, 0);
 }
 
+// Distance-bounded sphere casts (k_move).  MeshBVH::sphereCast prunes boxes
+// beyond its current hit, so with t_max = B it visits the same boxes in the
+// same order as the unbounded cast minus those entered beyond B, and
+// returns the same hit and normal whenever the unbounded cast's hit is
+// nearer than B -- except through the vertex-test quirk (scene.h
+// quirkGrid), which makes far triangles return t = 0.  A bounded cast is
+// therefore only used when the cell of 2o is clear of vertices; otherwise,
+// and where the caller needs more than "hit nearer than B or not", the
+// full cast runs.
+__device__ __forceinline__ bool castQuirkFreeD(const SceneDev &sc, Vec3 o)
+{
+    const float fx = ((o.x + o.x) - sc.qgMinX) * sc.qgInvCell;
+    const float fy = ((o.y + o.y) - sc.qgMinY) * sc.qgInvCell;
+    if (!(fx >= 0.f && fx < (float)sc.qgW && fy >= 0.f && fy < (float)sc.qgH)) return true;
+    const uint32_t bit = (uint32_t)(int)fy * (uint32_t)sc.qgW + (uint32_t)(int)fx;
+    return !((sc.quirkGrid[bit >> 5] >> (bit & 31)) & 1u);
+}
+
+// The cast's hit if nearer than `near_b`, else t = kFltMax: for callers to
+// which every hit at or beyond near_b acts like no hit.
+__device__ __forceinline__ SphereHit castNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
+{
+    if (!castQuirkFreeD(sc, o)) return bvhSphereCastD(bvh, o, d, kSphereR);
+    SphereHit h = bvhSphereCastD(bvh, o, d, kSphereR, near_b);
+    if (!(h.t < near_b)) h.t = kFltMax;
+    return h;
+}
+
+// The full cast's t, searched within near_b first.
+__device__ __forceinline__ float castFirstNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
+{
+    if (castQuirkFreeD(sc, o)) {
+        const float t = bvhSphereCastD(bvh, o, d, kSphereR, near_b).t;
+        if (t < near_b) return t;
+    }
+    return bvhSphereCastD(bvh, o, d, kSphereR).t;
+}
+
 // sim.cpp:889-1039 applyVelocitySystem + updateMoveStateSystem
-__device__ void applyVelocityD(const DevState &S, const LBVH &bvh, int64_t g)
+__device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
 {
     const Vec3 x = ldPos(S, g);
     Vec3 v = ldVel(S, g);
@@ -426,11 +464,16 @@ __device__ void applyVelocityD(const DevState &S, const LBVH &bvh, int64_t g)
         }
         if (normal.z > 0.0f && (double)normal.z < 0.7 && dot(normal, v_norm) < 0.0f) break;
 
+        // The forward casts only matter nearer than move_dist + buffer: a
+        // farther hit leaves hit_pos at move_dist, takes no slide and the
+        // normal / high_hit it sets are read only by the slide (bound with a
+        // wide margin so no value near a decision is ever cut).
+        const float fwd_b = 2.f * (move_dist + buffer) + 10.f;
         ray_o = x + v_norm * buffer * 0.5f;
         ray_o.z += low_check;
         float low_dist;
         {
-            SphereHit h = bvhSphereCastD(bvh, ray_o, v_norm, r);
+            SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
             low_dist = h.t;
             if (h.t < kFltMax) normal = h.n;
         }
@@ -438,7 +481,7 @@ __device__ void applyVelocityD(const DevState &S, const LBVH &bvh, int64_t g)
         bool high_hit = false;
         if (pose != kProne) {
             ray_o.z = x.z + top;
-            SphereHit h = bvhSphereCastD(bvh, ray_o, v_norm, r);
+            SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
             high_dist = h.t;
             if (high_dist < low_dist) {
                 low_dist = high_dist;
@@ -456,16 +499,18 @@ __device__ void applyVelocityD(const DevState &S, const LBVH &bvh, int64_t g)
             if (dot(slide_dir, v_norm) < 0) slide_dir = -slide_dir;
             ray_o = x + v_norm * low_dist;
             ray_o.z += high_hit ? top : low_check;
-            float slide = bvhSphereCastD(bvh, ray_o, slide_dir, r).t;
-            slide = fmaxD(0.0f, slide - buffer);
             float max_move = move_dist - low_dist;
+            // only min(slide - buffer, max_move) is used
+            float slide = castNearD(bvh, sc, ray_o, slide_dir, 2.f * (max_move + buffer) + 10.f).t;
+            slide = fmaxD(0.0f, slide - buffer);
             slide = fminD(slide, max_move);
             if (slide > 0.0f) hit_pos = hit_pos + slide_dir * slide;
         }
 
         Vec3 ground_check = hit_pos;
         ground_check.z += top;
-        float ground_dist = bvhSphereCastD(bvh, ground_check, -kUp, r).t;
+        // min(ground_dist, top) is used, and whether there is ground at all
+        float ground_dist = castFirstNearD(bvh, sc, ground_check, -kUp, 2.f * top + 10.f);
         if (ground_dist == kFltMax) break;
 
         if (ground_dist <= 0.0f || stuck) {
@@ -506,7 +551,7 @@ __device__ void applyVelocityD(const DevState &S, const LBVH &bvh, int64_t g)
 }
 
 // sim.cpp:1041-1104 fallSystem + updateMoveStatePostFallSystem
-__device__ void fallD(const DevState &S, const LBVH &bvh, int64_t g)
+__device__ void fallD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
 {
     if (S.alive[g] == 0.f) return;
     const float fall_rate = 386.08858267717f;
@@ -514,7 +559,9 @@ __device__ void fallD(const DevState &S, const LBVH &bvh, int64_t g)
     Vec3 pos = ldPos(S, g);
     Vec3 ray_o = pos;
     ray_o.z += c::kAgentRadius + cast_offset;
-    float ground = bvhSphereCastD(bvh, ray_o, -kUp, c::kAgentRadius).t;
+    // min(ground - cast_offset, fall_rate * dt) is used, and whether there
+    // is ground at all
+    float ground = castFirstNearD(bvh, sc, ray_o, -kUp, 2.f * (cast_offset + fall_rate * c::kDeltaT) + 10.f);
     if (ground == kFltMax || ground < cast_offset) return;
     float fall = fminD(ground - cast_offset, fall_rate * c::kDeltaT);
     pos.z -= fall;
@@ -1926,8 +1973,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPE
     applyBotActionsD(S, g);
     pvpMovementD(S, g);
     pvpAimD(S, g);
-    applyVelocityD(S, bvh, g);
-    fallD(S, bvh, g);
+    applyVelocityD(S, sc, bvh, g);
+    fallD(S, sc, bvh, g);
 }
 
 // Step graph part 2 (fireSystem onward): per-world phases.  A workgroup

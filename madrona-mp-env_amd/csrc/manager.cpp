@@ -443,6 +443,18 @@ static void buildSceneDev(mpenv_manager &m)
         m.upload(d_pre, pre.data(), sizeof(float) * pre.size());
         sc.triPre = d_pre;
     }
+    {
+        // the sphere-cast radius is always consts::agentRadius (k_move)
+        const QuirkGrid q = quirkGrid(s.bvhVerts, 15.f, 2.f, 16.f);
+        uint32_t *d_q = m.alloc<uint32_t>(std::max<size_t>(q.bits.size(), 1));
+        if (!q.bits.empty()) m.upload(d_q, q.bits.data(), sizeof(uint32_t) * q.bits.size());
+        sc.quirkGrid = d_q;
+        sc.qgMinX = q.minX;
+        sc.qgMinY = q.minY;
+        sc.qgInvCell = 1.f / q.cell;
+        sc.qgW = q.w;
+        sc.qgH = q.h;
+    }
     sc.nodes = d_nodes;
     sc.verts = d_verts;
     sc.numNodes = (int32_t)s.nodes.size();

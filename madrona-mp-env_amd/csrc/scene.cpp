@@ -395,6 +395,40 @@ std::vector<BVHNode> octantNodeImages(const std::vector<BVHNode> &nodes)
     return out;
 }
 
+QuirkGrid quirkGrid(const std::vector<Vec3> &verts, float r, float margin, float cell)
+{
+    QuirkGrid q;
+    q.cell = cell;
+    if (verts.empty()) return q;
+    float lo[2] = { verts[0].x, verts[0].y }, hi[2] = { verts[0].x, verts[0].y };
+    for (const Vec3 &v : verts) {
+        lo[0] = std::min(lo[0], v.x); lo[1] = std::min(lo[1], v.y);
+        hi[0] = std::max(hi[0], v.x); hi[1] = std::max(hi[1], v.y);
+    }
+    const float reach = r + margin;
+    q.minX = std::floor((lo[0] - reach - cell) / cell) * cell;
+    q.minY = std::floor((lo[1] - reach - cell) / cell) * cell;
+    q.w = (int32_t)std::ceil((hi[0] + reach + cell - q.minX) / cell) + 1;
+    q.h = (int32_t)std::ceil((hi[1] + reach + cell - q.minY) / cell) + 1;
+    q.bits.assign(((size_t)q.w * q.h + 31) / 32, 0u);
+    for (const Vec3 &v : verts) {
+        const int x0 = (int)std::floor((v.x - reach - q.minX) / cell), x1 = (int)std::floor((v.x + reach - q.minX) / cell);
+        const int y0 = (int)std::floor((v.y - reach - q.minY) / cell), y1 = (int)std::floor((v.y + reach - q.minY) / cell);
+        for (int y = std::max(0, y0); y <= std::min(q.h - 1, y1); y++)
+            for (int x = std::max(0, x0); x <= std::min(q.w - 1, x1); x++) {
+                // distance from v to the square, in double
+                const double cx0 = q.minX + (double)x * cell, cy0 = q.minY + (double)y * cell;
+                const double dx = std::max({ cx0 - v.x, 0.0, (double)v.x - (cx0 + cell) });
+                const double dy = std::max({ cy0 - v.y, 0.0, (double)v.y - (cy0 + cell) });
+                if (dx * dx + dy * dy <= (double)reach * reach) {
+                    const size_t bit = (size_t)y * q.w + x;
+                    q.bits[bit >> 5] |= 1u << (bit & 31);
+                }
+            }
+    }
+    return q;
+}
+
 Scene loadScene(const std::string &dir, bool spawn_in_middle)
 {
     Scene s;

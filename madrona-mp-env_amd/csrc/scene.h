@@ -118,4 +118,19 @@ void buildBVH(const std::vector<mp::Vec3> &tri_verts, Scene &out);
 // Node indices, bounds and leaves are unchanged; only slot order differs.
 std::vector<BVHNode> octantNodeImages(const std::vector<BVHNode> &nodes);
 
+// The sphere cast's vertex test (mesh_bvh.inl:1073-1104) subtracts a vertex
+// already taken relative to the origin o from o again, and returns t = 0
+// for any visited triangle with a vertex v within the cast radius r of 2o
+// (|2o - v| <= r, up to rounding).  quirkGrid marks, on a grid of `cell`
+// x `cell` squares of the xy plane starting at (minX, minY), every square
+// within xy distance r + margin of a vertex: when the square holding 2o is
+// clear, no triangle can trigger the quirk for a cast from o, so the
+// cast's result does not depend on which far triangles it visits.
+struct QuirkGrid {
+    float minX = 0.f, minY = 0.f, cell = 16.f;
+    int32_t w = 0, h = 0;
+    std::vector<uint32_t> bits; // row-major, w * h bits
+};
+QuirkGrid quirkGrid(const std::vector<mp::Vec3> &verts, float r, float margin, float cell);
+
 } // namespace mpenv
