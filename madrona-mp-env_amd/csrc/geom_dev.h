@@ -283,6 +283,49 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
     return true;
 }
 
+// rayTri with one data-dependent branch (the accepted hit's division) plus
+// the rare f64 edge fallback: the rejection tests are folded into one
+// predicate instead of nested early returns, so a wave whose lanes reject
+// at different tests runs no extra exec-mask rounds.  Every value is
+// computed exactly as in rayTri (T and det of a rejected lane are computed
+// and dropped), so the accepted set and out_t are identical.
+__device__ __forceinline__ bool rayTriFlat(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, const RayTxfmD &tx, mp::Vec3 org,
+                                           float t_max, float &out_t)
+{
+    using namespace mp;
+    const Vec3 A = ta - org, B = tb - org, C = tc - org;
+    const float Az_ = comp(A, tx.kz), Bz_ = comp(B, tx.kz), Cz_ = comp(C, tx.kz);
+    const float Ax = fma_(-tx.Sx, Az_, comp(A, tx.kx));
+    const float Ay = fma_(-tx.Sy, Az_, comp(A, tx.ky));
+    const float Bx = fma_(-tx.Sx, Bz_, comp(B, tx.kx));
+    const float By = fma_(-tx.Sy, Bz_, comp(B, tx.ky));
+    const float Cx = fma_(-tx.Sx, Cz_, comp(C, tx.kx));
+    const float Cy = fma_(-tx.Sy, Cz_, comp(C, tx.ky));
+    float U = fma_(Cx, By, -(Cy * Bx));
+    float V = fma_(Ax, Cy, -(Ay * Cx));
+    float W = fma_(Bx, Ay, -(By * Ax));
+    bool ok = !(U < 0.0f || V < 0.0f || W < 0.0f);
+    if (ok && (U == 0.0f || V == 0.0f || W == 0.0f)) {
+        double CxBy = (double)Cx * (double)By;
+        double CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        double AxCy = (double)Ax * (double)Cy;
+        double AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        double BxAy = (double)Bx * (double)Ay;
+        double ByAx = (double)By * (double)Ax;
+        W = (float)(BxAy - ByAx);
+        ok = !(U < 0.0f || V < 0.0f || W < 0.0f);
+    }
+    const float det = U + V + W;
+    const float Az = tx.Sz * Az_;
+    const float Bz = tx.Sz * Bz_;
+    const float Cz = tx.Sz * Cz_;
+    const float T = fma_(U, Az, fma_(V, Bz, W * Cz));
+    ok = ok && det != 0.f && !(T < 0.0f || T > t_max * det);
+    if (ok) out_t = T * (1.0f / det);
+    return ok;
+}
 
 // rayTri with the vertex components read in the ray's (kx, ky, kz) order
 // straight from LDS (per-lane byte offsets ko = 4 * k) instead of selected
@@ -336,6 +379,10 @@ __device__ __forceinline__ bool rayTriPermD(const LBVH &b, int tri, const RayTxf
     out_t = T * rcpDet;
     return true;
 }
+
+#ifndef MPENV_TRI_FLAT
+#define MPENV_TRI_FLAT 0
+#endif
 
 // MeshBVH::traceRay (mesh_bvh.inl:110-208) over the LDS-resident BVH.
 // Returns hit flag; *t_out = closest hit t when hit.
@@ -409,7 +456,12 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
 #ifdef MPENV_LAB_NO_TRI
                     for (int k = 0; k < 0; k++) {
 #else
-                    for (int k = 0; k < ntri; k++) {
+                    // Leaves hold at most 2 triangles (scene.cpp Builder):
+                    // the unrolled pair runs without a loop counter
+                    // (k_lidar -3%, k_vis -3%, identical outputs).
+#pragma unroll
+                    for (int k = 0; k < 2; k++) {
+                        if (k >= ntri) break;
 #endif
                         bool h;
                         if constexpr (kPerm) {
@@ -417,7 +469,11 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                         } else {
                             Vec3 a, bb, c;
                             loadTri(b, leaf + k, a, bb, c);
+#if MPENV_TRI_FLAT
+                            h = rayTriFlat(a, bb, c, tx, ray_o, leaf_tmax, hit_t);
+#else
                             h = rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t);
+#endif
                         }
                         if (h) {
                             hit_tri = true;
@@ -678,10 +734,16 @@ struct WorldHit {
 
 // traceRayAgainstWorld (utils.cpp:10-72): BVH then the world's N capsules.
 // Capsule bases are read from the SoA position columns (cached).
+// `self`: the casting agent's index in the world when the ray starts on its
+// own capsule's axis (org.xy == its position's xy, so tr.xy is exactly 0,
+// and org.z - base.z - r in [0, segment] up to rounding: the lidar and shot
+// origins sit r, viewHeight - r... above the feet, 0-35 units up the axis).
+// intersectRayZOriginCapsule returns 0 for an origin inside the capsule, so
+// that capsule can never be the hit and its test is skipped; -1: test all.
 template <bool kPerm = false>
 __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__restrict__ px,
                                                 const float *__restrict__ py, const float *__restrict__ pz,
-                                                int64_t g0, int N, mp::Vec3 org, mp::Vec3 d)
+                                                int64_t g0, int N, mp::Vec3 org, mp::Vec3 d, int self = -1)
 {
     using namespace mp;
     float min_t = kFltMax;
@@ -705,6 +767,9 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     const float dxy2 = d.x * d.x + d.y * d.y;
     const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
     for (int j = 0; j < N; j++) {
+#ifndef MPENV_LAB_NO_SELF_SKIP
+        if (j == self) continue;
+#endif
         Vec3 co = v3(px[g0 + j], py[g0 + j], pz[g0 + j]);
         co.z += kCapsuleRadius;
         Vec3 tr = org - co;

@@ -641,7 +641,7 @@ __device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, con
     stAim(S, g, a);
     Vec3 fire_dir = rotateVec(a.rot, kFwd);
 
-    WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, fire_from, fire_dir);
+    WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, fire_from, fire_dir, i); // from its own axis
     if (S.stats) statAdd(S.stats + kStatShots, 1u);
     S.firedT[g] = h.hit ? h.t : kFltMax;
     bool success = h.hit;
@@ -2423,14 +2423,120 @@ __device__ __forceinline__ Vec3 normalizedPosUnclampedD(const SceneDev &sc, Vec3
     return v3((p.x - min_x) / xr, (p.y - min_y) / yr, (p.z - min_z) / zr);
 }
 
-__device__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int64_t g, int team, int off)
+// pvpOpponentMasksSystem (sim.cpp:2562-2614) + pvpObservationsSystem
+// (sim.cpp:2645-3052).  Lane = agent.
+//
+// Teammate / opponent observation rows ([A][slots][32] f32, 128 B each) leave
+// through LDS: written straight from the lane, one store instruction would
+// put a 16-byte piece into each of 64 rows (64 partial lines for the L2 to
+// merge); transposed per wave, each instruction writes 8 whole rows.
+constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
+
+__device__ __forceinline__ void waveSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Flushes the wave's staged 32-float rows (lane l's row at buf + l *
+// kObsRowPad, written there by the lane) to arr[(gw0 + r) * slots + k].
+__device__ __forceinline__ void flushRowsWave(float *arr, int slots, int k, int64_t gw0, int64_t A, const float *buf,
+                                              int lane)
+{
+    // Cross-lane exchange through LDS inside one wave: the wave's DS
+    // instructions execute in issue order, so the hardware needs no wait;
+    // what must be ordered is the compiler's view.  A wavefront-scope
+    // release/acquire fence pair around a wave barrier makes the other
+    // lanes' row writes visible to this lane's reads (and, below, the reads
+    // complete before the next rows overwrite the buffer) without a
+    // data race in the source.
+    waveSync();
+    // the wave's m live lanes (a tail wave's lanes past A have returned)
+    // share its m rows x 8 chunks
+    const int m = (int)(A - gw0 < 64 ? A - gw0 : 64);
+#pragma unroll
+    for (int j = 0; j < kOtherObs / 4; j++) {
+        const int c = lane + j * m, r = c >> 3, col = c & 7;
+        reinterpret_cast<float4 *>(arr + ((gw0 + r) * slots + k) * kOtherObs)[col] =
+            reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col];
+    }
+    waveSync(); // reads done before the next rows land
+}
+
+// The other per-agent rows (self obs, positions, masks, last-known rows,
+// the full-team slots) are short (3-33 floats) and laid out at a per-lane
+// row offset.  Written straight from the lane, each dword store instruction
+// touches 64 different rows; staged here, lane l's n floats go to LDS (row
+// stride P, odd: conflict-free), then each store instruction writes 64
+// consecutive staged floats -- a handful of whole rows, a few cache lines.
+// `off` is the lane's row offset in floats within dst, < 0 for "no row"
+// (conditional rows: the last-known slots); `zero` stores zeros instead of
+// the staged values.  Every live lane of the wave takes part (m = live
+// lanes, the wave's first m).
+struct WaveStage {
+    float *buf;
+    int64_t *offs;
+    int lane, m;
+
+    template <int P> __device__ __forceinline__ void stage(const float *vals, int n) const
+    {
+        for (int k = 0; k < n; k++) buf[lane * P + k] = vals[k];
+    }
+    template <int n, int P> __device__ __forceinline__ void flush(float *dst, int64_t off, bool zero = false) const
+    {
+        // which rows exist / are zeros: wave-wide bit masks (lane r = row r)
+        const uint64_t wbits = __ballot(off >= 0), zbits = __ballot(zero);
+        offs[lane] = off;
+        waveSync();
+        // the m live lanes (a tail wave's lanes past A have returned) share
+        // the m x n staged floats
+#pragma unroll 1
+        for (int j = 0; j < n; j++) {
+            const int c = lane + m * j;
+            const int r = c / n, col = c - r * n;
+            if ((wbits >> r) & 1u) {
+                const float v = ((zbits >> r) & 1u) ? 0.f : buf[r * P + col];
+                dst[offs[r] + col] = v;
+            }
+        }
+        waveSync(); // reads done before the next rows land
+    }
+    // The same for rows of n4 float4 (16-B aligned rows, P a multiple of 4):
+    // one 16-B store per lane per instruction, 4 lanes per 64-B row piece.
+    template <int n4, int P> __device__ __forceinline__ void flush4(float *dst, int64_t off, bool zero = false) const
+    {
+        static_assert(P % 4 == 0, "float4 rows");
+        const uint64_t wbits = __ballot(off >= 0), zbits = __ballot(zero);
+        offs[lane] = off;
+        waveSync();
+#pragma unroll
+        for (int j = 0; j < n4; j++) {
+            const int c = lane + m * j;
+            const int r = c / n4, col = c - r * n4;
+            if ((wbits >> r) & 1u) {
+                const float4 v = ((zbits >> r) & 1u) ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                                     : reinterpret_cast<const float4 *>(buf + r * P)[col];
+                reinterpret_cast<float4 *>(dst + offs[r])[col] = v;
+            }
+        }
+        waveSync();
+    }
+    template <int n> __device__ __forceinline__ void put(float *dst, int64_t off, const float *vals) const
+    {
+        constexpr int P = n | 1;
+        static_assert(P <= kObsRowPad, "span larger than the row buffer");
+        stage<P>(vals, n);
+        flush<n, P>(dst, off);
+    }
+};
+
+__device__ __forceinline__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int64_t g, int team,
+                                              int off, const WaveStage &ws)
 {
     const int T = S.T;
-    const int64_t g0 = (int64_t)w * S.N;
     const int64_t mine = (int64_t)w * 2 + team, theirs = (int64_t)w * 2 + (team ^ 1);
-    float *pl = &S.ftPlayers[(mine * 6 + off) * MPENV_FT_PLAYER_DIM];
-    float *en = &S.ftEnemies[(theirs * 6 + off) * MPENV_FT_ENEMY_DIM];
-    float *lk = &S.ftLastKnown[(theirs * 6 + off) * MPENV_FT_COMMON_DIM];
+    const int64_t g0 = (int64_t)w * S.N;
     const bool alive = S.alive[g] != 0.f;
 
     // enemy-only fields first: they decide whether the last-known slot
@@ -2443,43 +2549,54 @@ __device__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int6
         for (int m = 0; m < T; m++) los |= ((S.visMask[gm0 + m] >> off) & 1u) << m;
         knows = knows || los != 0;
     }
-    en[24] = alive ? (float)S.wasShot[g] : 0.f;
-    en[25] = fired;
-    for (int m = 0; m < kMaxTeamSize; m++) en[26 + m] = (los >> m) & 1u ? 1.f : 0.f;
-    en[32] = knows ? 1.f : 0.f;
 
-    // the common block, stored to all three slots as it is produced
-    auto put = [&](int k, float v) {
-        pl[k] = v;
-        en[k] = v;
-        lk[k] = knows ? v : 0.f;
-    };
-    put(0, 1.f);
-    for (int k = 0; k < kMaxTeamSize; k++) put(1 + k, k == off ? 1.f : 0.f);
+    // the common block (same in the player, enemy and last-known slots)
+    float cm[MPENV_FT_COMMON_DIM];
+    cm[0] = 1.f;
+    for (int k = 0; k < kMaxTeamSize; k++) cm[1 + k] = k == off ? 1.f : 0.f;
+    for (int k = 7; k < MPENV_FT_COMMON_DIM; k++) cm[k] = 0.f;
+    float ext[4] = { 0.f, 0.f, 0.f, 0.f };
     if (alive) {
-        put(7, 1.f);
+        cm[7] = 1.f;
         const Vec3 np = normalizedPosUnclampedD(sc, ldPos(S, g));
-        put(8, np.x); put(9, np.y); put(10, np.z);
-        put(11, 0.5f * ((S.ayaw[g] / kPi) + 1.f));
-        put(12, 0.5f * (S.apitch[g] / (0.25f * kPi) + 1.f));
-        put(13, S.vx[g]); put(14, S.vy[g]); put(15, S.vz[g]);
+        cm[8] = np.x; cm[9] = np.y; cm[10] = np.z;
+        cm[11] = 0.5f * ((S.ayaw[g] / kPi) + 1.f);
+        cm[12] = 0.5f * (S.apitch[g] / (0.25f * kPi) + 1.f);
+        cm[13] = S.vx[g]; cm[14] = S.vy[g]; cm[15] = S.vz[g];
         const int cp = S.curPose[g], tp = S.tgtPose[g];
-        put(16, cp == kStand ? 1.f : 0.f);
-        put(17, cp == kCrouch ? 1.f : 0.f);
-        put(18, cp == kProne ? 1.f : 0.f);
-        put(19, tp == kStand ? 1.f : 0.f);
-        put(20, tp == kCrouch ? 1.f : 0.f);
-        put(21, tp == kProne ? 1.f : 0.f);
-        put(22, (float)S.transRem[g] / (float)c::kPoseTransitionSpeed);
-        put(23, (S.flags[g] & kFlagInZone) ? 1.f : 0.f);
-        pl[24] = S.hp[g] / 100.f;
-        pl[25] = (float)S.magazine[2 * g] / 30;
-        pl[26] = (float)S.magazine[2 * g + 1];
-        pl[27] = float(S.autohealSteps[g]) / float(c::kOutOfCombatSteps);
-    } else {
-        for (int k = 7; k < MPENV_FT_COMMON_DIM; k++) put(k, 0.f);
-        for (int k = MPENV_FT_COMMON_DIM; k < MPENV_FT_PLAYER_DIM; k++) pl[k] = 0.f;
+        cm[16] = cp == kStand ? 1.f : 0.f;
+        cm[17] = cp == kCrouch ? 1.f : 0.f;
+        cm[18] = cp == kProne ? 1.f : 0.f;
+        cm[19] = tp == kStand ? 1.f : 0.f;
+        cm[20] = tp == kCrouch ? 1.f : 0.f;
+        cm[21] = tp == kProne ? 1.f : 0.f;
+        cm[22] = (float)S.transRem[g] / (float)c::kPoseTransitionSpeed;
+        cm[23] = (S.flags[g] & kFlagInZone) ? 1.f : 0.f;
+        ext[0] = S.hp[g] / 100.f;
+        ext[1] = (float)S.magazine[2 * g] / 30;
+        ext[2] = (float)S.magazine[2 * g + 1];
+        ext[3] = float(S.autohealSteps[g]) / float(c::kOutOfCombatSteps);
     }
+    // one staged row (stride kObsRowPad) serves all three slots: the common
+    // block, then the enemy tail; the player tail is staged over the enemy
+    // tail after the enemy row has left
+    constexpr int P = kObsRowPad;
+    static_assert(MPENV_FT_ENEMY_DIM <= P && MPENV_FT_PLAYER_DIM <= P, "ft rows");
+    ws.stage<P>(cm, MPENV_FT_COMMON_DIM);
+    {
+        float et[MPENV_FT_ENEMY_DIM - MPENV_FT_COMMON_DIM];
+        et[0] = alive ? (float)S.wasShot[g] : 0.f;
+        et[1] = fired;
+        for (int m = 0; m < kMaxTeamSize; m++) et[2 + m] = (los >> m) & 1u ? 1.f : 0.f;
+        et[8] = knows ? 1.f : 0.f;
+        for (int k = 0; k < MPENV_FT_ENEMY_DIM - MPENV_FT_COMMON_DIM; k++)
+            ws.buf[ws.lane * P + MPENV_FT_COMMON_DIM + k] = et[k];
+    }
+    static_assert(MPENV_FT_COMMON_DIM % 4 == 0 && MPENV_FT_PLAYER_DIM % 4 == 0, "16-B ft rows");
+    ws.flush<MPENV_FT_ENEMY_DIM, P>(S.ftEnemies, (theirs * 6 + off) * MPENV_FT_ENEMY_DIM);
+    ws.flush4<MPENV_FT_COMMON_DIM / 4, P>(S.ftLastKnown, (theirs * 6 + off) * MPENV_FT_COMMON_DIM, !knows);
+    for (int k = 0; k < 4; k++) ws.buf[ws.lane * P + MPENV_FT_COMMON_DIM + k] = ext[k];
+    ws.flush4<MPENV_FT_PLAYER_DIM / 4, P>(S.ftPlayers, (mine * 6 + off) * MPENV_FT_PLAYER_DIM);
 
     if (off != 0) return;
     for (int s = T; s < kMaxTeamSize; s++) {
@@ -2506,49 +2623,6 @@ __device__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int6
     storeVec(&S.ftGlobal[mine * MPENV_FT_GLOBAL_DIM], gob, MPENV_FT_GLOBAL_DIM);
 }
 
-// pvpOpponentMasksSystem (sim.cpp:2562-2614) + pvpObservationsSystem
-// (sim.cpp:2645-3052).  Lane = agent.
-//
-// Teammate / opponent observation rows ([A][slots][32] f32, 128 B each) leave
-// through LDS: written straight from the lane, one store instruction would
-// put a 16-byte piece into each of 64 rows (64 partial lines for the L2 to
-// merge); transposed per wave, each instruction writes 8 whole rows.
-constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
-
-__device__ __forceinline__ void waveSync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ void storeRowsWave(float *arr, int slots, int k, const float *row, int64_t gw0, int64_t A,
-                                              float *buf, int lane)
-{
-    float4 *mine = reinterpret_cast<float4 *>(buf + lane * kObsRowPad);
-#pragma unroll
-    for (int q = 0; q < kOtherObs / 4; q++)
-        mine[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
-    // Cross-lane exchange through LDS inside one wave: the wave's DS
-    // instructions execute in issue order, so the hardware needs no wait;
-    // what must be ordered is the compiler's view.  A wavefront-scope
-    // release/acquire fence pair around a wave barrier makes the other
-    // lanes' row writes visible to this lane's reads (and, below, the reads
-    // complete before the next rows overwrite the buffer) without a
-    // data race in the source.
-    waveSync();
-    // the wave's m live lanes (a tail wave's lanes past A have returned)
-    // share its m rows x 8 chunks
-    const int m = (int)(A - gw0 < 64 ? A - gw0 : 64);
-#pragma unroll
-    for (int j = 0; j < kOtherObs / 4; j++) {
-        const int c = lane + j * m, r = c >> 3, col = c & 7;
-        reinterpret_cast<float4 *>(arr + ((gw0 + r) * slots + k) * kOtherObs)[col] =
-            reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col];
-    }
-    waveSync(); // reads done before the next rows land
-}
-
 #ifndef MPENV_OBS_NOUNROLL
 #define MPENV_OBS_NOUNROLL 0
 #endif
@@ -2560,11 +2634,17 @@ __device__ __forceinline__ void storeRowsWave(float *arr, int slots, int k, cons
 __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev sc)
 {
     __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsRowPad];
+    __shared__ int64_t offBuf[kBlock / 64][64];
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const int64_t gw0 = g - lane; // first agent of the wave
     float *wbuf = rowBuf[threadIdx.x >> 6];
-    if (g >= S.A) return; // the tail wave's lanes past A (storeRowsWave counts the live ones)
+    if (g >= S.A) return; // the tail wave's lanes past A (the flushes count the live ones)
+    WaveStage ws;
+    ws.buf = wbuf;
+    ws.offs = offBuf[threadIdx.x >> 6];
+    ws.lane = lane;
+    ws.m = (int)(S.A - gw0 < 64 ? S.A - gw0 : 64);
     const int T = S.T, N = S.N;
     const int w = (int)(g / N);
     const int i = (int)(g - (int64_t)w * N);
@@ -2588,7 +2668,7 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
         if (can_see) mask[k] = 1.f;
         if (S.firedT[go] >= 0) mask[k] = 1.f;
     }
-    storeVec(&S.masks[g * 6], mask, 6);
+    ws.put<6>(S.masks, g * 6, mask);
     // teamKnowsLocation (mask[k] == 1) as bits for the opponent loop.
     // Reading the float array there instead gives wrong last-known updates
     // on the 2v2_navmesh_curriculum golden case at init (agents 4, 6, 9
@@ -2636,17 +2716,21 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
         zo[14] = cz == 2 ? 1.f : 0.f;
         zo[15] = cz == 3 ? 1.f : 0.f;
     }
-    storeVec(&S.selfObs[g * kSelfObs], ob, kSelfObs);
-    storeVec(&S.selfPos[g * 3], pos3, 3);
+    static_assert(kSelfObs == 43, "self obs split");
+    ws.put<22>(S.selfObs, g * kSelfObs, ob);
+    ws.put<21>(S.selfObs, g * kSelfObs + 22, ob + 22);
+    ws.put<3>(S.selfPos, g * 3, pos3);
 
+    // teammate / opponent rows are built in place in the lane's LDS row
+    float *row = wbuf + lane * kObsRowPad;
     // teammates
 #if MPENV_OBS_NOUNROLL
 #pragma unroll 1
 #endif
     for (int k = 0; k < kMaxTeamSize - 1; k++) {
-        float tob[kOtherObs];
+        float *tob = row;
         float tpos[3];
-        for (int q = 0; q < kOtherObs; q++) tob[q] = 0.f;
+        for (int q = 0; q < kOtherObs / 4; q++) reinterpret_cast<float4 *>(tob)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         tpos[0] = tpos[1] = tpos[2] = -1000.f;
         if (alive_ok && k < T - 1) {
             const int64_t gj = g0 + team * T + (k < off ? k : k + 1);
@@ -2655,8 +2739,8 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
                 fillCombatD(S, gj, &tob[28]);
             }
         }
-        storeRowsWave(S.tmObs, 5, k, tob, gw0, S.A, wbuf, lane);
-        storeVec(&S.tmPos[(g * 5 + k) * 3], tpos, 3);
+        flushRowsWave(S.tmObs, 5, k, gw0, S.A, wbuf, lane);
+        ws.put<3>(S.tmPos, (g * 5 + k) * 3, tpos);
     }
 
     // opponents (+ last known)
@@ -2664,39 +2748,43 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
 #pragma unroll 1
 #endif
     for (int k = 0; k < kMaxTeamSize; k++) {
-        float oob[kOtherObs];
+        float *oob = row;
         float opos[3];
-        for (int q = 0; q < kOtherObs; q++) oob[q] = 0.f;
+        for (int q = 0; q < kOtherObs / 4; q++) reinterpret_cast<float4 *>(oob)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         opos[0] = opos[1] = opos[2] = -1000.f;
-        float *lk = &S.lkObs[(g * 6 + k) * kOtherObs];
-        float *lkp = &S.lkPos[(g * 6 + k) * 3];
+        // last-known slot: cleared (opponent dead / just killed), then
+        // overwritten with the observation when the team knows the location
+        bool lk_write = false, lk_keep = false;
         if (alive_ok && k < T) {
             const int64_t gj = g0 + (team ^ 1) * T + k;
             if (!fillCommonD(S, sc, sf, gj, oob, opos)) {
-                for (int q = 0; q < kOtherObs; q++) lk[q] = 0.f;
-                lkp[0] = lkp[1] = lkp[2] = -1000.f;
+                lk_write = true;
             } else {
                 fillOtherD(S, sf, gj, oob);
-                if (S.flags[gj] & kFlagWasKilled) {
-                    for (int q = 0; q < kOtherObs; q++) lk[q] = 0.f;
-                    lkp[0] = lkp[1] = lkp[2] = -1000.f;
-                }
+                if (S.flags[gj] & kFlagWasKilled) lk_write = true;
                 oob[28] = (float)S.wasShot[gj];
                 oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
                 oob[30] = ((vm[g] >> k) & 1) ? 1.f : 0.f;
                 const bool knows = (knowsBits >> k) & 1u; // teamKnowsLocation (sim.cpp:2995-3003)
                 oob[31] = knows ? 1.f : 0.f;
-                if (knows) {
-                    storeVec(lk, oob, kOtherObs);
-                    storeVec(lkp, opos, 3);
-                }
+                lk_keep = knows;
+                lk_write = lk_write || knows;
             }
         }
-        storeRowsWave(S.oppObs, 6, k, oob, gw0, S.A, wbuf, lane);
-        storeVec(&S.oppPos[(g * 6 + k) * 3], opos, 3);
+        flushRowsWave(S.oppObs, 6, k, gw0, S.A, wbuf, lane);
+        // the rows are still staged (stride kObsRowPad): the last-known copy
+        ws.flush4<kOtherObs / 4, kObsRowPad>(S.lkObs, lk_write ? (g * 6 + k) * kOtherObs : -1, !lk_keep);
+        ws.put<3>(S.oppPos, (g * 6 + k) * 3, opos);
+        {
+            float lpos[3];
+            for (int q = 0; q < 3; q++) lpos[q] = lk_keep ? opos[q] : -1000.f;
+            ws.put<3>(S.lkPos, lk_write ? (g * 6 + k) * 3 : -1, lpos);
+        }
     }
 
-    fullTeamSlotD(S, sc, w, g, team, off);
+#ifndef MPENV_LAB_OBS_NO_FT
+    fullTeamSlotD(S, sc, w, g, team, off, ws);
+#endif
 }
 
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray.  Rays are dealt to
@@ -2786,7 +2874,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
 #ifndef MPENV_LIDAR_PERM
 #define MPENV_LIDAR_PERM 0
 #endif
-        WorldHit hw = traceWorldD<MPENV_LIDAR_PERM != 0>(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir);
+        WorldHit hw = traceWorldD<MPENV_LIDAR_PERM != 0>(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir, (int)i);
         const bool second = i >= T; // team of the casting agent
         float4 out;
         if (hw.hit) {

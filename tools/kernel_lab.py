@@ -117,7 +117,8 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
     hip.hipDeviceSynchronize()
     dig = hashlib.sha1()
-    for eid in (6, 10, 12, 13, 18, 19, 20, 23, 24, 65, 66, 67):
+    per = {}
+    for eid in (6, 10, 12, 13, 18, 19, 20, 23, 24, 65, 66, 67, 11, 14, 15, 16, 17, 27, 28, 29, 30, 31, 32):
         p, dt, nd, gid = C.c_void_p(), C.c_int32(), C.c_int32(), C.c_int32()
         dims = (C.c_int64 * 8)()
         assert lib.mpenv_export_tensor(h, eid, C.byref(p), C.byref(dt), C.byref(nd), dims, C.byref(gid)) == 0
@@ -126,10 +127,15 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
             nbytes *= dims[i]
         buf = (C.c_char * nbytes)()
         assert hip.hipMemcpy(buf, p, C.c_size_t(nbytes), 2) == 0
-        dig.update(bytes(buf))
+        if eid in (6, 10, 12, 13, 18, 19, 20, 23, 24, 65, 66, 67):
+            dig.update(bytes(buf))
+        per[eid] = hashlib.sha1(bytes(buf)).hexdigest()[:6]
+        if str(eid) in os.environ.get("LAB_DUMP", "").split(","):
+            os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+            open(os.path.join(ROOT, "gpurun_out", f"dump_{label or name}_{eid}.bin"), "wb").write(bytes(buf))
     print(json.dumps({"variant": label or name, "ms_per_step": round(1e3 * el_groups / steps, 4),
                       "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
-                      "digest": dig.hexdigest()[:16]}), flush=True)
+                      "digest": dig.hexdigest()[:16], "per_export": per}), flush=True)
 
 
 if __name__ == "__main__":
