@@ -740,6 +740,10 @@ struct WorldHit {
 // origins sit r, viewHeight - r... above the feet, 0-35 units up the axis).
 // intersectRayZOriginCapsule returns 0 for an origin inside the capsule, so
 // that capsule can never be the hit and its test is skipped; -1: test all.
+__device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, const float *__restrict__ py,
+                                              const float *__restrict__ pz, int64_t g0, int N, mp::Vec3 org,
+                                              mp::Vec3 d, int self, bool hit, float min_t);
+
 template <bool kPerm = false>
 __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__restrict__ px,
                                                 const float *__restrict__ py, const float *__restrict__ pz,
@@ -758,6 +762,16 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
 #ifdef MPENV_LAB_NO_CAPSULE
     N = 0;
 #endif
+    return capsulesD(px, py, pz, g0, N, org, d, self, hit, min_t);
+}
+
+// traceRayAgainstWorld's capsule loop (utils.cpp:40-69) after the BVH hit
+// (hit, min_t).
+__device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, const float *__restrict__ py,
+                                              const float *__restrict__ pz, int64_t g0, int N, mp::Vec3 org,
+                                              mp::Vec3 d, int self, bool hit, float min_t)
+{
+    using namespace mp;
     int ent = -1;
     // Conservative cull: every point of a Z-capsule lies within r of its
     // vertical axis, so a ray whose xy line passes farther than r from the
@@ -798,6 +812,17 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     h.t = min_t;
     h.entity = ent;
     return h;
+}
+
+// Orders one wave's LDS writes before other lanes' reads of them (and those
+// reads before the next overwrite): a wavefront-scope release/acquire fence
+// pair around a wave barrier.  The wave's DS instructions execute in issue
+// order, so this constrains the compiler only.
+__device__ __forceinline__ void waveSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // traceRayAgainstWorld(org, d).entity == target (utils.cpp:10-72, as

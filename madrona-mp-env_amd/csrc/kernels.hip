@@ -1385,12 +1385,36 @@ __device__ __forceinline__ uint32_t matchAgentBitsD(const DevState &S, int w, in
     return b;
 }
 
-// sim.cpp:128-291 updateFiltersState from the world's agent bits
-__device__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const uint8_t *mb)
+// Agent bit masks (bit i = agent i of the world) from the LDS bytes.
+struct MatchMasks {
+    uint32_t killed, died, f0, f1, f2;
+};
+
+__device__ __forceinline__ MatchMasks matchMasksD(const uint8_t *mb, int N)
 {
-    const int N = S.N;
-    int32_t *last = &S.filtLast[(int64_t)w * 6]; // [team][filter]
+    MatchMasks m = { 0u, 0u, 0u, 0u, 0u };
+    #pragma unroll 1
+    for (int i = 0; i < N; i++) {
+        const uint32_t b = mb[i];
+        m.killed |= ((b & kMbKilled) ? 1u : 0u) << i;
+        m.died |= ((b & kMbDied) ? 1u : 0u) << i;
+        m.f0 |= ((b & kMbF0) ? 1u : 0u) << i;
+        m.f1 |= ((b & kMbF1) ? 1u : 0u) << i;
+        m.f2 |= ((b & kMbF2) ? 1u : 0u) << i;
+    }
+    return m;
+}
+
+// sim.cpp:128-291 updateFiltersState from the world's agent bits.  The
+// filter state is read once and written once (act/last in registers).
+__device__ __forceinline__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const MatchMasks &mm)
+{
+    const int T = S.T;
+    int32_t *lastp = &S.filtLast[(int64_t)w * 6]; // [team][filter]
+    int32_t last[6];
+    for (int k = 0; k < 6; k++) last[k] = lastp[k];
     uint32_t act[2] = { (uint32_t)S.filtAct0[w], (uint32_t)S.filtAct1[w] };
+    const uint32_t team0 = (1u << T) - 1u, team1 = team0 << T;
     const int min_num[2] = { 5, 1 };
     for (int fi = 0; fi < 3; fi++) {
         for (int t = 0; t < 2; t++) {
@@ -1399,19 +1423,16 @@ __device__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const
             }
         }
         if (fi == 2) {
-            #pragma unroll 1
-            for (int p = 0; p < N; p++) {
-                if (!(mb[p] & kMbF2)) continue;
-                const int team = p / S.T;
-                act[team] |= 1u << fi;
-                last[team * 3 + fi] = cur_step;
+            // any landed shot inside box 2 activates the shooter's team
+            for (int t = 0; t < 2; t++) {
+                if (mm.f2 & (t == 0 ? team0 : team1)) {
+                    act[t] |= 1u << fi;
+                    last[t * 3 + fi] = cur_step;
+                }
             }
         } else {
-            const uint32_t bit = fi == 0 ? kMbF0 : kMbF1;
-            int cnt[2] = { 0, 0 };
-            #pragma unroll 1
-            for (int p = 0; p < N; p++)
-                if (mb[p] & bit) cnt[p / S.T] += 1;
+            const uint32_t in = fi == 0 ? mm.f0 : mm.f1;
+            const int cnt[2] = { __builtin_popcount(in & team0), __builtin_popcount(in & team1) };
             for (int t = 0; t < 2; t++) {
                 if (cnt[t] >= min_num[fi]) {
                     act[t] |= 1u << fi;
@@ -1420,6 +1441,7 @@ __device__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const
             }
         }
     }
+    for (int k = 0; k < 6; k++) lastp[k] = last[k];
     S.filtAct0[w] = (int32_t)act[0];
     S.filtAct1[w] = (int32_t)act[1];
     if (__builtin_popcount(act[0]) == 3) S.filtMatched0[w] = cur_step;
@@ -1429,72 +1451,87 @@ __device__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const
 // sim.cpp:4470-4673 zoneMatchInfoSystem
 __device__ void writeSnapshotD(const DevState &S, const SceneDev &sc, int w, bool new_captured);
 
+// Run by one lane per world: every world value it reads is loaded up front
+// and the results are stored once at the end, so its global accesses are a
+// couple of round trips (the agent bytes come from LDS as a char pointer,
+// which may alias anything: read-modify-writes through memory next to them
+// were reloaded after every LDS read).  The snapshot (events mode) reads
+// captured / stepsUntilPoint after this step's update, curStep before it.
 __device__ __forceinline__ void zoneMatchInfoD(const DevState &S, const SceneDev &sc, int w, const uint8_t *mb)
 {
-    const int N = S.N;
-    const int64_t g0 = (int64_t)w * N;
+    const int N = S.N, T = S.T;
     int32_t *mr = &S.matchResult[(int64_t)w * 30];
     int32_t *zs_all = &S.zoneStats[(int64_t)w * 25];
+    const MatchMasks mm = matchMasksD(mb, N);
     const int cur_step = S.curStep[w] + 1;
-    bool finished = false;
-    if (cur_step >= c::kEpisodeLen || S.reset[w] == 1) finished = true;
-    if (cur_step == 1) {
-        mr[0] = -1; mr[1] = 0; mr[2] = 0; mr[3] = 0; mr[4] = 0;
-    }
-    #pragma unroll 1
-    for (int i = 0; i < N; i++) {
-        if (mb[i] & kMbKilled) mr[1 + ((i / S.T) ^ 1)] += 1;
-    }
-    bool earned = false;
-    bool new_captured = false;
+    const int reset_w = S.reset[w];
+    int m[5] = { mr[0], mr[1], mr[2], mr[3], mr[4] };
     const int ctrl = S.controlling[w];
     int sup = S.stepsUntilPoint[w];
     bool captured = S.captured[w] != 0;
+    const int cz = S.curZone[w];
+    const bool contested = S.contested[w] != 0;
+    const int team_a = S.teamA[w];
+    int32_t *zs = &zs_all[cz * 5];
+    int z[5] = { zs[0], zs[1], zs[2], zs[3], zs[4] };
+
+    bool finished = cur_step >= c::kEpisodeLen || reset_w == 1;
+    if (cur_step == 1) {
+        m[0] = -1; m[1] = 0; m[2] = 0; m[3] = 0; m[4] = 0;
+    }
+    const uint32_t team0 = (1u << T) - 1u, team1 = team0 << T;
+    // a killed agent of team t scores for team t ^ 1 (mr[1 + (t ^ 1)])
+    m[2] += __builtin_popcount(mm.killed & team0);
+    m[1] += __builtin_popcount(mm.killed & team1);
+    bool earned = false;
+    bool new_captured = false;
     if (sup == 0) {
         sup = c::kZonePointInterval;
         if (!captured) {
             captured = true;
             new_captured = true;
         }
-        if (ctrl >= 0) mr[3 + ctrl] += 1;
+        if (ctrl >= 0) m[3 + ctrl] += 1;
         earned = true;
     }
-    S.stepsUntilPoint[w] = sup;
-    S.captured[w] = captured ? 1 : 0;
-    S.earned[w] = earned ? 1 : 0;
-    if (mr[3] >= c::kZoneWinPoints || mr[4] >= c::kZoneWinPoints) finished = true;
+    if (m[3] >= c::kZoneWinPoints || m[4] >= c::kZoneWinPoints) finished = true;
     // sim.cpp:4534-4575: ZoneCaptureDefend ends on the attacker's first
     // point, the defender's 8th, or when every attacker has died once
     const bool zcd = sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND;
-    const int attacker = S.teamA[w] == 1 ? 1 : 0, defender = attacker ^ 1;
+    const int attacker = team_a == 1 ? 1 : 0, defender = attacker ^ 1;
     bool attackers_all_died = true;
     if (zcd) {
-        if (mr[3 + attacker] == 1) finished = true;
-        if (mr[3 + defender] == 8) finished = true;
-        for (int i = attacker * S.T; i < (attacker + 1) * S.T; i++)
-            if (!(mb[i] & kMbDied)) attackers_all_died = false;
+        if (m[3 + attacker] == 1) finished = true;
+        if (m[3 + defender] == 8) finished = true;
+        const uint32_t am = attacker == 0 ? team0 : team1;
+        attackers_all_died = (mm.died & am) == am;
         if (attackers_all_died) finished = true;
     }
-    {
-        int32_t *zs = &zs_all[S.curZone[w] * 5];
-        zs[4] += 1;
-        if (captured && ctrl >= 0) zs[1 + ctrl] += 1;
-        if (S.contested[w]) zs[3] += 1;
-        if (new_captured) zs[0] += 1;
-        updateFiltersBitsD(S, w, cur_step, mb);
-        if (sc.eventsOn) writeSnapshotD(S, sc, w, new_captured);
-    }
+    z[4] += 1;
+    if (captured && ctrl >= 0) z[1 + ctrl] += 1;
+    if (contested) z[3] += 1;
+    if (new_captured) z[0] += 1;
+
+    S.stepsUntilPoint[w] = sup;
+    S.captured[w] = captured ? 1 : 0;
+    S.earned[w] = earned ? 1 : 0;
+    for (int k = 0; k < 5; k++) zs[k] = z[k];
+    updateFiltersBitsD(S, w, cur_step, mm);
+    if (sc.eventsOn) writeSnapshotD(S, sc, w, new_captured);
     if (finished) {
         if (zcd) {
-            if (mr[3 + attacker] == 1) mr[0] = attacker;
-            else if (mr[3 + defender] == 8 || attackers_all_died) mr[0] = defender;
-            else mr[0] = 2;
-        } else if (mr[3] > mr[4]) mr[0] = 0;
-        else if (mr[4] > mr[3]) mr[0] = 1;
-        else mr[0] = 2;
+            if (m[3 + attacker] == 1) m[0] = attacker;
+            else if (m[3 + defender] == 8 || attackers_all_died) m[0] = defender;
+            else m[0] = 2;
+        } else if (m[3] > m[4]) m[0] = 0;
+        else if (m[4] > m[3]) m[0] = 1;
+        else m[0] = 2;
+        #pragma unroll 1
         for (int k = 0; k < 25; k++) mr[5 + k] = zs_all[k];
+        #pragma unroll 1
         for (int k = 0; k < 25; k++) zs_all[k] = 0;
     }
+    for (int k = 0; k < 5; k++) mr[k] = m[k];
     S.curStep[w] = cur_step;
     S.finished[w] = finished ? 1 : 0;
 }
@@ -1884,6 +1921,25 @@ __device__ __forceinline__ void zoneRewardD(const DevState &S, const SceneDev &s
 // ====================================================== kernels
 constexpr int kBlock = 256;
 
+// XCD-aware block order (cdna_hip_programming.md T1): the dispatcher deals
+// consecutive blocks round-robin to the 8 XCDs, each with its own L2; the
+// step kernels index worlds / agents by block, so neighbouring blocks share
+// cache lines of the per-world and per-agent columns.  Renumbered, each XCD
+// runs one contiguous range of blocks (bijective for any grid size).
+#ifndef MPENV_XCD_REMAP
+#define MPENV_XCD_REMAP 1
+#endif
+__device__ __forceinline__ uint32_t xcdBlockId()
+{
+#if MPENV_XCD_REMAP
+    const uint32_t nwg = gridDim.x, orig = blockIdx.x;
+    const uint32_t xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
+    return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
+#else
+    return blockIdx.x;
+#endif
+}
+
 // Persistent-entity setup + the Sim constructor's initWorld(ctx, true)
 // (sim.cpp:5850-5980, level_gen.cpp:19-328).  One thread per world.
 __global__ void __launch_bounds__(64) k_construct(DevState S, SceneDev sc, int32_t tc0, int32_t tc1, int32_t tc2)
@@ -1964,7 +2020,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPE
     bvh.stats = S.stats;
     const int lane = threadIdx.x & 63;
     if (lane >= apw) return;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t wave = ((int64_t)xcdBlockId() * blockDim.x + threadIdx.x) >> 6;
     const int64_t g = wave * apw + lane;
     if (g >= S.A) return;
     if (S.stats) statAdd(S.stats + kStatAliveAgents, S.alive[g] != 0.f ? 1u : 0u);
@@ -2005,7 +2061,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     const int wpb = kSimBlock / N;
     const int wl = threadIdx.x / N;
     const int i = threadIdx.x - wl * N;
-    const int w = blockIdx.x * wpb + wl;
+    const int w = (int)xcdBlockId() * wpb + wl;
     const bool act = (wl < wpb) && (w < S.W);
     const bool wlane = act && i == 0;
     const int64_t g = (int64_t)w * N + i;
@@ -2225,8 +2281,8 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
     const int T = S.T, N = S.N;
     const int apw = 64 / T;
     const int wl = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t agent0 = (((int64_t)blockIdx.x * blockDim.x) >> 6) * apw; // first agent of the block
+    const int64_t wave = ((int64_t)xcdBlockId() * blockDim.x + threadIdx.x) >> 6;
+    const int64_t agent0 = (((int64_t)xcdBlockId() * blockDim.x) >> 6) * apw; // first agent of the block
 
     // ---- phase A: view tests, reserve ray slots
     {
@@ -2293,7 +2349,7 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         const uint32_t d = rays[r];
         const int lane = (int)(d >> 2), p = (int)(d & 3);
         const int lwl = lane & 63;
-        const int64_t g = ((((int64_t)blockIdx.x * blockDim.x + lane) >> 6) * apw) + lwl / T;
+        const int64_t g = ((((int64_t)xcdBlockId() * blockDim.x + lane) >> 6) * apw) + lwl / T;
         const int k = lwl % T;
         const int w = (int)(g / N);
         const int i = (int)(g - (int64_t)w * N);
@@ -2432,12 +2488,6 @@ __device__ __forceinline__ Vec3 normalizedPosUnclampedD(const SceneDev &sc, Vec3
 // merge); transposed per wave, each instruction writes 8 whole rows.
 constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
 
-__device__ __forceinline__ void waveSync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Flushes the wave's staged 32-float rows (lane l's row at buf + l *
 // kObsRowPad, written there by the lane) to arr[(gw0 + r) * slots + k].
@@ -2635,7 +2685,7 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
 {
     __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsRowPad];
     __shared__ int64_t offBuf[kBlock / 64][64];
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = (int64_t)xcdBlockId() * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const int64_t gw0 = g - lane; // first agent of the wave
     float *wbuf = rowBuf[threadIdx.x >> 6];
@@ -2842,7 +2892,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
     const uint32_t ntasks = (uint32_t)lidarTasks(S.A);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int it = 0; it < iters; it++) {
-        const uint32_t task = (blockIdx.x * iters + it) * kLidarWaves + wave; // wave-uniform
+        const uint32_t task = (xcdBlockId() * iters + it) * kLidarWaves + wave; // wave-uniform
         if (task >= ntasks) break;
         // Lane id read inside the loop (volatile: not hoisted), so the
         // lane-derived offsets are formed per task instead of living as
@@ -2852,8 +2902,11 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         const uint32_t unit = task / 5u, sub = task - unit * 5u;
         const bool fwd = sub < 4u;
-        const uint32_t g = unit * 4u + (fwd ? sub : (lane >> 4));
-        if (g >= A) continue;
+        // a tail unit's lanes past A trace a copy of the last agent's rays
+        // and store nothing
+        const uint32_t g_raw = unit * 4u + (fwd ? sub : (lane >> 4));
+        const bool valid = g_raw < A;
+        const uint32_t g = valid ? g_raw : A - 1u;
         const uint32_t kk = fwd ? lane : (lane & 15u); // ray slot within the forward / rear fan
         const uint32_t w = __umulhi(g, S.nMagic); // g / N (engine.h)
         const uint32_t i = g - w * N;
@@ -2874,7 +2927,9 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
 #ifndef MPENV_LIDAR_PERM
 #define MPENV_LIDAR_PERM 0
 #endif
+
         WorldHit hw = traceWorldD<MPENV_LIDAR_PERM != 0>(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir, (int)i);
+        if (!valid) continue;
         const bool second = i >= T; // team of the casting agent
         float4 out;
         if (hw.hit) {
