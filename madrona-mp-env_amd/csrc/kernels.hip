@@ -2505,10 +2505,13 @@ __device__ __forceinline__ void flushRowsWave(float *arr, int slots, int k, int6
     // the wave's m live lanes (a tail wave's lanes past A have returned)
     // share its m rows x 8 chunks
     const int m = (int)(A - gw0 < 64 ? A - gw0 : 64);
+    // wave-uniform base + 32-bit per-lane offsets (64-bit per-lane row
+    // addresses were hoisted out of the slot loops and held ~60 VGPRs)
+    float *base = arr + (gw0 * slots + k) * kOtherObs;
 #pragma unroll
     for (int j = 0; j < kOtherObs / 4; j++) {
         const int c = lane + j * m, r = c >> 3, col = c & 7;
-        reinterpret_cast<float4 *>(arr + ((gw0 + r) * slots + k) * kOtherObs)[col] =
+        reinterpret_cast<float4 *>(base + r * slots * kOtherObs)[col] =
             reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col];
     }
     waveSync(); // reads done before the next rows land
@@ -2676,6 +2679,9 @@ __device__ __forceinline__ void fullTeamSlotD(const DevState &S, const SceneDev 
 #ifndef MPENV_OBS_NOUNROLL
 #define MPENV_OBS_NOUNROLL 0
 #endif
+#ifndef MPENV_OBS_MASK_FLOAT
+#define MPENV_OBS_MASK_FLOAT 0
+#endif
 #ifdef MPENV_OBS_WPE
 #define MP_OBS_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_OBS_WPE)))
 #else
@@ -2815,7 +2821,11 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
                 oob[28] = (float)S.wasShot[gj];
                 oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
                 oob[30] = ((vm[g] >> k) & 1) ? 1.f : 0.f;
+#if MPENV_OBS_MASK_FLOAT
+                const bool knows = mask[k] == 1.f; // lab: the float form ("k_obs mask read")
+#else
                 const bool knows = (knowsBits >> k) & 1u; // teamKnowsLocation (sim.cpp:2995-3003)
+#endif
                 oob[31] = knows ? 1.f : 0.f;
                 lk_keep = knows;
                 lk_write = lk_write || knows;
