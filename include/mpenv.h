@@ -416,6 +416,12 @@ int mpenv_read_stats(mpenv_manager *mgr, uint64_t *out, int32_t n);
 int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes,
                     float *verts_out, int32_t *num_verts, int32_t *max_stack);
 
+/* The sphere-cast quirk guard k_move uses (scene.h quirkGrid, radius 15,
+ * margin 2, 16-unit cells): header[0..2] = minX, minY, cell (float bits),
+ * header[3..4] = w, h; bits [ceil(w*h/32)] row-major.  Pass *num_words = 0
+ * to query the size.  For tests. */
+int mpenv_scene_quirk_grid(const char *scene_path, int32_t *header_out, uint32_t *bits_out, int32_t *num_words);
+
 /* Host-side navmesh (Navmesh::initFromPolygons, mgr.cpp:1301-1327) and A*
  * next-hop table (buildAStarLookup, mgr.cpp:1155-1211) of a scene, for
  * tests and the oracle.  Two-call pattern: pass *num_tris = 0 to query the

@@ -1181,6 +1181,29 @@ int mpenv_scene_navmesh(const char *scene_path, float *tri_verts_out, int32_t *n
     return MPENV_OK;
 }
 
+// The quirk guard k_move uploads (for tests).
+int mpenv_scene_quirk_grid(const char *scene_path, int32_t *header_out, uint32_t *bits_out, int32_t *num_words)
+{
+    if (!num_words) return fail(MPENV_ERR_INVALID, "num_words is null");
+    try {
+        Scene s = loadScene(scene_path);
+        const QuirkGrid q = quirkGrid(s.bvhVerts, 15.f, 2.f, 16.f);
+        if (header_out) {
+            std::memcpy(&header_out[0], &q.minX, 4);
+            std::memcpy(&header_out[1], &q.minY, 4);
+            std::memcpy(&header_out[2], &q.cell, 4);
+            header_out[3] = q.w;
+            header_out[4] = q.h;
+        }
+        if (bits_out && *num_words >= (int32_t)q.bits.size())
+            std::memcpy(bits_out, q.bits.data(), q.bits.size() * 4);
+        *num_words = (int32_t)q.bits.size();
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_IO, e.what());
+    }
+    return MPENV_OK;
+}
+
 // Host-side access to the scene BVH (for the parity oracle and tests).
 int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes, float *verts_out,
                     int32_t *num_verts, int32_t *max_stack)

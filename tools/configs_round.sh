@@ -2,7 +2,7 @@
 # Bench lines for the other BASELINE.json configurations and an N=2
 # rehearsal on one GPU (run under gpurun; outputs under gpurun_out/configs_<tag>/).
 set -o pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
 OUT=gpurun_out/configs_$TAG
 mkdir -p $OUT
 cd "$GRAFT_REPO_ROOT"
