@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--worlds", type=int, default=16384, help="worlds per GPU")
     ap.add_argument("--team-size", type=int, default=6)
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "simple_map"))
-    ap.add_argument("--world-groups", type=int, default=3,
+    ap.add_argument("--world-groups", type=int, default=2,
                     help="world ranges stepped on concurrent streams in the timed pass (engine option); "
                          "the profile pass always runs one group so kernel times are exclusive")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
