@@ -152,7 +152,11 @@ enum StatId {
     kStatLosSeen = 3,     // of those, rays that found their target
     kStatSphereCasts = 4, // MeshBVH::sphereCast calls (k_move)
     kStatShots = 5,       // fireSystem rays (k_sim)
+#ifdef MPENV_LAB_PHASE_T
+    kNumStats = 24, // lab: k_sim phase cycles in slots 8..
+#else
     kNumStats = 8,
+#endif
 };
 
 struct ZOBBDev {
@@ -172,12 +176,22 @@ struct GoalRegionDev {
 // by-value kernel-argument arrays of SceneDev dynamically makes the compiler
 // copy the whole argument struct into registers (k_sim's zoneSystem alone
 // needed ~200 VGPRs that way).
+// A rotated box's frame: qinv(angleAxis(rot, up)) and its corners rotated
+// into it -- what zoneSystem / distToZOBB recompute per call.  Filled on the
+// device by k_scene_frames with the same functions, so every bit matches.
+struct FrameDev {
+    mp::Quat toFrame;
+    mp::Vec3 pMin, pMax;
+};
+
 struct SceneTables {
     mp::AABB zoneAABB[kMaxZones];
     float zoneRot[kMaxZones];
     ZOBBDev subZones[8];
     GoalRegionDev goals[4];
     int32_t zoneGoalTri[kMaxZones];
+    FrameDev zoneFrame[kMaxZones];
+    FrameDev goalFrame[4][3];
 };
 
 // Read-only scene + task constants, passed by value as a kernel argument.
@@ -263,5 +277,6 @@ int launchTraceRays(const SceneDev &sc, const float *o, const float *d, int n, i
 int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, float *wf, uint32_t *explore,
                       float *crumbs, void *stream);
 int launchFillActions(const DevState &s, const int32_t *src6, void *stream);
+int computeSceneFrames(SceneTables *d_tab, void *stream); // fills zoneFrame / goalFrame in place
 
 } // namespace mpenv

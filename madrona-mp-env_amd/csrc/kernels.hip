@@ -195,6 +195,28 @@ __device__ int nearestNavTriD(const SceneDev &sc, Vec3 pos)
     return closest_idx;
 }
 
+__device__ __forceinline__ FrameDev makeFrameD(Vec3 pmin, Vec3 pmax, float rot)
+{
+    FrameDev f;
+    f.toFrame = qinv(angleAxis(rot, kUp));
+    f.pMin = rotateVec(f.toFrame, pmin);
+    f.pMax = rotateVec(f.toFrame, pmax);
+    return f;
+}
+
+// Zone and goal-region frames, once at scene upload (see FrameDev).
+__global__ void k_scene_frames(SceneTables *tab)
+{
+    const int t = threadIdx.x;
+    if (t < kMaxZones) {
+        tab->zoneFrame[t] = makeFrameD(tab->zoneAABB[t].pMin, tab->zoneAABB[t].pMax, tab->zoneRot[t]);
+    } else if (t >= 16 && t < 16 + 12) {
+        const int r = (t - 16) / 3, k = (t - 16) % 3;
+        const ZOBBDev &z = tab->goals[r].sub[k];
+        tab->goalFrame[r][k] = makeFrameD(z.pMin, z.pMax, z.rotation);
+    }
+}
+
 // The bots' goal is always a zone centroid: its NearestNavTri is computed
 // once per zone at scene upload (same function, same input).
 __global__ void k_zone_goals(SceneDev sc, int32_t *out)
@@ -668,23 +690,28 @@ __device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, con
 // sim.cpp:1794-1836 applyDmgSystem
 __device__ void applyDmgD(const DevState &S, int64_t g)
 {
+    // every input read before the first store (the damage slots are floats
+    // like the stores between them, which would serialise the loads)
     int32_t flags = S.flags[g] & ~kFlagWasKilled;
-    int was_shot = 0;
-    int rs = S.respawnSteps[g];
-    if (rs > 0) S.respawnSteps[g] = rs - 1;
+    const int rs = S.respawnSteps[g];
     float hp = S.hp[g];
-    for (int k = 0; k < S.T; k++) {
-        const int64_t di = (int64_t)k * S.dmgStride + g;
-        float d = S.dmg[di];
-        if (d > 0.f) {
-            was_shot += 1;
-            S.autohealSteps[g] = c::kOutOfCombatSteps;
-        }
-        hp -= d;
-        S.dmg[di] = 0.f;
+    const bool was_alive = S.alive[g] == 1.f;
+    const int T = S.T;
+    float dm[kMaxTeamSize];
+    #pragma unroll
+    for (int k = 0; k < kMaxTeamSize; k++) dm[k] = k < T ? S.dmg[(int64_t)k * S.dmgStride + g] : 0.f;
+    if (rs > 0) S.respawnSteps[g] = rs - 1;
+    int was_shot = 0;
+    #pragma unroll
+    for (int k = 0; k < kMaxTeamSize; k++) {
+        if (k >= T) break;
+        if (dm[k] > 0.f) was_shot += 1;
+        hp -= dm[k];
+        S.dmg[(int64_t)k * S.dmgStride + g] = 0.f;
     }
+    if (was_shot > 0) S.autohealSteps[g] = c::kOutOfCombatSteps;
     S.wasShot[g] = was_shot;
-    if (S.alive[g] == 1.f && hp <= 0.f) flags |= kFlagWasKilled | kFlagHasDied;
+    if (was_alive && hp <= 0.f) flags |= kFlagWasKilled | kFlagHasDied;
     if (hp <= 0.f) {
         hp = 0.f;
         S.alive[g] = 0.f;
@@ -1192,6 +1219,75 @@ __device__ void zoneSystemD(const DevState &S, const SceneDev &sc, int w)
     S.contested[w] = contested ? 1 : 0;
 }
 
+// zoneSystem split for the step kernel: the world lane rotates the zone
+// (zonePreD), every agent lane tests itself against the zone box in
+// parallel (zoneInD; the world lane walked the N agents one load round trip
+// at a time), and the world lane counts the teams and stores (zonePostD).
+// Same arithmetic and stores as zoneSystemD, which the replay path keeps.
+struct ZonePre {
+    int cz, ctrl, zsr, sup;
+    bool captured;
+};
+
+__device__ __forceinline__ ZonePre zonePreD(const DevState &S, const SceneDev &sc, int w)
+{
+    const int N = S.N;
+    const int64_t g0 = (int64_t)w * N;
+    ZonePre z;
+    z.cz = S.curZone[w];
+    z.ctrl = S.controlling[w];
+    z.zsr = S.zoneSteps[w];
+    z.sup = S.stepsUntilPoint[w];
+    z.captured = S.captured[w] != 0;
+    if (z.ctrl != -1) z.zsr -= 1;
+    if (z.zsr == 0) {
+        z.cz += 1;
+        if (z.cz == sc.numZones) z.cz = 0;
+        z.captured = false;
+        z.zsr = c::kNumStepsPerZone;
+        z.sup = c::kZonePointInterval;
+        AABB za = sc.tab->zoneAABB[z.cz];
+        Vec3 center = (za.pMax + za.pMin) / 2.f;
+#pragma unroll 1
+        for (int i = 0; i < N; i++) S.minDistZone[g0 + i] = distance(ldPos(S, g0 + i), center);
+    }
+    return z;
+}
+
+__device__ __forceinline__ bool zoneInD(const DevState &S, const SceneDev &sc, int cz, int64_t g)
+{
+    const FrameDev &f = sc.tab->zoneFrame[cz];
+    AABB za;
+    za.pMin = f.pMin;
+    za.pMax = f.pMax;
+    Vec3 p = ldPos(S, g);
+    p.z += c::kStandHeight / 2.f;
+    const bool in = aabbContains(za, rotateVec(f.toFrame, p));
+    setFlag(S, g, kFlagInZone, in);
+    return in;
+}
+
+__device__ __forceinline__ void zonePostD(const DevState &S, int w, ZonePre z, int na, int nb)
+{
+    z.sup -= 1;
+    bool contested = na > 0 && nb > 0;
+    if (contested || (na == 0 && nb == 0)) {
+        z.ctrl = -1;
+        z.captured = false;
+        z.sup = c::kZonePointInterval;
+    } else if (na > 0 && nb == 0) {
+        if (z.ctrl != 0) { z.ctrl = 0; z.captured = false; z.sup = c::kZonePointInterval; }
+    } else if (na == 0 && nb > 0) {
+        if (z.ctrl != 1) { z.ctrl = 1; z.captured = false; z.sup = c::kZonePointInterval; }
+    }
+    S.curZone[w] = z.cz;
+    S.controlling[w] = z.ctrl;
+    S.zoneSteps[w] = z.zsr;
+    S.stepsUntilPoint[w] = z.sup;
+    S.captured[w] = z.captured ? 1 : 0;
+    S.contested[w] = contested ? 1 : 0;
+}
+
 // SubZone state packed 4 bits per sub-zone k at bit 4k: controlling team + 1,
 // contested << 2, captured << 3 (the DEBUG_WORLD_I32 layout).
 __device__ __forceinline__ int subCtrlD(uint32_t st, int k) { return (int)((st >> (4 * k)) & 3u) - 1; }
@@ -1252,16 +1348,26 @@ __device__ void leaveBreadcrumbAgentD(const DevState &S, int w, int64_t g)
     if (last != -1) {
         float4 *cr = crumbPtr(S, w);
         const int n = S.numCrumbs[w];
-        for (int k = 0; k < n; k++) {
-            float4 meta = cr[2 * k + 1];
-            if (__float_as_int(meta.z) != last) continue;
-            float4 p = cr[2 * k];
+        // the first crumb with id `last`, its ids read 4 at a time (one
+        // round of loads per 4 crumbs; past the end re-reads the last)
+        int hit = -1;
+        #pragma unroll 1
+        for (int k0 = 0; k0 < n && hit < 0; k0 += 4) {
+            const int k1 = min(k0 + 1, n - 1), k2 = min(k0 + 2, n - 1), k3 = min(k0 + 3, n - 1);
+            const int i0 = __float_as_int(cr[2 * k0 + 1].z), i1 = __float_as_int(cr[2 * k1 + 1].z);
+            const int i2 = __float_as_int(cr[2 * k2 + 1].z), i3 = __float_as_int(cr[2 * k3 + 1].z);
+            if (i0 == last) hit = k0;
+            else if (k0 + 1 < n && i1 == last) hit = k0 + 1;
+            else if (k0 + 2 < n && i2 == last) hit = k0 + 2;
+            else if (k0 + 3 < n && i3 == last) hit = k0 + 3;
+        }
+        if (hit >= 0) {
+            const float4 p = cr[2 * hit];
             if (distance(pos, v3(p.x, p.y, p.z)) < c::kAgentRadius * 4) {
-                cr[2 * k].w = 1.f;
+                cr[2 * hit].w = 1.f;
                 updated = true;
                 S.bcSteps[g] = 0;
             }
-            break;
         }
     }
     if (!updated) {
@@ -1314,11 +1420,21 @@ __device__ void accumulateCrumbsD(const DevState &S, int w, int i)
     const float4 *cr = crumbPtr(S, w);
     const int n = S.numCrumbs[w];
     float total = S.bcPenalty[g];
-    for (int k = 0; k < n; k++) {
-        float4 meta = cr[2 * k + 1];
-        if ((int)meta.x != team || (int)meta.y == off) continue;
-        float4 p = cr[2 * k];
+    // 4 crumbs per round of loads (past the end re-reads the last, unused);
+    // the sum keeps creation order
+    auto add = [&](float4 meta, float4 p) {
+        if ((int)meta.x != team || (int)meta.y == off) return;
         if (distance(pos, v3(p.x, p.y, p.z)) <= c::kAgentRadius * 4.f) total += p.w;
+    };
+    #pragma unroll 1
+    for (int k0 = 0; k0 < n; k0 += 4) {
+        const int k1 = min(k0 + 1, n - 1), k2 = min(k0 + 2, n - 1), k3 = min(k0 + 3, n - 1);
+        const float4 m0 = cr[2 * k0 + 1], p0 = cr[2 * k0], m1 = cr[2 * k1 + 1], p1 = cr[2 * k1];
+        const float4 m2 = cr[2 * k2 + 1], p2 = cr[2 * k2], m3 = cr[2 * k3 + 1], p3 = cr[2 * k3];
+        add(m0, p0);
+        if (k0 + 1 < n) add(m1, p1);
+        if (k0 + 2 < n) add(m2, p2);
+        if (k0 + 3 < n) add(m3, p3);
     }
     S.bcPenalty[g] = total;
 }
@@ -1663,25 +1779,38 @@ __device__ void replayAgentD(const DevState &S, int w, int i)
 }
 
 // sim.cpp:3998-4087 distToZOBB + evaluateGoalRegionsSystem
-__device__ float distToZOBBD(const ZOBBDev &z, Vec3 pos)
+// distToZOBB (sim.cpp:3998-4020) with the frame precomputed (k_scene_frames)
+__device__ __forceinline__ float distToFrameD(const FrameDev &f, Vec3 pos)
 {
-    Quat to_frame = qinv(angleAxis(z.rotation, kUp));
-    Vec3 pmin = rotateVec(to_frame, z.pMin);
-    Vec3 pmax = rotateVec(to_frame, z.pMax);
-    Vec3 p = rotateVec(to_frame, pos);
+    const Vec3 p = rotateVec(f.toFrame, pos);
     float sq = 0.f;
     for (int i = 0; i < 3; i++) {
         float v = comp(p, i);
-        if (v < comp(pmin, i)) { float d = comp(pmin, i) - v; sq += d * d; }
-        if (v > comp(pmax, i)) { float d = v - comp(pmax, i); sq += d * d; }
+        if (v < comp(f.pMin, i)) { float d = comp(f.pMin, i) - v; sq += d * d; }
+        if (v > comp(f.pMax, i)) { float d = v - comp(f.pMax, i); sq += d * d; }
     }
     return sqrt_(sq);
 }
 
-__device__ __forceinline__ void goalRegionsD(const DevState &S, const SceneDev &sc, int w)
+// Agent lanes: the agent's distance to each sub-region of the goals its team
+// is scored on (the world lane's inner loop, spread over the agents);
+// d[r * 3 + s], unused entries left alone.
+__device__ __forceinline__ void goalDistAgentD(const DevState &S, const SceneDev &sc, int w, int i, Vec3 pos, float *d)
+{
+    const int attacker = S.teamA[w];
+    const int team = i / S.T;
+    for (int r = 0; r < sc.numGoals && r < 2; r++) {
+        const GoalRegionDev &gr = sc.tab->goals[r];
+        const int region_team = gr.attackerTeam ? attacker : (attacker ^ 1);
+        if (team != region_team) continue;
+        for (int s = 0; s < gr.numSub; s++) d[r * 3 + s] = distToFrameD(sc.tab->goalFrame[r][s], pos);
+    }
+}
+
+// gd: the world's agents' goalDistAgentD rows in LDS (stride 6).
+__device__ __forceinline__ void goalRegionsD(const DevState &S, const SceneDev &sc, int w, const float *gd)
 {
     const int N = S.N;
-    const int64_t g0 = (int64_t)w * N;
     float team_step[2] = { 0.f, 0.f };
     float mins[2] = { S.goalMin0[w], S.goalMin1[w] };
     const int attacker = S.teamA[w];
@@ -1694,7 +1823,7 @@ __device__ __forceinline__ void goalRegionsD(const DevState &S, const SceneDev &
             #pragma unroll 1
             for (int i = 0; i < N; i++) {
                 if (i / S.T != region_team) continue;
-                float d = distToZOBBD(gr.sub[s], ldPos(S, g0 + i));
+                float d = gd[i * 6 + r * 3 + s];
                 if (d < min_d) min_d = d;
             }
             if (min_d > max_min) max_min = min_d;
@@ -2055,6 +2184,23 @@ __device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &
 // scratch for the whole kernel and spills around the call).
 __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)) k_sim(DevState S, SceneDev sc)
 {
+#ifdef MPENV_LAB_PHASE_T
+    // lab: per-block phase durations (thread 0, after each barrier)
+    uint64_t pt_prev = clock64();
+    int pt_k = 0;
+    auto PT = [&]() {
+        if (threadIdx.x == 0 && S.stats) {
+            const uint64_t t = clock64();
+            atomicAdd(&S.stats[8 + pt_k], (unsigned long long)(t - pt_prev));
+            pt_prev = t;
+        }
+        pt_k++;
+    };
+#define MP_PT() PT()
+#else
+#define MP_PT() ((void)0)
+#endif
+
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const LBVH bvh = stageBVH(smem, sc);
     const int N = S.N;
@@ -2077,50 +2223,88 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         if (act) replayAgentD(S, w, i);
         if (wlane) S.curStep[w] = S.replayLog[w].cur_step;
         __syncthreads();
+    MP_PT();
         if (wlane) zoneSystemD(S, sc, w);
         __syncthreads();
+    MP_PT();
     } else {
         if (!(MPENV_LAB_SIM_SKIP & 1) && act) fireD(S, sc, bvh, w, i);
         __syncthreads();
+    MP_PT();
         if (!(MPENV_LAB_SIM_SKIP & 2048) && act) applyDmgD(S, g);
         __syncthreads();
+    MP_PT();
         if (!(MPENV_LAB_SIM_SKIP & 2) && wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
         __syncthreads();
+    MP_PT();
         if (act) autoHealD(S, g);
         __syncthreads();
-        if (!(MPENV_LAB_SIM_SKIP & 4) && wlane) {
-            zoneSystemD(S, sc, w);
-            if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
+    MP_PT();
+        {
+            __shared__ int zoneCz[kSimBlock];
+            __shared__ uint8_t zoneIn[kSimBlock];
+            ZonePre zp;
+            if (wlane) {
+                zp = zonePreD(S, sc, w);
+                zoneCz[wl] = zp.cz;
+            }
+            __syncthreads();
+            if (act) zoneIn[threadIdx.x] = zoneInD(S, sc, zoneCz[wl], g) ? 1 : 0;
+            __syncthreads();
+            if (wlane) {
+                int na = 0, nb = 0;
+                #pragma unroll 1
+                for (int k = 0; k < N; k++) {
+                    if (!zoneIn[wl * N + k]) continue;
+                    if (k / S.T == 0) na += 1;
+                    else nb += 1;
+                }
+                zonePostD(S, w, zp, na, nb);
+                if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
+            }
         }
         __syncthreads();
+    MP_PT();
         if (sc.recordOn) {
             if (act) recordAgentD(S, w, i);
             if (wlane) S.recordLog[w].cur_step = S.curStep[w];
         }
         if (!(MPENV_LAB_SIM_SKIP & 256) && act) leaveBreadcrumbAgentD(S, w, g);
         __syncthreads();
+    MP_PT();
         if (!(MPENV_LAB_SIM_SKIP & 256) && wlane) appendCrumbsD(S, w);
         __syncthreads();
+    MP_PT();
         if (!(MPENV_LAB_SIM_SKIP & 512) && act) accumulateCrumbsD(S, w, i);
         __syncthreads();
+    MP_PT();
     }
     // zoneMatchInfoSystem's per-agent reads, one lane per agent (the world
     // lane would otherwise walk them serially)
     __shared__ uint8_t matchBits[kSimBlock];
-    if (act) matchBits[threadIdx.x] = (uint8_t)matchAgentBitsD(S, w, i);
-    __syncthreads();
-    if (wlane) {
-        if (!(MPENV_LAB_SIM_SKIP & 256) && !sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem
-        if (!(MPENV_LAB_SIM_SKIP & 8)) zoneMatchInfoD(S, sc, w, &matchBits[wl * N]);
-        if (!(MPENV_LAB_SIM_SKIP & 16)) goalRegionsD(S, sc, w);
+    __shared__ float goalDist[kSimBlock * 6];
+    if (act) {
+        matchBits[threadIdx.x] = (uint8_t)matchAgentBitsD(S, w, i);
+        goalDistAgentD(S, sc, w, i, ldPos(S, g), &goalDist[threadIdx.x * 6]);
     }
     __syncthreads();
+    MP_PT();
+    if (wlane) {
+        if (!(MPENV_LAB_SIM_SKIP & 256) && !sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem
+        MP_PT(); // (lab: thread 0 is world 0's lane)
+        if (!(MPENV_LAB_SIM_SKIP & 8)) zoneMatchInfoD(S, sc, w, &matchBits[wl * N]);
+        MP_PT();
+        if (!(MPENV_LAB_SIM_SKIP & 16)) goalRegionsD(S, sc, w, &goalDist[wl * N * 6]);
+    }
+    __syncthreads();
+    MP_PT();
     if (act) {
         if (!(MPENV_LAB_SIM_SKIP & 1024)) exploreVisitedD(S, w, g);
         if (sc.flank && sc.task == MPENV_TASK_ZONE) flankRewardD(S, sc, bvh, w, i);
         else if (!(MPENV_LAB_SIM_SKIP & 64)) zoneRewardD(S, sc, w, i);
     }
     __syncthreads();
+    MP_PT();
     if (wlane) {
         // pvpTeamRewardSystem (sim.cpp:4292-4313)
         float tr[2] = { 0.f, 0.f };
@@ -2137,6 +2321,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         S.teamRew1[w] = tr[1];
     }
     __syncthreads();
+    MP_PT();
     if (act) {
         // pvpFinalRewardSystem (sim.cpp:4315-4339) + doneSystem (4712-4717)
         const int team = i / S.T;
@@ -2150,6 +2335,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     RandKey *pre = S.resetKeys + ((int64_t)w * N) * (kPreDraws + 1);
     if (act && resetDueD(S, sc, w)) resetPreD(S, sc, w, i, pre + i * (kPreDraws + 1));
     __syncthreads();
+    MP_PT();
     if (wlane) {
         // fullTeamDoneRewardSystem (sim.cpp:4720-4747)
         for (int t = 0; t < 2; t++) {
@@ -2912,6 +3098,9 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         const uint32_t unit = task / 5u, sub = task - unit * 5u;
         const bool fwd = sub < 4u;
+#ifdef MPENV_LAB_NO_REAR
+        if (!fwd) continue;
+#endif
         // a tail unit's lanes past A trace a copy of the last agent's rays
         // and store nothing
         const uint32_t g_raw = unit * 4u + (fwd ? sub : (lane >> 4));
@@ -3150,6 +3339,14 @@ int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
     const int blocks = (int)((s.A + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
+}
+
+int computeSceneFrames(SceneTables *d_tab, void *stream)
+{
+    hipLaunchKernelGGL(k_scene_frames, dim3(1), dim3(64), 0, (hipStream_t)stream, d_tab);
+    int rc = check(hipGetLastError());
+    if (!rc) rc = check(hipStreamSynchronize((hipStream_t)stream));
+    return rc;
 }
 
 int computeZoneGoalTris(const SceneDev &sc, int32_t *dev_scratch, int32_t *host_out, void *stream)

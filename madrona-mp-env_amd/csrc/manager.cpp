@@ -547,6 +547,7 @@ static void buildSceneDev(mpenv_manager &m)
         std::memcpy(t.zoneGoalTri, sc.zoneGoalTri, sizeof(t.zoneGoalTri));
         SceneTables *d_tab = m.alloc<SceneTables>(1);
         m.upload(d_tab, &t, sizeof(t));
+        if (computeSceneFrames(d_tab, m.stream)) throw std::runtime_error("k_scene_frames launch failed");
         sc.tab = d_tab;
     }
     sc.simFlags = m.cfg.sim_flags;

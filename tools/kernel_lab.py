@@ -117,7 +117,7 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
     hip.hipDeviceSynchronize()
     dig = hashlib.sha1()
-    per = {}
+    pex = {}
     for eid in (6, 10, 12, 13, 18, 19, 20, 23, 24, 65, 66, 67, 11, 14, 15, 16, 17, 27, 28, 29, 30, 31, 32):
         p, dt, nd, gid = C.c_void_p(), C.c_int32(), C.c_int32(), C.c_int32()
         dims = (C.c_int64 * 8)()
@@ -129,13 +129,26 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
         assert hip.hipMemcpy(buf, p, C.c_size_t(nbytes), 2) == 0
         if eid in (6, 10, 12, 13, 18, 19, 20, 23, 24, 65, 66, 67):
             dig.update(bytes(buf))
-        per[eid] = hashlib.sha1(bytes(buf)).hexdigest()[:6]
+        pex[eid] = hashlib.sha1(bytes(buf)).hexdigest()[:6]
         if str(eid) in os.environ.get("LAB_DUMP", "").split(","):
             os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
             open(os.path.join(ROOT, "gpurun_out", f"dump_{label or name}_{eid}.bin"), "wb").write(bytes(buf))
-    print(json.dumps({"variant": label or name, "ms_per_step": round(1e3 * el_groups / steps, 4),
+    phases = None
+    if os.environ.get("LAB_STATS"):
+        # lab builds with -DMPENV_LAB_PHASE_T: k_sim per-phase block cycles
+        lib.mpenv_enable_stats.argtypes = [C.c_void_p, C.c_int32]
+        lib.mpenv_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
+        lib.mpenv_enable_stats(h, 1)
+        ns = 50
+        for s in range(ns):
+            step(s)
+        st = (C.c_uint64 * 24)()
+        n = lib.mpenv_read_stats(h, st, 24)
+        lib.mpenv_enable_stats(h, 0)
+        phases = [round(st[k] / ns / 1e6, 2) for k in range(8, n)]
+    print(json.dumps({"variant": label or name, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
                       "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
-                      "digest": dig.hexdigest()[:16], "per_export": per}), flush=True)
+                      "digest": dig.hexdigest()[:16], "per_export": pex}), flush=True)
 
 
 if __name__ == "__main__":
