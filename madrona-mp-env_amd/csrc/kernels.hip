@@ -481,6 +481,8 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         ray_o.z += top;
         Vec3 normal = v3(0.f, 0.f, 0.f);
         {
+            // the ground below, wherever it is (a bounded first try gains
+            // nothing here: the downward cast prunes at the floor anyway)
             SphereHit h = bvhSphereCastD(bvh, ray_o, -kUp, r);
             if (h.t < kFltMax) normal = h.n;
         }
@@ -2249,8 +2251,19 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
                 zoneCz[wl] = zp.cz;
             }
             __syncthreads();
-            if (act) zoneIn[threadIdx.x] = zoneInD(S, sc, zoneCz[wl], g) ? 1 : 0;
+            // Agent phase shared by the zone test, the recorder and
+            // leaveBreadcrumbs: none reads what another writes (InZone and
+            // CrumbRequest are different flag bits of the lane's own agent;
+            // the recorder reads neither), so they run between one pair of
+            // barriers instead of three.
+            if (act) {
+                zoneIn[threadIdx.x] = zoneInD(S, sc, zoneCz[wl], g) ? 1 : 0;
+                if (sc.recordOn) recordAgentD(S, w, i);
+                if (!(MPENV_LAB_SIM_SKIP & 256)) leaveBreadcrumbAgentD(S, w, g);
+            }
+            if (wlane && sc.recordOn) S.recordLog[w].cur_step = S.curStep[w];
             __syncthreads();
+    MP_PT();
             if (wlane) {
                 int na = 0, nb = 0;
                 #pragma unroll 1
@@ -2261,23 +2274,15 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
                 }
                 zonePostD(S, w, zp, na, nb);
                 if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
+                if (!(MPENV_LAB_SIM_SKIP & 256)) appendCrumbsD(S, w);
             }
         }
         __syncthreads();
     MP_PT();
-        if (sc.recordOn) {
-            if (act) recordAgentD(S, w, i);
-            if (wlane) S.recordLog[w].cur_step = S.curStep[w];
-        }
-        if (!(MPENV_LAB_SIM_SKIP & 256) && act) leaveBreadcrumbAgentD(S, w, g);
-        __syncthreads();
-    MP_PT();
-        if (!(MPENV_LAB_SIM_SKIP & 256) && wlane) appendCrumbsD(S, w);
-        __syncthreads();
-    MP_PT();
+        // accumulateBreadcrumbPenalties shares its agent phase with the
+        // match-info / goal-region reads below (each lane reads its own
+        // agent and the crumbs, which nothing in that phase writes)
         if (!(MPENV_LAB_SIM_SKIP & 512) && act) accumulateCrumbsD(S, w, i);
-        __syncthreads();
-    MP_PT();
     }
     // zoneMatchInfoSystem's per-agent reads, one lane per agent (the world
     // lane would otherwise walk them serially)
