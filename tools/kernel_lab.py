@@ -45,7 +45,7 @@ def build(name, defines):
 
 
 def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.environ.get("LAB_TEAM", 6)),
-             warm=100, steps=200, label=None):
+             warm=int(os.environ.get("LAB_WARM", 100)), steps=int(os.environ.get("LAB_STEPS", 200)), label=None):
     import mpenv_testlib as T
 
     path = os.path.join(LAB, name, "libmpenv.so") if name != "main" else os.path.join(PKG, "libmpenv.so")
