@@ -1441,7 +1441,10 @@ __device__ void accumulateCrumbsD(const DevState &S, int w, int i)
     S.bcPenalty[g] = total;
 }
 
-// In chunks of 4 crumbs loaded before any is written back: the world lane
+#ifndef MPENV_CRUMB_CHUNK
+#define MPENV_CRUMB_CHUNK 4
+#endif
+// In chunks of MPENV_CRUMB_CHUNK crumbs loaded before any is written back: the world lane
 // waits for one round of loads per chunk instead of per crumb, and the
 // compaction only ever writes to slots at or below the chunk being read.
 __device__ void decayCrumbsD(const DevState &S, int w)
@@ -1458,16 +1461,19 @@ __device__ void decayCrumbsD(const DevState &S, int w)
             m += 1;
         }
     };
+    constexpr int CK = MPENV_CRUMB_CHUNK;
     #pragma unroll 1
-    for (int k0 = 0; k0 < n; k0 += 4) {
+    for (int k0 = 0; k0 < n; k0 += CK) {
         // past the end: re-read the last crumb (unused)
-        const int k1 = min(k0 + 1, n - 1), k2 = min(k0 + 2, n - 1), k3 = min(k0 + 3, n - 1);
-        const float4 p0 = cr[2 * k0], m0 = cr[2 * k0 + 1], p1 = cr[2 * k1], m1 = cr[2 * k1 + 1];
-        const float4 p2 = cr[2 * k2], m2 = cr[2 * k2 + 1], p3 = cr[2 * k3], m3 = cr[2 * k3 + 1];
-        keep(p0, m0, k0);
-        keep(p1, m1, k0 + 1);
-        keep(p2, m2, k0 + 2);
-        keep(p3, m3, k0 + 3);
+        float4 pp[CK], mm[CK];
+        #pragma unroll
+        for (int j = 0; j < CK; j++) {
+            const int kj = min(k0 + j, n - 1);
+            pp[j] = cr[2 * kj];
+            mm[j] = cr[2 * kj + 1];
+        }
+        #pragma unroll
+        for (int j = 0; j < CK; j++) keep(pp[j], mm[j], k0 + j);
     }
     S.numCrumbs[w] = m;
 }
