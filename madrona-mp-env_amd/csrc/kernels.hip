@@ -2685,6 +2685,25 @@ __device__ __forceinline__ Vec3 normalizedPosUnclampedD(const SceneDev &sc, Vec3
 // merge); transposed per wave, each instruction writes 8 whole rows.
 constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
 
+// Observation stores: plain, or nontemporal (MPENV_OBS_NT=1: the streamed
+// outputs, ~1.2 GB per C3 step, bypass the L2's normal allocation).
+#ifndef MPENV_OBS_NT
+#define MPENV_OBS_NT 0
+#endif
+__device__ __forceinline__ void ntStore(float *p, float v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void ntStore(float4 *p, float4 v)
+{
+    __builtin_nontemporal_store(lf4{ v.x, v.y, v.z, v.w }, reinterpret_cast<lf4 *>(p));
+}
+template <typename V> __device__ __forceinline__ void obsStore(V *p, V v)
+{
+#if MPENV_OBS_NT
+    ntStore(p, v);
+#else
+    *p = v;
+#endif
+}
+
 
 // Flushes the wave's staged 32-float rows (lane l's row at buf + l *
 // kObsRowPad, written there by the lane) to arr[(gw0 + r) * slots + k].
@@ -2708,8 +2727,8 @@ __device__ __forceinline__ void flushRowsWave(float *arr, int slots, int k, int6
 #pragma unroll
     for (int j = 0; j < kOtherObs / 4; j++) {
         const int c = lane + j * m, r = c >> 3, col = c & 7;
-        reinterpret_cast<float4 *>(base + r * slots * kOtherObs)[col] =
-            reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col];
+        obsStore(reinterpret_cast<float4 *>(base + r * slots * kOtherObs) + col,
+                 reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col]);
     }
     waveSync(); // reads done before the next rows land
 }
@@ -2747,7 +2766,7 @@ struct WaveStage {
             const int r = c / n, col = c - r * n;
             if ((wbits >> r) & 1u) {
                 const float v = ((zbits >> r) & 1u) ? 0.f : buf[r * P + col];
-                dst[offs[r] + col] = v;
+                obsStore(dst + offs[r] + col, v);
             }
         }
         waveSync(); // reads done before the next rows land
@@ -2767,7 +2786,7 @@ struct WaveStage {
             if ((wbits >> r) & 1u) {
                 const float4 v = ((zbits >> r) & 1u) ? make_float4(0.f, 0.f, 0.f, 0.f)
                                                      : reinterpret_cast<const float4 *>(buf + r * P)[col];
-                reinterpret_cast<float4 *>(dst + offs[r])[col] = v;
+                obsStore(reinterpret_cast<float4 *>(dst + offs[r]) + col, v);
             }
         }
         waveSync();
@@ -2928,7 +2947,9 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
     // and 10 see knows(1) = 0 while their stored mask[1] is 1), with the
     // row exchange synchronised either by s_waitcnt or by the wave barrier
     // and wavefront fences below -- so the LDS exchange is not the cause;
-    // the bits form passes under both ("k_obs mask read").
+    // the bits form passes under both.  Cause (ISA, DESIGN.md §4 "k_obs
+    // mask read"): hipcc keeps a second copy of mask[] as a VGPR tuple that
+    // misses the teammate loop's can_see update (register miscompile).
     uint32_t knowsBits = 0;
     for (int k = 0; k < kMaxTeamSize; k++) knowsBits |= (mask[k] == 1.f ? 1u : 0u) << k;
 
@@ -3059,6 +3080,9 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
 #define MPENV_LIDAR_ITERS 4 // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 ms (k_lidar alone, C3)
 #endif
 constexpr int kLidarIters = MPENV_LIDAR_ITERS;
+#ifndef MPENV_LIDAR_NT
+#define MPENV_LIDAR_NT 0 // 1: the full-team lidar copy (written, never read here) as a nontemporal store
+#endif
 // 1024-thread blocks: the 8 octant node images + vertices (43 KB on
 // simple_map) are staged once per 16 waves, so 2 blocks per CU (8 waves per
 // SIMD) fit the 160 KB of LDS.
@@ -3160,7 +3184,11 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // overwrites it (sim.cpp:5283-5310): the previous value moves into
         // the team interface's slot.
         const float4 prev = *dst;
+#if MPENV_LIDAR_NT
+        ntStore(tdst, prev);
+#else
         *tdst = prev;
+#endif
         *dst = out;
     }
 }
