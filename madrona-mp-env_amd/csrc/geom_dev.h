@@ -742,12 +742,13 @@ struct WorldHit {
 // that capsule can never be the hit and its test is skipped; -1: test all.
 __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, const float *__restrict__ py,
                                               const float *__restrict__ pz, int64_t g0, int N, mp::Vec3 org,
-                                              mp::Vec3 d, int self, bool hit, float min_t);
+                                              mp::Vec3 d, int self, bool hit, float min_t, uint32_t capMask = ~0u);
 
 template <bool kPerm = false>
 __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__restrict__ px,
                                                 const float *__restrict__ py, const float *__restrict__ pz,
-                                                int64_t g0, int N, mp::Vec3 org, mp::Vec3 d, int self = -1)
+                                                int64_t g0, int N, mp::Vec3 org, mp::Vec3 d, int self = -1,
+                                                uint32_t capMask = ~0u)
 {
     using namespace mp;
     float min_t = kFltMax;
@@ -762,17 +763,48 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
 #ifdef MPENV_LAB_NO_CAPSULE
     N = 0;
 #endif
-    return capsulesD(px, py, pz, g0, N, org, d, self, hit, min_t);
+    return capsulesD(px, py, pz, g0, N, org, d, self, hit, min_t, capMask);
 }
 
 // traceRayAgainstWorld's capsule loop (utils.cpp:40-69) after the BVH hit
 // (hit, min_t).
 __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, const float *__restrict__ py,
                                               const float *__restrict__ pz, int64_t g0, int N, mp::Vec3 org,
-                                              mp::Vec3 d, int self, bool hit, float min_t)
+                                              mp::Vec3 d, int self, bool hit, float min_t, uint32_t capMask)
 {
     using namespace mp;
     int ent = -1;
+    // capMask (wave-uniform): capsules a caller has proven unreachable for
+    // every ray of the wave are skipped (k_lidar's forward fans); the rest
+    // are visited in the same ascending order, so ties resolve as before.
+    if (capMask != ~0u) {
+        for (uint32_t m = capMask & ((1u << N) - 1u); m; m &= m - 1u) {
+            const int j = __builtin_ctz(m);
+            if (j == self) continue;
+            Vec3 co = v3(px[g0 + j], py[g0 + j], pz[g0 + j]);
+            co.z += kCapsuleRadius;
+            Vec3 tr = org - co;
+            const float dxy2 = d.x * d.x + d.y * d.y;
+            const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
+            const float cr = tr.x * d.y - tr.y * d.x;
+            if (cr * cr > cull_r2 * dxy2) continue;
+            const float along = -(tr.x * d.x + tr.y * d.y + tr.z * d.z);
+            const float ahead = along + fmaxD(0.f, kCapsuleSegment * d.z) + kCapsuleRadius * 1.01f;
+            if (ahead < 0.f) continue;
+            if (along + fminD(0.f, kCapsuleSegment * d.z) - kCapsuleRadius * 1.01f > min_t) continue;
+            float t = intersectRayZOriginCapsule(tr, d, kCapsuleRadius, kCapsuleSegment);
+            if (t != 0 && t < min_t) {
+                min_t = t;
+                hit = true;
+                ent = j;
+            }
+        }
+        WorldHit h;
+        h.hit = hit;
+        h.t = min_t;
+        h.entity = ent;
+        return h;
+    }
     // Conservative cull: every point of a Z-capsule lies within r of its
     // vertical axis, so a ray whose xy line passes farther than r from the
     // axis cannot hit it and the exact test would return 0.  The 1% radius
