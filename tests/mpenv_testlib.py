@@ -471,7 +471,7 @@ _YAW_TURN = np.array([0, 1 / 256, 1 / 128, 1 / 64, 1 / 32, 1 / 16, 1 / 8]) * np.
 _PITCH_TURN = np.array([0, 1 / 128, 1 / 64, 1 / 32]) * np.pi
 
 
-def combat_actions(sim, step, seed=1234):
+def combat_actions(sim, step, seed=1234, base=None):
     """Tape actions overridden by a greedy aim-bot for agents that see an
     opponent: turn toward the first visible opponent (relative yaw/pitch are
     opponent-observation fields 24/25, sim.cpp obs layout) and fire when
@@ -480,7 +480,8 @@ def combat_actions(sim, step, seed=1234):
     exercise kills, respawns and combat rewards, which a pure random tape on
     simple_map rarely reaches."""
     A = sim.W * sim.N
-    acts = mpenv_tape.tape_actions(seed, step, 0, A)
+    # base: the tape rows to override (default: the hash tape from agent 0)
+    acts = mpenv_tape.tape_actions(seed, step, 0, A) if base is None else np.array(base, np.int32)
     opp = sim.get("OPPONENT_OBSERVATIONS")  # [A, 6, 32]
     mask = sim.get("OPPONENT_MASKS").reshape(A, -1)
     vis = mask[:, :opp.shape[1]] > 0

@@ -263,7 +263,10 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
     Actions: the bench's hash tape (ring of 64 steps resident in HBM, copied
     by gpuStreamStep's input copy) with team slot 1 of every even world an A*
     bot (AgentPolicy -1, planAStarAISystem), which walks to the zone and
-    holds it.  That drives the zone systems through their natural events
+    holds it; in the probed worlds the tape rows are overridden by the
+    combat aim-bot (mpenv_testlib.combat_actions, computed from the oracle's
+    observations and written into the device ring before the copy), so
+    kills, respawns and combat rewards happen over the long horizon too.  That drives the zone systems through their natural events
     (sim.cpp:1892-1976 rotation after 600 controlled steps, 4470-4673 a point
     every 20 controlled steps and the 3,000-step end).  A 125-point win needs
     2,500 controlled steps, which the bots reach too rarely, so at steps
@@ -305,10 +308,11 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
     prev = [o.get("DEBUG_WORLD_I32").copy() for o in oracles]
     prev_kills = [np.zeros(PW, np.int32) for _ in oracles]
 
+    acts = [None] * len(oracles)
+
     def ostep(k, s):
-        o, w0 = oracles[k], probes[k]
-        o.set_actions(ring[s % RING, w0 * N:(w0 + PW) * N])
-        o.step()
+        oracles[k].set_actions(acts[k])
+        oracles[k].step()
 
     compare("init")
     with ThreadPoolExecutor(len(oracles)) as pool:
@@ -319,7 +323,11 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
                     mr[:, 3] = np.maximum(mr[:, 3], 124)
                     mr[:, 4] = np.maximum(mr[:, 4], 124)
                     e.put_rows("MATCH_RESULT", w0, mr)
-            e.copy_actions(dev_ring + (s % RING) * W * N * 6 * 4)
+            slot = dev_ring + (s % RING) * W * N * 6 * 4
+            for k, (w0, o) in enumerate(zip(probes, oracles)):
+                acts[k] = T.combat_actions(o, s, base=ring[s % RING, w0 * N:(w0 + PW) * N])
+                e.mem.h2d(slot + w0 * N * 6 * 4, acts[k])
+            e.copy_actions(slot)
             e.step()
             list(pool.map(lambda k: ostep(k, s), range(len(oracles))))
             for k, o in enumerate(oracles):
@@ -340,7 +348,7 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
     e.mem.free(dev_ring)
     print(f"\n{ts}v{ts} x {W}, {steps} steps, {len(probes)} x {PW} probed worlds: {ev}")
     # every zone/match event fired in the probed worlds
-    assert ev["rotations"] > 0 and ev["points"] > 0 and ev["wins"] > 0, ev
+    assert ev["rotations"] > 0 and ev["points"] > 0 and ev["wins"] > 0 and ev["kills"] > 0, ev
     assert ev["episode_ends"] >= len(probes) * PW, ev  # every world passed a 3,000-step end or a win
     # size-independent properties over the whole batch
     hp = e.get("HP")
