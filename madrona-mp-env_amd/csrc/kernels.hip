@@ -2760,7 +2760,10 @@ struct WaveStage {
         waveSync();
         // the m live lanes (a tail wave's lanes past A have returned) share
         // the m x n staged floats
-#pragma unroll 1
+#ifndef MPENV_FLUSH_UNROLL
+#define MPENV_FLUSH_UNROLL 1
+#endif
+#pragma unroll MPENV_FLUSH_UNROLL
         for (int j = 0; j < n; j++) {
             const int c = lane + m * j;
             const int r = c / n, col = c - r * n;
