@@ -72,9 +72,20 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline timed budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPUs this process may use")
-    ap.add_argument("--gather", action="store_true",
-                    help="N>1: learner exchange -- every trainInterface output gathered to rank 0 each "
-                         "step over RCCL, overlapped with the next step (double-buffered)")
+    ap.add_argument("--exchange", choices=["auto", "none", "gather", "local"], default="auto",
+                    help="learner exchange over RCCL (named in config.parallelism): gather = every shipped "
+                         "trainInterface output to rank 0 each step, overlapped with the next step "
+                         "(config C4 as named; the default for N>1); local = each rank's learner keeps "
+                         "its shard, a gradient-sized all-reduce every --update-every steps; none = "
+                         "simulators only (the default at N=1)")
+    ap.add_argument("--gather", action="store_true", help="alias of --exchange gather")
+    ap.add_argument("--grad-mb", type=float, default=16.0, help="local exchange: all-reduced gradient MB")
+    ap.add_argument("--update-every", type=int, default=50,
+                    help="local exchange: steps per policy update (jax_train.py --steps-per-update)")
+    ap.add_argument("--actions", choices=["tape", "combat"], default="tape",
+                    help="tape = the hash action tape (headline); combat = the tape overridden on the "
+                         "device by the zone-seeking aim-bot (mpenv_combat_actions mode 1), so agents "
+                         "meet, fight, die and respawn inside the timed window")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--share-device", action="store_true",
                     help="debug: map every rank to GPU 0 (rehearse N>1 on a one-GPU box; no --gather)")
@@ -165,18 +176,23 @@ def main():
     gpu = 0 if args.share_device else local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    gather_group = None
+    exchange = "gather" if args.gather else args.exchange
+    if exchange == "auto":
+        exchange = "gather" if world_size > 1 and not args.share_device else "none"
+    if world_size == 1:
+        exchange = "none"
+    xgroup = None
     if world_size > 1:
         # Control plane (barriers, max-over-ranks time) on gloo: the step has
-        # no data-path collective.  The optional learner gather runs on RCCL.
+        # no data-path collective.  The learner exchange runs on RCCL.
         dist.init_process_group("gloo")
-        if args.gather:
+        if exchange != "none":
             if args.share_device:
-                raise SystemExit("--gather needs one GPU per rank")
-            gather_group = dist.new_group(backend="nccl")
+                raise SystemExit("--exchange gather/local needs one GPU per rank")
+            xgroup = dist.new_group(backend="nccl")
 
     import madrona_mp_env as m
-    from mpenv_dist import LearnerGather
+    from mpenv_dist import make_exchange
     import mpenv_tape
 
     W, ts = args.worlds, args.team_size
@@ -210,10 +226,17 @@ def main():
     ring = torch.from_numpy(mpenv_tape.tape_ring(TAPE_SEED, offset * N, A, RING)).to(dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    learner = LearnerGather(sim, dst=0, group=gather_group) if args.gather and world_size > 1 else None
+    learner = make_exchange(exchange, sim, group=xgroup, grad_bytes=int(args.grad_mb * (1 << 20)),
+                            update_every=args.update_every) if exchange == "local" else \
+        make_exchange(exchange, sim, group=xgroup)
 
     def one_step(s):
-        sim.copy_actions(ring[s % RING].data_ptr(), sptr)
+        if args.actions == "combat":
+            # the aim-bot reads the previous step's observations and writes
+            # the step inputs directly (replaces the input copy)
+            sim.combat_actions(ring[s % RING].data_ptr(), 0, 1, sptr)
+        else:
+            sim.copy_actions(ring[s % RING].data_ptr(), sptr)
         sim.step_async(sptr)
         if learner is not None:
             learner.submit(sptr)
@@ -273,7 +296,8 @@ def main():
         sim.set_world_groups(groups)
         prof_pass = (timings, counts)
 
-    workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})")
+    workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})") \
+        + ("" if args.actions == "tape" else " + combat actions")
     result = {
         "metric": f"env steps/sec x agents (whole node), simple_map {ts}v{ts} @ {W} worlds"
                   + ("" if world_size == 1 else f"/GPU x {world_size} GPUs"),
@@ -287,7 +311,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (hash action tape, seed 1234; 64-step ring resident in HBM)",
+        "data": "synthetic (hash action tape, seed 1234; 64-step ring resident in HBM"
+                + (")" if args.actions == "tape" else "; overridden on the device by the zone-seeking aim-bot)"),
         "config": {
             "workload": workload,
             "worlds_per_gpu": W,
@@ -299,10 +324,15 @@ def main():
             "bots": args.bots,
             "rand_seed": 5,
             "world_groups": groups,
-            "parallelism": f"world-sharded x{world_size}" + (" + RCCL learner gather" if learner else ""),
+            "actions": args.actions,
+            "parallelism": f"world-sharded x{world_size}" + ("" if learner is None else
+                                                             f" + RCCL learner exchange ({exchange})"),
+            "exchange": exchange,
         },
         "world_steps_per_s": round(value / N, 1),
     }
+    if learner is not None:
+        result["exchange_bytes_per_step"] = learner.bytes_per_step()
     if prof_pass is not None:
         timings, counts = prof_pass
         steps = args.steps
@@ -354,6 +384,8 @@ def main():
             "los_seen": round(counts["los_seen"] / steps, 1),
             "lidar_rays": 80 * A,
             "shot_rays": round(counts["shot_rays"] / steps, 1),
+            "hit_agents": round(counts["hit_agents"] / steps, 1),
+            "kills": round(counts["kills"] / steps, 2),
             "sphere_casts": round(counts["sphere_casts"] / steps, 1),
             "rays_per_s": round(rays / steps / (ms_per_step * 1e-3), 1),
             "bvh_queries_per_s": round((rays + counts["sphere_casts"]) / steps / (ms_per_step * 1e-3), 1),

@@ -107,7 +107,8 @@ enum mpenv_export_id {
     MPENV_EXPORT_DEBUG_AGENT_I32 = 66, /* [A][MPENV_DBG_AI_COUNT] */
     MPENV_EXPORT_DEBUG_WORLD_I32 = 67, /* [W][MPENV_DBG_WI_COUNT] */
     MPENV_EXPORT_DEBUG_WORLD_F32 = 68, /* [W][MPENV_DBG_WF_COUNT] */
-    MPENV_EXPORT_DEBUG_EXPLORE = 69,   /* [A][81*81] u32 ExploreTracker.visited */
+    MPENV_EXPORT_DEBUG_EXPLORE = 69,   /* [A][81*81] u32: 1 = cell visited in the agent's
+                                          current episode (ExploreTracker.visited == curEpisodeIdx) */
     MPENV_EXPORT_DEBUG_CRUMBS = 70,    /* [W][MPENV_MAX_CRUMBS][8] f32 breadcrumb pool */
     MPENV_EXPORT_RECORD_LOG = 71,      /* [W] mpenv_step_log as i32[W][217] (record mode) */
     MPENV_EXPORT_REPLAY_LOG = 72,      /* [W] mpenv_step_log as i32[W][217] (replay mode) */
@@ -362,6 +363,16 @@ int mpenv_train_interface_entry(int32_t is_output, int32_t idx,
  * 2 discrete-aim actions per agent), asynchronous on hip_stream. */
 int mpenv_copy_actions(mpenv_manager *mgr, const int32_t *src_device, void *hip_stream);
 
+/* Extension (synthetic action source for benchmarks and tests; no reference
+ * counterpart): the tape rows tape_device [A][6] i32 overridden by a greedy
+ * aim-bot computed from the engine's current observations (opponent masks
+ * and relative yaw / pitch; mode 1 also turns and runs toward the zone when
+ * no opponent is visible).  out_device [A][6] i32, or null to write the
+ * step-input columns directly (as mpenv_copy_actions would).  Asynchronous
+ * on hip_stream. */
+int mpenv_combat_actions(mpenv_manager *mgr, const int32_t *tape_device, int32_t *out_device, int32_t mode,
+                         void *hip_stream);
+
 /* Test hook (no reference counterpart): closest-hit BVH queries
  * (MeshBVH::traceRay, mesh_bvh.inl:110-208) for n caller rays in device
  * memory (o, d: [n][3] f32).  mode 0 = the traversal inlined in the step
@@ -405,7 +416,8 @@ int mpenv_enable_kernel_timing(mpenv_manager *mgr, int32_t enable);
  * accumulated by the step kernels while enabled (enabling zeroes them):
  * [0] alive agents at k_move, [1] (viewer, opponent) pairs both alive,
  * [2] visibility rays traced, [3] visibility rays that saw their target,
- * [4] sphere casts, [5] shot rays.  read_stats copies min(n, 8) counters
+ * [4] sphere casts, [5] shot rays, [6] agents that took damage, [7] agents
+ * killed.  read_stats copies min(n, 8) counters
  * and returns the number of counters (8). */
 int mpenv_enable_stats(mpenv_manager *mgr, int32_t enable);
 int mpenv_read_stats(mpenv_manager *mgr, uint64_t *out, int32_t n);

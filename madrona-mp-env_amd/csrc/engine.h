@@ -24,6 +24,11 @@ constexpr int kMaxAgents = 2 * kMaxTeamSize;
 constexpr int kMaxZones = 5;
 constexpr int kGridW = 81;
 constexpr int kGridCells = kGridW * kGridW;
+// ExploreTracker as a per-agent bitset over the 81 x 81 cells (6,561 bits,
+// padded to 208 words = 832 B so rows stay 16-B aligned): bit c = cell c
+// holds the agent's current episode index (exploreEp).  Exact for
+// exploreVisitedSystem (sim.cpp:3508-3536), see DESIGN.md §2.
+constexpr int kExploreWords = 208;
 constexpr int kSelfObs = 43;
 constexpr int kOtherObs = 32;
 constexpr int kFwdRays = 64;   // 2 x 32
@@ -41,7 +46,7 @@ constexpr int kMaxBVHStack = 16; // register byte-stack capacity
 #define MP_AGENT_I32(X) \
     X(curPose) X(tgtPose) X(transRem) X(rngA) X(rngB) X(rngCtr) X(landedOn) \
     X(respawnSteps) X(autohealSteps) X(flags) X(wasShot) X(weapon) X(bcLast) \
-    X(bcSteps) X(newCells)
+    X(bcSteps) X(newCells) X(exploreEp)
 
 #define MP_WORLD_I32(X) \
     X(teamA) X(curStep) X(finished) X(curZone) X(controlling) X(contested) \
@@ -81,7 +86,7 @@ struct DevState {
 
     float *dmg;            // [6][A] DamageDealt
     uint8_t *visMask;      // [A] OpponentsVisibility, bit k = sees opponent k
-    uint32_t *visited;     // [A][81*81] ExploreTracker
+    uint32_t *exploreBits; // [A][kExploreWords] ExploreTracker bitset for episode exploreEp
     int32_t *filtLast;     // [W][2][3] FiltersMatchState::lastMatches (3 filters used)
     int32_t *zoneStats;    // [W][5][5]
     uint32_t *spawnTrack;  // [W][3][spawnTrackLen] SpawnUsageCounter
@@ -152,6 +157,8 @@ enum StatId {
     kStatLosSeen = 3,     // of those, rays that found their target
     kStatSphereCasts = 4, // MeshBVH::sphereCast calls (k_move)
     kStatShots = 5,       // fireSystem rays (k_sim)
+    kStatHits = 6,        // agents that took damage (applyDmgSystem)
+    kStatKills = 7,       // agents killed (alive -> hp <= 0)
 #ifdef MPENV_LAB_PHASE_T
     kNumStats = 24, // lab: k_sim phase cycles in slots 8..
 #else
@@ -277,6 +284,7 @@ int launchTraceRays(const SceneDev &sc, const float *o, const float *d, int n, i
 int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, float *wf, uint32_t *explore,
                       float *crumbs, void *stream);
 int launchFillActions(const DevState &s, const int32_t *src6, void *stream);
+int launchCombatActions(const DevState &s, const int32_t *tape6, int32_t *out6, int32_t mode, void *stream);
 int computeSceneFrames(SceneTables *d_tab, void *stream); // fills zoneFrame / goalFrame in place
 
 } // namespace mpenv

@@ -419,10 +419,20 @@ __device__ __forceinline__ Vec3 rotate2DD(Vec3 dir, float radians) // sim.cpp:87
 // same order as the unbounded cast minus those entered beyond B, and
 // returns the same hit and normal whenever the unbounded cast's hit is
 // nearer than B -- except through the vertex-test quirk (scene.h
-// quirkGrid), which makes far triangles return t = 0.  A bounded cast is
-// therefore only used when the cell of 2o is clear of vertices; otherwise,
-// and where the caller needs more than "hit nearer than B or not", the
-// full cast runs.
+// quirkGrid): testVert tests the ray 2o + t·d against a sphere of radius r
+// around each vertex, so a visited triangle with a vertex within r of that
+// ray at some t < B returns t (0 when 2o itself is inside) although the
+// geometry is far away; a bounded cast may never visit that triangle.  A
+// bounded cast is therefore only used when every grid cell under the xy
+// path 2o .. 2o + B·d is clear (each clear cell is farther than r + 2 from
+// every vertex); otherwise, and where the caller needs more than "hit
+// nearer than B or not", the full cast runs.  Vertical casts have a
+// one-cell path.  DESIGN.md §2.
+// Bound = the largest distance the caller compares a hit with + this slack
+// (a bounded miss then reads as a hit that far away, well past every
+// comparison, whatever the rounding).
+constexpr float kCastSlack = 4.f;
+
 __device__ __forceinline__ bool castQuirkFreeD(const SceneDev &sc, Vec3 o)
 {
     const float fx = ((o.x + o.x) - sc.qgMinX) * sc.qgInvCell;
@@ -432,17 +442,37 @@ __device__ __forceinline__ bool castQuirkFreeD(const SceneDev &sc, Vec3 o)
     return !((sc.quirkGrid[bit >> 5] >> (bit & 31)) & 1u);
 }
 
+// Every cell of the xy bounding box of the segment 2o .. 2o + B·d is clear
+// (cells outside the grid are clear by construction: the grid reaches
+// r + margin + one cell beyond every vertex).
+__device__ __forceinline__ bool castPathQuirkFreeD(const SceneDev &sc, Vec3 o, Vec3 d, float B)
+{
+    const float px = o.x + o.x, py = o.y + o.y;
+    const float qx = px + d.x * B, qy = py + d.y * B;
+    const int x0 = max((int)floorf((fminf(px, qx) - sc.qgMinX) * sc.qgInvCell), 0);
+    const int x1 = min((int)floorf((fmaxf(px, qx) - sc.qgMinX) * sc.qgInvCell), sc.qgW - 1);
+    const int y0 = max((int)floorf((fminf(py, qy) - sc.qgMinY) * sc.qgInvCell), 0);
+    const int y1 = min((int)floorf((fmaxf(py, qy) - sc.qgMinY) * sc.qgInvCell), sc.qgH - 1);
+    for (int y = y0; y <= y1; y++)
+        for (int x = x0; x <= x1; x++) {
+            const uint32_t bit = (uint32_t)y * (uint32_t)sc.qgW + (uint32_t)x;
+            if ((sc.quirkGrid[bit >> 5] >> (bit & 31)) & 1u) return false;
+        }
+    return true;
+}
+
 // The cast's hit if nearer than `near_b`, else t = kFltMax: for callers to
-// which every hit at or beyond near_b acts like no hit.
+// which every hit at or beyond near_b acts like no hit.  Horizontal d.
 __device__ __forceinline__ SphereHit castNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
 {
-    if (!castQuirkFreeD(sc, o)) return bvhSphereCastD(bvh, o, d, kSphereR);
+    if (!castPathQuirkFreeD(sc, o, d, near_b)) return bvhSphereCastD(bvh, o, d, kSphereR);
     SphereHit h = bvhSphereCastD(bvh, o, d, kSphereR, near_b);
     if (!(h.t < near_b)) h.t = kFltMax;
     return h;
 }
 
-// The full cast's t, searched within near_b first.
+// The full cast's t, searched within near_b first.  Vertical d only (the
+// path guard is the cell of 2o).
 __device__ __forceinline__ float castFirstNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
 {
     if (castQuirkFreeD(sc, o)) {
@@ -491,8 +521,8 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         // The forward casts only matter nearer than move_dist + buffer: a
         // farther hit leaves hit_pos at move_dist, takes no slide and the
         // normal / high_hit it sets are read only by the slide (bound with a
-        // wide margin so no value near a decision is ever cut).
-        const float fwd_b = 2.f * (move_dist + buffer) + 10.f;
+        // margin of kCastSlack so no value near a decision is ever cut).
+        const float fwd_b = (move_dist + buffer) + kCastSlack;
         ray_o = x + v_norm * buffer * 0.5f;
         ray_o.z += low_check;
         float low_dist;
@@ -525,7 +555,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
             ray_o.z += high_hit ? top : low_check;
             float max_move = move_dist - low_dist;
             // only min(slide - buffer, max_move) is used
-            float slide = castNearD(bvh, sc, ray_o, slide_dir, 2.f * (max_move + buffer) + 10.f).t;
+            float slide = castNearD(bvh, sc, ray_o, slide_dir, (max_move + buffer) + kCastSlack).t;
             slide = fmaxD(0.0f, slide - buffer);
             slide = fminD(slide, max_move);
             if (slide > 0.0f) hit_pos = hit_pos + slide_dir * slide;
@@ -714,6 +744,10 @@ __device__ void applyDmgD(const DevState &S, int64_t g)
     if (was_shot > 0) S.autohealSteps[g] = c::kOutOfCombatSteps;
     S.wasShot[g] = was_shot;
     if (was_alive && hp <= 0.f) flags |= kFlagWasKilled | kFlagHasDied;
+    if (S.stats) {
+        statAdd(S.stats + kStatHits, was_shot > 0 ? 1u : 0u);
+        statAdd(S.stats + kStatKills, (was_alive && hp <= 0.f) ? 1u : 0u);
+    }
     if (hp <= 0.f) {
         hp = 0.f;
         S.alive[g] = 0.f;
@@ -1853,7 +1887,14 @@ __device__ __forceinline__ void goalRegionsD(const DevState &S, const SceneDev &
     S.goalTeam1[w] = team_step[1];
 }
 
-// sim.cpp:3508-3536 exploreVisitedSystem
+// sim.cpp:3508-3536 exploreVisitedSystem.  The reference keeps a u32
+// episode tag per cell and counts a cell when its tag differs from the
+// current episode index, then stores the index.  Tags only ever take the
+// current, increasing index (curEpisodeIdx = worldEpisodeCounter++), so
+// "tag == current episode" is all the state that matters: one bit per cell
+// for the agent's episode exploreEp, cleared when the episode moves on
+// (lazily, here).  Episode 0 starts from level_gen.cpp:166-171's tags: 0 on
+// cells outside the y<40, x<40 quadrant, i.e. already set (k_init_explore).
 __device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
 {
     Vec3 delta = ldPos(S, g) - v3(S.sx[g], S.sy[g], S.sz[g]);
@@ -1861,10 +1902,18 @@ __device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
     int32_t y = f2iSatD((delta.y + 0.5f) / (c::kAgentRadius * 2.f));
     int64_t cx = (int64_t)x + c::kGridMax, cy = (int64_t)y + c::kGridMax;
     if (cx < 0 || cx >= kGridW || cy < 0 || cy >= kGridW) return;
-    uint32_t *cell = &S.visited[g * kGridCells + cy * kGridW + cx];
-    const uint32_t cur = (uint32_t)S.episode[w];
-    if (*cell != cur) {
-        *cell = cur;
+    uint32_t *row = &S.exploreBits[g * kExploreWords];
+    const int32_t cur = S.episode[w];
+    if (S.exploreEp[g] != cur) {
+        uint4 *r4 = reinterpret_cast<uint4 *>(row);
+        for (int k = 0; k < kExploreWords / 4; k++) r4[k] = make_uint4(0u, 0u, 0u, 0u);
+        S.exploreEp[g] = cur;
+    }
+    const int cell = (int)(cy * kGridW + cx);
+    const uint32_t bit = 1u << (cell & 31);
+    const uint32_t word = row[cell >> 5];
+    if (!(word & bit)) {
+        row[cell >> 5] = word | bit;
         if (length2(delta) > 2.f) S.newCells[g] += 1;
     }
 }
@@ -2121,14 +2170,22 @@ __global__ void __launch_bounds__(64) k_construct(DevState S, SceneDev sc, int32
     S.filtMatched0[w] = -1; S.filtMatched1[w] = -1;
 }
 
-// ExploreTracker initial contents (level_gen.cpp:166-171; cells outside the
-// y<40, x<40 quadrant start at 0).
-__global__ void __launch_bounds__(256) k_init_explore(uint32_t *visited, int64_t total)
+// ExploreTracker initial contents (level_gen.cpp:166-171: 0xFFFFFFFF on the
+// y<40, x<40 quadrant; the other cells start at 0) as the
+// bitset of episode 0: the cells whose tag is 0 are set.
+__global__ void __launch_bounds__(256) k_init_explore(uint32_t *bits, int32_t *ep, int64_t total)
 {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
-        int cell = (int)(k % kGridCells);
-        int y = cell / kGridW, x = cell - y * kGridW;
-        visited[k] = (y < c::kGridMax && x < c::kGridMax) ? 0xFFFFFFFFu : 0u;
+        const int wd = (int)(k % kExploreWords);
+        uint32_t v = 0u;
+        for (int b = 0; b < 32; b++) {
+            const int cell = wd * 32 + b;
+            if (cell >= kGridCells) break;
+            const int y = cell / kGridW, x = cell - y * kGridW;
+            if (!(y < c::kGridMax && x < c::kGridMax)) v |= 1u << b;
+        }
+        bits[k] = v;
+        if (wd == 0) ep[k / kExploreWords] = 0;
     }
 }
 
@@ -3165,40 +3222,68 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
 #define MPENV_LIDAR_PERM 0
 #endif
 
-#ifndef MPENV_LIDAR_CAPCULL
-#define MPENV_LIDAR_CAPCULL 0 // 1: fan-wide capsule cull (identical outputs, k_lidar 0.756 -> 0.785 ms)
+#ifndef MPENV_LIDAR_WAVECULL
+#define MPENV_LIDAR_WAVECULL 1
 #endif
-        uint32_t capMask = ~0u;
-#if MPENV_LIDAR_CAPCULL
-        if (fwd) {
-            // Fan-wide capsule cull (wave-uniform: one agent per forward
-            // task).  Every forward ray has d . F > 0 (F = dir_fwd: its fan
-            // angles keep sin(theta) >= sin(pi/8) = 0.38), so a point o + t d
-            // with t > 0 lies in front of the plane through either origin
-            // with normal F.  A capsule whose farthest point along F, over
-            // both origins (heights), is still behind that plane by a margin
-            // cannot be entered at any t > 0, and intersectRayZOriginCapsule
-            // returns only t > 0 hits: its exact test would return 0 for
-            // every ray of the fan.  Margin: 1% of the radius plus 4 units,
-            // far above the rounding of the per-ray capsule test (entry
-            // points are off by < 0.2 units even for grazing rays).  Lane j
-            // < N tests capsule j; the ballot is the wave's capsule mask.
+        WorldHit hw;
+        if (MPENV_LIDAR_WAVECULL && fwd) {
+            // Forward fan (one agent, one xy origin per wave): the BVH first,
+            // then only the capsules some ray of the wave could hit before
+            // its BVH hit.  Any point of capsule j lies within r of its
+            // vertical axis, so a ray entering it at t has t >= d_xy - r
+            // (d_xy = xy distance from the origin to the axis); a capsule
+            // with d_xy - 1.01 r - 1 > max over the wave's rays of the BVH
+            // hit t can enter no ray's `t < min_hit_t` (utils.cpp:57-69) and
+            // is dropped for the whole wave (the margin dwarfs the rounding
+            // of t ~ 1e-3 at these distances).  Lane j < N loads capsule j
+            // once; the per-ray loop reads the survivors' bases from those
+            // lanes (readlane) in ascending j, so ties resolve as before.
+            float tb;
+            const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0>(ob, ray_o, dir, tb, kFltMax, 0.f);
+            float min_t = bhit ? tb : kFltMax;
+            float mx = min_t;
+#pragma unroll
+            for (int sh = 32; sh >= 1; sh >>= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
+            float cx = 0.f, cy = 0.f, cz = 0.f;
             bool keep = false;
             if (lane < N) {
-                const Vec3 p0 = ldPos(S, g);
-                const float oz0 = p0.z + c::kAgentRadius;
-                const float oz1 = p0.z + c::kAgentRadius + (top - 2.f * c::kAgentRadius);
-                const float cz0 = S.pz[g0 + lane] + kCapsuleRadius, cz1 = cz0 + kCapsuleSegment;
-                const float fxy = (S.px[g0 + lane] - p0.x) * dir_fwd.x + (S.py[g0 + lane] - p0.y) * dir_fwd.y;
-                const float fz = fmaxD(fmaxD((cz0 - oz0) * dir_fwd.z, (cz1 - oz0) * dir_fwd.z),
-                                       fmaxD((cz0 - oz1) * dir_fwd.z, (cz1 - oz1) * dir_fwd.z));
-                keep = fxy + fz + kCapsuleRadius * 1.01f + 4.f >= 0.f;
+                cx = S.px[g0 + lane]; cy = S.py[g0 + lane]; cz = S.pz[g0 + lane];
+                const float dx = cx - ray_o.x, dy = cy - ray_o.y;
+                keep = lane != i && !(sqrtf(dx * dx + dy * dy) - c::kAgentRadius * 1.01f - 1.f > mx);
             }
-            capMask = (uint32_t)__ballot(keep);
+            uint64_t cm = __ballot(keep);
+            bool hit = bhit;
+            int ent = -1;
+            const float dxy2 = dir.x * dir.x + dir.y * dir.y;
+            const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
+            while (cm) {
+                const int j = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                Vec3 co = v3(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), j)),
+                             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), j)),
+                             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), j)));
+                co.z += kCapsuleRadius;
+                const Vec3 tr = ray_o - co;
+                // the per-ray conservative culls of capsulesD
+                const float cr = tr.x * dir.y - tr.y * dir.x;
+                if (cr * cr > cull_r2 * dxy2) continue;
+                const float along = -(tr.x * dir.x + tr.y * dir.y + tr.z * dir.z);
+                const float ahead = along + fmaxD(0.f, kCapsuleSegment * dir.z) + kCapsuleRadius * 1.01f;
+                if (ahead < 0.f) continue;
+                if (along + fminD(0.f, kCapsuleSegment * dir.z) - kCapsuleRadius * 1.01f > min_t) continue;
+                const float t = intersectRayZOriginCapsule(tr, dir, kCapsuleRadius, kCapsuleSegment);
+                if (t != 0 && t < min_t) {
+                    min_t = t;
+                    hit = true;
+                    ent = j;
+                }
+            }
+            hw.hit = hit;
+            hw.t = min_t;
+            hw.entity = ent;
+        } else {
+            hw = traceWorldD<MPENV_LIDAR_PERM != 0>(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir, (int)i);
         }
-#endif
-        WorldHit hw = traceWorldD<MPENV_LIDAR_PERM != 0>(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir, (int)i,
-                                                         capMask);
         if (!valid) continue;
         const bool second = i >= T; // team of the casting agent
         float4 out;
@@ -3219,11 +3304,15 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // fullTeamObservationsSystem copies the lidar before this system
         // overwrites it (sim.cpp:5283-5310): the previous value moves into
         // the team interface's slot.
+#ifndef MPENV_LAB_NO_FT_LIDAR
         const float4 prev = *dst;
 #if MPENV_LIDAR_NT
         ntStore(tdst, prev);
 #else
         *tdst = prev;
+#endif
+#else
+        (void)tdst;
 #endif
         *dst = out;
     }
@@ -3289,7 +3378,11 @@ __global__ void __launch_bounds__(256) k_debug(DevState S, float *af, int32_t *a
         n[14] = S.visMask[g];
         n[15] = S.newCells[g];
         if (explore) {
-            for (int k = 0; k < kGridCells; k++) explore[g * kGridCells + k] = S.visited[g * kGridCells + k];
+            // 1 = visited in the agent's current episode (the reference's
+            // tag == curEpisodeIdx), 0 otherwise
+            const bool cur = S.exploreEp[g] == S.episode[g / S.N];
+            for (int k = 0; k < kGridCells; k++)
+                explore[g * kGridCells + k] = cur ? (S.exploreBits[g * kExploreWords + (k >> 5)] >> (k & 31)) & 1u : 0u;
         }
     }
     if (t < S.W) {
@@ -3334,6 +3427,66 @@ __global__ void __launch_bounds__(256) k_fill_actions(DevState S, const int32_t 
     reinterpret_cast<int2 *>(S.discreteAim)[g] = make_int2(s[4], s[5]);
 }
 
+// Synthetic combat action source (bench / tests; no reference counterpart):
+// the tape row of each agent, overridden by a greedy aim-bot that reads the
+// agent's current observations -- the same function as the tests'
+// mpenv_testlib.combat_actions (mode 0) / seek_combat_actions (mode 1), so
+// engine and oracle see identical actions while parity holds.
+//   an opponent visible (first k with OPPONENT_MASKS[k] > 0): discrete aim
+//   toward its relative yaw / pitch (opponent obs 24 / 25) through the
+//   pvpDiscreteAimSystem turn tables (sim.cpp:2284-2370), fire iff
+//   |yaw| < 0.05;  mode 1 and none visible: turn toward the zone (self obs
+//   31, toCenterYaw) and run forward once within 0.5 rad of it, else stand;
+//   mode 1 also reloads an empty magazine (self obs 24 == 0, not reloading).
+// The bucket compares run in double against the double turn tables, as
+// numpy does with its float64 tables.
+__device__ __forceinline__ int32_t aimBucketD(float delta, bool yaw_table, int32_t centre)
+{
+    const double mag = (double)fabsf(delta);
+    const double pi = 3.141592653589793;
+    int32_t idx = 0;
+    if (yaw_table) {
+        idx += (1.0 / 256.0) * pi <= mag; idx += (1.0 / 128.0) * pi <= mag; idx += (1.0 / 64.0) * pi <= mag;
+        idx += (1.0 / 32.0) * pi <= mag; idx += (1.0 / 16.0) * pi <= mag; idx += (1.0 / 8.0) * pi <= mag;
+    } else {
+        idx += (1.0 / 128.0) * pi <= mag; idx += (1.0 / 64.0) * pi <= mag; idx += (1.0 / 32.0) * pi <= mag;
+    }
+    return delta > 0.f ? centre + idx : (delta < 0.f ? centre - idx : centre);
+}
+
+__global__ void __launch_bounds__(256) k_combat_actions(DevState S, const int32_t *tape, int32_t *out, int32_t mode)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= S.A) return;
+    const int32_t *t = tape + 6 * g;
+    int32_t a[6] = { t[0], t[1], t[2], t[3], t[4], t[5] };
+    const float *mk = S.masks + 6 * g;
+    int k = -1;
+    for (int j = 5; j >= 0; j--)
+        if (mk[j] > 0.f) k = j;
+    if (k >= 0) {
+        const float *ob = S.oppObs + (g * 6 + k) * kOtherObs;
+        const float yaw = ob[24], pitch = ob[25];
+        a[4] = aimBucketD(yaw, true, 6);
+        a[5] = aimBucketD(pitch, false, 3);
+        a[2] = fabsf(yaw) < 0.05f ? 1 : 0;
+    } else if (mode == 1) {
+        const float zy = S.selfObs[g * kSelfObs + 31];
+        a[4] = aimBucketD(zy, true, 6);
+        if (fabsf(zy) < 0.5f) { a[0] = 2; a[1] = 0; } else { a[0] = 0; }
+    }
+    // mode 1: an empty magazine that is not already reloading is reloaded
+    // (self obs 24 / 25: bullets, reload steps left)
+    if (mode == 1 && S.selfObs[g * kSelfObs + 24] == 0.f && S.selfObs[g * kSelfObs + 25] == 0.f) a[2] = 2;
+    if (out) {
+        int32_t *o = out + 6 * g;
+        for (int j = 0; j < 6; j++) o[j] = a[j];
+    } else {
+        reinterpret_cast<int4 *>(S.discreteAction)[g] = make_int4(a[0], a[1], a[2], a[3]);
+        reinterpret_cast<int2 *>(S.discreteAim)[g] = make_int2(a[4], a[5]);
+    }
+}
+
 // ============================================================ host side
 const char *kernelName(int k)
 {
@@ -3358,9 +3511,9 @@ size_t bvhLdsBytesOct(const SceneDev &sc)
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
-    const int64_t total = s.A * kGridCells;
+    const int64_t total = s.A * kExploreWords;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
-    hipLaunchKernelGGL(k_init_explore, dim3(blocks), dim3(256), 0, st, s.visited, total);
+    hipLaunchKernelGGL(k_init_explore, dim3(blocks), dim3(256), 0, st, s.exploreBits, s.exploreEp, total);
     if (check(hipGetLastError())) return -1;
     hipLaunchKernelGGL(k_construct, dim3((s.W + 63) / 64), dim3(64), 0, st, s, sc, tc[0], tc[1], tc[2]);
     return check(hipGetLastError());
@@ -3459,6 +3612,13 @@ int launchFillActions(const DevState &s, const int32_t *src6, void *stream)
 {
     hipLaunchKernelGGL(k_fill_actions, dim3((unsigned)((s.A + 255) / 256)), dim3(256), 0, (hipStream_t)stream, s,
                        src6);
+    return check(hipGetLastError());
+}
+
+int launchCombatActions(const DevState &s, const int32_t *tape6, int32_t *out6, int32_t mode, void *stream)
+{
+    hipLaunchKernelGGL(k_combat_actions, dim3((unsigned)((s.A + 255) / 256)), dim3(256), 0, (hipStream_t)stream, s,
+                       tape6, out6, mode);
     return check(hipGetLastError());
 }
 

@@ -276,7 +276,7 @@ struct mpenv_manager {
     }
 
     bool exportDesc(int32_t id, TensorDesc &d);
-    void gatherDebug();
+    void gatherDebug(bool explore = false);
 };
 
 bool mpenv_manager::exportDesc(int32_t id, TensorDesc &d)
@@ -350,23 +350,24 @@ bool mpenv_manager::exportDesc(int32_t id, TensorDesc &d)
     case MPENV_EXPORT_DEBUG_AGENT_I32: gatherDebug(); return set(dbgAI, MPENV_DTYPE_INT32, { A, MPENV_DBG_AI_COUNT });
     case MPENV_EXPORT_DEBUG_WORLD_I32: gatherDebug(); return set(dbgWI, MPENV_DTYPE_INT32, { W, MPENV_DBG_WI_COUNT });
     case MPENV_EXPORT_DEBUG_WORLD_F32: gatherDebug(); return set(dbgWF, MPENV_DTYPE_FLOAT32, { W, MPENV_DBG_WF_COUNT });
-    case MPENV_EXPORT_DEBUG_EXPLORE: gatherDebug(); return set(dbgExplore, MPENV_DTYPE_UINT32, { A, kGridCells });
+    case MPENV_EXPORT_DEBUG_EXPLORE: gatherDebug(true); return set(dbgExplore, MPENV_DTYPE_UINT32, { A, kGridCells });
     case MPENV_EXPORT_DEBUG_CRUMBS: gatherDebug(); return set(dbgCrumbs, MPENV_DTYPE_FLOAT32, { W, kMaxCrumbs, 8 });
     default: return false;
     }
 }
 
-void mpenv_manager::gatherDebug()
+void mpenv_manager::gatherDebug(bool explore)
 {
     if (!dbgAF) {
         dbgAF = alloc<float>((size_t)S.A * MPENV_DBG_AF_COUNT);
         dbgAI = alloc<int32_t>((size_t)S.A * MPENV_DBG_AI_COUNT);
         dbgWI = alloc<int32_t>((size_t)S.W * MPENV_DBG_WI_COUNT);
         dbgWF = alloc<float>((size_t)S.W * MPENV_DBG_WF_COUNT);
-        dbgExplore = alloc<uint32_t>((size_t)S.A * kGridCells);
         dbgCrumbs = alloc<float>((size_t)S.W * kMaxCrumbs * 8);
     }
-    if (launchDebugGather(S, dbgAF, dbgAI, dbgWI, dbgWF, dbgExplore, dbgCrumbs, stream))
+    // the expanded explore grid (4 B per cell, 26 KB per agent) only on request
+    if (explore && !dbgExplore) dbgExplore = alloc<uint32_t>((size_t)S.A * kGridCells);
+    if (launchDebugGather(S, dbgAF, dbgAI, dbgWI, dbgWF, explore ? dbgExplore : nullptr, dbgCrumbs, stream))
         throw std::runtime_error("debug gather launch failed");
     HIP_CHECK(hipStreamSynchronize(stream));
 }
@@ -576,7 +577,7 @@ static void allocState(mpenv_manager &m)
     S.dmg = m.alloc<float>(A * kMaxTeamSize);
     S.dmgStride = (int64_t)A;
     S.visMask = m.alloc<uint8_t>(A);
-    S.visited = m.alloc<uint32_t>(A * kGridCells);
+    S.exploreBits = m.alloc<uint32_t>(A * kExploreWords);
     S.filtLast = m.alloc<int32_t>(W * 6);
     S.zoneStats = m.alloc<int32_t>(W * 25);
     S.resetKeys = m.alloc<mp::RandKey>(A * 11);
@@ -679,7 +680,7 @@ static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_
 #undef MP_SL_W
     G.dmg = S.dmg + g0; // stride stays S.dmgStride
     G.visMask = S.visMask + g0;
-    G.visited = S.visited + g0 * kGridCells;
+    G.exploreBits = S.exploreBits + g0 * kExploreWords;
     G.filtLast = S.filtLast + w0 * 6;
     G.resetKeys = S.resetKeys + g0 * 11;
     G.zoneStats = S.zoneStats + w0 * 25;
@@ -995,6 +996,15 @@ int mpenv_copy_actions(mpenv_manager *m, const int32_t *src, void *stream)
     if (!m || !src) return fail(MPENV_ERR_INVALID, "null argument");
     if (launchFillActions(m->S, src, stream ? stream : (void *)m->stream))
         return fail(MPENV_ERR_HIP, "action copy launch failed");
+    return MPENV_OK;
+}
+
+int mpenv_combat_actions(mpenv_manager *m, const int32_t *tape, int32_t *out, int32_t mode, void *stream)
+{
+    if (!m || !tape) return fail(MPENV_ERR_INVALID, "null argument");
+    if (mode != 0 && mode != 1) return fail(MPENV_ERR_INVALID, "combat action mode must be 0 or 1");
+    if (launchCombatActions(m->S, tape, out, mode, stream ? stream : (void *)m->stream))
+        return fail(MPENV_ERR_HIP, "combat action launch failed");
     return MPENV_OK;
 }
 

@@ -222,6 +222,10 @@ PYBIND11_MODULE(madrona_mp_env, m)
         .def("copy_actions", [](PySimManager &s, uintptr_t src, uintptr_t stream) {
             check(mpenv_copy_actions(s.h->mgr, reinterpret_cast<const int32_t *>(src), reinterpret_cast<void *>(stream)));
         }, py::arg("src"), py::arg("stream") = 0)
+        .def("combat_actions", [](PySimManager &s, uintptr_t tape, uintptr_t out, int32_t mode, uintptr_t stream) {
+            check(mpenv_combat_actions(s.h->mgr, reinterpret_cast<const int32_t *>(tape),
+                                       reinterpret_cast<int32_t *>(out), mode, reinterpret_cast<void *>(stream)));
+        }, py::arg("tape"), py::arg("out") = 0, py::arg("mode") = 1, py::arg("stream") = 0)
         .def("set_world_groups", [](PySimManager &s, int32_t g) { check(mpenv_set_world_groups(s.h->mgr, g)); })
         .def("world_groups", [](PySimManager &s) { int32_t g = 0; check(mpenv_world_groups(s.h->mgr, &g)); return g; })
         .def("enable_kernel_timing", [](PySimManager &s, bool on) { check(mpenv_enable_kernel_timing(s.h->mgr, on)); })
@@ -230,10 +234,10 @@ PYBIND11_MODULE(madrona_mp_env, m)
             uint64_t v[8] = {};
             int n = mpenv_read_stats(s.h->mgr, v, 8);
             if (n < 0) check(n);
-            static const char *names[6] = { "alive_agents", "los_pairs", "los_rays", "los_seen",
-                                            "sphere_casts", "shot_rays" };
+            static const char *names[8] = { "alive_agents", "los_pairs", "los_rays", "los_seen",
+                                            "sphere_casts", "shot_rays", "hit_agents", "kills" };
             py::dict d;
-            for (int k = 0; k < 6; k++) d[py::str(names[k])] = v[k];
+            for (int k = 0; k < 8; k++) d[py::str(names[k])] = v[k];
             return d;
         })
         .def("kernel_timings", [](PySimManager &s) {

@@ -25,6 +25,41 @@ all-reduces gradients) moves only the gradients.
 """
 from typing import Dict, List, Sequence, Tuple
 
+# trainInterface outputs never written by the simulator:
+# agent_map / unmasked_agent_map, 4 KB per agent each, constant zeros the
+# learner already has, so no exchange ships them.
+NOT_SHIPPED = ("agent_map", "unmasked_agent_map")
+
+
+def flat_layout(sources) -> Tuple[list, int]:
+    """Segments of one flat byte buffer holding every source tensor:
+    [(name, byte offset, nbytes, dtype, shape)], 256-B aligned, and the
+    total size.  The learner exchange ships (and the learner reads) this
+    layout."""
+    layout, off = [], 0
+    for n, t in sources.items():
+        nb = t.numel() * t.element_size()
+        layout.append((n, off, nb, t.dtype, tuple(t.shape)))
+        off += (nb + 255) // 256 * 256
+    return layout, off
+
+
+def pack_flat(layout, srcs, buf) -> None:
+    """Copy each source into its segment of `buf` (uint8, on the current
+    stream)."""
+    import torch
+
+    for (n, off, nb, dt, shape), t in zip(layout, srcs):
+        buf[off:off + nb].copy_(t.view(-1).view(torch.uint8))
+
+
+def unpack_flat(layout, recv) -> Dict[str, object]:
+    """Zero-copy views {name: [ranks, rows, ...]} of a received
+    [ranks, nbytes] buffer; flattening the first two axes gives global world
+    order when rank r holds global worlds [r W, (r + 1) W)."""
+    ws = recv.shape[0]
+    return {n: recv[:, off:off + nb].view(dt).view((ws,) + shape) for n, off, nb, dt, shape in layout}
+
 
 def shard_worlds(total_worlds: int, rank: int, world_size: int) -> Tuple[int, int]:
     """Contiguous split of [0, total_worlds): returns (world_id_offset, count).
@@ -74,15 +109,14 @@ class LearnerGather:
     r holds global worlds [r W, (r + 1) W) (shard_worlds), so flattening the
     first two axes is global world order.
 
-    sources: {name: tensor} (contiguous; same shapes on every rank), e.g.
+    sources: {name: tensor} (contiguous; same shapes on every rank, checked
+    at construction), e.g.
     SimManager.train_interface()["outputs"] as torch tensors, or
     `from_sim(sim)`.
     """
 
-    # agent_map / unmasked_agent_map (4 KB per agent each) are never written
-    # by the simulator (SURVEY.md §8a): constant zeros the learner already
-    # has, so they are not shipped.
-    NOT_SHIPPED = ("agent_map", "unmasked_agent_map")
+    NOT_SHIPPED = NOT_SHIPPED
+    mode = "gather"
 
     def __init__(self, sources, dst: int = 0, group=None, slots: int = 2, exclude=NOT_SHIPPED):
         import torch
@@ -91,21 +125,31 @@ class LearnerGather:
         if hasattr(sources, "train_interface"):
             sources = self.from_sim(sources)
         sources = {n: t for n, t in sources.items() if n not in exclude}
+        # the live engine buffers themselves: a .contiguous() copy would be a
+        # snapshot that every later submit() ships unchanged
+        for n, t in sources.items():
+            if not t.is_contiguous():
+                raise ValueError(f"LearnerGather source {n!r} is not contiguous")
         self.dist = dist
         self.group = group
         self.dst = dst
         self.rank = dist.get_rank(group)
         self.ws = dist.get_world_size(group)
         self.names = list(sources.keys())
-        self.src = [sources[n].contiguous() for n in self.names]
+        self.src = [sources[n] for n in self.names]
         dev = self.src[0].device
-        self.layout = []  # (name, byte offset, nbytes, dtype, shape)
-        off = 0
-        for n, t in zip(self.names, self.src):
-            nb = t.numel() * t.element_size()
-            self.layout.append((n, off, nb, t.dtype, tuple(t.shape)))
-            off += (nb + 255) // 256 * 256  # 256-B aligned segments
+        self.layout, off = flat_layout(sources)  # (name, byte offset, nbytes, dtype, shape)
         self.nbytes = off
+        # The receive buffers and outputs() views assume every rank ships the
+        # same layout (equal shards): a gather of unequal buffers errors on
+        # gloo and truncates or overruns silently on RCCL, so check up front.
+        sig = [(n, nb, str(dt), shape) for n, _, nb, dt, shape in self.layout]
+        sigs = [None] * self.ws
+        dist.all_gather_object(sigs, sig, group=group)
+        for r, other in enumerate(sigs):
+            if other != sig:
+                raise ValueError(f"LearnerGather: rank {r} ships a different layout than rank {self.rank} "
+                                 "(unequal shards? total worlds must be divisible by the world size)")
         self.flat = [torch.empty(off, dtype=torch.uint8, device=dev) for _ in range(slots)]
         self.recv = None
         if self.rank == dst:
@@ -121,17 +165,18 @@ class LearnerGather:
         outs = sim.train_interface()["outputs"]
         return {n: t.to_torch() for n, t in outs.items()}
 
-    def submit(self, stream_ptr=None):
-        import torch
+    def bytes_per_step(self) -> dict:
+        """Bytes this rank sends and the learner receives per step."""
+        return {"sent_per_rank": self.nbytes, "learner_ingress": self.nbytes * (self.ws - 1)}
 
+    def submit(self, stream_ptr=None):
         slot = self.k % len(self.flat)
         self.k += 1
         if self.pending[slot] is not None:
             self.pending[slot].wait()
             self.pending[slot] = None
         buf = self.flat[slot]
-        for (n, off, nb, dt, shape), t in zip(self.layout, self.src):
-            buf[off:off + nb].copy_(t.view(-1).view(torch.uint8))
+        pack_flat(self.layout, self.src, buf)
         gl = list(self.recv[slot].unbind(0)) if self.recv is not None else None
         self.pending[slot] = self.dist.gather(buf, gl, dst=self.dst, group=self.group, async_op=True)
         self.last_slot = slot
@@ -151,12 +196,81 @@ class LearnerGather:
         if self.pending[slot] is not None:
             self.pending[slot].wait()
             self.pending[slot] = None
-        r = self.recv[slot]
-        out = {}
-        for n, off, nb, dt, shape in self.layout:
-            out[n] = r[:, off:off + nb].view(dt).view((self.ws,) + shape)
-        return out
+        return unpack_flat(self.layout, self.recv[slot])
 
     def close(self):
         self.drain()
 
+
+
+class LearnerLocal:
+    """Learner-local exchange (data-parallel learner): each rank's learner
+    trains on the shard its simulator produced, so observations never leave
+    the GPU that made them (`outputs()` are the engine's own zero-copy
+    buffers, [1, rows, ...] like LearnerGather's on one rank); what crosses
+    xGMI is the gradient all-reduce of the policy update.  Here that is a
+    stand-in: every `update_every` steps (jax_train.py --steps-per-update,
+    default 50) one asynchronous RCCL all-reduce of a `grad_bytes` f32
+    buffer (the policy's parameter count x 4 B), overlapping the next steps;
+    the learner's compute itself is out of scope."""
+
+    NOT_SHIPPED = NOT_SHIPPED
+    mode = "local"
+
+    def __init__(self, sources, grad_bytes: int = 16 << 20, update_every: int = 50, group=None,
+                 exclude=NOT_SHIPPED):
+        import torch
+        import torch.distributed as dist
+
+        if hasattr(sources, "train_interface"):
+            sources = LearnerGather.from_sim(sources)
+        self.sources = {n: t for n, t in sources.items() if n not in exclude}
+        self.dist = dist
+        self.group = group
+        self.ws = dist.get_world_size(group)
+        self.update_every = max(1, int(update_every))
+        dev = next(iter(self.sources.values())).device
+        self.grad = torch.ones(max(1, grad_bytes // 4), dtype=torch.float32, device=dev)
+        self.layout, self.nbytes = flat_layout(self.sources)
+        self.pending = None
+        self.k = 0
+        self.updates = 0
+
+    def bytes_per_step(self) -> dict:
+        # ring all-reduce: each rank sends and receives 2 (ws - 1) / ws of the buffer
+        ar = 2 * (self.ws - 1) * self.grad.numel() * 4 // self.ws
+        return {"sent_per_rank": ar / self.update_every, "learner_ingress": ar / self.update_every}
+
+    def submit(self, stream_ptr=None):
+        self.k += 1
+        if self.k % self.update_every:
+            return None
+        if self.pending is not None:
+            self.pending.wait()
+        self.pending = self.dist.all_reduce(self.grad, group=self.group, async_op=True)
+        self.updates += 1
+        return self.updates
+
+    def drain(self):
+        if self.pending is not None:
+            self.pending.wait()
+            self.pending = None
+
+    def outputs(self, slot=None):
+        return {n: t.unsqueeze(0) for n, t in self.sources.items()}
+
+    def close(self):
+        self.drain()
+
+
+def make_exchange(mode: str, sim, group=None, **kw):
+    """The learner exchange a multi-GPU run names in config.parallelism:
+    "none" (simulators only), "gather" (LearnerGather: every shipped output
+    to one learner rank each step) or "local" (LearnerLocal)."""
+    if mode == "none":
+        return None
+    if mode == "gather":
+        return LearnerGather(sim, dst=0, group=group)
+    if mode == "local":
+        return LearnerLocal(sim, group=group, **kw)
+    raise ValueError(f"unknown exchange {mode!r}")

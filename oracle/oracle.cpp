@@ -3526,6 +3526,19 @@ float oracle_sphere_cast(void *h, const float *org, const float *d, float r, flo
     return t;
 }
 
+void oracle_sphere_cast_batch(void *h, int32_t n, const float *org, const float *d, float r,
+                              const float *t_max, float *t_out, float *n_out)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    for (int32_t k = 0; k < n; k++) {
+        Vec3 nn = v3(0.f, 0.f, 0.f);
+        const float tm = t_max ? t_max[k] : kFltMax;
+        t_out[k] = bvhSphereCast(o, v3(org[3 * k], org[3 * k + 1], org[3 * k + 2]),
+                                 v3(d[3 * k], d[3 * k + 1], d[3 * k + 2]), r, &nn, tm);
+        n_out[3 * k] = nn.x; n_out[3 * k + 1] = nn.y; n_out[3 * k + 2] = nn.z;
+    }
+}
+
 int oracle_trace_ray_brute(void *h, const float *org, const float *d, float *t_out)
 {
     Oracle &o = *static_cast<Oracle *>(h);

@@ -83,6 +83,10 @@ void oracle_cast_stats(int32_t leaf_read_two, uint64_t *out2);
 int oracle_trace_ray(void *h, const float *o, const float *d, float *t_out);
 float oracle_sphere_cast(void *h, const float *o, const float *d, float r,
                          float *normal_out);
+/* n casts of MeshBVH::sphereCast with its t_max argument (mesh_bvh.inl:743-747;
+ * t_max null = FLT_MAX): o, d, n_out [n][3]; normals are (0,0,0) on a miss. */
+void oracle_sphere_cast_batch(void *h, int32_t n, const float *o, const float *d, float r,
+                              const float *t_max, float *t_out, float *n_out);
 int oracle_trace_ray_brute(void *h, const float *o, const float *d, float *t_out);
 float oracle_sphere_cast_brute(void *h, const float *o, const float *d, float r);
 

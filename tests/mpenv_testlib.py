@@ -52,6 +52,18 @@ STEP_OUTPUTS = [
     "OPPONENT_MASKS", "REWARD", "DONE", "MATCH_RESULT", "REWARD_HYPER_PARAMS", "RESET",
     "WORLD_CURRICULUM", "PVP_DISCRETE_ACTION", "PVP_DISCRETE_AIM_ACTION", "PVP_AIM_ACTION",
 ] + FULL_TEAM_OUTPUTS
+# trainInterface outputs (mgr.cpp:2383-2431, csrc/manager.cpp kTIOutputs) ->
+# export names; agent_map / unmasked_agent_map (never written) are not shipped.
+TRAIN_OUTPUTS = {
+    "fwd_lidar": "FWD_LIDAR", "rear_lidar": "REAR_LIDAR", "hp": "HP", "magazine": "MAGAZINE",
+    "alive": "ALIVE", "self": "SELF_OBSERVATION", "filters_state": "FILTERS_STATE",
+    "teammates": "TEAMMATE_OBSERVATIONS", "opponents": "OPPONENT_OBSERVATIONS",
+    "opponents_last_known": "OPPONENT_LAST_KNOWN_OBSERVATIONS", "self_pos": "SELF_POSITION",
+    "teammate_positions": "TEAMMATE_POSITIONS", "opponent_positions": "OPPONENT_POSITIONS",
+    "opponent_last_known_positions": "OPPONENT_LAST_KNOWN_POSITIONS", "opponent_masks": "OPPONENT_MASKS",
+    "reward_coefs": "REWARD_HYPER_PARAMS", "rewards": "REWARD", "dones": "DONE",
+    "pbt.episode_results": "MATCH_RESULT",
+}
 DEBUG_OUTPUTS = ["DEBUG_AGENT_F32", "DEBUG_AGENT_I32", "DEBUG_WORLD_I32", "DEBUG_WORLD_F32",
                  "DEBUG_CRUMBS"]
 
@@ -87,6 +99,19 @@ class MpenvConfig(C.Structure):
 
 
 _libs = {}
+
+
+def usable_cpus():
+    """CPUs this process may use: affinity, capped by a cgroup v2 CPU quota
+    (the GPU box shows the whole host's CPUs but grants 16)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def ensure_built():
@@ -143,6 +168,7 @@ def lib_oracle():
         lib.oracle_trace_ray_brute.argtypes = [C.c_void_p, fp, fp, fp]
         lib.oracle_sphere_cast.argtypes = [C.c_void_p, fp, fp, C.c_float, fp]
         lib.oracle_sphere_cast.restype = C.c_float
+        lib.oracle_sphere_cast_batch.argtypes = [C.c_void_p, C.c_int32, fp, fp, C.c_float, fp, fp, fp]
         lib.oracle_sphere_cast_brute.argtypes = [C.c_void_p, fp, fp, C.c_float]
         lib.oracle_sphere_cast_brute.restype = C.c_float
         lib.oracle_navmesh.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -415,6 +441,32 @@ class Engine:
         row = int(np.prod(shape[1:])) * 4
         self.mem.h2d(ptr + r0 * row, np.ascontiguousarray(arr, dtype=dt))
 
+    def combat_actions(self, tape_dev, out_dev=None, mode=1):
+        """mpenv_combat_actions: the device aim-bot over the tape rows at
+        tape_dev ([A][6] i32), into out_dev or straight into the step inputs."""
+        self.lib.mpenv_combat_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        assert self.lib.mpenv_combat_actions(self.h, tape_dev, out_dev, mode, None) == 0, \
+            self.lib.mpenv_last_error().decode()
+        if out_dev is not None:
+            self.mem.hip.hipDeviceSynchronize()
+
+    def set_world_groups(self, groups):
+        self.lib.mpenv_set_world_groups.argtypes = [C.c_void_p, C.c_int32]
+        assert self.lib.mpenv_set_world_groups(self.h, groups) == 0, self.lib.mpenv_last_error().decode()
+
+    def enable_stats(self, on=True):
+        self.lib.mpenv_enable_stats.argtypes = [C.c_void_p, C.c_int32]
+        assert self.lib.mpenv_enable_stats(self.h, int(on)) == 0, self.lib.mpenv_last_error().decode()
+
+    def read_stats(self):
+        """Workload counters (include/mpenv.h mpenv_read_stats)."""
+        self.lib.mpenv_read_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        v = np.zeros(8, np.uint64)
+        assert self.lib.mpenv_read_stats(self.h, v.ctypes.data, 8) >= 0, self.lib.mpenv_last_error().decode()
+        names = ("alive_agents", "los_pairs", "los_rays", "los_seen", "sphere_casts", "shot_rays",
+                 "hit_agents", "kills")
+        return dict(zip(names, (int(x) for x in v)))
+
     def copy_actions(self, dev_ptr):
         """Step inputs from device memory [A][6] i32 (gpuStreamStep's copy)."""
         assert self.lib.mpenv_copy_actions(self.h, dev_ptr, None) == 0, self.lib.mpenv_last_error().decode()
@@ -444,6 +496,18 @@ class Engine:
     def step(self):
         rc = self.lib.mpenv_step(self.h)
         assert rc == 0, self.lib.mpenv_last_error().decode()
+
+
+def explore_visited(sim):
+    """[A, 81*81] u32: 1 where the ExploreTracker cell holds the agent's
+    current episode index.  The engine exports exactly this (its bitset);
+    the oracle keeps the reference's u32 tags, reduced here with the world's
+    current episode (DEBUG_WORLD_I32[10])."""
+    if isinstance(sim, Oracle):
+        tags = sim.get("DEBUG_EXPLORE")
+        ep = np.repeat(sim.get("DEBUG_WORLD_I32")[:, 10].astype(np.uint32), sim.N)
+        return (tags == ep[:, None]).astype(np.uint32)
+    return sim.get("DEBUG_EXPLORE")
 
 
 def compare(a, b, name, float_rtol=0.0):
@@ -490,14 +554,37 @@ def combat_actions(sim, step, seed=1234, base=None):
     yaw = opp[np.arange(A), k, 24]
     pitch = opp[np.arange(A), k, 25]
 
-    def bucket(delta, table, centre):
-        mag = np.abs(delta)[:, None]
-        idx = np.sum(table[None, 1:] <= mag, axis=1)
-        return (centre + np.sign(delta) * idx).astype(np.int32)
-
-    yb = bucket(yaw, _YAW_TURN, 6)
-    pb = bucket(pitch, _PITCH_TURN, 3)
+    yb = _bucket(yaw, _YAW_TURN, 6)
+    pb = _bucket(pitch, _PITCH_TURN, 3)
     acts[has, 4] = yb[has]
     acts[has, 5] = pb[has]
     acts[has, 2] = np.where(np.abs(yaw[has]) < 0.05, 1, 0)
+    return acts
+
+
+def _bucket(delta, table, centre):
+    mag = np.abs(delta)[:, None]
+    idx = np.sum(table[None, 1:] <= mag, axis=1)
+    return (centre + np.sign(delta) * idx).astype(np.int32)
+
+
+def seek_combat_actions(sim, step, seed=1234, base=None):
+    """combat_actions, and agents that see no opponent turn toward the zone
+    (self-observation 31, ZoneObservation.toCenterYaw) and run forward once
+    within 0.5 rad of it, else stand still: both teams converge on the zone,
+    so fights, kills and respawns are frequent; an empty magazine (self obs
+    24 == 0, not reloading: obs 25 == 0) is reloaded.  The engine's
+    mpenv_combat_actions(mode 1) computes the same function on the device."""
+    A = sim.W * sim.N
+    acts = combat_actions(sim, step, seed, base)
+    mask = sim.get("OPPONENT_MASKS").reshape(A, -1)
+    no = ~(mask[:, :6] > 0).any(1)
+    so = sim.get("SELF_OBSERVATION").reshape(A, -1)
+    zy = so[:, 31]
+    face = np.abs(zy) < np.float32(0.5)
+    acts[no, 4] = _bucket(zy, _YAW_TURN, 6)[no]
+    acts[no & face, 0] = 2
+    acts[no & face, 1] = 0
+    acts[no & ~face, 0] = 0
+    acts[(so[:, 24] == 0) & (so[:, 25] == 0), 2] = 2
     return acts

@@ -27,6 +27,7 @@ GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.j
 def _compare_all(e, o, where):
     for n in ALL:
         T.compare(e.get(n), o.get(n), f"{n} @ {where}")
+    T.compare(T.explore_visited(e), T.explore_visited(o), f"explore cells @ {where}")
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-5] for p in GOLDEN])
@@ -94,6 +95,53 @@ def test_engine_matches_oracle_live(ts, worlds, steps, flags, ctrl, policy):
         else:
             for n in ("SELF_OBSERVATION", "REWARD", "DONE", "HP", "DEBUG_AGENT_I32"):
                 T.compare(e.get(n), o.get(n), f"{n} @ step {s}")
+    e.close()
+    o.close()
+
+
+def test_device_combat_actions_match_numpy_and_drive_combat():
+    """mpenv_combat_actions (the bench's combat action source) equals the
+    tests' numpy aim-bots on the engine's own observations -- mode 0
+    (combat_actions) and mode 1 (seek_combat_actions) -- and the fused form
+    (written straight into the step inputs) keeps the engine bit-exact with
+    the oracle stepped with the numpy actions; kills and respawns happen."""
+    ts, W, steps = 6, 64, 600
+    N = 2 * ts
+    A = W * N
+    e = T.Engine(W, ts)
+    o = T.Oracle(W, ts)
+    for sim in (e, o):
+        sim.put_ctrl([0, 1, 1])
+        sim.init()
+    ring = T.mpenv_tape.tape_ring(1234, 0, A, 8)
+    dev_ring = e.mem.upload(ring)
+    out = e.mem.upload(np.zeros((A, 6), np.int32))
+    got = np.empty((A, 6), np.int32)
+    deaths, prev_alive = 0, o.get("ALIVE")
+    for s in range(steps):
+        mode = 0 if s < 40 else 1
+        fn = T.combat_actions if mode == 0 else T.seek_combat_actions
+        slot = dev_ring + (s % 8) * A * 24
+        e.combat_actions(slot, out, mode)
+        e.mem.d2h(out, got.nbytes, got)
+        np.testing.assert_array_equal(got, fn(e, s, base=ring[s % 8]), err_msg=f"mode {mode} step {s}")
+        acts = fn(o, s, base=ring[s % 8])
+        e.combat_actions(slot, None, mode)
+        o.set_actions(acts)
+        e.step()
+        o.step()
+        alive = o.get("ALIVE")
+        deaths += int(((prev_alive == 1) & (alive == 0)).sum())
+        prev_alive = alive
+        if s % 10 == 0 or s == steps - 1:
+            _compare_all(e, o, f"step {s}")
+        else:
+            for n in ("SELF_OBSERVATION", "PVP_DISCRETE_ACTION", "PVP_DISCRETE_AIM_ACTION", "HP", "REWARD"):
+                T.compare(e.get(n), o.get(n), f"{n} @ step {s}")
+    e.mem.free(dev_ring)
+    e.mem.free(out)
+    print(f"\n{W} worlds {ts}v{ts}, {steps} steps of device combat actions: {deaths} deaths")
+    assert deaths > 0
     e.close()
     o.close()
 
@@ -260,13 +308,15 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
     3-world slices of the same global worlds (world_id_offset), bit-exact on
     every STEP_OUTPUT and the internal state every 50 steps.
 
-    Actions: the bench's hash tape (ring of 64 steps resident in HBM, copied
-    by gpuStreamStep's input copy) with team slot 1 of every even world an A*
-    bot (AgentPolicy -1, planAStarAISystem), which walks to the zone and
-    holds it; in the probed worlds the tape rows are overridden by the
-    combat aim-bot (mpenv_testlib.combat_actions, computed from the oracle's
-    observations and written into the device ring before the copy), so
-    kills, respawns and combat rewards happen over the long horizon too.  That drives the zone systems through their natural events
+    Actions: the bench's hash tape (ring of 64 steps resident in HBM) with
+    team slot 1 of every even world an A* bot (AgentPolicy -1,
+    planAStarAISystem), which walks to the zone and holds it; every other
+    agent of the whole batch follows the zone-seeking aim-bot computed on the
+    device from the engine's own observations (mpenv_combat_actions mode 1,
+    written straight into the step inputs), the oracle slices the same
+    function in numpy (mpenv_testlib.seek_combat_actions) from theirs, so
+    both teams converge on the zone and kills, respawns and combat rewards
+    happen throughout the horizon.  That drives the zone systems through their natural events
     (sim.cpp:1892-1976 rotation after 600 controlled steps, 4470-4673 a point
     every 20 controlled steps and the 3,000-step end).  A 125-point win needs
     2,500 controlled steps, which the bots reach too rarely, so at steps
@@ -315,6 +365,7 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
         oracles[k].step()
 
     compare("init")
+    e.enable_stats(True)  # whole-batch hit / kill counters
     with ThreadPoolExecutor(len(oracles)) as pool:
         for s in range(steps):
             if s in (1000, 2000):
@@ -325,9 +376,8 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
                     e.put_rows("MATCH_RESULT", w0, mr)
             slot = dev_ring + (s % RING) * W * N * 6 * 4
             for k, (w0, o) in enumerate(zip(probes, oracles)):
-                acts[k] = T.combat_actions(o, s, base=ring[s % RING, w0 * N:(w0 + PW) * N])
-                e.mem.h2d(slot + w0 * N * 6 * 4, acts[k])
-            e.copy_actions(slot)
+                acts[k] = T.seek_combat_actions(o, s, base=ring[s % RING, w0 * N:(w0 + PW) * N])
+            e.combat_actions(slot, None, 1)
             e.step()
             list(pool.map(lambda k: ostep(k, s), range(len(oracles))))
             for k, o in enumerate(oracles):
@@ -346,9 +396,14 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
             if s % 50 == 49 or s == steps - 1:
                 compare(f"step {s}")
     e.mem.free(dev_ring)
-    print(f"\n{ts}v{ts} x {W}, {steps} steps, {len(probes)} x {PW} probed worlds: {ev}")
-    # every zone/match event fired in the probed worlds
-    assert ev["rotations"] > 0 and ev["points"] > 0 and ev["wins"] > 0 and ev["kills"] > 0, ev
+    batch = e.read_stats()
+    e.enable_stats(False)
+    print(f"\n{ts}v{ts} x {W}, {steps} steps, {len(probes)} x {PW} probed worlds: {ev}; whole batch: "
+          f"{batch['kills']} kills, {batch['hit_agents']} agent-steps hit, {batch['los_seen']} LOS rays seen")
+    # every zone/match event fired in the probed worlds, and combat throughout
+    assert ev["rotations"] > 0 and ev["points"] > 0 and ev["wins"] > 0, ev
+    assert ev["kills"] > 0, ev
+    assert batch["kills"] >= 1000 * W // 4096, batch
     assert ev["episode_ends"] >= len(probes) * PW, ev  # every world passed a 3,000-step end or a win
     # size-independent properties over the whole batch
     hp = e.get("HP")

@@ -87,3 +87,169 @@ def test_quirk_grid_covers_every_vertex_neighbourhood():
     verts = verts.reshape(-1, 3)
     # the vertices themselves (2o == v) are never clear
     assert not guard_clear(q, verts[:, 0], verts[:, 1]).any()
+
+
+# --------------------------------------------------------------------------
+# Bounded vs full sphere casts (the exactness claim itself, not only the grid)
+
+KFLT_MAX = np.float32(np.finfo(np.float32).max)
+BUFFER = np.float32(0.05 * 15.0)
+CAST_SLACK = np.float32(4.0)  # kernels.hip kCastSlack
+
+
+def guard_path_clear(q, px, py, qx, qy):
+    """castPathQuirkFreeD: every cell of the xy box of 2o .. 2o + B·d clear
+    (px, py = 2o; qx, qy = 2o + B·d, float32 as the kernel forms them)."""
+    min_x, min_y, cell, w, h, bits = q
+    inv = np.float32(1.0) / cell
+    x0 = np.maximum(np.floor((np.minimum(px, qx) - min_x) * inv).astype(np.int64), 0)
+    x1 = np.minimum(np.floor((np.maximum(px, qx) - min_x) * inv).astype(np.int64), w - 1)
+    y0 = np.maximum(np.floor((np.minimum(py, qy) - min_y) * inv).astype(np.int64), 0)
+    y1 = np.minimum(np.floor((np.maximum(py, qy) - min_y) * inv).astype(np.int64), h - 1)
+    clear = np.ones(len(px), bool)
+    span = int(max((x1 - x0).max(initial=0), (y1 - y0).max(initial=0))) + 1
+    for dy in range(span):
+        for dx in range(span):
+            x, y = x0 + dx, y0 + dy
+            live = (x <= x1) & (y <= y1)
+            bit = np.where(live, y * w + x, 0)
+            marked = ((bits[bit >> 5] >> (bit & 31).astype(np.uint32)) & 1) == 1
+            clear &= ~(live & marked)
+    return clear
+
+
+def casts(o, origins, dirs, t_max=None):
+    lib = o.lib
+    n = len(origins)
+    org = np.ascontiguousarray(origins, np.float32)
+    d = np.ascontiguousarray(dirs, np.float32)
+    t = np.zeros(n, np.float32)
+    nrm = np.zeros((n, 3), np.float32)
+    tm = None if t_max is None else T.fptr(np.ascontiguousarray(t_max, np.float32))
+    lib.oracle_sphere_cast_batch(o.h, n, T.fptr(org), T.fptr(d), np.float32(R), tm, T.fptr(t), T.fptr(nrm))
+    return t, nrm
+
+
+def k_move_origins(n, rng):
+    """Cast origins like applyVelocity's: agent positions from an oracle
+    rollout raised by the pose heights, and origins whose 2o lands near a
+    vertex (where the testVert quirk lives)."""
+    o = T.Oracle(8, 6)
+    o.put_ctrl([0, 1, 1])
+    o.init()
+    pos = []
+    for s in range(120):
+        o.set_actions(T.mpenv_tape.tape_actions(4321, s, 0, 8 * 12))
+        o.step()
+        if s % 6 == 5:
+            pos.append(o.get("DEBUG_AGENT_F32")[:, :3].copy())
+    pos = np.concatenate(pos).astype(np.float32)
+    _, verts, _ = T.scene_bvh()
+    verts = verts.reshape(-1, 3)
+    z_off = np.array([9.0, 50.0, 35.0, 9.75], np.float32)  # low_check / top (stand, crouch, prone)
+    a = pos[rng.integers(0, len(pos), n)] + np.stack(
+        [rng.uniform(-40, 40, n), rng.uniform(-40, 40, n), z_off[rng.integers(0, 4, n)]], 1)
+    # 2o within ~60 units of a vertex, z from the rollout
+    vi = rng.integers(0, len(verts), n)
+    b = np.stack([(verts[vi, 0] + rng.uniform(-60, 60, n)) * 0.5, (verts[vi, 1] + rng.uniform(-60, 60, n)) * 0.5,
+                  pos[rng.integers(0, len(pos), n), 2] + z_off[rng.integers(0, 4, n)]], 1)
+    return o, np.concatenate([a, b]).astype(np.float32)
+
+
+def test_bounded_sphere_casts_equal_full_casts_where_guard_is_clear():
+    """castNearD (kernels.hip) returns the bounded cast's hit when the path
+    guard is clear: its (t, normal) must equal the full cast's whenever
+    either is nearer than the bound, and both must read "no hit" otherwise.
+    Horizontal casts with the bounds k_move uses (forward: move_dist + buffer
+    + slack, move_dist in [0, 20]; slide: the same with max_move); origins
+    from an oracle rollout and origins whose 2o sits near vertices."""
+    rng = np.random.default_rng(11)
+    o, org = k_move_origins(40000, rng)
+    n = len(org)
+    ang = rng.uniform(0, 2 * np.pi, n)
+    d = np.stack([np.sin(ang), np.cos(ang), np.zeros(n)], 1).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    move = rng.uniform(0, 20.0, n).astype(np.float32)
+    B = (move + BUFFER) + CAST_SLACK
+    q = quirk_grid()
+    px, py = org[:, 0] + org[:, 0], org[:, 1] + org[:, 1]
+    clear = guard_path_clear(q, px, py, px + d[:, 0] * B, py + d[:, 1] * B)
+    t_full, n_full = casts(o, org, d)
+    t_b, n_b = casts(o, org, d, B)
+    near_full = t_full < B
+    near_b = t_b < B
+    c = clear
+    assert c.mean() > 0.3, c.mean()  # the guard is not vacuous
+    assert (near_full[c] == near_b[c]).all()
+    both = c & near_b
+    assert both.sum() > 1000, both.sum()  # many bounded hits compared
+    assert np.array_equal(t_full[both], t_b[both])
+    assert np.array_equal(n_full[both], n_b[both])
+    # the single-cell guard (round 2) was not enough for horizontal casts:
+    # report how often it would have taken a bounded cast that differs
+    old_clear = guard_clear(q, px, py)
+    old_b = (move + BUFFER) * 2 + 10
+    t_ob, _ = casts(o, org, d, old_b)
+    bad = old_clear & ((t_full < old_b) != (t_ob < old_b))
+    bad |= old_clear & (t_full < old_b) & (t_ob < old_b) & (t_full != t_ob)
+    print(f"\n{n} casts: path guard clear {c.mean():.3f}, bounded hits compared {both.sum()}, "
+          f"single-cell guard clear {old_clear.mean():.3f} with {bad.sum()} differing bounded casts")
+    o.close()
+
+
+def test_bounded_ground_casts_equal_full_casts_where_cell_is_clear():
+    """castFirstNearD (vertical casts): where the cell of 2o is clear, a hit
+    found within the bound equals the full cast's t."""
+    rng = np.random.default_rng(12)
+    o, org = k_move_origins(20000, rng)
+    n = len(org)
+    d = np.tile(np.array([0, 0, -1], np.float32), (n, 1))
+    B = np.full(n, 2 * 50.0 + 10, np.float32)  # 2·top + 10 (stand)
+    q = quirk_grid()
+    clear = guard_clear(q, org[:, 0] + org[:, 0], org[:, 1] + org[:, 1])
+    t_full, n_full = casts(o, org, d)
+    t_b, n_b = casts(o, org, d, B)
+    sel = clear & (t_b < B)
+    assert sel.sum() > 1000, sel.sum()
+    assert np.array_equal(t_full[sel], t_b[sel])
+    assert np.array_equal(n_full[sel], n_b[sel])
+    assert ((t_full < B) == (t_b < B))[clear].all()
+    o.close()
+
+
+def test_path_guard_covers_quirk_hits_ahead_of_2o():
+    """Casts aimed so that the ray 2o + t·d passes a vertex at t in (r, r + 50):
+    the cell of 2o can be clear while the testVert quirk still fires before
+    the bound (the round-2 single-cell guard with its old bounds
+    takes bounded casts that differ from the full cast here).  The path guard
+    must never do so."""
+    rng = np.random.default_rng(3)
+    o = T.Oracle(1, 1)
+    _, verts, _ = T.scene_bvh()
+    verts = verts.reshape(-1, 3)
+    q = quirk_grid()
+    n = 150000
+    vi = rng.integers(0, len(verts), n)
+    ang = rng.uniform(0, 2 * np.pi, n)
+    d = np.stack([np.sin(ang), np.cos(ang), np.zeros(n)], 1).astype(np.float32)
+    P = verts[vi, :2] - d[:, :2] * (R + rng.uniform(2, 50, n))[:, None]
+    org = np.stack([P[:, 0] / 2, P[:, 1] / 2, rng.uniform(-150, 600, n)], 1).astype(np.float32)
+    move = rng.uniform(0, 20, n).astype(np.float32)
+    px, py = org[:, 0] + org[:, 0], org[:, 1] + org[:, 1]
+    t_full, _ = casts(o, org, d)
+
+    def differing(clear, B):
+        t_b, _ = casts(o, org, d, B)
+        nf, nb = t_full < B, t_b < B
+        return clear & ((nf != nb) | (nf & nb & (t_full != t_b)))
+
+    old_b = (move + BUFFER) * 2 + 10
+    old_bad = differing(guard_clear(q, px, py), old_b)
+    B = (move + BUFFER) + CAST_SLACK
+    clear = guard_path_clear(q, px, py, px + d[:, 0] * B, py + d[:, 1] * B)
+    new_bad = differing(clear, B)
+    print(f"\nsingle-cell guard: {old_bad.sum()} differing of {n}; path guard clear {clear.mean():.3f}, "
+          f"{new_bad.sum()} differing")
+    assert old_bad.sum() > 0  # the construction does reach the quirk
+    assert clear.sum() > n // 4 and new_bad.sum() == 0
+    o.close()

@@ -78,18 +78,7 @@ def test_two_rank_shards_equal_single_run(tmp_path):
         np.testing.assert_array_equal(got[f"arr_{k}"], full[k].numpy(), err_msg=name)
 
 
-# trainInterface outputs (mgr.cpp:2383-2431, csrc/manager.cpp TIEntry) ->
-# oracle export names; agent_map / unmasked_agent_map are not shipped.
-TRAIN_OUTPUTS = {
-    "fwd_lidar": "FWD_LIDAR", "rear_lidar": "REAR_LIDAR", "hp": "HP", "magazine": "MAGAZINE",
-    "alive": "ALIVE", "self": "SELF_OBSERVATION", "filters_state": "FILTERS_STATE",
-    "teammates": "TEAMMATE_OBSERVATIONS", "opponents": "OPPONENT_OBSERVATIONS",
-    "opponents_last_known": "OPPONENT_LAST_KNOWN_OBSERVATIONS", "self_pos": "SELF_POSITION",
-    "teammate_positions": "TEAMMATE_POSITIONS", "opponent_positions": "OPPONENT_POSITIONS",
-    "opponent_last_known_positions": "OPPONENT_LAST_KNOWN_POSITIONS", "opponent_masks": "OPPONENT_MASKS",
-    "reward_coefs": "REWARD_HYPER_PARAMS", "rewards": "REWARD", "dones": "DONE",
-    "pbt.episode_results": "MATCH_RESULT",
-}
+TRAIN_OUTPUTS = T.TRAIN_OUTPUTS
 LG_STEPS = 40
 
 
@@ -142,3 +131,94 @@ def test_learner_gather_ships_every_train_output_in_global_order(tmp_path):
             for n, e in TRAIN_OUTPUTS.items():
                 np.testing.assert_array_equal(got[f"{s}:{n}"], o.get(e), err_msg=f"{n} @ {s}")
     assert len(TRAIN_OUTPUTS) == 19  # 21 outputs minus the two never-written agent maps
+
+
+def _local_worker(rank, world_size, port, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from mpenv_dist import make_exchange
+
+        off, cnt = shard_worlds(TOTAL_WORLDS, rank, world_size)
+        N = 2 * TEAM
+        o = T.Oracle(cnt, TEAM, world_id_offset=off)
+        o.put_ctrl([0, 1, 1])
+        o.init()
+        src = {n: torch.from_numpy(o.view(e)) for n, e in TRAIN_OUTPUTS.items()}
+        ex = make_exchange("local", src, grad_bytes=4096, update_every=10)
+        ex.grad.fill_(float(rank + 1))
+        for s in range(LG_STEPS):
+            o.set_actions(T.mpenv_tape.tape_actions(1234, s, off * N, cnt * N))
+            o.step()
+            ex.submit()
+        ex.drain()
+        outs = ex.outputs()
+        np.savez(result_path + f".{rank}.npz", grad=ex.grad.numpy(), updates=ex.updates,
+                 bytes=ex.bytes_per_step()["sent_per_rank"],
+                 **{n: t[0].numpy().copy() for n, t in outs.items()})
+        ex.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_learner_local_exchange_keeps_shards_and_allreduces_gradients(tmp_path):
+    """LearnerLocal (the data-parallel learner layout, bench.py --exchange
+    local): each rank's outputs stay its own shard's (equal to the single
+    run's rows of those worlds), and every `update_every` steps one
+    all-reduce of the gradient-sized buffer runs (sum over ranks)."""
+    path = str(tmp_path / "loc")
+    mp.spawn(_local_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    o = T.Oracle(TOTAL_WORLDS, TEAM)
+    o.put_ctrl([0, 1, 1])
+    o.init()
+    A = TOTAL_WORLDS * 2 * TEAM
+    for s in range(LG_STEPS):
+        o.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, A))
+        o.step()
+    for rank in range(2):
+        got = np.load(path + f".{rank}.npz")
+        off, cnt = shard_worlds(TOTAL_WORLDS, rank, 2)
+        assert int(got["updates"]) == LG_STEPS // 10
+        # ranks start at 1 and 2: the first all-reduce gives 3, each later one doubles it
+        np.testing.assert_array_equal(got["grad"], np.full(1024, 3.0 * 2 ** (LG_STEPS // 10 - 1), np.float32))
+        assert float(got["bytes"]) == 2 * 1 * 4096 / 2 / 10
+        for n, e in TRAIN_OUTPUTS.items():
+            full = o.get(e)
+            rpw = full.shape[0] // TOTAL_WORLDS
+            np.testing.assert_array_equal(got[n], full[off * rpw:(off + cnt) * rpw], err_msg=n)
+
+
+def _uneven_worker(rank, world_size, port, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        off, cnt = shard_worlds(5, rank, world_size)  # 3 + 2 worlds
+        o = T.Oracle(cnt, TEAM, world_id_offset=off)
+        src = {n: torch.from_numpy(o.view(e)) for n, e in TRAIN_OUTPUTS.items()}
+        try:
+            LearnerGather(src, dst=0)
+            msg = "no error"
+        except ValueError as ex:
+            msg = str(ex)
+        open(result_path + f".{rank}", "w").write(msg)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_learner_gather_rejects_unequal_shards(tmp_path):
+    """An uneven split (5 worlds on 2 ranks) would make RCCL's gather truncate
+    or overrun silently: LearnerGather checks every rank's layout up front."""
+    path = str(tmp_path / "uneven")
+    mp.spawn(_uneven_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    for rank in range(2):
+        assert "different layout" in open(path + f".{rank}").read()
+
+
+def test_learner_gather_rejects_non_contiguous_sources():
+    """A strided source would be snapshotted by .contiguous(); LearnerGather
+    refuses it instead (the live engine buffer is what must ship)."""
+    t = torch.zeros(8, 4)[:, :2]
+    with pytest.raises(ValueError, match="contiguous"):
+        LearnerGather.__init__(object.__new__(LearnerGather), {"x": t})
