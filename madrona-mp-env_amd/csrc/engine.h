@@ -24,11 +24,16 @@ constexpr int kMaxAgents = 2 * kMaxTeamSize;
 constexpr int kMaxZones = 5;
 constexpr int kGridW = 81;
 constexpr int kGridCells = kGridW * kGridW;
-// ExploreTracker as a per-agent bitset over the 81 x 81 cells (6,561 bits,
-// padded to 208 words = 832 B so rows stay 16-B aligned): bit c = cell c
-// holds the agent's current episode index (exploreEp).  Exact for
-// exploreVisitedSystem (sim.cpp:3508-3536), see DESIGN.md §2.
-constexpr int kExploreWords = 208;
+// ExploreTracker as a per-agent bitset over the 81 x 81 cells: bit = the
+// cell holds the agent's current episode index (exploreEp).  Exact for
+// exploreVisitedSystem (sim.cpp:3508-3536), see DESIGN.md §2.  Cells are
+// grouped in 8 x 8 tiles, one u64 each (11 x 11 tiles, 968 B per agent);
+// the tile the agent stands in lives in SoA columns (exploreTile,
+// exploreLo / exploreHi), so consecutive steps inside one tile (240 x 240
+// units) touch only coalesced columns and the row is read / written once
+// per tile change.
+constexpr int kExploreTilesX = 11;
+constexpr int kExploreTiles = kExploreTilesX * kExploreTilesX;
 constexpr int kSelfObs = 43;
 constexpr int kOtherObs = 32;
 constexpr int kFwdRays = 64;   // 2 x 32
@@ -46,7 +51,7 @@ constexpr int kMaxBVHStack = 16; // register byte-stack capacity
 #define MP_AGENT_I32(X) \
     X(curPose) X(tgtPose) X(transRem) X(rngA) X(rngB) X(rngCtr) X(landedOn) \
     X(respawnSteps) X(autohealSteps) X(flags) X(wasShot) X(weapon) X(bcLast) \
-    X(bcSteps) X(newCells) X(exploreEp)
+    X(bcSteps) X(newCells) X(exploreEp) X(exploreTile) X(exploreLo) X(exploreHi)
 
 #define MP_WORLD_I32(X) \
     X(teamA) X(curStep) X(finished) X(curZone) X(controlling) X(contested) \
@@ -86,7 +91,8 @@ struct DevState {
 
     float *dmg;            // [6][A] DamageDealt
     uint8_t *visMask;      // [A] OpponentsVisibility, bit k = sees opponent k
-    uint32_t *exploreBits; // [A][kExploreWords] ExploreTracker bitset for episode exploreEp
+    uint64_t *exploreBits; // [A][kExploreTiles] ExploreTracker tiles for episode exploreEp
+                           // (the tile exploreTile is current in exploreLo / exploreHi)
     int32_t *filtLast;     // [W][2][3] FiltersMatchState::lastMatches (3 filters used)
     int32_t *zoneStats;    // [W][5][5]
     uint32_t *spawnTrack;  // [W][3][spawnTrackLen] SpawnUsageCounter

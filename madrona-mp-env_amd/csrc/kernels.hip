@@ -1895,6 +1895,11 @@ __device__ __forceinline__ void goalRegionsD(const DevState &S, const SceneDev &
 // for the agent's episode exploreEp, cleared when the episode moves on
 // (lazily, here).  Episode 0 starts from level_gen.cpp:166-171's tags: 0 on
 // cells outside the y<40, x<40 quadrant, i.e. already set (k_init_explore).
+// Bits live in 8 x 8-cell u64 tiles; the current tile is cached in SoA
+// columns and written back to the row when the agent leaves it.
+__device__ __forceinline__ int exploreBitD(int cx, int cy) { return (cy & 7) * 8 + (cx & 7); }
+__device__ __forceinline__ int exploreTileD(int cx, int cy) { return (cy >> 3) * kExploreTilesX + (cx >> 3); }
+
 __device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
 {
     Vec3 delta = ldPos(S, g) - v3(S.sx[g], S.sy[g], S.sz[g]);
@@ -1902,20 +1907,29 @@ __device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
     int32_t y = f2iSatD((delta.y + 0.5f) / (c::kAgentRadius * 2.f));
     int64_t cx = (int64_t)x + c::kGridMax, cy = (int64_t)y + c::kGridMax;
     if (cx < 0 || cx >= kGridW || cy < 0 || cy >= kGridW) return;
-    uint32_t *row = &S.exploreBits[g * kExploreWords];
+    uint64_t *row = &S.exploreBits[g * kExploreTiles];
     const int32_t cur = S.episode[w];
+    int32_t tile = S.exploreTile[g];
+    uint64_t word = (uint64_t)(uint32_t)S.exploreLo[g] | ((uint64_t)(uint32_t)S.exploreHi[g] << 32);
     if (S.exploreEp[g] != cur) {
-        uint4 *r4 = reinterpret_cast<uint4 *>(row);
-        for (int k = 0; k < kExploreWords / 4; k++) r4[k] = make_uint4(0u, 0u, 0u, 0u);
+        for (int k = 0; k < kExploreTiles; k++) row[k] = 0ull;
         S.exploreEp[g] = cur;
+        tile = -1;
     }
-    const int cell = (int)(cy * kGridW + cx);
-    const uint32_t bit = 1u << (cell & 31);
-    const uint32_t word = row[cell >> 5];
+    const int t = exploreTileD((int)cx, (int)cy);
+    if (t != tile) {
+        if (tile >= 0) row[tile] = word;
+        word = row[t];
+        tile = t;
+        S.exploreTile[g] = t;
+    }
+    const uint64_t bit = 1ull << exploreBitD((int)cx, (int)cy);
     if (!(word & bit)) {
-        row[cell >> 5] = word | bit;
+        word |= bit;
         if (length2(delta) > 2.f) S.newCells[g] += 1;
     }
+    S.exploreLo[g] = (int32_t)(uint32_t)word;
+    S.exploreHi[g] = (int32_t)(uint32_t)(word >> 32);
 }
 
 // sim.cpp:4089-4200 zoneCaptureDefendRewardSystem: goal-region progress,
@@ -2172,20 +2186,26 @@ __global__ void __launch_bounds__(64) k_construct(DevState S, SceneDev sc, int32
 
 // ExploreTracker initial contents (level_gen.cpp:166-171: 0xFFFFFFFF on the
 // y<40, x<40 quadrant; the other cells start at 0) as the
-// bitset of episode 0: the cells whose tag is 0 are set.
-__global__ void __launch_bounds__(256) k_init_explore(uint32_t *bits, int32_t *ep, int64_t total)
+// bitset of episode 0: the cells whose tag is 0 are set; no tile cached.
+__global__ void __launch_bounds__(256) k_init_explore(DevState S, int64_t total)
 {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
-        const int wd = (int)(k % kExploreWords);
-        uint32_t v = 0u;
-        for (int b = 0; b < 32; b++) {
-            const int cell = wd * 32 + b;
-            if (cell >= kGridCells) break;
-            const int y = cell / kGridW, x = cell - y * kGridW;
-            if (!(y < c::kGridMax && x < c::kGridMax)) v |= 1u << b;
+        const int t = (int)(k % kExploreTiles);
+        const int tx = t % kExploreTilesX, ty = t / kExploreTilesX;
+        uint64_t v = 0ull;
+        for (int b = 0; b < 64; b++) {
+            const int x = tx * 8 + (b & 7), y = ty * 8 + (b >> 3);
+            if (x >= kGridW || y >= kGridW) continue;
+            if (!(y < c::kGridMax && x < c::kGridMax)) v |= 1ull << b;
         }
-        bits[k] = v;
-        if (wd == 0) ep[k / kExploreWords] = 0;
+        S.exploreBits[k] = v;
+        if (t == 0) {
+            const int64_t g = k / kExploreTiles;
+            S.exploreEp[g] = 0;
+            S.exploreTile[g] = -1;
+            S.exploreLo[g] = 0;
+            S.exploreHi[g] = 0;
+        }
     }
 }
 
@@ -2811,6 +2831,9 @@ struct WaveStage {
     }
     template <int n, int P> __device__ __forceinline__ void flush(float *dst, int64_t off, bool zero = false) const
     {
+#ifdef MPENV_LAB_NO_DWORD_FLUSH
+        if (off != -12345) return; // lab: every dword-flushed row dropped (upper bound of their cost)
+#endif
         // which rows exist / are zeros: wave-wide bit masks (lane r = row r)
         const uint64_t wbits = __ballot(off >= 0), zbits = __ballot(zero);
         offs[lane] = off;
@@ -2955,9 +2978,6 @@ __device__ __forceinline__ void fullTeamSlotD(const DevState &S, const SceneDev 
 #ifndef MPENV_OBS_NOUNROLL
 #define MPENV_OBS_NOUNROLL 0
 #endif
-#ifndef MPENV_OBS_MASK_FLOAT
-#define MPENV_OBS_MASK_FLOAT 0
-#endif
 #ifdef MPENV_OBS_WPE
 #define MP_OBS_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_OBS_WPE)))
 #else
@@ -3099,11 +3119,9 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
                 oob[28] = (float)S.wasShot[gj];
                 oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
                 oob[30] = ((vm[g] >> k) & 1) ? 1.f : 0.f;
-#if MPENV_OBS_MASK_FLOAT
-                const bool knows = mask[k] == 1.f; // lab: the float form ("k_obs mask read")
-#else
-                const bool knows = (knowsBits >> k) & 1u; // teamKnowsLocation (sim.cpp:2995-3003)
-#endif
+                // teamKnowsLocation (sim.cpp:2995-3003) from the bits taken
+                // where the masks are computed ("k_obs mask read")
+                const bool knows = (knowsBits >> k) & 1u;
                 oob[31] = knows ? 1.f : 0.f;
                 lk_keep = knows;
                 lk_write = lk_write || knows;
@@ -3381,8 +3399,14 @@ __global__ void __launch_bounds__(256) k_debug(DevState S, float *af, int32_t *a
             // 1 = visited in the agent's current episode (the reference's
             // tag == curEpisodeIdx), 0 otherwise
             const bool cur = S.exploreEp[g] == S.episode[g / S.N];
-            for (int k = 0; k < kGridCells; k++)
-                explore[g * kGridCells + k] = cur ? (S.exploreBits[g * kExploreWords + (k >> 5)] >> (k & 31)) & 1u : 0u;
+            const int ct = S.exploreTile[g];
+            const uint64_t cw = (uint64_t)(uint32_t)S.exploreLo[g] | ((uint64_t)(uint32_t)S.exploreHi[g] << 32);
+            for (int k = 0; k < kGridCells; k++) {
+                const int cy = k / kGridW, cx = k - cy * kGridW;
+                const int t = exploreTileD(cx, cy);
+                const uint64_t word = t == ct ? cw : S.exploreBits[g * kExploreTiles + t];
+                explore[g * kGridCells + k] = cur ? (uint32_t)((word >> exploreBitD(cx, cy)) & 1ull) : 0u;
+            }
         }
     }
     if (t < S.W) {
@@ -3511,9 +3535,9 @@ size_t bvhLdsBytesOct(const SceneDev &sc)
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
-    const int64_t total = s.A * kExploreWords;
+    const int64_t total = s.A * kExploreTiles;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
-    hipLaunchKernelGGL(k_init_explore, dim3(blocks), dim3(256), 0, st, s.exploreBits, s.exploreEp, total);
+    hipLaunchKernelGGL(k_init_explore, dim3(blocks), dim3(256), 0, st, s, total);
     if (check(hipGetLastError())) return -1;
     hipLaunchKernelGGL(k_construct, dim3((s.W + 63) / 64), dim3(64), 0, st, s, sc, tc[0], tc[1], tc[2]);
     return check(hipGetLastError());

@@ -577,7 +577,7 @@ static void allocState(mpenv_manager &m)
     S.dmg = m.alloc<float>(A * kMaxTeamSize);
     S.dmgStride = (int64_t)A;
     S.visMask = m.alloc<uint8_t>(A);
-    S.exploreBits = m.alloc<uint32_t>(A * kExploreWords);
+    S.exploreBits = m.alloc<uint64_t>(A * kExploreTiles);
     S.filtLast = m.alloc<int32_t>(W * 6);
     S.zoneStats = m.alloc<int32_t>(W * 25);
     S.resetKeys = m.alloc<mp::RandKey>(A * 11);
@@ -680,7 +680,7 @@ static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_
 #undef MP_SL_W
     G.dmg = S.dmg + g0; // stride stays S.dmgStride
     G.visMask = S.visMask + g0;
-    G.exploreBits = S.exploreBits + g0 * kExploreWords;
+    G.exploreBits = S.exploreBits + g0 * kExploreTiles;
     G.filtLast = S.filtLast + w0 * 6;
     G.resetKeys = S.resetKeys + g0 * 11;
     G.zoneStats = S.zoneStats + w0 * 25;

@@ -355,6 +355,12 @@ bool rayTriangleIntersection(Vec3 ta, Vec3 tb, Vec3 tc, const RayTxfm &tx, Vec3 
 
 float expScale(int8_t e) { return u2f((uint32_t)((int32_t)e + 127) << 23); }
 
+// Slab rounding (analysis hook oracle_set_slab_fma): 1 = q * dirQuant +
+// originQuant fused (the definition the engine and the oracle share,
+// DESIGN.md §2 definition 13), 0 = multiply then add, each rounded.
+int g_slabFma = 1;
+inline float slabT(float q, float dq, float oq) { return g_slabFma ? fma_(q, dq, oq) : q * dq + oq; }
+
 // mesh_bvh.inl:110-208 (MeshBVH::traceRay) + 360-431 (traceRayLeaf)
 bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_max = kFltMax, bool octant = false)
 {
@@ -387,12 +393,12 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
             if (node.children[i] == -1) continue;
             // q * dirQuant + originQuant, fused: the reference's GPU build is
             // compiled with NVRTC's default --fmad=true, which contracts it
-            float t_near_x = fma_((float)node.qMinX[i], dirQuantX, originQuantX);
-            float t_near_y = fma_((float)node.qMinY[i], dirQuantY, originQuantY);
-            float t_near_z = fma_((float)node.qMinZ[i], dirQuantZ, originQuantZ);
-            float t_far_x = fma_((float)node.qMaxX[i], dirQuantX, originQuantX);
-            float t_far_y = fma_((float)node.qMaxY[i], dirQuantY, originQuantY);
-            float t_far_z = fma_((float)node.qMaxZ[i], dirQuantZ, originQuantZ);
+            float t_near_x = slabT((float)node.qMinX[i], dirQuantX, originQuantX);
+            float t_near_y = slabT((float)node.qMinY[i], dirQuantY, originQuantY);
+            float t_near_z = slabT((float)node.qMinZ[i], dirQuantZ, originQuantZ);
+            float t_far_x = slabT((float)node.qMaxX[i], dirQuantX, originQuantX);
+            float t_far_y = slabT((float)node.qMaxY[i], dirQuantY, originQuantY);
+            float t_far_z = slabT((float)node.qMaxZ[i], dirQuantZ, originQuantZ);
             float t_near = fmax_(fmin_(t_near_x, t_far_x),
                                  fmax_(fmin_(t_near_y, t_far_y), fmax_(fmin_(t_near_z, t_far_z), 0.f)));
             float t_far = fmin_(fmax_(t_far_x, t_near_x),
@@ -3524,6 +3530,20 @@ float oracle_sphere_cast(void *h, const float *org, const float *d, float r, flo
     float t = bvhSphereCast(o, v3(org[0], org[1], org[2]), v3(d[0], d[1], d[2]), r, &n);
     n_out[0] = n.x; n_out[1] = n.y; n_out[2] = n.z;
     return t;
+}
+
+void oracle_set_slab_fma(int32_t on) { g_slabFma = on ? 1 : 0; }
+
+void oracle_trace_ray_batch(void *h, int32_t n, const float *org, const float *d, int32_t octant, float *t_out,
+                            int32_t *hit_out)
+{
+    Oracle &o = *static_cast<Oracle *>(h);
+    for (int32_t k = 0; k < n; k++) {
+        float t = 0.f;
+        hit_out[k] = bvhTraceRay(o, v3(org[3 * k], org[3 * k + 1], org[3 * k + 2]),
+                                 v3(d[3 * k], d[3 * k + 1], d[3 * k + 2]), &t, kFltMax, octant != 0) ? 1 : 0;
+        t_out[k] = t;
+    }
 }
 
 void oracle_sphere_cast_batch(void *h, int32_t n, const float *org, const float *d, float r,

@@ -83,6 +83,13 @@ void oracle_cast_stats(int32_t leaf_read_two, uint64_t *out2);
 int oracle_trace_ray(void *h, const float *o, const float *d, float *t_out);
 float oracle_sphere_cast(void *h, const float *o, const float *d, float r,
                          float *normal_out);
+/* Analysis hook (DESIGN.md §2 definition 13): ray-slab products fused (1,
+ * the shared definition) or multiplied then added (0). Process-wide. */
+void oracle_set_slab_fma(int32_t on);
+/* n closest-hit queries (MeshBVH::traceRay, slot order or octant order):
+ * o, d [n][3]; t_out, hit_out [n]. */
+void oracle_trace_ray_batch(void *h, int32_t n, const float *o, const float *d, int32_t octant, float *t_out,
+                            int32_t *hit_out);
 /* n casts of MeshBVH::sphereCast with its t_max argument (mesh_bvh.inl:743-747;
  * t_max null = FLT_MAX): o, d, n_out [n][3]; normals are (0,0,0) on a miss. */
 void oracle_sphere_cast_batch(void *h, int32_t n, const float *o, const float *d, float r,

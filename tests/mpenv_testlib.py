@@ -168,6 +168,8 @@ def lib_oracle():
         lib.oracle_trace_ray_brute.argtypes = [C.c_void_p, fp, fp, fp]
         lib.oracle_sphere_cast.argtypes = [C.c_void_p, fp, fp, C.c_float, fp]
         lib.oracle_sphere_cast.restype = C.c_float
+        lib.oracle_set_slab_fma.argtypes = [C.c_int32]
+        lib.oracle_trace_ray_batch.argtypes = [C.c_void_p, C.c_int32, fp, fp, C.c_int32, fp, C.c_void_p]
         lib.oracle_sphere_cast_batch.argtypes = [C.c_void_p, C.c_int32, fp, fp, C.c_float, fp, fp, fp]
         lib.oracle_sphere_cast_brute.argtypes = [C.c_void_p, fp, fp, C.c_float]
         lib.oracle_sphere_cast_brute.restype = C.c_float
@@ -588,3 +590,19 @@ def seek_combat_actions(sim, step, seed=1234, base=None):
     acts[no & ~face, 0] = 0
     acts[(so[:, 24] == 0) & (so[:, 25] == 0), 2] = 2
     return acts
+
+
+def edge_aimed_rays(verts, n_origins, seed):
+    """Rays aimed exactly at every triangle vertex and edge midpoint (shared
+    edges/vertices are where two triangles tie) from random origins."""
+    rng = np.random.default_rng(seed)
+    tris = verts.reshape(-1, 3, 3).astype(np.float64)
+    targets = np.concatenate([tris.reshape(-1, 3),
+                              0.5 * (tris[:, 0] + tris[:, 1]), 0.5 * (tris[:, 1] + tris[:, 2]),
+                              0.5 * (tris[:, 2] + tris[:, 0])])
+    o = rng.uniform([-1500, -1500, -50], [1500, 1500, 300], (n_origins, 3))
+    oo = np.repeat(o, len(targets), axis=0)
+    tt = np.tile(targets, (n_origins, 1))
+    d = tt - oo
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return oo.astype(np.float32), d.astype(np.float32)

@@ -117,7 +117,7 @@ def test_device_combat_actions_match_numpy_and_drive_combat():
     dev_ring = e.mem.upload(ring)
     out = e.mem.upload(np.zeros((A, 6), np.int32))
     got = np.empty((A, 6), np.int32)
-    deaths, prev_alive = 0, o.get("ALIVE")
+    e.enable_stats(True)  # kill counter (a killed agent respawns within its step)
     for s in range(steps):
         mode = 0 if s < 40 else 1
         fn = T.combat_actions if mode == 0 else T.seek_combat_actions
@@ -130,9 +130,6 @@ def test_device_combat_actions_match_numpy_and_drive_combat():
         o.set_actions(acts)
         e.step()
         o.step()
-        alive = o.get("ALIVE")
-        deaths += int(((prev_alive == 1) & (alive == 0)).sum())
-        prev_alive = alive
         if s % 10 == 0 or s == steps - 1:
             _compare_all(e, o, f"step {s}")
         else:
@@ -140,8 +137,10 @@ def test_device_combat_actions_match_numpy_and_drive_combat():
                 T.compare(e.get(n), o.get(n), f"{n} @ step {s}")
     e.mem.free(dev_ring)
     e.mem.free(out)
-    print(f"\n{W} worlds {ts}v{ts}, {steps} steps of device combat actions: {deaths} deaths")
-    assert deaths > 0
+    st = e.read_stats()
+    print(f"\n{W} worlds {ts}v{ts}, {steps} steps of device combat actions: {st['kills']} kills, "
+          f"{st['hit_agents']} agent-steps hit")
+    assert st["kills"] > 0 and st["hit_agents"] > st["kills"]
     e.close()
     o.close()
 
@@ -402,8 +401,8 @@ def test_full_batch_long_horizon_matches_oracle(ts, W, steps, probes):
           f"{batch['kills']} kills, {batch['hit_agents']} agent-steps hit, {batch['los_seen']} LOS rays seen")
     # every zone/match event fired in the probed worlds, and combat throughout
     assert ev["rotations"] > 0 and ev["points"] > 0 and ev["wins"] > 0, ev
-    assert ev["kills"] > 0, ev
-    assert batch["kills"] >= 1000 * W // 4096, batch
+    assert ev["kills"] >= 20, ev
+    assert batch["kills"] >= W, batch  # more kills than worlds over the horizon
     assert ev["episode_ends"] >= len(probes) * PW, ev  # every world passed a 3,000-step end or a win
     # size-independent properties over the whole batch
     hp = e.get("HP")
@@ -531,20 +530,7 @@ def test_gpu_stream_step_buffers_abi():
                 np.testing.assert_array_equal(b.cpu().numpy(), o.get(ename), err_msg=f"{nm} @ {s}")
 
 
-def _edge_aimed_rays(verts, n_origins, seed):
-    """Rays aimed exactly at every triangle vertex and edge midpoint (shared
-    edges/vertices are where two triangles tie) from random origins."""
-    rng = np.random.default_rng(seed)
-    tris = verts.reshape(-1, 3, 3).astype(np.float64)
-    targets = np.concatenate([tris.reshape(-1, 3),
-                              0.5 * (tris[:, 0] + tris[:, 1]), 0.5 * (tris[:, 1] + tris[:, 2]),
-                              0.5 * (tris[:, 2] + tris[:, 0])])
-    o = rng.uniform([-1500, -1500, -50], [1500, 1500, 300], (n_origins, 3))
-    oo = np.repeat(o, len(targets), axis=0)
-    tt = np.tile(targets, (n_origins, 1))
-    d = tt - oo
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    return oo.astype(np.float32), d.astype(np.float32)
+_edge_aimed_rays = T.edge_aimed_rays
 
 
 def test_bvh_traversal_matches_oracle_on_edge_cases():

@@ -170,6 +170,98 @@ static void trace(const float *o, const float *d, int mode, Stats &st)
     }
 }
 
+// While-while traversal with postponed triangles (Aila & Laine 2009), one
+// wave of up to 64 lanes in lockstep.  Each lane keeps its octant-order
+// stack and a FIFO of discovered-but-untested triangles.  Node phase: every
+// lane with stack entries and fewer than `cap` pending triangles pops one
+// node per lockstep iteration (boxes tested with its current t_max; leaf
+// children's triangles queued in slot order); the phase ends when fewer
+// than `need` lanes still pop.  Triangle phase: every lane tests its queued
+// triangles, one per lockstep iteration (t_max updated).  Closest-hit
+// results are order-independent under the min-over-candidates definition,
+// so only the work differs.  Returns lockstep (node iterations, triangle
+// iterations, phases) summed over the wave, and the per-lane totals.
+struct WW {
+    double nodeIters = 0, triIters = 0, phases = 0, pops = 0, tris = 0;
+};
+
+static void traceWaveWW(const float *rays, size_t r0, size_t n, int cap, int need, WW &out)
+{
+    struct Lane {
+        std::vector<int> stack;
+        std::vector<int> pending;
+        float o[3], d[3], inv[3], tmax;
+        int oct;
+    };
+    std::vector<Lane> L(n);
+    for (size_t k = 0; k < n; k++) {
+        Lane &l = L[k];
+        for (int j = 0; j < 3; j++) {
+            l.o[j] = rays[6 * (r0 + k) + j];
+            l.d[j] = rays[6 * (r0 + k) + 3 + j];
+            l.inv[j] = l.d[j] == 0 ? 1e7f : 1.f / l.d[j];
+        }
+        l.tmax = 3.4e38f;
+        l.oct = (l.d[0] < 0 ? 1 : 0) | (l.d[1] < 0 ? 2 : 0) | (l.d[2] < 0 ? 4 : 0);
+        l.stack = { 0 };
+    }
+    auto popNode = [&](Lane &l) {
+        int ni = l.stack.back();
+        l.stack.pop_back();
+        out.pops++;
+        const Node &nd = nodes[ni];
+        int kids[4], nk = 0;
+        for (int ii = 0; ii < 4; ii++) {
+            const int i = octOrder[ni][l.oct][ii];
+            if (nd.children[i] == -1) continue;
+            float sx = std::ldexp(1.f, nd.expX), sy = std::ldexp(1.f, nd.expY), sz = std::ldexp(1.f, nd.expZ);
+            float lo[3] = { nd.minX + sx * nd.qMinX[i], nd.minY + sy * nd.qMinY[i], nd.minZ + sz * nd.qMinZ[i] };
+            float hi[3] = { nd.minX + sx * nd.qMaxX[i], nd.minY + sy * nd.qMaxY[i], nd.minZ + sz * nd.qMaxZ[i] };
+            float tn = 0, tf = l.tmax;
+            for (int k = 0; k < 3; k++) {
+                float a = (lo[k] - l.o[k]) * l.inv[k], b = (hi[k] - l.o[k]) * l.inv[k];
+                tn = std::max(tn, std::min(a, b));
+                tf = std::min(tf, std::max(a, b));
+            }
+            if (tn > tf) continue;
+            if (nd.children[i] & 0x80000000) {
+                int leaf = nd.children[i] & 0x7fffffff;
+                for (int k = 0; k < nd.triSize[i]; k++) l.pending.push_back(leaf + k);
+            } else {
+                kids[nk++] = nd.children[i];
+            }
+        }
+        for (int k = nk - 1; k >= 0; k--) l.stack.push_back(kids[k]);
+    };
+    for (;;) {
+        bool any = false;
+        for (auto &l : L) any = any || !l.stack.empty() || !l.pending.empty();
+        if (!any) break;
+        out.phases++;
+        for (;;) {
+            int popping = 0;
+            for (auto &l : L)
+                if (!l.stack.empty() && (int)l.pending.size() < cap) popping++;
+            if (popping == 0) break;
+            out.nodeIters++;
+            for (auto &l : L)
+                if (!l.stack.empty() && (int)l.pending.size() < cap) popNode(l);
+            if (popping < need) break;
+        }
+        size_t mx = 0;
+        for (auto &l : L) mx = std::max(mx, l.pending.size());
+        out.triIters += mx;
+        for (auto &l : L) {
+            for (int t : l.pending) {
+                out.tris++;
+                float th;
+                if (tri(&verts[t * 9], l.o, l.d, l.tmax, th)) l.tmax = th;
+            }
+            l.pending.clear();
+        }
+    }
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3) {
@@ -242,6 +334,17 @@ int main(int argc, char **argv)
         printf("%s: rays %zu  pops/ray %.2f  boxes/ray %.2f  tris/ray %.2f  maxStack %.0f | wave-max pops/ray %.2f tris %.2f\n",
                ftb == 1 ? "front-to-back" : ftb == 2 ? "octant order " : ftb == 3 ? "octant rev 1L" : "reference    ", n, st.pops / n, st.boxes / n, st.tris / n, st.maxStack,
                wave_pops / n, wave_tris / n);
+    }
+    // while-while with postponed triangles, octant order
+    const int caps[] = { 1, 2, 3, 4, 8 };
+    for (int cap : caps) {
+        for (int need : { 64, 48, 32, 16, 1 }) {
+            WW ww;
+            for (size_t w0 = 0; w0 < n; w0 += 64) traceWaveWW(rays.data(), w0, std::min<size_t>(64, n - w0), cap, need, ww);
+            printf("while-while cap %d need %2d: lockstep node iters/ray %.2f, tri iters/ray %.2f, phases/wave %.2f | "
+                   "pops/ray %.2f tris/ray %.2f\n", cap, need, ww.nodeIters * 64 / n, ww.triIters * 64 / n,
+                   ww.phases * 64 / n, ww.pops / n, ww.tris / n);
+        }
     }
     return 0;
 }
