@@ -45,7 +45,17 @@ __device__ __forceinline__ void statAdd(unsigned long long *p, uint32_t v)
 __device__ __forceinline__ float expScaleD(int e) { return mp::u2f((uint32_t)(e + 127) << 23); }
 
 constexpr float kSphereR = 15.f;  // consts::agentRadius: the radius of every k_move sphere cast
-constexpr int kSNodeFloats = 32;  // sphere-cast node image: loR[3][4], hiR[3][4], children[4], leaf tri count[4]
+// Sphere-cast node image: loR[3][4], hiR[3][4], children[4], leaf tri
+// count[4] (32 floats) at a stride of kSNodeFloats.  The casts read it with
+// ds_read_b32 (bank = dword address mod 32): at a stride of 32 the same field
+// of every node sits in one bank, so lanes at different nodes conflict (PMC:
+// 44% of k_move's LDS cycles are conflict cycles); an odd stride puts node
+// k's field in bank (k + field) mod 32, but k_move does not get faster (it
+// waits on its cast chain, not on LDS).
+#ifndef MPENV_SNODE_STRIDE
+#define MPENV_SNODE_STRIDE 32 // 33: no measurable change (k_move 0.2182 vs 0.2181 ms, r03e lab)
+#endif
+constexpr int kSNodeFloats = MPENV_SNODE_STRIDE;
 
 // Byte stack: push shifts left by 8 across a 128-bit register pair.
 struct ByteStack {
@@ -145,14 +155,24 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
 }
 
 // k_lidar's LDS image: the 8 octant node images (scene.h octantNodeImages,
-// 8 x numNodes x 64 B) then the vertices as float4.  The traversal of a ray
-// reads image (d.x < 0) | (d.y < 0) << 1 | (d.z < 0) << 2.
+// 8 x numNodes nodes) then the vertices as float4.  The traversal of a ray
+// reads image (d.x < 0) | (d.y < 0) << 1 | (d.z < 0) << 2.  Each node takes
+// kOctNodeQ 16-B slots: 4 = packed 64-B nodes; 5 = one pad slot, so the
+// slots of nodes k and k' sit in different LDS bank groups whenever
+// k != k' (mod 16) (with 64-B nodes only k mod 4 decides the bank group of a
+// ds_read_b128, and divergent lanes reading distinct nodes conflict).
+#ifndef MPENV_OCT_NODE_Q
+#define MPENV_OCT_NODE_Q 4
+#endif
+constexpr int kOctNodeQ = MPENV_OCT_NODE_Q;
+
 __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
 {
-    const int node_q = sc.numNodes * 4 * 8;
+    const int node_q = sc.numNodes * kOctNodeQ * 8;
     const uint4 *src_n = reinterpret_cast<const uint4 *>(sc.octNodes);
     uint4 *dst_n = reinterpret_cast<uint4 *>(smem);
-    for (int k = threadIdx.x; k < node_q; k += blockDim.x) dst_n[k] = src_n[k];
+    for (int k = threadIdx.x; k < sc.numNodes * 4 * 8; k += blockDim.x)
+        dst_n[(k >> 2) * kOctNodeQ + (k & 3)] = src_n[k];
     const float *src_v = sc.verts;
     float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
     for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
@@ -197,9 +217,10 @@ struct NodeR {
 
 __device__ __forceinline__ float qb(uint32_t w, int i) { return (float)((w >> (8 * i)) & 0xffu); }
 
+template <int kNodeQ = 4>
 __device__ __forceinline__ NodeR loadNode(const LBVH &b, uint32_t idx)
 {
-    const MP_LDS lu4 *p = reinterpret_cast<const MP_LDS lu4 *>(b.nodes + idx);
+    const MP_LDS lu4 *p = reinterpret_cast<const MP_LDS lu4 *>(b.nodes) + idx * kNodeQ;
     const lu4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
     NodeR n;
     n.minX = __uint_as_float(q0.x);
@@ -392,7 +413,7 @@ __device__ __forceinline__ bool rayTriPermD(const LBVH &b, int tri, const RayTxf
 // kExit: stop as soon as a hit at t <= exit_at is found (t_out is then
 // that hit, not necessarily the closest; callers that only compare the
 // closest hit with exit_at get the same answer).
-template <bool kExit, bool kPerm = false>
+template <bool kExit, bool kPerm = false, int kNodeQ = 4>
 __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
                                              float t_max0, float exit_at)
 {
@@ -423,7 +444,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
     bsPush(st, 0);
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
-        const NodeR node = loadNode(b, node_idx);
+        const NodeR node = loadNode<kNodeQ>(b, node_idx);
         const float dirQuantX = expScaleD(node.expX) * rayXInv;
         const float dirQuantY = expScaleD(node.expY) * rayYInv;
         const float dirQuantZ = expScaleD(node.expZ) * rayZInv;
@@ -744,7 +765,7 @@ __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, cons
                                               const float *__restrict__ pz, int64_t g0, int N, mp::Vec3 org,
                                               mp::Vec3 d, int self, bool hit, float min_t, uint32_t capMask = ~0u);
 
-template <bool kPerm = false>
+template <bool kPerm = false, int kNodeQ = 4>
 __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__restrict__ px,
                                                 const float *__restrict__ py, const float *__restrict__ pz,
                                                 int64_t g0, int N, mp::Vec3 org, mp::Vec3 d, int self = -1,
@@ -757,7 +778,7 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     bool hit = false;
     tb = 0.f;
 #else
-    bool hit = bvhTraceRayT<false, kPerm>(b, org, d, tb, mp::kFltMax, 0.f);
+    bool hit = bvhTraceRayT<false, kPerm, kNodeQ>(b, org, d, tb, mp::kFltMax, 0.f);
 #endif
     if (hit) min_t = tb;
 #ifdef MPENV_LAB_NO_CAPSULE

@@ -2761,6 +2761,8 @@ __device__ __forceinline__ Vec3 normalizedPosUnclampedD(const SceneDev &sc, Vec3
 // put a 16-byte piece into each of 64 rows (64 partial lines for the L2 to
 // merge); transposed per wave, each instruction writes 8 whole rows.
 constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
+constexpr int kObsSpanPad = 44;            // rowBuf floats per lane: >= kObsRowPad and the 43-float self obs
+constexpr int kPosPad = 19;                // posBuf floats per lane: 6 slots x 3, odd stride
 
 // Observation stores: plain, or nontemporal (MPENV_OBS_NT=1: the streamed
 // outputs, ~1.2 GB per C3 step, bypass the L2's normal allocation).
@@ -2874,6 +2876,38 @@ struct WaveStage {
         }
         waveSync();
     }
+    // A contiguous span: every live lane's row of n floats, rows back to
+    // back from dst (the row of lane r at dst + r * n -- per-agent exports
+    // whose rows the wave's agents fill completely), staged at stride P.
+    // Written as float4 (a quarter of the dword flush's store instructions;
+    // each float4 gathers its 4 floats from up to two staged rows), dwords
+    // when dst is not 16-B aligned (a world group starting off a 4-agent
+    // boundary).
+    template <int n, int P> __device__ __forceinline__ void flushSpan(float *dst) const
+    {
+        waveSync();
+        const int total = m * n;
+        auto val = [&](int f) {
+            const int r = f / n;
+            return buf[r * P + (f - r * n)];
+        };
+        if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+            const int q4 = total >> 2;
+            for (int j = lane; j < q4; j += 64)
+                obsStore(reinterpret_cast<float4 *>(dst) + j,
+                         make_float4(val(4 * j), val(4 * j + 1), val(4 * j + 2), val(4 * j + 3)));
+            if (lane < (total & 3)) obsStore(dst + 4 * q4 + lane, val(4 * q4 + lane));
+        } else {
+            for (int f = lane; f < total; f += 64) obsStore(dst + f, val(f));
+        }
+        waveSync(); // reads done before the next rows land
+    }
+    template <int n> __device__ __forceinline__ void putSpan(float *dst, const float *vals) const
+    {
+        constexpr int P = n | 1;
+        stage<P>(vals, n);
+        flushSpan<n, P>(dst);
+    }
     template <int n> __device__ __forceinline__ void put(float *dst, int64_t off, const float *vals) const
     {
         constexpr int P = n | 1;
@@ -2985,7 +3019,10 @@ __device__ __forceinline__ void fullTeamSlotD(const DevState &S, const SceneDev 
 #endif
 __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev sc)
 {
-    __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsRowPad];
+    // per wave: observation rows (stride kObsRowPad) or a whole self-obs
+    // span (stride 43); position rows of the slot loops (stride kPosPad)
+    __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsSpanPad];
+    __shared__ float posBuf[kBlock / 64][64 * kPosPad];
     __shared__ int64_t offBuf[kBlock / 64][64];
     const int64_t g = (int64_t)xcdBlockId() * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
@@ -3020,7 +3057,7 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
         if (can_see) mask[k] = 1.f;
         if (S.firedT[go] >= 0) mask[k] = 1.f;
     }
-    ws.put<6>(S.masks, g * 6, mask);
+    ws.putSpan<6>(S.masks + gw0 * 6, mask);
     // teamKnowsLocation (mask[k] == 1) as bits for the opponent loop.
     // Reading the float array there instead gives wrong last-known updates
     // on the 2v2_navmesh_curriculum golden case at init (agents 4, 6, 9
@@ -3070,10 +3107,14 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
         zo[14] = cz == 2 ? 1.f : 0.f;
         zo[15] = cz == 3 ? 1.f : 0.f;
     }
-    static_assert(kSelfObs == 43, "self obs split");
-    ws.put<22>(S.selfObs, g * kSelfObs, ob);
-    ws.put<21>(S.selfObs, g * kSelfObs + 22, ob + 22);
-    ws.put<3>(S.selfPos, g * 3, pos3);
+    static_assert(kSelfObs == 43 && (kSelfObs | 1) <= kObsSpanPad, "self obs span");
+    ws.putSpan<kSelfObs>(S.selfObs + gw0 * kSelfObs, ob);
+    ws.putSpan<3>(S.selfPos + gw0 * 3, pos3);
+    // slot positions are staged per slot into posBuf and leave as one span
+    // per export after the slot loop
+    float *prow = posBuf[threadIdx.x >> 6] + lane * kPosPad;
+    WaveStage wp = ws;
+    wp.buf = posBuf[threadIdx.x >> 6];
 
     // teammate / opponent rows are built in place in the lane's LDS row
     float *row = wbuf + lane * kObsRowPad;
@@ -3094,8 +3135,9 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
             }
         }
         flushRowsWave(S.tmObs, 5, k, gw0, S.A, wbuf, lane);
-        ws.put<3>(S.tmPos, (g * 5 + k) * 3, tpos);
+        for (int q = 0; q < 3; q++) prow[3 * k + q] = tpos[q];
     }
+    wp.flushSpan<15, kPosPad>(S.tmPos + gw0 * 15);
 
     // opponents (+ last known)
 #if MPENV_OBS_NOUNROLL
@@ -3130,13 +3172,14 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
         flushRowsWave(S.oppObs, 6, k, gw0, S.A, wbuf, lane);
         // the rows are still staged (stride kObsRowPad): the last-known copy
         ws.flush4<kOtherObs / 4, kObsRowPad>(S.lkObs, lk_write ? (g * 6 + k) * kOtherObs : -1, !lk_keep);
-        ws.put<3>(S.oppPos, (g * 6 + k) * 3, opos);
+        for (int q = 0; q < 3; q++) prow[3 * k + q] = opos[q];
         {
             float lpos[3];
             for (int q = 0; q < 3; q++) lpos[q] = lk_keep ? opos[q] : -1000.f;
             ws.put<3>(S.lkPos, lk_write ? (g * 6 + k) * 3 : -1, lpos);
         }
     }
+    wp.flushSpan<18, kPosPad>(S.oppPos + gw0 * 18);
 
 #ifndef MPENV_LAB_OBS_NO_FT
     fullTeamSlotD(S, sc, w, g, team, off, ws);
@@ -3220,9 +3263,6 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         const bool valid = g_raw < A;
         const uint32_t g = valid ? g_raw : A - 1u;
         const uint32_t kk = fwd ? lane : (lane & 15u); // ray slot within the forward / rear fan
-        const uint32_t w = __umulhi(g, S.nMagic); // g / N (engine.h)
-        const uint32_t i = g - w * N;
-        const int64_t g0 = (int64_t)w * N;
         const uint32_t h = fwd ? (kk >> 5) : (kk >> 3), x = fwd ? (kk & 31u) : (kk & 7u);
         const Quat q = fwd ? ldAimRot(S, g) : ldRot(S, g);
         const Vec3 dir_fwd = rotateVec(q, kFwd);
@@ -3235,7 +3275,8 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // the ray's octant image: same nodes and leaves, near-first slot
         // order (scene.h octantNodeImages); the oracle visits the same order
         LBVH ob = bvh;
-        ob.nodes = bvh.nodes + rayOctant(dir) * sc.numNodes;
+        ob.nodes = reinterpret_cast<const MP_LDS BVHNode *>(reinterpret_cast<const MP_LDS uint4 *>(bvh.nodes) +
+                                                             rayOctant(dir) * sc.numNodes * kOctNodeQ);
 #ifndef MPENV_LIDAR_PERM
 #define MPENV_LIDAR_PERM 0
 #endif
@@ -3257,8 +3298,15 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             // once; the per-ray loop reads the survivors' bases from those
             // lanes (readlane) in ascending j, so ties resolve as before.
             float tb;
-            const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0>(ob, ray_o, dir, tb, kFltMax, 0.f);
+            const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ>(ob, ray_o, dir, tb, kFltMax, 0.f);
             float min_t = bhit ? tb : kFltMax;
+            // world / agent indices formed after the traversal, from an
+            // opaque copy of g (nothing but the ray lives across it)
+            uint32_t go = g;
+            asm volatile("" : "+v"(go));
+            const uint32_t w = __umulhi(go, S.nMagic); // g / N (engine.h)
+            const uint32_t i = go - w * N;
+            const int64_t g0 = (int64_t)w * N;
             float mx = min_t;
 #pragma unroll
             for (int sh = 32; sh >= 1; sh >>= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
@@ -3300,9 +3348,19 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             hw.t = min_t;
             hw.entity = ent;
         } else {
-            hw = traceWorldD<MPENV_LIDAR_PERM != 0>(ob, S.px, S.py, S.pz, g0, (int)N, ray_o, dir, (int)i);
+            float tb;
+            const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ>(ob, ray_o, dir, tb, kFltMax, 0.f);
+            uint32_t go = g;
+            asm volatile("" : "+v"(go));
+            const uint32_t w = __umulhi(go, S.nMagic);
+            const uint32_t i = go - w * N;
+            hw = capsulesD(S.px, S.py, S.pz, (int64_t)w * N, (int)N, ray_o, dir, (int)i, bhit, bhit ? tb : kFltMax);
         }
         if (!valid) continue;
+        uint32_t go = g;
+        asm volatile("" : "+v"(go));
+        const uint32_t w = __umulhi(go, S.nMagic);
+        const uint32_t i = go - w * N;
         const bool second = i >= T; // team of the casting agent
         float4 out;
         if (hw.hit) {
@@ -3529,7 +3587,7 @@ size_t bvhLdsBytesSphere(const SceneDev &sc)
 
 size_t bvhLdsBytesOct(const SceneDev &sc)
 {
-    return (size_t)sc.numNodes * 64 * 8 + (size_t)sc.numVerts * 16;
+    return (size_t)sc.numNodes * 16 * kOctNodeQ * 8 + (size_t)sc.numVerts * 16;
 }
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
