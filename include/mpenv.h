@@ -382,7 +382,7 @@ int mpenv_debug_trace_rays(mpenv_manager *mgr, const float *o_device, const floa
 
 /* Extension: step the worlds as `groups` contiguous ranges on concurrent
  * HIP streams (fork/join on the step stream; results identical for any
- * split).  Default: 3 for >= 3072 worlds, else 1; env MPENV_WORLD_GROUPS
+ * split).  Default: 2 for >= 3072 worlds, else 1; env MPENV_WORLD_GROUPS
  * overrides at creation.  Capped at 3. */
 int mpenv_set_world_groups(mpenv_manager *mgr, int32_t groups);
 int mpenv_world_groups(mpenv_manager *mgr, int32_t *groups);

@@ -2891,14 +2891,15 @@ struct WaveStage {
             const int r = f / n;
             return buf[r * P + (f - r * n)];
         };
+        // only the m live lanes run (a tail wave's others have returned)
         if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
             const int q4 = total >> 2;
-            for (int j = lane; j < q4; j += 64)
+            for (int j = lane; j < q4; j += m)
                 obsStore(reinterpret_cast<float4 *>(dst) + j,
                          make_float4(val(4 * j), val(4 * j + 1), val(4 * j + 2), val(4 * j + 3)));
             if (lane < (total & 3)) obsStore(dst + 4 * q4 + lane, val(4 * q4 + lane));
         } else {
-            for (int f = lane; f < total; f += 64) obsStore(dst + f, val(f));
+            for (int f = lane; f < total; f += m) obsStore(dst + f, val(f));
         }
         waveSync(); // reads done before the next rows land
     }
