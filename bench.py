@@ -44,7 +44,8 @@ TAPE_SEED = 1234
 #            quat, pose x3, maxVel, aim velocities) x 4 B r+w (160)  = 184
 #   k_sim  : 20 combat/bookkeeping columns r+w (160); pos/rot/alive r (32);
 #            DamageDealt 6 x 4 r+w (48); hp/magazine r+w (24); reward+done
-#            w (8); 1 explore cell r+w (8); rewardCoefs r (4)      = 284
+#            w (8); explore tile cache (tile, 64-bit word) r+w (24);
+#            rewardCoefs r (4)                                      = 300
 #   k_vis  : pos 12 + aim rot 16 + pose 4 + alive 4 r; mask w 1   = 37
 #   k_obs  : state r ~124; self 172 + teammates 640 + opponents 768 +
 #            last-known 768 w, last-known 768 r; positions 12+60+72 w,
@@ -54,7 +55,7 @@ TAPE_SEED = 1234
 #            previous rays 80 x 16 B r + full-team copy 80 x 16 B w = 3888
 # plus per world-step: 32 singleton columns x 4 B r+w (256) and full-team
 # reward/done 16 w in k_sim; full-team global 2 x 64 w in k_obs.
-KERNEL_BYTES_PER_AGENT = {"k_move": 184, "k_sim": 284, "k_vis": 37, "k_obs": 3893, "k_lidar": 3888}
+KERNEL_BYTES_PER_AGENT = {"k_move": 184, "k_sim": 300, "k_vis": 37, "k_obs": 3893, "k_lidar": 3888}
 KERNEL_BYTES_PER_WORLD = {"k_move": 0, "k_sim": 272, "k_vis": 0, "k_obs": 128, "k_lidar": 0}
 
 
