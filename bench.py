@@ -180,8 +180,6 @@ def main():
     exchange = "gather" if args.gather else args.exchange
     if exchange == "auto":
         exchange = "gather" if world_size > 1 and not args.share_device else "none"
-    if world_size == 1:
-        exchange = "none"
     xgroup = None
     if world_size > 1:
         # Control plane (barriers, max-over-ranks time) on gloo: the step has
@@ -191,6 +189,13 @@ def main():
             if args.share_device:
                 raise SystemExit("--exchange gather/local needs one GPU per rank")
             xgroup = dist.new_group(backend="nccl")
+    elif exchange != "none":
+        # one rank, exchange asked for explicitly: a one-rank RCCL group, so
+        # the line carries the exchange's per-rank cost (pack copy + the RCCL
+        # launch; nothing crosses xGMI)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 
     import madrona_mp_env as m
     from mpenv_dist import make_exchange
@@ -397,7 +402,7 @@ def main():
         print(json.dumps(result), flush=True)
     if learner is not None:
         learner.close()
-    if world_size > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
