@@ -53,10 +53,12 @@ TAPE_SEED = 1234
 #            full-team player 112 + enemy 132 + last-known 96 w  = 3893
 #   k_lidar: pos 12 + rot 16 + aim rot 16 + pose 4 r; 80 rays x 16 B w;
 #            previous rays 80 x 16 B r + full-team copy 80 x 16 B w = 3888
-# plus per world-step: 32 singleton columns x 4 B r+w (256) and full-team
-# reward/done 16 w in k_sim; full-team global 2 x 64 w in k_obs.
+# plus per world-step: 32 singleton columns x 4 B r+w (256), full-team
+# reward/done 16 w and the live breadcrumbs r+w (32 B each; 18.8 per world
+# at steady state under the tape, oracle rollout of 256 worlds, steps
+# 100-1100: 1,203 B) in k_sim; full-team global 2 x 64 w in k_obs.
 KERNEL_BYTES_PER_AGENT = {"k_move": 184, "k_sim": 300, "k_vis": 37, "k_obs": 3893, "k_lidar": 3888}
-KERNEL_BYTES_PER_WORLD = {"k_move": 0, "k_sim": 272, "k_vis": 0, "k_obs": 128, "k_lidar": 0}
+KERNEL_BYTES_PER_WORLD = {"k_move": 0, "k_sim": 1475, "k_vis": 0, "k_obs": 128, "k_lidar": 0}
 
 
 def parse():
