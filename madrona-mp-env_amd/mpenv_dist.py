@@ -97,10 +97,12 @@ class LearnerGather:
 
     Each step, `submit()` copies this rank's outputs (on the current
     stream, after the step that produced them) into one flat byte buffer of
-    a 2-slot ring and starts ONE asynchronous gather of that buffer to rank
-    `dst`; the collective runs on the process group's own stream, so it
-    overlaps the next step, and the engine's output buffers are free for
-    that step as soon as the copy is done.  A slot is reused only after its
+    a 2-slot ring -- on the learner, its own row of the receive buffer --
+    and starts the slot's transfers to rank `dst` (one send per rank,
+    batched point-to-point, so the learner does not copy its own segment
+    again); they run on the process group's own stream, so they overlap the
+    next step, and the engine's output buffers are free for that step as
+    soon as the copy is done.  A slot is reused only after its
     previous gather completed (work.wait() orders the current stream after
     it).  Nothing is allocated or concatenated per step.
 
@@ -150,10 +152,16 @@ class LearnerGather:
             if other != sig:
                 raise ValueError(f"LearnerGather: rank {r} ships a different layout than rank {self.rank} "
                                  "(unequal shards? total worlds must be divisible by the world size)")
-        self.flat = [torch.empty(off, dtype=torch.uint8, device=dev) for _ in range(slots)]
+        # the learner packs its own outputs straight into its row of the
+        # receive buffer (no copy of its own segment); the others pack into a
+        # flat send buffer
         self.recv = None
+        self.flat = None
         if self.rank == dst:
             self.recv = [torch.empty((self.ws, off), dtype=torch.uint8, device=dev) for _ in range(slots)]
+        else:
+            self.flat = [torch.empty(off, dtype=torch.uint8, device=dev) for _ in range(slots)]
+        self.slots = slots
         self.pending = [None] * slots
         self.k = 0
         self.last_slot = None
@@ -169,33 +177,44 @@ class LearnerGather:
         """Bytes this rank sends and the learner receives per step."""
         return {"sent_per_rank": self.nbytes, "learner_ingress": self.nbytes * (self.ws - 1)}
 
-    def submit(self, stream_ptr=None):
-        slot = self.k % len(self.flat)
-        self.k += 1
+    def _wait(self, slot):
         if self.pending[slot] is not None:
-            self.pending[slot].wait()
+            for w in self.pending[slot]:
+                w.wait()
             self.pending[slot] = None
-        buf = self.flat[slot]
-        pack_flat(self.layout, self.src, buf)
-        gl = list(self.recv[slot].unbind(0)) if self.recv is not None else None
-        self.pending[slot] = self.dist.gather(buf, gl, dst=self.dst, group=self.group, async_op=True)
+
+    def submit(self, stream_ptr=None):
+        """Pack this step's outputs into the next ring slot (on the current
+        stream) and start the slot's point-to-point transfers: every other
+        rank sends its buffer, the learner receives one row per peer (RCCL
+        runs them on its own stream, overlapping the next step)."""
+        dist = self.dist
+        slot = self.k % self.slots
+        self.k += 1
+        self._wait(slot)
+        if self.rank == self.dst:
+            pack_flat(self.layout, self.src, self.recv[slot][self.rank])
+            ops = [dist.P2POp(dist.irecv, self.recv[slot][r], dist.get_global_rank(self.group, r)
+                              if self.group is not None else r, self.group)
+                   for r in range(self.ws) if r != self.dst]
+        else:
+            pack_flat(self.layout, self.src, self.flat[slot])
+            peer = dist.get_global_rank(self.group, self.dst) if self.group is not None else self.dst
+            ops = [dist.P2POp(dist.isend, self.flat[slot], peer, self.group)]
+        self.pending[slot] = dist.batch_isend_irecv(ops) if ops else None
         self.last_slot = slot
         return slot
 
     def drain(self):
-        for i, w in enumerate(self.pending):
-            if w is not None:
-                w.wait()
-                self.pending[i] = None
+        for i in range(self.slots):
+            self._wait(i)
 
     def outputs(self, slot=None):
         """{name: [world_size, rows, ...] view} of a completed gather (dst only)."""
         if self.recv is None:
             return {}
         slot = self.last_slot if slot is None else slot
-        if self.pending[slot] is not None:
-            self.pending[slot].wait()
-            self.pending[slot] = None
+        self._wait(slot)
         return unpack_flat(self.layout, self.recv[slot])
 
     def close(self):
