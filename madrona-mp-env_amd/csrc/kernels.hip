@@ -3285,6 +3285,16 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
 #ifndef MPENV_LIDAR_WAVECULL
 #define MPENV_LIDAR_WAVECULL 1
 #endif
+        // The BVH first (one traversal for both fan kinds), then the world's
+        // capsules.  World / agent indices are formed after the traversal,
+        // from an opaque copy of g (nothing but the ray lives across it).
+        float tb;
+        const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ>(ob, ray_o, dir, tb, kFltMax, 0.f);
+        uint32_t go = g;
+        asm volatile("" : "+v"(go));
+        const uint32_t w = __umulhi(go, S.nMagic); // g / N (engine.h)
+        const uint32_t i = go - w * N;
+        const int64_t g0 = (int64_t)w * N;
         WorldHit hw;
         if (MPENV_LIDAR_WAVECULL && fwd) {
             // Forward fan (one agent, one xy origin per wave): the BVH first,
@@ -3298,16 +3308,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             // of t ~ 1e-3 at these distances).  Lane j < N loads capsule j
             // once; the per-ray loop reads the survivors' bases from those
             // lanes (readlane) in ascending j, so ties resolve as before.
-            float tb;
-            const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ>(ob, ray_o, dir, tb, kFltMax, 0.f);
             float min_t = bhit ? tb : kFltMax;
-            // world / agent indices formed after the traversal, from an
-            // opaque copy of g (nothing but the ray lives across it)
-            uint32_t go = g;
-            asm volatile("" : "+v"(go));
-            const uint32_t w = __umulhi(go, S.nMagic); // g / N (engine.h)
-            const uint32_t i = go - w * N;
-            const int64_t g0 = (int64_t)w * N;
             float mx = min_t;
 #pragma unroll
             for (int sh = 32; sh >= 1; sh >>= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
@@ -3349,19 +3350,9 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             hw.t = min_t;
             hw.entity = ent;
         } else {
-            float tb;
-            const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ>(ob, ray_o, dir, tb, kFltMax, 0.f);
-            uint32_t go = g;
-            asm volatile("" : "+v"(go));
-            const uint32_t w = __umulhi(go, S.nMagic);
-            const uint32_t i = go - w * N;
-            hw = capsulesD(S.px, S.py, S.pz, (int64_t)w * N, (int)N, ray_o, dir, (int)i, bhit, bhit ? tb : kFltMax);
+            hw = capsulesD(S.px, S.py, S.pz, g0, (int)N, ray_o, dir, (int)i, bhit, bhit ? tb : kFltMax);
         }
         if (!valid) continue;
-        uint32_t go = g;
-        asm volatile("" : "+v"(go));
-        const uint32_t w = __umulhi(go, S.nMagic);
-        const uint32_t i = go - w * N;
         const bool second = i >= T; // team of the casting agent
         float4 out;
         if (hw.hit) {
