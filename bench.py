@@ -85,10 +85,14 @@ def parse():
     ap.add_argument("--grad-mb", type=float, default=16.0, help="local exchange: all-reduced gradient MB")
     ap.add_argument("--update-every", type=int, default=50,
                     help="local exchange: steps per policy update (jax_train.py --steps-per-update)")
-    ap.add_argument("--actions", choices=["tape", "combat"], default="tape",
+    ap.add_argument("--actions", choices=["tape", "combat", "policy"], default="tape",
                     help="tape = the hash action tape (headline); combat = the tape overridden on the "
                          "device by the zone-seeking aim-bot (mpenv_combat_actions mode 1), so agents "
-                         "meet, fight, die and respawn inside the timed window")
+                         "meet, fight, die and respawn inside the timed window; policy = a closed "
+                         "loop: a random-init bf16 MLP reads every trainInterface observation each step "
+                         "and its argmax actions are the next step inputs (the env side of a "
+                         "jax_train-style self-play loop; the policy forward is inside the timed window)")
+    ap.add_argument("--policy-hidden", type=int, default=512, help="policy MLP width (--actions policy)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--share-device", action="store_true",
                     help="debug: map every rank to GPU 0 (rehearse N>1 on a one-GPU box; no --gather)")
@@ -166,6 +170,51 @@ def load_profile(path, workload):
     return d if d.get("workload") == workload else {}
 
 
+# Action heads of the discrete policy (PvPDiscreteAction + discrete aim,
+# jax_policy.py actions_config): move amount, move angle, fire, stand, yaw, pitch.
+POLICY_HEADS = (3, 8, 3, 3, 13, 7)
+
+
+def make_policy(sim, hidden, dev):
+    """A random-init two-layer bf16 MLP over every observation tensor of the
+    trainInterface (jax_policy.py's encoder widths, no LSTM), one argmax per
+    action head.  Returns a callable that runs it on the engine's current
+    outputs (zero-copy views) and returns the device pointer of an [A][6]
+    int32 action buffer for copy_actions."""
+    import torch
+
+    outs = sim.train_interface()["outputs"]
+    names = ["self", "teammates", "opponents", "opponents_last_known", "self_pos", "teammate_positions",
+             "opponent_positions", "opponent_last_known_positions", "opponent_masks", "fwd_lidar",
+             "rear_lidar", "hp", "magazine", "alive", "filters_state"]
+    views = [outs[n].to_torch() for n in names]
+    A = views[0].shape[0]
+    flat = [v.reshape(A, -1) for v in views]
+    width = sum(v.shape[1] for v in flat)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    w1 = (torch.randn(width, hidden, device=dev, generator=g) / width ** 0.5).to(torch.bfloat16)
+    w2 = (torch.randn(hidden, hidden, device=dev, generator=g) / hidden ** 0.5).to(torch.bfloat16)
+    wh = (torch.randn(hidden, sum(POLICY_HEADS), device=dev, generator=g) / hidden ** 0.5).to(torch.bfloat16)
+    x = torch.empty(A, width, dtype=torch.bfloat16, device=dev)
+    act = torch.empty(A, 6, dtype=torch.int32, device=dev)
+    splits = list(POLICY_HEADS)
+
+    def run():
+        col = 0
+        for v in flat:
+            x[:, col:col + v.shape[1]].copy_(v)
+            col += v.shape[1]
+        h = torch.relu(x @ w1)
+        h = torch.relu(h @ w2)
+        logits = h @ wh
+        for k, part in enumerate(torch.split(logits, splits, dim=1)):
+            act[:, k] = part.argmax(dim=1).to(torch.int32)
+        return act.data_ptr()
+
+    return run
+
+
 def main():
     args = parse()
     import torch
@@ -238,8 +287,13 @@ def main():
                             update_every=args.update_every) if exchange == "local" else \
         make_exchange(exchange, sim, group=xgroup)
 
+    policy = make_policy(sim, args.policy_hidden, dev) if args.actions == "policy" else None
+
     def one_step(s):
-        if args.actions == "combat":
+        if policy is not None:
+            # actions from the observations the previous step left (no tape)
+            sim.copy_actions(policy(), sptr)
+        elif args.actions == "combat":
             # the aim-bot reads the previous step's observations and writes
             # the step inputs directly (replaces the input copy)
             sim.combat_actions(ring[s % RING].data_ptr(), 0, 1, sptr)
@@ -305,7 +359,7 @@ def main():
         prof_pass = (timings, counts)
 
     workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})") \
-        + ("" if args.actions == "tape" else " + combat actions")
+        + {"tape": "", "combat": " + combat actions", "policy": f" + MLP policy loop (bf16, {args.policy_hidden} wide)"}[args.actions]
     result = {
         "metric": f"env steps/sec x agents (whole node), simple_map {ts}v{ts} @ {W} worlds"
                   + ("" if world_size == 1 else f"/GPU x {world_size} GPUs"),
@@ -319,8 +373,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (hash action tape, seed 1234; 64-step ring resident in HBM"
-                + (")" if args.actions == "tape" else "; overridden on the device by the zone-seeking aim-bot)"),
+        "data": {"tape": "synthetic (hash action tape, seed 1234; 64-step ring resident in HBM)",
+                 "combat": "synthetic (hash action tape, seed 1234; 64-step ring resident in HBM; overridden on "
+                           "the device by the zone-seeking aim-bot)",
+                 "policy": "synthetic (actions = argmax of a random-init bf16 MLP over every trainInterface "
+                           "observation of the previous step)"}[args.actions],
         "config": {
             "workload": workload,
             "worlds_per_gpu": W,
