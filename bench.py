@@ -212,6 +212,7 @@ def make_policy(sim, hidden, dev):
             act[:, k] = part.argmax(dim=1).to(torch.int32)
         return act.data_ptr()
 
+    run.actions = act
     return run
 
 

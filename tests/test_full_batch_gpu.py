@@ -14,6 +14,9 @@
   aim-bot over the global tape; oracle slices straddling every shard boundary
   compared every 25 steps; the outputs then assembled through the learner
   exchange's flat layout (mpenv_dist) in global world order.
+* Config C5's loop on one GPU: team 1 A* bots in every world, team 0 driven
+  by bench.py's policy MLP reading the previous step's observations; oracle
+  slices fed the same policy actions.
 """
 import time
 
@@ -186,5 +189,73 @@ def test_c4_shards_on_one_gpu_match_oracle_across_boundaries():
     print(f"\nC4 on one GPU: {R} shards x {W} worlds {ts}v{ts}, {C4_STEPS} steps, {len(slices)} boundary "
           f"slices bit-exact every 25 steps; {kills} kills in the whole job; gathered layout {nbytes / 1e6:.1f} MB per rank; test {time.time() - t_start:.1f} s")
     assert kills > 0
+    for o in oracles:
+        o.close()
+
+
+def test_c5_policy_loop_with_bots_matches_oracle():
+    """Config C5's shape on one GPU: 6v6 x 16,384 worlds, team 1 of every
+    world an A* bot (AgentPolicy -1, planAStarAISystem over the nav mesh),
+    team 0 driven by a closed policy loop -- bench.py's random-init bf16 MLP
+    reads every trainInterface observation of the previous step and its
+    argmax actions are the next step's inputs (the engine side of the
+    jax_train self-play loop; JAX itself is absent from the image).  Oracle
+    slices of the same global worlds are fed the very actions the policy
+    produced and compared on every trainInterface output every 25 steps."""
+    import sys
+
+    import torch
+
+    import madrona_mp_env as m
+
+    sys.path.insert(0, T.ROOT)
+    from bench import make_policy
+
+    W, ts, steps = 16384, 6, 300
+    N = 2 * ts
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    sim = m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=0, num_worlds=W, rand_seed=5,
+                       auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                       team_size=ts, num_pbt_policies=0, policy_history_size=0, scene_path=T.SCENE)
+    ctrl = sim.sim_control_tensor().to_torch()
+    ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=dev).view_as(ctrl))
+    torch.cuda.synchronize()
+    sim.init()
+    pol = np.zeros((W, 2, ts), np.int32)
+    pol[:, 1, :] = -1
+    sim.policy_assignment_tensor().to_torch().copy_(torch.from_numpy(pol.reshape(-1, 1)).to(dev))
+    torch.cuda.synchronize()
+    policy = make_policy(sim, 512, dev)
+    outs = {n: t.to_torch() for n, t in sim.train_interface()["outputs"].items()}
+    slices = [(0, 3), (5000, 3), (W - 3, 3)]
+    oracles = []
+    for g0, nw in slices:
+        o = T.Oracle(nw, ts, world_id_offset=g0)
+        o.put_ctrl([0, 1, 1])
+        o.init()
+        o.view("AGENT_POLICY")[:] = pol[g0:g0 + nw].reshape(-1, 1)
+        oracles.append(o)
+    sim.enable_stats(True)
+    for s in range(steps):
+        ptr = policy()
+        sim.copy_actions(ptr, stream.cuda_stream)
+        sim.step_async(stream.cuda_stream)
+        for (g0, nw), o in zip(slices, oracles):
+            o.set_actions(policy.actions[g0 * N:(g0 + nw) * N].cpu().numpy())
+            o.step()
+        if s % 25 == 24:
+            for (g0, nw), o in zip(slices, oracles):
+                for n, ex in T.TRAIN_OUTPUTS.items():
+                    t = outs[n]
+                    rpw = t.shape[0] // W
+                    T.compare(t[g0 * rpw:(g0 + nw) * rpw].cpu().numpy(),
+                              o.get(ex).reshape((-1,) + tuple(t.shape[1:])), f"{n} worlds {g0}.. @ {s}")
+    torch.cuda.synchronize()
+    st = sim.read_stats()
+    print(f"\nC5 loop on one GPU: {W} worlds {ts}v{ts}, {steps} policy steps, team 1 A* bots; "
+          f"{len(slices)} slices bit-exact every 25 steps; pairs seen {st['los_seen']}, shots {st['shot_rays']}, "
+          f"hits {st['hit_agents']}, kills {st['kills']}")
+    assert st["los_seen"] > 0 and st["shot_rays"] > 0  # the bots see and fire on the policy team
     for o in oracles:
         o.close()
