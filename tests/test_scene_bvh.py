@@ -223,3 +223,75 @@ def test_vertical_rays_closed_form(oracle, scene):
     ts = oracle.lib.oracle_sphere_cast(oracle.h, T.fptr(o), T.fptr(d), 5.0, T.fptr(nrm))
     if abs(nrm[2]) > 0.999:
         assert ts == pytest.approx(expect - 5.0, abs=1e-2)
+
+
+def test_node_bytes_follow_the_documented_quantisation(bvh):
+    """Pins the node bytes both sides traverse (the visited sets, and through
+    the sphere-cast testVert quirk the casts' results, depend on them)
+    independently of the builder's code: every node's origin, exponents and
+    quantised child boxes are recomputed here from the triangles below each
+    child, by the rule DESIGN.md §2 documents (csrc/scene.cpp): node origin =
+    the children's exact float32 lower corner; per axis the smallest e with
+    253·2^e >= range (clamped to [-100, 100]); child box = floor / ceil of
+    its exact bounds in 2^e units, widened by one quantum each way and
+    clamped to [0, 255].  The reference quantises the same 64-byte node
+    format (mesh_bvh_builder.cpp:452-474, 513-530: floor / ceil against
+    2^ceil(log2(range / 255)), no widening) over Embree's topology, which
+    this image cannot build; the widening is this builder's own margin."""
+    raw, verts, _ = bvh
+    nodes = _nodes(raw)
+    tris = verts.reshape(-1, 3, 3).astype(np.float64)
+    boxes = {}
+
+    def child_box(n, i):
+        c = int(n["children"][i])
+        if c & 0x80000000 or c < 0:
+            leaf = c & 0x7FFFFFFF
+            pts = tris[leaf:leaf + int(n["triSize"][i])].reshape(-1, 3)
+            return pts.min(0), pts.max(0)
+        return node_box(c)
+
+    def node_box(oid):
+        if oid not in boxes:
+            n = nodes[oid]
+            kids = [child_box(n, i) for i in range(4) if int(n["children"][i]) != -1]
+            boxes[oid] = (np.min([k[0] for k in kids], 0), np.max([k[1] for k in kids], 0))
+        return boxes[oid]
+
+    for oid in range(len(nodes) - 1, -1, -1):
+        n = nodes[oid]
+        lo, hi = node_box(oid)
+        mn = lo.astype(np.float32)
+        assert (mn.astype(np.float64) == lo).all()  # exact: triangle coordinates are float32
+        np.testing.assert_array_equal(n["min"], mn)
+        exps = []
+        for a in range(3):
+            rng_ = hi[a] - float(mn[a])
+            e = -100
+            if rng_ > 0:
+                e = int(np.ceil(np.log2(rng_ / 253.0)))
+                while np.ldexp(253.0, e) < rng_:
+                    e += 1
+            exps.append(max(-100, min(100, e)))
+        assert list(n["exp"]) == exps, oid
+        internal = 0
+        for i in range(4):
+            c = int(n["children"][i])
+            if c == -1:
+                assert n["triSize"][i] == 0
+                continue
+            cl, ch = child_box(n, i)
+            for a in range(3):
+                s = np.ldexp(1.0, exps[a])
+                ql = max(0.0, np.floor((cl[a] - float(mn[a])) / s) - 1.0)
+                qh = min(255.0, np.ceil((ch[a] - float(mn[a])) / s) + 1.0)
+                assert n["qmin"][a][i] == ql and n["qmax"][a][i] == qh, (oid, i, a)
+                # conservative in exact arithmetic: the dequantised box holds every
+                # triangle of the child's subtree
+                assert float(mn[a]) + s * ql <= cl[a] and float(mn[a]) + s * qh >= ch[a]
+            if c & 0x80000000 or c < 0:
+                assert 1 <= n["triSize"][i] <= 2
+            else:
+                assert c > oid and n["triSize"][i] == 0  # DFS pre-order ids
+                internal += 1
+        assert n["internal"] == internal

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -262,6 +263,74 @@ static void traceWaveWW(const float *rays, size_t r0, size_t n, int cap, int nee
     }
 }
 
+// Packet traversal: one wave-uniform stack per wave of up to 64 rays.  A
+// popped node is box-tested by every lane against its own t_max; a child is
+// pushed if any lane enters it, a leaf's triangles are tested (lockstep:
+// the leaf's triSize iterations) by the lanes that entered it.  Child order
+// from the octant of lane `ref`'s direction (mode 0) or of the wave's mean
+// direction (mode 1).  Returns lockstep node iterations and triangle
+// iterations summed over the wave, and the per-lane box / triangle tests.
+struct PK {
+    double nodeIters = 0, triIters = 0, laneBoxes = 0, laneTris = 0;
+};
+
+static void traceWavePacket(const float *rays, size_t r0, size_t n, int mode, PK &out)
+{
+    std::vector<float> tmax(n, 3.4e38f), inv(3 * n);
+    for (size_t k = 0; k < n; k++)
+        for (int j = 0; j < 3; j++) {
+            const float d = rays[6 * (r0 + k) + 3 + j];
+            inv[3 * k + j] = d == 0 ? 1e7f : 1.f / d;
+        }
+    float md[3] = { 0, 0, 0 };
+    for (size_t k = 0; k < n; k++)
+        for (int j = 0; j < 3; j++) md[j] += rays[6 * (r0 + k) + 3 + j];
+    const float *rd = mode == 0 ? &rays[6 * r0 + 3] : md;
+    const int oct = (rd[0] < 0 ? 1 : 0) | (rd[1] < 0 ? 2 : 0) | (rd[2] < 0 ? 4 : 0);
+    std::vector<int> stack = { 0 };
+    while (!stack.empty()) {
+        const int ni = stack.back();
+        stack.pop_back();
+        out.nodeIters++;
+        const Node &nd = nodes[ni];
+        int kids[4], nk = 0;
+        for (int ii = 0; ii < 4; ii++) {
+            const int i = octOrder[ni][oct][ii];
+            if (nd.children[i] == -1) continue;
+            float sx = std::ldexp(1.f, nd.expX), sy = std::ldexp(1.f, nd.expY), sz = std::ldexp(1.f, nd.expZ);
+            float lo[3] = { nd.minX + sx * nd.qMinX[i], nd.minY + sy * nd.qMinY[i], nd.minZ + sz * nd.qMinZ[i] };
+            float hi[3] = { nd.minX + sx * nd.qMaxX[i], nd.minY + sy * nd.qMaxY[i], nd.minZ + sz * nd.qMaxZ[i] };
+            std::vector<int> in;
+            for (size_t k = 0; k < n; k++) {
+                out.laneBoxes++;
+                const float *o = &rays[6 * (r0 + k)];
+                float tn = 0, tf = tmax[k];
+                for (int j = 0; j < 3; j++) {
+                    float a = (lo[j] - o[j]) * inv[3 * k + j], b = (hi[j] - o[j]) * inv[3 * k + j];
+                    tn = std::max(tn, std::min(a, b));
+                    tf = std::min(tf, std::max(a, b));
+                }
+                if (tn <= tf) in.push_back((int)k);
+            }
+            if (in.empty()) continue;
+            if (nd.children[i] & 0x80000000) {
+                const int leaf = nd.children[i] & 0x7fffffff;
+                out.triIters += nd.triSize[i];
+                for (int k : in)
+                    for (int q = 0; q < nd.triSize[i]; q++) {
+                        out.laneTris++;
+                        float th;
+                        if (tri(&verts[(leaf + q) * 9], &rays[6 * (r0 + k)], &rays[6 * (r0 + k) + 3], tmax[k], th))
+                            tmax[k] = th;
+                    }
+            } else {
+                kids[nk++] = nd.children[i];
+            }
+        }
+        for (int k = nk - 1; k >= 0; k--) stack.push_back(kids[k]);
+    }
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3) {
@@ -335,6 +404,21 @@ int main(int argc, char **argv)
                ftb == 1 ? "front-to-back" : ftb == 2 ? "octant order " : ftb == 3 ? "octant rev 1L" : "reference    ", n, st.pops / n, st.boxes / n, st.tris / n, st.maxStack,
                wave_pops / n, wave_tris / n);
     }
+    for (int mode = 0; mode < 2; mode++) {
+        PK fw, rr;
+        size_t nf = 0, nr = 0;
+        for (size_t w0 = 0; w0 < n; w0 += 64) {
+            // dump_lidar_rays order: per 320-ray unit, 4 forward waves then 1 rear wave
+            const bool fwd = ((w0 / 64) % 5) != 4;
+            traceWavePacket(rays.data(), w0, std::min<size_t>(64, n - w0), mode, fwd ? fw : rr);
+            (fwd ? nf : nr) += std::min<size_t>(64, n - w0);
+        }
+        printf("packet (%s order) forward waves: lockstep node iters/ray %.2f tri iters/ray %.2f | lane boxes/ray %.2f lane tris/ray %.2f\n",
+               mode ? "mean-dir" : "lane-0  ", fw.nodeIters * 64 / nf, fw.triIters * 64 / nf, fw.laneBoxes / nf, fw.laneTris / nf);
+        printf("packet (%s order) rear waves:    lockstep node iters/ray %.2f tri iters/ray %.2f | lane boxes/ray %.2f lane tris/ray %.2f\n",
+               mode ? "mean-dir" : "lane-0  ", rr.nodeIters * 64 / nr, rr.triIters * 64 / nr, rr.laneBoxes / nr, rr.laneTris / nr);
+    }
+    if (getenv("TRAV_PACKET_ONLY")) return 0;
     // while-while with postponed triangles, octant order
     const int caps[] = { 1, 2, 3, 4, 8 };
     for (int cap : caps) {
