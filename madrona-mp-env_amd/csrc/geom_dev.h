@@ -670,9 +670,39 @@ struct SphereHit {
 // t_max0: MeshBVH::sphereCast's own t_max argument (mesh_bvh.inl:743-747):
 // the search starts with hit_t = t_max0 and returns it when nothing is
 // nearer.
+#ifdef MPENV_LAB_WORK
+// kernel_lab only: per-thread sphere-cast work (casts, nodes popped, triangle
+// tests) of the last k_move, indexed by global thread id; read by
+// mpenv_lab_work (kernels.hip).
+// Rows 3..10: nodes popped per cast site (MP_LAB_SITE before each call).
+constexpr int kLabWorkMax = 1 << 18;
+constexpr int kLabWorkRows = 11;
+__device__ uint32_t g_labWork[kLabWorkRows][kLabWorkMax];
+__device__ uint32_t g_labSite[kLabWorkMax];
+__device__ __forceinline__ void labWorkAdd(int k, uint32_t v)
+{
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid < (uint32_t)kLabWorkMax) {
+        g_labWork[k][tid] += v;
+        if (k == 1) g_labWork[3 + (g_labSite[tid] & 7u)][tid] += v;
+    }
+}
+__device__ __forceinline__ void labSite(uint32_t s)
+{
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid < (uint32_t)kLabWorkMax) g_labSite[tid] = s;
+}
+#define MP_LAB_WORK(k, v) labWorkAdd(k, v)
+#define MP_LAB_SITE(s) labSite(s)
+#else
+#define MP_LAB_WORK(k, v) ((void)0)
+#define MP_LAB_SITE(s) ((void)0)
+#endif
+
 __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r,
                                                  float t_max0 = mp::kFltMax)
 {
+    MP_LAB_WORK(0, 1u);
     using namespace mp;
     Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
     Vec3 closest = v3(0.f, 0.f, 0.f);
@@ -703,6 +733,7 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
     bsPush(st, 0);
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
+        MP_LAB_WORK(1, 1u);
         const MP_LDS float *nd = b.snodes + node_idx * kSNodeFloats;
 #pragma unroll 1
         for (int i = 0; i < 4; i++) {
@@ -719,6 +750,7 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
                     const int ntri = (int)__float_as_uint(nd[28 + i]);
                     Vec3 leaf_n = v3(0.f, 0.f, 0.f);
                     float leaf_t = hit_t;
+                    MP_LAB_WORK(2, (uint32_t)ntri);
                     for (int k = 0; k < ntri; k++) {
                         Vec3 a, bb, c;
                         loadTri(b, leaf + k, a, bb, c);

@@ -463,9 +463,12 @@ __device__ __forceinline__ bool castPathQuirkFreeD(const SceneDev &sc, Vec3 o, V
 
 // The cast's hit if nearer than `near_b`, else t = kFltMax: for callers to
 // which every hit at or beyond near_b acts like no hit.  Horizontal d.
+#ifndef MPENV_LAB_MOVE_SKIP
+#define MPENV_LAB_MOVE_SKIP 0 // kernel_lab only: cut parts of k_move to time them (wrong results)
+#endif
 __device__ __forceinline__ SphereHit castNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
 {
-    if (!castPathQuirkFreeD(sc, o, d, near_b)) return bvhSphereCastD(bvh, o, d, kSphereR);
+    if (!(MPENV_LAB_MOVE_SKIP & 2) && !castPathQuirkFreeD(sc, o, d, near_b)) return bvhSphereCastD(bvh, o, d, kSphereR);
     SphereHit h = bvhSphereCastD(bvh, o, d, kSphereR, near_b);
     if (!(h.t < near_b)) h.t = kFltMax;
     return h;
@@ -475,14 +478,92 @@ __device__ __forceinline__ SphereHit castNearD(const LBVH &bvh, const SceneDev &
 // path guard is the cell of 2o).
 __device__ __forceinline__ float castFirstNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
 {
-    if (castQuirkFreeD(sc, o)) {
+    if ((MPENV_LAB_MOVE_SKIP & 4) || castQuirkFreeD(sc, o)) {
         const float t = bvhSphereCastD(bvh, o, d, kSphereR, near_b).t;
-        if (t < near_b) return t;
+        if ((MPENV_LAB_MOVE_SKIP & 4) || t < near_b) return t;
     }
     return bvhSphereCastD(bvh, o, d, kSphereR).t;
 }
 
-// sim.cpp:889-1039 applyVelocitySystem + updateMoveStateSystem
+// Index of the n-th set bit (0-based) of m; m has more than n set bits.
+__device__ __forceinline__ int nthSetBitD(uint64_t m, int n)
+{
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t low = m & ((1ull << w) - 1ull);
+        const int c = __popcll(low);
+        if (n >= c) {
+            n -= c;
+            m >>= w;
+            pos += w;
+        } else {
+            m = low;
+        }
+    }
+    return pos;
+}
+
+#ifndef MPENV_MOVE_COOP_STUCK
+#define MPENV_MOVE_COOP_STUCK 1
+#endif
+
+// The "stuck" fallback's four horizontal casts (sim.cpp:962-984), for the
+// lanes of the wave with `need` set: their 4·k casts are dealt one per lane
+// across the whole wave (rounds of 64) instead of four in a row on the
+// owning lane -- a wave holding one stuck agent runs one cast's time, not
+// four.  Each cast is the same function of the same owner inputs (x,
+// v_norm, low_check shuffled from the owner), so hd4 is bit-identical to
+// the serial loop's.  Called by every lane of a full wave; a partial wave
+// (batch tail) runs the serial loop.
+__device__ __forceinline__ void stuckCastsD(const LBVH &bvh, bool need, Vec3 x, Vec3 v_norm, float low_check,
+                                            float hd4[4])
+{
+    const float r = c::kAgentRadius;
+    const uint64_t act = __ballot(1);
+    const uint64_t m = __ballot(need);
+    if (m == 0ull) return;
+    if (!MPENV_MOVE_COOP_STUCK || act != ~0ull) {
+        if (need) {
+            for (int dir = 0; dir < 4; dir++) {
+                const Vec3 dv = rotate2DD(v_norm, (float)dir * 3.14159f * 0.5f);
+                Vec3 ray_o = x - dv * r * 2.0f;
+                ray_o.z += low_check;
+                MP_LAB_SITE(5);
+                hd4[dir] = bvhSphereCastD(bvh, ray_o, dv, r).t;
+            }
+        }
+        return;
+    }
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const int rank = __popcll(m & ((1ull << lane) - 1ull)); // owner's index among the stuck lanes
+    const int tasks = 4 * __popcll(m);
+    for (int base = 0; base < tasks; base += 64) {
+        const int t = base + lane;
+        const int owner = nthSetBitD(m, min(t, tasks - 1) >> 2);
+        const float ox = __shfl(x.x, owner), oy = __shfl(x.y, owner), oz = __shfl(x.z, owner);
+        const float vx = __shfl(v_norm.x, owner), vy = __shfl(v_norm.y, owner), vz = __shfl(v_norm.z, owner);
+        const float lc = __shfl(low_check, owner);
+        float hd = 0.f;
+        if (t < tasks) {
+            const Vec3 dv = rotate2DD(v3(vx, vy, vz), (float)(t & 3) * 3.14159f * 0.5f);
+            Vec3 ray_o = v3(ox, oy, oz) - dv * r * 2.0f;
+            ray_o.z += lc;
+            MP_LAB_SITE(5);
+            hd = bvhSphereCastD(bvh, ray_o, dv, r).t;
+        }
+#pragma unroll
+        for (int dir = 0; dir < 4; dir++) {
+            const int tt = 4 * rank + dir;
+            const float got = __shfl(hd, tt & 63);
+            if (need && tt >= base && tt < base + 64) hd4[dir] = got;
+        }
+    }
+}
+
+// sim.cpp:889-1039 applyVelocitySystem + updateMoveStateSystem.  Split at
+// the stuck fallback so the wave can share its casts (stuckCastsD): part 1
+// up to the ground check, the fallback's casts, part 2 to the end.
 __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
 {
     const Vec3 x = ldPos(S, g);
@@ -492,27 +573,32 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
     Vec3 new_vel = v3(0.f, 0.f, 0.f);
     const int pose = S.curPose[g];
     float v_len = length(v);
+    const float buffer = 0.05f * c::kAgentRadius;
+    const float r = c::kAgentRadius;
+    float top = c::kStandHeight - r;
+    float low_check = c::kProneHeight;
+    if (pose == kCrouch) {
+        top = c::kCrouchHeight - r;
+    } else if (pose == kProne) {
+        top = low_check;
+        low_check = c::kProneHeight - r + buffer;
+    }
+    Vec3 v_norm = v3(0.f, 0.f, 0.f);
+    Vec3 hit_pos = x, ground_check = x;
+    float ground_dist = 0.f;
+    bool cont = false, stuck_path = false;
     do {
         if (v_len == 0.f) break;
-        Vec3 v_norm = v / v_len;
+        v_norm = v / v_len;
         float move_dist = v_len * c::kDeltaT;
-        const float buffer = 0.05f * c::kAgentRadius;
-        const float r = c::kAgentRadius;
-        float top = c::kStandHeight - r;
-        float low_check = c::kProneHeight;
-        if (pose == kCrouch) {
-            top = c::kCrouchHeight - r;
-        } else if (pose == kProne) {
-            top = low_check;
-            low_check = c::kProneHeight - r + buffer;
-        }
 
         Vec3 ray_o = x;
         ray_o.z += top;
         Vec3 normal = v3(0.f, 0.f, 0.f);
-        {
+        if (!(MPENV_LAB_MOVE_SKIP & 1)) {
             // the ground below, wherever it is (a bounded first try gains
             // nothing here: the downward cast prunes at the floor anyway)
+            MP_LAB_SITE(0);
             SphereHit h = bvhSphereCastD(bvh, ray_o, -kUp, r);
             if (h.t < kFltMax) normal = h.n;
         }
@@ -527,6 +613,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         ray_o.z += low_check;
         float low_dist;
         {
+            MP_LAB_SITE(1);
             SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
             low_dist = h.t;
             if (h.t < kFltMax) normal = h.n;
@@ -535,6 +622,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         bool high_hit = false;
         if (pose != kProne) {
             ray_o.z = x.z + top;
+            MP_LAB_SITE(2);
             SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
             high_dist = h.t;
             if (high_dist < low_dist) {
@@ -546,7 +634,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         bool stuck = low_dist == 0.0f || high_dist == 0.0f;
         low_dist = fmaxD(0.0f, low_dist - buffer);
         high_dist = fmaxD(0.0f, high_dist - buffer);
-        Vec3 hit_pos = x + v_norm * fminD(low_dist, move_dist);
+        hit_pos = x + v_norm * fminD(low_dist, move_dist);
 
         if (move_dist > low_dist) {
             Vec3 slide_dir = normalize(cross(kUp, normal));
@@ -555,28 +643,33 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
             ray_o.z += high_hit ? top : low_check;
             float max_move = move_dist - low_dist;
             // only min(slide - buffer, max_move) is used
+            MP_LAB_SITE(3);
             float slide = castNearD(bvh, sc, ray_o, slide_dir, (max_move + buffer) + kCastSlack).t;
             slide = fmaxD(0.0f, slide - buffer);
             slide = fminD(slide, max_move);
             if (slide > 0.0f) hit_pos = hit_pos + slide_dir * slide;
         }
 
-        Vec3 ground_check = hit_pos;
+        ground_check = hit_pos;
         ground_check.z += top;
         // min(ground_dist, top) is used, and whether there is ground at all
-        float ground_dist = castFirstNearD(bvh, sc, ground_check, -kUp, 2.f * top + 10.f);
+        MP_LAB_SITE(4);
+        ground_dist = castFirstNearD(bvh, sc, ground_check, -kUp, 2.f * top + 10.f);
         if (ground_dist == kFltMax) break;
+        stuck_path = !(MPENV_LAB_MOVE_SKIP & 8) && (ground_dist <= 0.0f || stuck);
+        cont = true;
+    } while (false);
 
-        if (ground_dist <= 0.0f || stuck) {
+    float hd4[4] = { 0.f, 0.f, 0.f, 0.f };
+    stuckCastsD(bvh, stuck_path, x, v_norm, low_check, hd4);
+
+    while (cont) {
+        if (stuck_path) {
             float furthest = 0.0f;
             int best_dir = -1;
             for (int dir = 0; dir < 4; dir++) {
-                Vec3 dv = rotate2DD(v_norm, (float)dir * 3.14159f * 0.5f);
-                ray_o = x - dv * r * 2.0f;
-                ray_o.z += low_check;
-                float hd = bvhSphereCastD(bvh, ray_o, dv, r).t;
-                if (hd > furthest) {
-                    furthest = hd;
+                if (hd4[dir] > furthest) {
+                    furthest = hd4[dir];
                     best_dir = dir;
                 }
             }
@@ -585,6 +678,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
                 hit_pos = x + dv * (fminD(furthest - r * 2.0f, -buffer));
                 ground_check = hit_pos;
                 ground_check.z += top;
+                MP_LAB_SITE(6);
                 ground_dist = bvhSphereCastD(bvh, ground_check, -kUp, r).t;
                 if (ground_dist == kFltMax) break;
             }
@@ -598,7 +692,8 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         if (to_new_dist == 0.f) break;
         new_pos = np;
         new_vel = to_new / c::kDeltaT;
-    } while (false);
+        break;
+    }
     // updateMoveStateSystem (sim.cpp:1030-1039)
     stPos(S, g, new_pos);
     stVel(S, g, new_vel);
@@ -607,7 +702,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
 // sim.cpp:1041-1104 fallSystem + updateMoveStatePostFallSystem
 __device__ void fallD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
 {
-    if (S.alive[g] == 0.f) return;
+    if ((MPENV_LAB_MOVE_SKIP & 16) || S.alive[g] == 0.f) return;
     const float fall_rate = 386.08858267717f;
     const float cast_offset = c::kAgentRadius;
     Vec3 pos = ldPos(S, g);
@@ -615,6 +710,7 @@ __device__ void fallD(const DevState &S, const SceneDev &sc, const LBVH &bvh, in
     ray_o.z += c::kAgentRadius + cast_offset;
     // min(ground - cast_offset, fall_rate * dt) is used, and whether there
     // is ground at all
+    MP_LAB_SITE(7);
     float ground = castFirstNearD(bvh, sc, ray_o, -kUp, 2.f * (cast_offset + fall_rate * c::kDeltaT) + 10.f);
     if (ground == kFltMax || ground < cast_offset) return;
     float fall = fminD(ground - cast_offset, fall_rate * c::kDeltaT);
@@ -2230,21 +2326,47 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPENV_MOVE_WPE))) k_move(DevState S, SceneDev sc, int apw)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef MPENV_LAB_WAVE_HIST
+    const uint64_t wt0 = wall_clock64();
+#endif
     LBVH bvh = stageBVHSphere(smem, sc);
     bvh.stats = S.stats;
-    const int lane = threadIdx.x & 63;
-    if (lane >= apw) return;
-    const int64_t wave = ((int64_t)xcdBlockId() * blockDim.x + threadIdx.x) >> 6;
-    const int64_t g = wave * apw + lane;
-    if (g >= S.A) return;
-    if (S.stats) statAdd(S.stats + kStatAliveAgents, S.alive[g] != 0.f ? 1u : 0u);
-    planAStarD(S, sc, g);
-    if (sc.replayOn) return; // pvpReplayLogic replaces the gameplay systems (sim.cpp:5587-5605)
-    applyBotActionsD(S, g);
-    pvpMovementD(S, g);
-    pvpAimD(S, g);
-    applyVelocityD(S, sc, bvh, g);
-    fallD(S, sc, bvh, g);
+#ifdef MPENV_LAB_WAVE_HIST
+    const uint64_t wt1 = wall_clock64();
+    bvh.stats = nullptr; // the timeline only: no per-cast counters
+#endif
+    [&]() {
+        const int lane = threadIdx.x & 63;
+        if (lane >= apw) return;
+        const int64_t wave = ((int64_t)xcdBlockId() * blockDim.x + threadIdx.x) >> 6;
+        const int64_t g = wave * apw + lane;
+        if (g >= S.A) return;
+#ifndef MPENV_LAB_WAVE_HIST
+        if (S.stats) statAdd(S.stats + kStatAliveAgents, S.alive[g] != 0.f ? 1u : 0u);
+#endif
+        planAStarD(S, sc, g);
+        if (sc.replayOn) return; // pvpReplayLogic replaces the gameplay systems (sim.cpp:5587-5605)
+        applyBotActionsD(S, g);
+        pvpMovementD(S, g);
+        pvpAimD(S, g);
+        applyVelocityD(S, sc, bvh, g);
+        fallD(S, sc, bvh, g);
+    }();
+#ifdef MPENV_LAB_WAVE_HIST
+    // lab: per-wave timeline (100 MHz wall clock): slots 8 sum of wave
+    // durations, 9 waves, 10 sum of staging time, 11 latest end, 12 latest
+    // start, 13 ~earliest start, 14.. duration histogram (8 us bins)
+    if ((threadIdx.x & 63) == 0 && S.stats) {
+        const uint64_t wt2 = wall_clock64();
+        atomicAdd(&S.stats[8], (unsigned long long)(wt2 - wt0));
+        atomicAdd(&S.stats[9], 1ull);
+        atomicAdd(&S.stats[10], (unsigned long long)(wt1 - wt0));
+        atomicMax(&S.stats[11], (unsigned long long)wt2);
+        atomicMax(&S.stats[12], (unsigned long long)wt0);
+        atomicMax(&S.stats[13], (unsigned long long)(~wt0));
+        atomicAdd(&S.stats[14 + min(31ull, (unsigned long long)(wt2 - wt0) / 800ull)], 1ull);
+    }
+#endif
 }
 
 // Step graph part 2 (fireSystem onward): per-world phases.  A workgroup
@@ -3387,6 +3509,22 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
 }
 
 static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
+
+#ifdef MPENV_LAB_WORK
+// kernel_lab only: copy out (and clear) the per-thread sphere-cast work
+// counters, [11][n] u32 (casts, nodes popped, triangle tests, nodes per cast site 0..7).
+extern "C" int mpenv_lab_work(uint32_t *out, int32_t n)
+{
+    n = n < kLabWorkMax ? n : kLabWorkMax;
+    for (int k = 0; k < kLabWorkRows; k++) {
+        if (hipMemcpyFromSymbol(out + (size_t)k * n, HIP_SYMBOL(g_labWork), sizeof(uint32_t) * n,
+                                sizeof(uint32_t) * kLabWorkMax * k, hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+    }
+    static uint32_t zeros[kLabWorkRows * kLabWorkMax];
+    return check(hipMemcpyToSymbol(HIP_SYMBOL(g_labWork), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice));
+}
+#endif
 
 // Debug/test hook: closest-hit BVH queries for caller rays (mode 0 = the
 // traversal inlined into the step kernels, 1 = its out-of-line copy).

@@ -139,14 +139,45 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
         lib.mpenv_enable_stats.argtypes = [C.c_void_p, C.c_int32]
         lib.mpenv_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
         lib.mpenv_enable_stats(h, 1)
-        ns = 50
+        ns = int(os.environ.get("LAB_STATS_STEPS", 50))
         for s in range(ns):
             step(s)
-        st = (C.c_uint64 * 24)()
-        n = lib.mpenv_read_stats(h, st, 24)
+        st = (C.c_uint64 * 64)()
+        n = lib.mpenv_read_stats(h, st, 64)
         lib.mpenv_enable_stats(h, 0)
-        phases = [round(st[k] / ns / 1e6, 2) for k in range(8, n)]
-    print(json.dumps({"variant": label or name, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
+        if n == 48:  # -DMPENV_LAB_WAVE_HIST: k_move wave timeline (100 MHz ticks, one group)
+            phases = {"steps": ns, "mean_wave_us": st[8] / st[9] / 100, "mean_staging_us": st[10] / st[9] / 100,
+                      "last_end_minus_first_start_us": (st[11] - (~st[13] & (2 ** 64 - 1))) / 100,
+                      "last_start_minus_first_start_us": (st[12] - (~st[13] & (2 ** 64 - 1))) / 100,
+                      "dur_hist_8us": [st[k] for k in range(14, 46)]}
+        else:
+            phases = [round(st[k] / ns / 1e6, 2) for k in range(8, n)]
+    work = None
+    if hasattr(lib, "mpenv_lab_work"):
+        # -DMPENV_LAB_WORK: per-thread sphere-cast work of one step's k_move
+        import numpy as np
+
+        nthr = 1 << 18
+        buf = np.zeros(11 * nthr, np.uint32)
+        lib.mpenv_lab_work.argtypes = [C.c_void_p, C.c_int32]
+        hip.hipDeviceSynchronize()
+        lib.mpenv_lab_work(buf.ctypes.data, nthr)  # clears
+        step(0)
+        hip.hipDeviceSynchronize()
+        assert lib.mpenv_lab_work(buf.ctypes.data, nthr) == 0
+        a = worlds * 2 * team
+        wv = buf.reshape(11, nthr)[:, :a].reshape(11, -1, 64).astype(np.float64)
+        work = {}
+        sites = ("ground0", "fwd_low", "fwd_high", "slide", "ground_chk", "stuck4", "stuck_ground", "fall")
+        for k, nm in enumerate(("casts", "nodes", "tris") + tuple("nodes@" + x for x in sites)):
+            lane_mean = wv[k].mean()
+            wmax = wv[k].max(1)
+            work[nm] = {"lane_mean": round(lane_mean, 2), "wave_max_mean": round(wmax.mean(), 2),
+                        "simd_eff": round(lane_mean / max(wmax.mean(), 1e-9), 3),
+                        "wave_max_pct": [round(float(np.percentile(wmax, q)), 1) for q in (10, 50, 90, 99, 100)],
+                        "lane_pct": [round(float(np.percentile(wv[k], q)), 1) for q in (50, 90, 99, 99.9, 100)],
+                        "lanes_active": round(float((wv[k] > 0).mean()), 4)}
+    print(json.dumps({"variant": label or name, "work": work, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
                       "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
                       "digest": dig.hexdigest()[:16], "per_export": pex}), flush=True)
 
