@@ -165,9 +165,7 @@ enum StatId {
     kStatShots = 5,       // fireSystem rays (k_sim)
     kStatHits = 6,        // agents that took damage (applyDmgSystem)
     kStatKills = 7,       // agents killed (alive -> hp <= 0)
-#if defined(MPENV_LAB_WAVE_HIST)
-    kNumStats = 48, // lab: k_move wave timeline in slots 8..
-#elif defined(MPENV_LAB_PHASE_T)
+#if defined(MPENV_LAB_PHASE_T)
     kNumStats = 24, // lab: k_sim phase cycles in slots 8..
 #else
     kNumStats = 8,

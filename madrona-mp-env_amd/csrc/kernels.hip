@@ -2320,6 +2320,33 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 #ifndef MPENV_MOVE_WPE
 #define MPENV_MOVE_WPE 3
 #endif
+#ifdef MPENV_LAB_WAVE_HIST
+// kernel_lab only: per-wave timeline of the kernel MPENV_LAB_WAVE_HIST
+// names (1 k_move, 2 k_sim, 3 k_obs, 4 k_vis): lane 0 of each wave stores
+// its start / end on the 100 MHz wall clock in its own slot (no atomics:
+// same-address atomics from thousands of waves would stretch the tail they
+// measure); mpenv_lab_wave reads and clears them.
+constexpr int kLabWaves = 1 << 16;
+__device__ uint64_t g_labWaveT[kLabWaves][2];
+__device__ __forceinline__ void labWaveEnd(const DevState &S, uint64_t wt0, uint64_t wt1)
+{
+    (void)S;
+    (void)wt1;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0 && wave < (uint32_t)kLabWaves) {
+        g_labWaveT[wave][0] = wt0;
+        g_labWaveT[wave][1] = wall_clock64();
+    }
+}
+#define MP_WAVE_T0(id) const uint64_t labWt0 = wall_clock64()
+#define MP_WAVE_T1(id)                                                                                             \
+    do {                                                                                                           \
+        if (MPENV_LAB_WAVE_HIST == (id)) labWaveEnd(S, labWt0, labWt0);                                            \
+    } while (0)
+#else
+#define MP_WAVE_T0(id) ((void)0)
+#define MP_WAVE_T1(id) ((void)0)
+#endif
 // apw: agents per wave (64, or fewer on small batches: a wave runs the
 // longest of its lanes' sphere-cast chains, so when the batch leaves SIMDs
 // idle, fewer agents per wave shorten every wave; launchMove picks it).
@@ -2353,19 +2380,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPE
         fallD(S, sc, bvh, g);
     }();
 #ifdef MPENV_LAB_WAVE_HIST
-    // lab: per-wave timeline (100 MHz wall clock): slots 8 sum of wave
-    // durations, 9 waves, 10 sum of staging time, 11 latest end, 12 latest
-    // start, 13 ~earliest start, 14.. duration histogram (8 us bins)
-    if ((threadIdx.x & 63) == 0 && S.stats) {
-        const uint64_t wt2 = wall_clock64();
-        atomicAdd(&S.stats[8], (unsigned long long)(wt2 - wt0));
-        atomicAdd(&S.stats[9], 1ull);
-        atomicAdd(&S.stats[10], (unsigned long long)(wt1 - wt0));
-        atomicMax(&S.stats[11], (unsigned long long)wt2);
-        atomicMax(&S.stats[12], (unsigned long long)wt0);
-        atomicMax(&S.stats[13], (unsigned long long)(~wt0));
-        atomicAdd(&S.stats[14 + min(31ull, (unsigned long long)(wt2 - wt0) / 800ull)], 1ull);
-    }
+    if (MPENV_LAB_WAVE_HIST == 1) labWaveEnd(S, wt0, wt1);
 #endif
 }
 
@@ -2391,6 +2406,7 @@ __device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &
 // scratch for the whole kernel and spills around the call).
 __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)) k_sim(DevState S, SceneDev sc)
 {
+    MP_WAVE_T0(2);
 #ifdef MPENV_LAB_PHASE_T
     // lab: per-block phase durations (thread 0, after each barrier)
     uint64_t pt_prev = clock64();
@@ -2560,6 +2576,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         }
         if (!(MPENV_LAB_SIM_SKIP & 128)) resetSystemD(S, sc, w, pre);
     }
+    MP_WAVE_T1(2);
 }
 
 // utils.cpp:169-184 inFrustum
@@ -2667,6 +2684,7 @@ __device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &
 #endif
 __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev sc)
 {
+    MP_WAVE_T0(4);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ uint16_t rays[kVisMaxRays]; // (lane << 2) | point
     __shared__ uint32_t masks[kBlock]; // per agent of the block (<= 4 waves x 64/T)
@@ -2770,6 +2788,7 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         const bool valid = wl < apw * T && g < S.A;
         if (valid && wl % T == 0) S.visMask[g] = (uint8_t)masks[(int)(g - agent0)];
     }
+    MP_WAVE_T1(4);
 }
 
 __device__ __forceinline__ Vec3 normalizedPosD(const SceneDev &sc, Vec3 p) // sim.cpp:2693-2718
@@ -3142,6 +3161,7 @@ __device__ __forceinline__ void fullTeamSlotD(const DevState &S, const SceneDev 
 #endif
 __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev sc)
 {
+    MP_WAVE_T0(3);
     // per wave: observation rows (stride kObsRowPad) or a whole self-obs
     // span (stride 43); position rows of the slot loops (stride kPosPad)
     __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsSpanPad];
@@ -3307,6 +3327,7 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
 #ifndef MPENV_LAB_OBS_NO_FT
     fullTeamSlotD(S, sc, w, g, team, off, ws);
 #endif
+    MP_WAVE_T1(3);
 }
 
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray.  Rays are dealt to
@@ -3509,6 +3530,20 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
 }
 
 static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
+
+#ifdef MPENV_LAB_WAVE_HIST
+// kernel_lab only: copy out (and clear) the per-wave start / end stamps,
+// [n][2] u64 (zeros for waves that did not run).
+extern "C" int mpenv_lab_wave(uint64_t *out, int32_t n)
+{
+    n = n < kLabWaves ? n : kLabWaves;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_labWaveT), sizeof(uint64_t) * 2 * n, 0, hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return -1;
+    static uint64_t zeros[kLabWaves * 2];
+    return check(hipMemcpyToSymbol(HIP_SYMBOL(g_labWaveT), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice));
+}
+#endif
 
 #ifdef MPENV_LAB_WORK
 // kernel_lab only: copy out (and clear) the per-thread sphere-cast work

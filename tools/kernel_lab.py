@@ -145,13 +145,35 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
         st = (C.c_uint64 * 64)()
         n = lib.mpenv_read_stats(h, st, 64)
         lib.mpenv_enable_stats(h, 0)
-        if n == 48:  # -DMPENV_LAB_WAVE_HIST: k_move wave timeline (100 MHz ticks, one group)
-            phases = {"steps": ns, "mean_wave_us": st[8] / st[9] / 100, "mean_staging_us": st[10] / st[9] / 100,
-                      "last_end_minus_first_start_us": (st[11] - (~st[13] & (2 ** 64 - 1))) / 100,
-                      "last_start_minus_first_start_us": (st[12] - (~st[13] & (2 ** 64 - 1))) / 100,
-                      "dur_hist_8us": [st[k] for k in range(14, 46)]}
-        else:
-            phases = [round(st[k] / ns / 1e6, 2) for k in range(8, n)]
+        phases = [round(st[k] / ns / 1e6, 2) for k in range(8, n)]
+    timeline = None
+    if hasattr(lib, "mpenv_lab_wave"):
+        # -DMPENV_LAB_WAVE_HIST=k: per-wave start / end of one kernel in one
+        # step (100 MHz wall clock), the default world groups
+        import numpy as np
+
+        nw = 1 << 16
+        tb = np.zeros(2 * nw, np.uint64)
+        lib.mpenv_lab_wave.argtypes = [C.c_void_p, C.c_int32]
+        lib.mpenv_set_world_groups(h, 1)
+        hip.hipDeviceSynchronize()
+        lib.mpenv_lab_wave(tb.ctypes.data, nw)  # clears
+        step(1)
+        hip.hipDeviceSynchronize()
+        assert lib.mpenv_lab_wave(tb.ctypes.data, nw) == 0
+        tt = tb.reshape(nw, 2)
+        tt = tt[tt[:, 1] > 0].astype(np.float64)
+        t0 = tt[:, 0].min()
+        st_, en = (tt[:, 0] - t0) / 100.0, (tt[:, 1] - t0) / 100.0
+        dur = en - st_
+        span = en.max()
+        timeline = {"waves": int(len(tt)), "span_us": round(span, 1), "mean_wave_us": round(dur.mean(), 1),
+                    "dur_pct_us": [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 99, 100)],
+                    "start_pct_us": [round(float(np.percentile(st_, q)), 1) for q in (10, 50, 90, 99, 100)],
+                    "end_pct_us": [round(float(np.percentile(en, q)), 1) for q in (10, 50, 90, 99, 100)],
+                    # busy fraction: wave-time integral over (span x max concurrent waves)
+                    "waves_alive_at_pct_of_span": [int(((st_ <= f * span) & (en > f * span)).sum())
+                                                   for f in (0.1, 0.25, 0.5, 0.75, 0.9)]}
     work = None
     if hasattr(lib, "mpenv_lab_work"):
         # -DMPENV_LAB_WORK: per-thread sphere-cast work of one step's k_move
@@ -177,7 +199,7 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
                         "wave_max_pct": [round(float(np.percentile(wmax, q)), 1) for q in (10, 50, 90, 99, 100)],
                         "lane_pct": [round(float(np.percentile(wv[k], q)), 1) for q in (50, 90, 99, 99.9, 100)],
                         "lanes_active": round(float((wv[k] > 0).mean()), 4)}
-    print(json.dumps({"variant": label or name, "work": work, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
+    print(json.dumps({"variant": label or name, "work": work, "timeline": timeline, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
                       "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
                       "digest": dig.hexdigest()[:16], "per_export": pex}), flush=True)
 
