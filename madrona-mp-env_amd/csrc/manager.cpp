@@ -134,10 +134,25 @@ struct mpenv_manager {
     std::vector<hipEvent_t> eventPool;
     size_t eventsUsed = 0;
 
+    // The Step graph as a captured HIP graph (all world groups, fork/join
+    // included), replayed with one hipGraphLaunch per step.  Kernel
+    // arguments are captured by value, so the graph is keyed on the bytes of
+    // every argument struct and re-captured when any of them changes (world
+    // groups, stats buffer, ...).  MPENV_STEP_GRAPH=0 launches kernel by
+    // kernel instead; timed steps (events between kernels) always do.
+    bool useGraph = true;
+    hipStream_t capStream = nullptr;
+    hipGraph_t stepGraph = nullptr;
+    hipGraphExec_t stepExec = nullptr;
+    std::vector<char> graphKey;
+
     ~mpenv_manager()
     {
         if (stream) (void)hipStreamSynchronize(stream);
         for (hipStream_t gs : gstreams) (void)hipStreamSynchronize(gs);
+        if (stepExec) (void)hipGraphExecDestroy(stepExec);
+        if (stepGraph) (void)hipGraphDestroy(stepGraph);
+        if (capStream) (void)hipStreamDestroy(capStream);
         for (hipEvent_t e : eventPool) (void)hipEventDestroy(e);
         for (hipEvent_t e : joinEv) (void)hipEventDestroy(e);
         if (forkEv) (void)hipEventDestroy(forkEv);
@@ -244,7 +259,54 @@ struct mpenv_manager {
         postStep(st);
     }
 
+    std::vector<char> argKey() const
+    {
+        std::vector<char> k;
+        auto put = [&](const void *p, size_t n) {
+            const char *c = static_cast<const char *>(p);
+            k.insert(k.end(), c, c + n);
+        };
+        put(&groups, sizeof(groups));
+        put(&S, sizeof(S));
+        put(&sc, sizeof(sc));
+        for (const DevState &G : gS) put(&G, sizeof(G));
+        for (const SceneDev &g : gsc) put(&g, sizeof(g));
+        return k;
+    }
+
     void launchStep(hipStream_t st)
+    {
+        if (!useGraph || timing) {
+            launchStepDirect(st);
+            return;
+        }
+        std::vector<char> key = argKey();
+        if (!stepExec || key != graphKey) {
+            if (stepExec) HIP_CHECK(hipGraphExecDestroy(stepExec));
+            if (stepGraph) HIP_CHECK(hipGraphDestroy(stepGraph));
+            stepExec = nullptr;
+            stepGraph = nullptr;
+            if (!capStream) HIP_CHECK(hipStreamCreateWithFlags(&capStream, hipStreamNonBlocking));
+            // capture on a private stream (the caller's may be the legacy
+            // default stream, which cannot be captured); the group streams
+            // join the capture through the fork event
+            HIP_CHECK(hipStreamBeginCapture(capStream, hipStreamCaptureModeThreadLocal));
+            try {
+                launchStepDirect(capStream);
+            } catch (...) {
+                hipGraph_t g = nullptr;
+                (void)hipStreamEndCapture(capStream, &g);
+                if (g) (void)hipGraphDestroy(g);
+                throw;
+            }
+            HIP_CHECK(hipStreamEndCapture(capStream, &stepGraph));
+            HIP_CHECK(hipGraphInstantiate(&stepExec, stepGraph, nullptr, nullptr, 0));
+            graphKey = std::move(key);
+        }
+        HIP_CHECK(hipGraphLaunch(stepExec, st));
+    }
+
+    void launchStepDirect(hipStream_t st)
     {
         if (groups <= 1) {
             stepRange(S, sc, st);
@@ -826,6 +888,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
             if (const char *e = std::getenv("MPENV_WORLD_GROUPS")) want = std::atoi(e);
             m->setupGroups(want);
         }
+        if (const char *e = std::getenv("MPENV_STEP_GRAPH")) m->useGraph = std::atoi(e) != 0;
         // TrainControl from sim flags (mgr.cpp:1397-1413)
         int32_t tc[3] = { (cfg->sim_flags & MPENV_SIMFLAG_SIM_EVAL_MODE) ? 1 : 0,
                           (cfg->sim_flags & MPENV_SIMFLAG_STAGGER_STARTS) ? 1 : 0,

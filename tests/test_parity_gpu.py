@@ -607,6 +607,60 @@ def test_world_groups_on_streams_match_oracle(monkeypatch):
                     T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
 
 
+def test_step_graph_replay_equals_direct_launches(monkeypatch):
+    """The Step graph replayed as a captured HIP graph (the default) equals
+    kernel-by-kernel launches (MPENV_STEP_GRAPH=0) bit for bit, including
+    across re-captures: world groups 2 -> 3 -> 1 -> 2, the stats buffer
+    switched on and off (kernel arguments change), and timed steps (which
+    bypass the graph) in between; plus oracle slices at the group borders."""
+    ts, W, steps = 3, 3000, 48
+    N = 2 * ts
+    monkeypatch.setenv("MPENV_WORLD_GROUPS", "2")
+    monkeypatch.setenv("MPENV_STEP_GRAPH", "0")
+    ref = T.Engine(W, ts)
+    monkeypatch.setenv("MPENV_STEP_GRAPH", "1")
+    g = T.Engine(W, ts)
+    probes = [0, 999, 1499, 1999, W - 2]
+    oracles = []
+    for e in (ref, g):
+        e.put_ctrl([0, 1, 1])
+        e.init()
+    for w0 in probes:
+        o = T.Oracle(2, ts, world_id_offset=w0)
+        o.put_ctrl([0, 1, 1])
+        o.init()
+        oracles.append(o)
+    for s in range(steps):
+        if s == 8:
+            g.set_world_groups(3)
+        elif s == 16:
+            g.enable_stats(True)
+        elif s == 20:
+            g.enable_stats(False)
+            g.set_world_groups(1)
+        elif s == 28:
+            g.set_world_groups(2)
+        elif s == 34:
+            assert g.lib.mpenv_enable_kernel_timing(g.h, 1) == 0
+        elif s == 38:
+            assert g.lib.mpenv_enable_kernel_timing(g.h, 0) == 0
+        acts = T.mpenv_tape.tape_actions(1234, s, 0, W * N)
+        for e in (ref, g):
+            e.set_actions(acts)
+            e.step()
+        for w0, o in zip(probes, oracles):
+            o.set_actions(T.mpenv_tape.tape_actions(1234, s, w0 * N, 2 * N))
+            o.step()
+        if s % 4 == 3:
+            for n in T.STEP_OUTPUTS:
+                T.compare(g.get(n), ref.get(n), f"{n} graph vs direct @ {s}")
+            for w0, o in zip(probes, oracles):
+                for n in T.STEP_OUTPUTS:
+                    _, _, shape = g.desc(n)
+                    k = shape[0] // W
+                    T.compare(g.get_rows(n, w0 * k, (w0 + 2) * k), o.get(n), f"{n} worlds {w0}.. @ {s}")
+
+
 def test_logs_record_and_events_match_oracle(tmp_path):
     """record_log_path + event_log_path: the engine's StepLog file,
     events.bin and steps.bin equal, byte for byte, what the oracle's buffers
