@@ -28,6 +28,7 @@ struct LBVH {
     const MP_LDS float *pre; // sphere-casting kernels only (stageBVHSphere)
     const MP_LDS float *snodes; // sphere-cast node image (stageBVHSphere), else null
     unsigned long long *stats;  // workload counters (DevState::stats), null = off
+    int32_t rotStride;          // stageBVHOct with kLidarRot: float4s per rotated vertex copy
 };
 
 // Workload counter add, one atomic per wave: the active lanes' values
@@ -99,6 +100,7 @@ __device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc)
     b.pre = nullptr;
     b.snodes = nullptr;
     b.stats = nullptr;
+    b.rotStride = 0;
     return b;
 }
 
@@ -155,7 +157,8 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
 }
 
 // k_lidar's LDS image: the 8 octant node images (scene.h octantNodeImages,
-// 8 x numNodes nodes) then the vertices as float4.  The traversal of a ray
+// 8 x numNodes nodes) then the vertices as float4 (three rotated copies with
+// kLidarRot).  The traversal of a ray
 // reads image (d.x < 0) | (d.y < 0) << 1 | (d.z < 0) << 2.  Each node takes
 // kOctNodeQ 16-B slots: 4 = packed 64-B nodes; 5 = one pad slot, so the
 // slots of nodes k and k' sit in different LDS bank groups whenever
@@ -166,6 +169,13 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
 #endif
 constexpr int kOctNodeQ = MPENV_OCT_NODE_Q;
 
+// kLidarRot: the vertices three times, copy r as (v[r+1], v[r+2], v[r]) (mod
+// 3), for rayTriRot; else once as (x, y, z).
+#ifndef MPENV_LIDAR_ROT
+#define MPENV_LIDAR_ROT 1 // 0: one (x, y, z) copy and per-component gathers (k_lidar 0.730 -> 0.744 ms, r03y lab)
+#endif
+constexpr bool kLidarRot = MPENV_LIDAR_ROT != 0;
+
 __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
 {
     const int node_q = sc.numNodes * kOctNodeQ * 8;
@@ -175,8 +185,16 @@ __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
         dst_n[(k >> 2) * kOctNodeQ + (k & 3)] = src_n[k];
     const float *src_v = sc.verts;
     float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
-    for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
-        dst_v[k] = make_float4(src_v[3 * k], src_v[3 * k + 1], src_v[3 * k + 2], 0.f);
+    if constexpr (kLidarRot) {
+        for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
+            const int r = k / sc.numVerts, v = k - r * sc.numVerts;
+            const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
+            dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r], 0.f);
+        }
+    } else {
+        for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
+            dst_v[k] = make_float4(src_v[3 * k], src_v[3 * k + 1], src_v[3 * k + 2], 0.f);
+    }
     __syncthreads();
     LBVH b;
     b.nodes = (const MP_LDS BVHNode *)(smem);
@@ -184,12 +202,15 @@ __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
     b.pre = nullptr;
     b.snodes = nullptr;
     b.stats = nullptr;
+    b.rotStride = sc.numVerts;
     return b;
 }
 
+// sign bits: -0 counts as negative, as in the slab test's copysign'd inverse
 __device__ __forceinline__ int rayOctant(mp::Vec3 d)
 {
-    return (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
+    return (int)((__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
+                 ((__float_as_uint(d.z) >> 31) << 2));
 }
 
 typedef float lf4 __attribute__((ext_vector_type(4)));
@@ -401,6 +422,59 @@ __device__ __forceinline__ bool rayTriPermD(const LBVH &b, int tri, const RayTxf
     return true;
 }
 
+// rayTri over a rotated vertex copy: the LDS image holds every vertex three
+// times, copy kz as (v[kz+1], v[kz+2], v[kz]) (indices mod 3), so the ray's
+// copy yields each vertex already in (kx0, ky0, kz) order with kx0 = kz + 1,
+// ky0 = kz + 2 -- the shear frame before rayTxfm's swap -- and `sw` (the
+// swap: d[kz] < 0) exchanges the first two components.  o0 / o1 / oz are
+// the origin's components in the same order.  comp(ta - org, k) ==
+// ta[k] - org[k], so every value equals rayTri's bit for bit; per triangle
+// 6 selects replace the 18 of the per-component comp() gathers.
+__device__ __forceinline__ bool rayTriRot(const MP_LDS lf4 *p, float o0, float o1, float oz, bool sw,
+                                          const RayTxfmD &tx, float t_max, float &out_t)
+{
+    using namespace mp;
+    const lf4 a = p[0], b = p[1], c = p[2];
+    const float a0 = a.x - o0, a1 = a.y - o1, Az_ = a.z - oz;
+    const float b0 = b.x - o0, b1 = b.y - o1, Bz_ = b.z - oz;
+    const float c0 = c.x - o0, c1 = c.y - o1, Cz_ = c.z - oz;
+    const float Akx = sw ? a1 : a0, Aky = sw ? a0 : a1;
+    const float Bkx = sw ? b1 : b0, Bky = sw ? b0 : b1;
+    const float Ckx = sw ? c1 : c0, Cky = sw ? c0 : c1;
+    const float Ax = fma_(-tx.Sx, Az_, Akx);
+    const float Ay = fma_(-tx.Sy, Az_, Aky);
+    const float Bx = fma_(-tx.Sx, Bz_, Bkx);
+    const float By = fma_(-tx.Sy, Bz_, Bky);
+    const float Cx = fma_(-tx.Sx, Cz_, Ckx);
+    const float Cy = fma_(-tx.Sy, Cz_, Cky);
+    float U = fma_(Cx, By, -(Cy * Bx));
+    float V = fma_(Ax, Cy, -(Ay * Cx));
+    float W = fma_(Bx, Ay, -(By * Ax));
+    if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        double CxBy = (double)Cx * (double)By;
+        double CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        double AxCy = (double)Ax * (double)Cy;
+        double AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        double BxAy = (double)Bx * (double)Ay;
+        double ByAx = (double)By * (double)Ax;
+        W = (float)(BxAy - ByAx);
+        if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
+    }
+    float det = U + V + W;
+    if (det == 0.f) return false;
+    const float Az = tx.Sz * Az_;
+    const float Bz = tx.Sz * Bz_;
+    const float Cz = tx.Sz * Cz_;
+    const float T = fma_(U, Az, fma_(V, Bz, W * Cz));
+    if (T < 0.0f || T > t_max * det) return false;
+    const float rcpDet = 1.0f / det;
+    out_t = T * rcpDet;
+    return true;
+}
+
 #ifndef MPENV_TRI_FLAT
 #define MPENV_TRI_FLAT 0
 #endif
@@ -413,7 +487,7 @@ __device__ __forceinline__ bool rayTriPermD(const LBVH &b, int tri, const RayTxf
 // kExit: stop as soon as a hit at t <= exit_at is found (t_out is then
 // that hit, not necessarily the closest; callers that only compare the
 // closest hit with exit_at get the same answer).
-template <bool kExit, bool kPerm = false, int kNodeQ = 4>
+template <bool kExit, bool kPerm = false, int kNodeQ = 4, bool kRot = false, bool kOctImage = false>
 __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
                                              float t_max0, float exit_at)
 {
@@ -437,6 +511,19 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
         rp.ox = comp(ray_o, tx.kx); rp.oy = comp(ray_o, tx.ky); rp.oz = comp(ray_o, tx.kz);
     }
 
+    // kRot: the ray's rotated vertex copy and the origin in its order
+    const MP_LDS lf4 *vrot = nullptr;
+    float ro0 = 0.f, ro1 = 0.f, roz = 0.f;
+    bool rsw = false;
+    if constexpr (kRot) {
+        const int kx0 = tx.kz == 2 ? 0 : tx.kz + 1, ky0 = kx0 == 2 ? 0 : kx0 + 1;
+        vrot = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + tx.kz * b.rotStride;
+        ro0 = comp(ray_o, kx0);
+        ro1 = comp(ray_o, ky0);
+        roz = comp(ray_o, tx.kz);
+        rsw = tx.kx != kx0;
+    }
+
     float t_max = t_max0;
     bool ray_hit = false;
     ByteStack st;
@@ -451,9 +538,14 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
         const float originQuantX = (node.minX - ray_o.x) * rayXInv;
         const float originQuantY = (node.minY - ray_o.y) * rayYInv;
         const float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
-        const uint32_t nearX = negX ? node.qMaxX : node.qMinX, farX = negX ? node.qMinX : node.qMaxX;
-        const uint32_t nearY = negY ? node.qMaxY : node.qMinY, farY = negY ? node.qMinY : node.qMaxY;
-        const uint32_t nearZ = negZ ? node.qMaxZ : node.qMinZ, farZ = negZ ? node.qMinZ : node.qMaxZ;
+        // kOctImage: the ray's octant image (rayOctant) holds the near slab
+        // in qMin and the far one in qMax already (octantNodeImages)
+        const uint32_t nearX = (!kOctImage && negX) ? node.qMaxX : node.qMinX;
+        const uint32_t farX = (!kOctImage && negX) ? node.qMinX : node.qMaxX;
+        const uint32_t nearY = (!kOctImage && negY) ? node.qMaxY : node.qMinY;
+        const uint32_t farY = (!kOctImage && negY) ? node.qMinY : node.qMaxY;
+        const uint32_t nearZ = (!kOctImage && negZ) ? node.qMaxZ : node.qMinZ;
+        const uint32_t farZ = (!kOctImage && negZ) ? node.qMinZ : node.qMaxZ;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int32_t child = node.child[i];
@@ -485,7 +577,9 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                         if (k >= ntri) break;
 #endif
                         bool h;
-                        if constexpr (kPerm) {
+                        if constexpr (kRot) {
+                            h = rayTriRot(vrot + (leaf + k) * 3, ro0, ro1, roz, rsw, tx, leaf_tmax, hit_t);
+                        } else if constexpr (kPerm) {
                             h = rayTriPermD(b, leaf + k, tx, rp, leaf_tmax, hit_t);
                         } else {
                             Vec3 a, bb, c;

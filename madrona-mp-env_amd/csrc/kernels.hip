@@ -3345,12 +3345,18 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
 #define MPENV_LIDAR_ITERS 4 // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 ms (k_lidar alone, C3)
 #endif
 constexpr int kLidarIters = MPENV_LIDAR_ITERS;
+// 1: rear fans cull capsules per 16-lane group (positions by ds_bpermute); 0: capsulesD
+// per ray (with the rotated vertex copies k_lidar 0.7302 vs 0.7375 ms, r03y lab; through
+// a per-wave LDS slot table instead of ds_bpermute: no gain, dropped)
+#ifndef MPENV_LIDAR_REARCULL
+#define MPENV_LIDAR_REARCULL 1
+#endif
 #ifndef MPENV_LIDAR_NT
 #define MPENV_LIDAR_NT 0 // 1: the full-team lidar copy (written, never read here) as a nontemporal store
 #endif
-// 1024-thread blocks: the 8 octant node images + vertices (43 KB on
-// simple_map) are staged once per 16 waves, so 2 blocks per CU (8 waves per
-// SIMD) fit the 160 KB of LDS.
+// 1024-thread blocks: the 8 octant node images + the three rotated vertex
+// copies (31 + 36 KB on simple_map) are staged once per 16 waves, so 2
+// blocks per CU (8 waves per SIMD) fit the 160 KB of LDS.
 #ifndef MPENV_LIDAR_BLOCK
 #define MPENV_LIDAR_BLOCK 1024
 #endif
@@ -3394,28 +3400,38 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // lane-derived offsets are formed per task instead of living as
         // loop invariants across the traversal, which at 64 VGPRs the
         // compiler would spill to scratch.
-        uint32_t lane;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         const uint32_t unit = task / 5u, sub = task - unit * 5u;
         const bool fwd = sub < 4u;
 #ifdef MPENV_LAB_NO_REAR
         if (!fwd) continue;
 #endif
-        // a tail unit's lanes past A trace a copy of the last agent's rays
-        // and store nothing
-        const uint32_t g_raw = unit * 4u + (fwd ? sub : (lane >> 4));
-        const bool valid = g_raw < A;
-        const uint32_t g = valid ? g_raw : A - 1u;
-        const uint32_t kk = fwd ? lane : (lane & 15u); // ray slot within the forward / rear fan
-        const uint32_t h = fwd ? (kk >> 5) : (kk >> 3), x = fwd ? (kk & 31u) : (kk & 7u);
-        const Quat q = fwd ? ldAimRot(S, g) : ldRot(S, g);
-        const Vec3 dir_fwd = rotateVec(q, kFwd);
-        const Vec3 dir_right = rotateVec(q, kRight);
-        const float top = viewHeightD(S.curPose[g]) + c::kAgentRadius;
-        Vec3 ray_o = ldPos(S, g);
-        ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
-        const float2 cs = fan[fwd ? x : 32 + x];
-        Vec3 dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
+        // The ray of lane `ln`: a tail unit's lanes past A trace a copy of
+        // the last agent's rays and store nothing.
+        auto makeRay = [&](uint32_t ln, uint32_t &g, bool &valid, uint32_t &kk, Vec3 &ray_o, Vec3 &dir) {
+            const uint32_t g_raw = unit * 4u + (fwd ? sub : (ln >> 4));
+            valid = g_raw < A;
+            g = valid ? g_raw : A - 1u;
+            kk = fwd ? ln : (ln & 15u); // ray slot within the forward / rear fan
+            const uint32_t h = fwd ? (kk >> 5) : (kk >> 3), x = fwd ? (kk & 31u) : (kk & 7u);
+            const Quat q = fwd ? ldAimRot(S, g) : ldRot(S, g);
+            const Vec3 dir_fwd = rotateVec(q, kFwd);
+            const Vec3 dir_right = rotateVec(q, kRight);
+            const float top = viewHeightD(S.curPose[g]) + c::kAgentRadius;
+            ray_o = ldPos(S, g);
+            ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
+            const float2 cs = fan[fwd ? x : 32 + x];
+            dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
+        };
+        // Lane id read inside the loop (volatile: not hoisted), so the
+        // lane-derived offsets are formed per task instead of living as
+        // loop invariants across the traversal, which at 64 VGPRs the
+        // compiler would spill to scratch.
+        uint32_t lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        uint32_t g, kk;
+        bool valid;
+        Vec3 ray_o, dir;
+        makeRay(lane, g, valid, kk, ray_o, dir);
         // the ray's octant image: same nodes and leaves, near-first slot
         // order (scene.h octantNodeImages); the oracle visits the same order
         LBVH ob = bvh;
@@ -3432,7 +3448,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // capsules.  World / agent indices are formed after the traversal,
         // from an opaque copy of g (nothing but the ray lives across it).
         float tb;
-        const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ>(ob, ray_o, dir, tb, kFltMax, 0.f);
+        const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ, kLidarRot, true>(ob, ray_o, dir, tb, kFltMax, 0.f);
         uint32_t go = g;
         asm volatile("" : "+v"(go));
         const uint32_t w = __umulhi(go, S.nMagic); // g / N (engine.h)
@@ -3476,6 +3492,57 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
                 co.z += kCapsuleRadius;
                 const Vec3 tr = ray_o - co;
                 // the per-ray conservative culls of capsulesD
+                const float cr = tr.x * dir.y - tr.y * dir.x;
+                if (cr * cr > cull_r2 * dxy2) continue;
+                const float along = -(tr.x * dir.x + tr.y * dir.y + tr.z * dir.z);
+                const float ahead = along + fmaxD(0.f, kCapsuleSegment * dir.z) + kCapsuleRadius * 1.01f;
+                if (ahead < 0.f) continue;
+                if (along + fminD(0.f, kCapsuleSegment * dir.z) - kCapsuleRadius * 1.01f > min_t) continue;
+                const float t = intersectRayZOriginCapsule(tr, dir, kCapsuleRadius, kCapsuleSegment);
+                if (t != 0 && t < min_t) {
+                    min_t = t;
+                    hit = true;
+                    ent = j;
+                }
+            }
+            hw.hit = hit;
+            hw.t = min_t;
+            hw.entity = ent;
+        } else if (MPENV_LIDAR_REARCULL) {
+            // Rear fans: the same cull per 16-lane group (one agent, one xy
+            // origin per group; N <= 12 capsules).  Lane q*16 + j < q*16 + N
+            // loads capsule j of group q's world; the wave walks the union
+            // of the groups' surviving j in ascending order and each lane
+            // takes its group's copy (ds_bpermute) and tests only the j its
+            // group kept -- per ray the same capsules in the same order as
+            // capsulesD minus those no ray of the group can reach.
+            float min_t = bhit ? tb : kFltMax;
+            float mx = min_t;
+#pragma unroll
+            for (int sh = 8; sh >= 1; sh >>= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
+            const uint32_t gb = lane & 48u, jl = lane & 15u;
+            float cx = 0.f, cy = 0.f, cz = 0.f;
+            bool keep = false;
+            if (jl < N) {
+                cx = S.px[g0 + jl]; cy = S.py[g0 + jl]; cz = S.pz[g0 + jl];
+                const float dx = cx - ray_o.x, dy = cy - ray_o.y;
+                keep = jl != i && !(sqrtf(dx * dx + dy * dy) - c::kAgentRadius * 1.01f - 1.f > mx);
+            }
+            const uint64_t cm = __ballot(keep);
+            uint32_t um = (uint32_t)((cm | (cm >> 16) | (cm >> 32) | (cm >> 48)) & 0xffffu);
+            const uint32_t mine = (uint32_t)(cm >> gb) & 0xffffu;
+            bool hit = bhit;
+            int ent = -1;
+            const float dxy2 = dir.x * dir.x + dir.y * dir.y;
+            const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
+            while (um) {
+                const int j = __builtin_ctz(um);
+                um &= um - 1u;
+                const int src = (int)gb + j;
+                Vec3 co = v3(__shfl(cx, src, 64), __shfl(cy, src, 64), __shfl(cz, src, 64));
+                if (!((mine >> j) & 1u)) continue;
+                co.z += kCapsuleRadius;
+                const Vec3 tr = ray_o - co;
                 const float cr = tr.x * dir.y - tr.y * dir.x;
                 if (cr * cr > cull_r2 * dxy2) continue;
                 const float along = -(tr.x * dir.x + tr.y * dir.y + tr.z * dir.z);
@@ -3752,7 +3819,7 @@ size_t bvhLdsBytesSphere(const SceneDev &sc)
 
 size_t bvhLdsBytesOct(const SceneDev &sc)
 {
-    return (size_t)sc.numNodes * 16 * kOctNodeQ * 8 + (size_t)sc.numVerts * 16;
+    return (size_t)sc.numNodes * 16 * kOctNodeQ * 8 + (size_t)sc.numVerts * 16 * (kLidarRot ? 3 : 1);
 }
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)

@@ -388,6 +388,10 @@ std::vector<BVHNode> octantNodeImages(const std::vector<BVHNode> &nodes)
                 p.qMinX[k] = nd.qMinX[i]; p.qMinY[k] = nd.qMinY[i]; p.qMinZ[k] = nd.qMinZ[i];
                 p.qMaxX[k] = nd.qMaxX[i]; p.qMaxY[k] = nd.qMaxY[i]; p.qMaxZ[k] = nd.qMaxZ[i];
                 p.children[k] = nd.children[i];
+                // near slab first for this octant's direction signs
+                if (oct & 1) std::swap(p.qMinX[k], p.qMaxX[k]);
+                if (oct & 2) std::swap(p.qMinY[k], p.qMaxY[k]);
+                if (oct & 4) std::swap(p.qMinZ[k], p.qMaxZ[k]);
             }
             out[oct * n + ni] = p;
         }

@@ -107,15 +107,20 @@ void buildNavMesh(Scene &s, const std::string &navmesh_path);
 void buildBVH(const std::vector<mp::Vec3> &tri_verts, Scene &out);
 
 // Octant node images for closest-hit rays (k_lidar): 8 copies of the node
-// array, copy o for rays whose direction signs are o (bit 0 x < 0, bit 1
-// y < 0, bit 2 z < 0).  In each copy a node's child slots are permuted --
+// array, copy o for rays whose direction sign bits are o (bit 0 x, bit 1 y,
+// bit 2 z; a -0 component counts as negative, like the copysign'd inverse
+// the slab test uses).  In each copy a node's child slots are permuted --
 // leaf children first, nearest first, then internal children farthest
 // first, then empty slots -- where "near" orders the child boxes' centres
 // by their projection on the octant's diagonal (computed in double, ties
 // by slot).  The reference's traversal loop over such a copy (slots in
 // order, internal children pushed on a LIFO stack) therefore tests a
 // node's leaves near-to-far and pops its nearest internal child first.
-// Node indices, bounds and leaves are unchanged; only slot order differs.
+// Per axis whose bit is set, the copy also swaps the qMin / qMax bytes, so
+// a ray of that octant finds its near slab in qMin and its far slab in qMax
+// (mesh_bvh.inl:165-183 takes the min / max of the two; the slab t is
+// monotonic in q with the slope's sign, so the values are the same).
+// Node indices, unquantised bounds and leaves are unchanged.
 std::vector<BVHNode> octantNodeImages(const std::vector<BVHNode> &nodes);
 
 // The sphere cast's vertex test (mesh_bvh.inl:1073-1104) subtracts a vertex

@@ -367,7 +367,7 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
     // octant: visit each node's child slots in the order octantOrder()
     // defines for the ray's direction signs (the lidar's documented child
     // order); otherwise slot order, as mesh_bvh.inl:160-204.
-    const int oct = (ray_d.x < 0.f ? 1 : 0) | (ray_d.y < 0.f ? 2 : 0) | (ray_d.z < 0.f ? 4 : 0);
+    const int oct = (std::signbit(ray_d.x) ? 1 : 0) | (std::signbit(ray_d.y) ? 2 : 0) | (std::signbit(ray_d.z) ? 4 : 0);
     const float diveps = 0.0000001f;
     Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
     RayTxfm tx = computeRayIsectTxfm(ray_d, inv_d);
@@ -2825,8 +2825,8 @@ void addMiddleSpawnCells(Oracle &o)
 
 // ------------------------------------------------------- lidar child order
 // The documented lidar child order ("child visit order"): for
-// a ray whose direction signs are octant `oct` (bit 0 x < 0, bit 1 y < 0,
-// bit 2 z < 0), a node's leaf children first, by ascending key, then its
+// a ray whose direction sign bits are octant `oct` (bit 0 x, bit 1 y, bit 2
+// z; -0 counts as negative, scene.h octantNodeImages), a node's leaf children first, by ascending key, then its
 // internal children by descending key, then empty slots; key = the child
 // box centre projected on the octant diagonal, sum over axes a of
 // s_a * (min_a + 2^exp_a * (qMin_a + qMax_a) / 2), in double; ties keep slot
