@@ -91,6 +91,11 @@ struct DevState {
 
     float *dmg;            // [6][A] DamageDealt
     uint8_t *visMask;      // [A] OpponentsVisibility, bit k = sees opponent k
+    // [A][T][4] k_vis occluder hint per (agent, opponent slot, sample
+    // point): the triangle that last ended that line-of-sight ray (0xffff:
+    // none).  A performance hint only -- any value gives the same answer
+    // (geom_dev.h visibleRayD) -- so it is never reset.
+    uint16_t *visOcc;
     uint64_t *exploreBits; // [A][kExploreTiles] ExploreTracker tiles for episode exploreEp
                            // (the tile exploreTile is current in exploreLo / exploreHi)
     int32_t *filtLast;     // [W][2][3] FiltersMatchState::lastMatches (3 filters used)

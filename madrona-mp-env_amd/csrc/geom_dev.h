@@ -489,7 +489,7 @@ __device__ __forceinline__ bool rayTriRot(const MP_LDS lf4 *p, float o0, float o
 // closest hit with exit_at get the same answer).
 template <bool kExit, bool kPerm = false, int kNodeQ = 4, bool kRot = false, bool kOctImage = false>
 __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
-                                             float t_max0, float exit_at)
+                                             float t_max0, float exit_at, int *exit_tri = nullptr)
 {
     using namespace mp;
     const float diveps = 0.0000001f;
@@ -566,6 +566,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                     bool hit_tri = false;
                     float hit_t = 0.f;
                     float leaf_tmax = t_max;
+                    int hit_k = 0;
 #ifdef MPENV_LAB_NO_TRI
                     for (int k = 0; k < 0; k++) {
 #else
@@ -593,6 +594,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                         if (h) {
                             hit_tri = true;
                             leaf_tmax = hit_t;
+                            if constexpr (kExit) hit_k = k;
                         }
                     }
                     if (hit_tri) {
@@ -601,6 +603,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                         if constexpr (kExit) {
                             if (hit_t <= exit_at) {
                                 t_out = hit_t;
+                                if (exit_tri) *exit_tri = leaf + hit_k;
                                 return true;
                             }
                         }
@@ -1014,22 +1017,46 @@ __device__ __forceinline__ void waveSync()
 // whenever it can matter, and any other result is > t_c, which decides the
 // capsule loop exactly as the true nearest hit (also > t_c) would.
 // (3) The capsule loop then runs as in traceWorldD.
+// occ (k_vis, may be null): the ray's occluder hint, a triangle index that
+// ended this ray before (DevState::visOcc).  A triangle hit at t <= t_c
+// decides "not visible" whatever else lies on the ray: the full search
+// would also stop at some hit <= t_c (every triangle with t <= t_c is
+// reachable under its 1.001 t_c bound, and a hit strictly nearer than the
+// current t_max is always accepted), so testing the hint first returns the
+// same answer; on a miss the full search runs and records its occluder.
+// numTris bounds the hint (any stale or foreign value is merely a miss).
 __device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restrict__ px,
                                             const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
-                                            int N, mp::Vec3 org, mp::Vec3 d, int target)
+                                            int N, mp::Vec3 org, mp::Vec3 d, int target,
+                                            uint16_t *occ = nullptr, uint32_t numTris = 0)
 {
     using namespace mp;
     Vec3 ct = v3(px[g0 + target], py[g0 + target], pz[g0 + target]);
     ct.z += kCapsuleRadius;
     const float t_c = intersectRayZOriginCapsule(org - ct, d, kCapsuleRadius, kCapsuleSegment);
     if (t_c == 0) return false;
+    if (occ) {
+        const uint32_t hint = *occ;
+        if (hint < numTris) {
+            const Vec3 inv_d = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+            const RayTxfmD tx = rayTxfm(d, inv_d);
+            Vec3 a, bb, c;
+            loadTri(b, (int)hint, a, bb, c);
+            float th;
+            if (rayTri(a, bb, c, tx, org, t_c * 1.001f, th) && th <= t_c) return false;
+        }
+    }
     float min_t = kFltMax;
     float tb;
+    int occ_tri = -1;
     // Any triangle hit at t <= t_c already decides the query: the closest
     // hit is then <= t_c, and the target only wins with t_c < closest
     // (utils.cpp:57-69 `t < min_hit_t`), so the search stops there.
-    if (bvhTraceRayT<true>(b, org, d, tb, t_c * 1.001f, t_c)) {
-        if (tb <= t_c) return false;
+    if (bvhTraceRayT<true>(b, org, d, tb, t_c * 1.001f, t_c, occ ? &occ_tri : nullptr)) {
+        if (tb <= t_c) {
+            if (occ) *occ = (uint16_t)occ_tri;
+            return false;
+        }
         min_t = tb;
     }
     int ent = -1;

@@ -2776,7 +2776,12 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
         const float len = length(to_test);
         to_test = to_test / len;
-        const bool seen = visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target);
+#ifndef MPENV_VIS_OCC
+#define MPENV_VIS_OCC 1
+#endif
+        uint16_t *occ = MPENV_VIS_OCC ? S.visOcc + (g * T + k) * 4 + p : nullptr;
+        const bool seen = visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target, occ,
+                                      (uint32_t)(sc.numVerts / 3));
         if (seen) atomicOr(&masks[(int)(g - agent0)], 1u << k);
         if (S.stats) statAdd(S.stats + kStatLosSeen, seen ? 1u : 0u);
     }

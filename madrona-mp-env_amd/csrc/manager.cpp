@@ -639,6 +639,8 @@ static void allocState(mpenv_manager &m)
     S.dmg = m.alloc<float>(A * kMaxTeamSize);
     S.dmgStride = (int64_t)A;
     S.visMask = m.alloc<uint8_t>(A);
+    S.visOcc = m.alloc<uint16_t>((size_t)A * S.T * 4);
+    HIP_CHECK(hipMemsetAsync(S.visOcc, 0xff, sizeof(uint16_t) * (size_t)A * S.T * 4, m.stream));
     S.exploreBits = m.alloc<uint64_t>(A * kExploreTiles);
     S.filtLast = m.alloc<int32_t>(W * 6);
     S.zoneStats = m.alloc<int32_t>(W * 25);
@@ -742,6 +744,7 @@ static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_
 #undef MP_SL_W
     G.dmg = S.dmg + g0; // stride stays S.dmgStride
     G.visMask = S.visMask + g0;
+    G.visOcc = S.visOcc + g0 * S.T * 4;
     G.exploreBits = S.exploreBits + g0 * kExploreTiles;
     G.filtLast = S.filtLast + w0 * 6;
     G.resetKeys = S.resetKeys + g0 * 11;
