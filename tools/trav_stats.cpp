@@ -3,6 +3,10 @@
 // ray for the reference child order and for front-to-back order.
 //
 //   trav_stats SCENE_DIR RAYS.f32   (RAYS: n x 6 floats, origin + direction)
+//   TRAV_HINT=PREV.f32 trav_stats SCENE_DIR RAYS.f32
+//       temporal-hint model: PREV holds the same ray slots one step earlier
+//       (tools/dump_lidar_rays.py at step s - 1); each ray first tests the
+//       triangle its slot hit then and starts with t_max = that hit's t
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -122,13 +126,16 @@ static void buildOctOrder()
     }
 }
 
-static void trace(const float *o, const float *d, int mode, Stats &st)
+static int g_lastTri = -1; // closest-hit triangle of the last trace() (-1: none)
+
+static void trace(const float *o, const float *d, int mode, Stats &st, float tmax0 = 3.4e38f)
 {
     const bool ftb = mode == 1;
     const int oct = (d[0] < 0 ? 1 : 0) | (d[1] < 0 ? 2 : 0) | (d[2] < 0 ? 4 : 0);
     float inv[3];
     for (int k = 0; k < 3; k++) inv[k] = d[k] == 0 ? 1e7f : 1.f / d[k];
-    float tmax = 3.4e38f;
+    float tmax = tmax0;
+    g_lastTri = -1;
     std::vector<int> stack = { 0 };
     while (!stack.empty()) {
         st.maxStack = std::max(st.maxStack, (double)stack.size());
@@ -159,7 +166,10 @@ static void trace(const float *o, const float *d, int mode, Stats &st)
                     st.tris++;
                     st.slotTris.back()[i]++;
                     float t;
-                    if (tri(&verts[(leaf + k) * 9], o, d, tmax, t)) tmax = t;
+                    if (tri(&verts[(leaf + k) * 9], o, d, tmax, t)) {
+                        tmax = t;
+                        g_lastTri = leaf + k;
+                    }
                 }
             } else {
                 kids[nk++] = { tn, n.children[i] };
@@ -417,6 +427,63 @@ int main(int argc, char **argv)
                mode ? "mean-dir" : "lane-0  ", fw.nodeIters * 64 / nf, fw.triIters * 64 / nf, fw.laneBoxes / nf, fw.laneTris / nf);
         printf("packet (%s order) rear waves:    lockstep node iters/ray %.2f tri iters/ray %.2f | lane boxes/ray %.2f lane tris/ray %.2f\n",
                mode ? "mean-dir" : "lane-0  ", rr.nodeIters * 64 / nr, rr.triIters * 64 / nr, rr.laneBoxes / nr, rr.laneTris / nr);
+    }
+    if (const char *hp = getenv("TRAV_HINT")) {
+        // Temporal hint: HP holds the same ray slots one step earlier; each
+        // ray first tests the triangle its slot hit then (one test), and the
+        // octant traversal starts with t_max = that hit's t.  Also the ideal
+        // bound (t_max0 = the ray's own closest hit).
+        FILE *hf = fopen(hp, "rb");
+        std::vector<float> prev;
+        while (fread(buf, 4, 6, hf) == 6) prev.insert(prev.end(), buf, buf + 6);
+        fclose(hf);
+        if (prev.size() != rays.size()) { fprintf(stderr, "hint file size differs\n"); return 1; }
+        for (int variant = 0; variant < 3; variant++) {
+            double lsPops = 0, lsTris = 0, lanePops = 0, laneTris = 0, hintHits = 0;
+            for (size_t w0 = 0; w0 < n; w0 += 64) {
+                std::vector<Stats> lanes;
+                double mp = 0;
+                for (size_t r = w0; r < std::min(n, w0 + 64); r++) {
+                    float t0 = 3.4e38f;
+                    if (variant == 1) {
+                        Stats tmp;
+                        trace(&prev[6 * r], &prev[6 * r + 3], 2, tmp);
+                        const int ht = g_lastTri;
+                        float th;
+                        if (ht >= 0 && tri(&verts[ht * 9], &rays[6 * r], &rays[6 * r + 3], 3.4e38f, th)) {
+                            t0 = th;
+                            hintHits++;
+                        }
+                    } else if (variant == 2) {
+                        Stats tmp;
+                        trace(&rays[6 * r], &rays[6 * r + 3], 2, tmp);
+                        if (g_lastTri >= 0) {
+                            float th;
+                            tri(&verts[g_lastTri * 9], &rays[6 * r], &rays[6 * r + 3], 3.4e38f, th);
+                            t0 = th * 1.000001f;
+                        }
+                    }
+                    Stats one;
+                    trace(&rays[6 * r], &rays[6 * r + 3], 2, one, t0);
+                    lanes.push_back(one);
+                    mp = std::max(mp, one.pops);
+                    lanePops += one.pops;
+                    laneTris += one.tris;
+                }
+                lsPops += mp * 64;
+                for (int it = 0; it < (int)mp; it++)
+                    for (int i = 0; i < 4; i++) {
+                        int m = 0;
+                        for (auto &L : lanes)
+                            if (it < (int)L.slotTris.size()) m = std::max(m, L.slotTris[it][i]);
+                        lsTris += m * 64;
+                    }
+            }
+            printf("%s: lockstep node iters/ray %.2f tri tests/ray %.2f | lane pops/ray %.2f tris/ray %.2f | hint hits %.3f\n",
+                   variant == 0 ? "octant, no hint   " : variant == 1 ? "octant, prev hint " : "octant, ideal t0  ",
+                   lsPops / n, lsTris / n, lanePops / n, laneTris / n, hintHits / n);
+        }
+        return 0;
     }
     if (getenv("TRAV_PACKET_ONLY")) return 0;
     // while-while with postponed triangles, octant order
