@@ -3401,10 +3401,6 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
     for (int it = 0; it < iters; it++) {
         const uint32_t task = (xcdBlockId() * iters + it) * kLidarWaves + wave; // wave-uniform
         if (task >= ntasks) break;
-        // Lane id read inside the loop (volatile: not hoisted), so the
-        // lane-derived offsets are formed per task instead of living as
-        // loop invariants across the traversal, which at 64 VGPRs the
-        // compiler would spill to scratch.
         const uint32_t unit = task / 5u, sub = task - unit * 5u;
         const bool fwd = sub < 4u;
 #ifdef MPENV_LAB_NO_REAR
@@ -3412,11 +3408,14 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
 #endif
         // The ray of lane `ln`: a tail unit's lanes past A trace a copy of
         // the last agent's rays and store nothing.
-        auto makeRay = [&](uint32_t ln, uint32_t &g, bool &valid, uint32_t &kk, Vec3 &ray_o, Vec3 &dir) {
+        auto rayIndex = [&](uint32_t ln, uint32_t &g, bool &valid, uint32_t &kk) {
             const uint32_t g_raw = unit * 4u + (fwd ? sub : (ln >> 4));
             valid = g_raw < A;
             g = valid ? g_raw : A - 1u;
             kk = fwd ? ln : (ln & 15u); // ray slot within the forward / rear fan
+        };
+        auto makeRay = [&](uint32_t ln, uint32_t &g, bool &valid, uint32_t &kk, Vec3 &ray_o, Vec3 &dir) {
+            rayIndex(ln, g, valid, kk);
             const uint32_t h = fwd ? (kk >> 5) : (kk >> 3), x = fwd ? (kk & 31u) : (kk & 7u);
             const Quat q = fwd ? ldAimRot(S, g) : ldRot(S, g);
             const Vec3 dir_fwd = rotateVec(q, kFwd);
@@ -3454,10 +3453,17 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // from an opaque copy of g (nothing but the ray lives across it).
         float tb;
         const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ, kLidarRot, true>(ob, ray_o, dir, tb, kFltMax, 0.f);
-        uint32_t go = g;
-        asm volatile("" : "+v"(go));
-        const uint32_t w = __umulhi(go, S.nMagic); // g / N (engine.h)
-        const uint32_t i = go - w * N;
+        // The lane id again (volatile) and the ray's indices from it: integer
+        // work only, so they need not live across the traversal (at 64 VGPRs
+        // they were spilled to scratch).  Shuffles below address lanes from
+        // this id too (ds_bpermute), not from a lane id kept for the kernel.
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        rayIndex(lane, g, valid, kk);
+        auto shflLane = [](float v, uint32_t src) {
+            return __int_as_float(__builtin_amdgcn_ds_bpermute((int)(src << 2), __float_as_int(v)));
+        };
+        const uint32_t w = __umulhi(g, S.nMagic); // g / N (engine.h)
+        const uint32_t i = g - w * N;
         const int64_t g0 = (int64_t)w * N;
         WorldHit hw;
         if (MPENV_LIDAR_WAVECULL && fwd) {
@@ -3475,7 +3481,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             float min_t = bhit ? tb : kFltMax;
             float mx = min_t;
 #pragma unroll
-            for (int sh = 32; sh >= 1; sh >>= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
+            for (int sh = 32; sh >= 1; sh >>= 1) mx = fmaxf(mx, shflLane(mx, lane ^ (uint32_t)sh));
             float cx = 0.f, cy = 0.f, cz = 0.f;
             bool keep = false;
             if (lane < N) {
@@ -3524,7 +3530,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             float min_t = bhit ? tb : kFltMax;
             float mx = min_t;
 #pragma unroll
-            for (int sh = 8; sh >= 1; sh >>= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
+            for (int sh = 8; sh >= 1; sh >>= 1) mx = fmaxf(mx, shflLane(mx, lane ^ (uint32_t)sh));
             const uint32_t gb = lane & 48u, jl = lane & 15u;
             float cx = 0.f, cy = 0.f, cz = 0.f;
             bool keep = false;
@@ -3544,7 +3550,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
                 const int j = __builtin_ctz(um);
                 um &= um - 1u;
                 const int src = (int)gb + j;
-                Vec3 co = v3(__shfl(cx, src, 64), __shfl(cy, src, 64), __shfl(cz, src, 64));
+                Vec3 co = v3(shflLane(cx, (uint32_t)src), shflLane(cy, (uint32_t)src), shflLane(cz, (uint32_t)src));
                 if (!((mine >> j) & 1u)) continue;
                 co.z += kCapsuleRadius;
                 const Vec3 tr = ray_o - co;
