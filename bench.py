@@ -92,6 +92,11 @@ def parse():
                          "loop: a random-init bf16 MLP reads every trainInterface observation each step "
                          "and its argmax actions are the next step inputs (the env side of a "
                          "jax_train-style self-play loop; the policy forward is inside the timed window)")
+    ap.add_argument("--path", choices=["step", "stream"], default="step",
+                    help="step = copy_actions + step_async (the headline: outputs stay in the engine's "
+                         "zero-copy tensors); stream = Manager::gpuStreamStep (mgr.cpp:614-645), the XLA "
+                         "custom-call path of scripts/jax_train.py: every trainInterface input copied from "
+                         "caller buffers, the step, every output copied into caller buffers")
     ap.add_argument("--policy-hidden", type=int, default=512, help="policy MLP width (--actions policy)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--share-device", action="store_true",
@@ -167,6 +172,8 @@ def load_profile(path, workload):
         d = json.load(open(path))
     except (OSError, ValueError):
         return {}
+    if "workloads" in d:
+        return d["workloads"].get(workload, {})
     return d if d.get("workload") == workload else {}
 
 
@@ -214,6 +221,49 @@ def make_policy(sim, hidden, dev):
 
     run.actions = act
     return run
+
+
+def stream_buffers(sim, ring, dev):
+    """Caller-owned buffers for Manager::gpuStreamStep, ordered as the
+    trainInterface (inputs then outputs, mgr.cpp:2383-2431), the layout an
+    XLA custom call hands over.  The action inputs of step s point into the
+    HBM ring (split into the discrete [A][4] and discrete-aim [A][2]
+    tensors); the other inputs hold the engine's values after Manager::init,
+    so copying them in every step changes nothing; outputs are fresh
+    buffers.  Returns one pointer list per ring slot, the bytes each step
+    copies, and the tensors to keep alive."""
+    import torch
+
+    ti = sim.train_interface()
+    ins = {n: t.to_torch() for n, t in ti["inputs"].items()}
+    outs = {n: t.to_torch() for n, t in ti["outputs"].items()}
+    A = ring.shape[1]
+    disc = ring[:, :, :4].contiguous()
+    aim = ring[:, :, 4:6].contiguous()
+    keep = [disc, aim]
+    fixed = {}
+    for n, t in ins.items():
+        if n not in ("discrete", "aim"):
+            fixed[n] = t.clone()
+            keep.append(fixed[n])
+    obufs = [torch.empty_like(t) for t in outs.values()]
+    keep += obufs
+    ptrs = []
+    for k in range(ring.shape[0]):
+        row = []
+        for n, t in ins.items():
+            if n == "discrete":
+                row.append(disc[k].data_ptr())
+            elif n == "aim":
+                row.append(aim[k].data_ptr())
+            else:
+                row.append(fixed[n].data_ptr())
+        row += [b.data_ptr() for b in obufs]
+        ptrs.append(row)
+    nbytes = sum(t.numel() * t.element_size() for t in ins.values()) + \
+        sum(t.numel() * t.element_size() for t in outs.values())
+    assert disc[0].numel() == A * 4
+    return ptrs, nbytes, keep
 
 
 def main():
@@ -289,9 +339,18 @@ def main():
         make_exchange(exchange, sim, group=xgroup)
 
     policy = make_policy(sim, args.policy_hidden, dev) if args.actions == "policy" else None
+    stream_ptrs = None
+    if args.path == "stream":
+        if args.actions != "tape":
+            raise SystemExit("--path stream runs the tape actions only")
+        stream_ptrs, stream_bytes, _keep = stream_buffers(sim, ring, dev)
 
     def one_step(s):
-        if policy is not None:
+        if stream_ptrs is not None:
+            # gpuStreamStep: inputs from the caller's buffers (the step's
+            # actions straight from the ring), the step, outputs copied out
+            sim.gpu_stream_step(sptr, stream_ptrs[s % RING])
+        elif policy is not None:
             # actions from the observations the previous step left (no tape)
             sim.copy_actions(policy(), sptr)
         elif args.actions == "combat":
@@ -360,7 +419,8 @@ def main():
         prof_pass = (timings, counts)
 
     workload = f"simple_map {ts}v{ts} x {W} worlds/GPU" + ("" if args.bots == "none" else f" + A* bots ({args.bots})") \
-        + {"tape": "", "combat": " + combat actions", "policy": f" + MLP policy loop (bf16, {args.policy_hidden} wide)"}[args.actions]
+        + {"tape": "", "combat": " + combat actions", "policy": f" + MLP policy loop (bf16, {args.policy_hidden} wide)"}[args.actions] \
+        + ("" if args.path == "step" else " + gpuStreamStep buffer copies")
     result = {
         "metric": f"env steps/sec x agents (whole node), simple_map {ts}v{ts} @ {W} worlds"
                   + ("" if world_size == 1 else f"/GPU x {world_size} GPUs"),
@@ -399,6 +459,9 @@ def main():
     }
     if learner is not None:
         result["exchange_bytes_per_step"] = learner.bytes_per_step()
+    if stream_ptrs is not None:
+        result["config"]["path"] = "gpuStreamStep (mgr.cpp:614-645)"
+        result["stream_copy_bytes_per_step"] = stream_bytes
     if prof_pass is not None:
         timings, counts = prof_pass
         steps = args.steps

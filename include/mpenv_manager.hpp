@@ -6,10 +6,15 @@
 //   * madrona::py::Tensor -> madronaMPEnv::Tensor (ptr, type, dims, gpu id),
 //     still a zero-copy view of engine-owned device memory (mgr.cpp:295-301).
 //   * Errors throw std::runtime_error (the reference FATALs / asserts).
-//   * ExecMode::CPU, the viewer (VizState, vizStep), getWorldContext and
-//     the ExploreAction/CoarsePvPAction setters are out of scope
-//     and throw.  Full-team tensors, record/replay and event logs are
-//     implemented (fullTeam*Tensor getters, Config log paths).
+//   * Out of scope, declared with the reference's signatures
+//     so callers written against mgr.hpp compile, and throwing
+//     std::runtime_error when called: ExecMode::CPU (rejected at
+//     construction), a non-null VizState* (the viewer), vizStep,
+//     getWorldContext (Madrona's per-world ECS context, opaque Engine here),
+//     setExploreAction and setCoarsePvPAction (Task::Explore and the
+//     coarse-action path, neither on the Zone step graph).  Full-team
+//     tensors, record/replay and event logs are implemented (fullTeam*Tensor
+//     getters, Config log paths).  cpuJAXInit/Step are no-ops as in mgr.hpp.
 //   * gpuStreamInit/Step take the HIP stream as void*.
 #pragma once
 
@@ -57,6 +62,13 @@ struct PvPDiscreteAction { int32_t moveAmount, moveAngle, fire, stand; };
 struct PvPAimAction { float yaw, pitch; };
 struct PvPDiscreteAimAction { int32_t yaw, pitch; };
 struct AgentPolicy { int32_t idx; };
+struct ExploreAction { int32_t moveAmount, moveAngle, rotate, mantle; }; // types.hpp:166-171
+struct CoarsePvPAction { int32_t moveAmount, moveAngle, facing; };       // types.hpp:205-209
+
+// Opaque: the viewer's state (viz.hpp:16) and Madrona's per-world context
+// (mgr.hpp:130); neither exists in this engine.
+struct VizState;
+struct Engine;
 
 // mgr.hpp:16-24
 struct MapConfig {
@@ -121,8 +133,10 @@ public:
         uint32_t worldIDOffset = 0; // extension: first global world id (sharding)
     };
 
-    explicit Manager(const Config &cfg)
+    // mgr.hpp:54-56; viz must be null (there is no viewer)
+    explicit Manager(const Config &cfg, VizState *viz = nullptr)
     {
+        if (viz != nullptr) throw std::runtime_error("mpenv: the viewer (VizState) is not part of this engine");
         const std::string dir = sceneDir(cfg.map);
         if (cfg.map.mapOffset.x != 0.f || cfg.map.mapOffset.y != 0.f || cfg.map.mapOffset.z != 0.f ||
             cfg.map.mapRotation != 0.f)
@@ -155,6 +169,9 @@ public:
 
     void init() { check(mpenv_init(mgr_)); }
     void step() { check(mpenv_step(mgr_)); }
+    void vizStep() { outOfScope("vizStep (viewer)"); }
+    inline void cpuJAXInit(void **, void **) {} // mgr.hpp:64-65: no-ops there too
+    inline void cpuJAXStep(void **, void **) {}
     void gpuStreamInit(void *strm, void **buffers) { check(mpenv_gpu_stream_init(mgr_, strm, buffers)); }
     void gpuStreamStep(void *strm, void **buffers) { check(mpenv_gpu_stream_step(mgr_, strm, buffers)); }
     // extension: the Step graph enqueued on a caller stream without a sync
@@ -225,7 +242,11 @@ public:
 
     ExecMode execMode() const { return execMode_; }
 
+    Engine &getWorldContext(int32_t) { outOfScope("getWorldContext (Madrona ECS context)"); }
+
     void triggerReset(int32_t world_idx) { check(mpenv_trigger_reset(mgr_, world_idx)); }
+    void setExploreAction(int32_t, ExploreAction) { outOfScope("setExploreAction (Task::Explore)"); }
+    void setCoarsePvPAction(int32_t, int32_t, CoarsePvPAction) { outOfScope("setCoarsePvPAction"); }
     void setPvPAction(int32_t world_idx, int32_t agent_idx, PvPDiscreteAction discrete, PvPAimAction aim,
                       PvPDiscreteAimAction aim_discrete)
     {
@@ -250,6 +271,11 @@ public:
     mpenv_manager *handle() const { return mgr_; }
 
 private:
+    [[noreturn]] static void outOfScope(const char *what)
+    {
+        throw std::runtime_error(std::string("mpenv: ") + what + " is out of scope for this engine (DESIGN.md §8)");
+    }
+
     static void check(int rc)
     {
         if (rc != MPENV_OK) throw std::runtime_error(std::string("mpenv: ") + mpenv_last_error());

@@ -226,6 +226,19 @@ PYBIND11_MODULE(madrona_mp_env, m)
             check(mpenv_combat_actions(s.h->mgr, reinterpret_cast<const int32_t *>(tape),
                                        reinterpret_cast<int32_t *>(out), mode, reinterpret_cast<void *>(stream)));
         }, py::arg("tape"), py::arg("out") = 0, py::arg("mode") = 1, py::arg("stream") = 0)
+        // Manager::gpuStreamInit / gpuStreamStep (mgr.cpp:507-645): the flat
+        // buffer array of the XLA custom call -- trainInterface inputs then
+        // outputs, caller-owned device pointers (0 = skip that tensor).
+        .def("gpu_stream_init", [](PySimManager &s, uintptr_t stream, const std::vector<uintptr_t> &bufs) {
+            std::vector<void *> b(bufs.size());
+            for (size_t k = 0; k < bufs.size(); k++) b[k] = reinterpret_cast<void *>(bufs[k]);
+            check(mpenv_gpu_stream_init(s.h->mgr, reinterpret_cast<void *>(stream), b.data()));
+        }, py::arg("stream"), py::arg("buffers"))
+        .def("gpu_stream_step", [](PySimManager &s, uintptr_t stream, const std::vector<uintptr_t> &bufs) {
+            std::vector<void *> b(bufs.size());
+            for (size_t k = 0; k < bufs.size(); k++) b[k] = reinterpret_cast<void *>(bufs[k]);
+            check(mpenv_gpu_stream_step(s.h->mgr, reinterpret_cast<void *>(stream), b.data()));
+        }, py::arg("stream"), py::arg("buffers"))
         .def("set_world_groups", [](PySimManager &s, int32_t g) { check(mpenv_set_world_groups(s.h->mgr, g)); })
         .def("world_groups", [](PySimManager &s) { int32_t g = 0; check(mpenv_world_groups(s.h->mgr, &g)); return g; })
         .def("enable_kernel_timing", [](PySimManager &s, bool on) { check(mpenv_enable_kernel_timing(s.h->mgr, on)); })

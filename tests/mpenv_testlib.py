@@ -513,17 +513,24 @@ def explore_visited(sim):
 
 
 def compare(a, b, name, float_rtol=0.0):
-    """Bit-exact for integer/bool data; floats exact unless float_rtol > 0."""
+    """Byte-exact: integers by value, floats by their bit patterns (as
+    uint32), so +0 / -0 differ and a NaN only matches a NaN with the same
+    payload and sign.  float_rtol > 0 (no caller uses it; the north star's
+    1e-5 ceiling) relaxes non-NaN floats to that relative tolerance."""
     assert a.shape == b.shape, (name, a.shape, b.shape)
     if a.dtype.kind == "f":
-        same = (a == b) | (np.isnan(a) & np.isnan(b))
+        assert a.dtype == np.float32 and b.dtype == np.float32, (name, a.dtype, b.dtype)
+        same = np.ascontiguousarray(a).view(np.uint32) == np.ascontiguousarray(b).view(np.uint32)
         if float_rtol > 0:
             same |= np.abs(a - b) <= float_rtol * np.maximum(np.abs(a), np.abs(b))
         if not same.all():
             idx = np.argwhere(~same)
             i0 = tuple(idx[0])
+            ab = np.ascontiguousarray(a).view(np.uint32)[i0]
+            bb = np.ascontiguousarray(b).view(np.uint32)[i0]
             raise AssertionError(
-                f"{name}: {len(idx)} mismatches, first at {i0}: engine={a[i0]!r} oracle={b[i0]!r}")
+                f"{name}: {len(idx)} mismatches, first at {i0}: engine={a[i0]!r} (0x{ab:08x}) "
+                f"oracle={b[i0]!r} (0x{bb:08x})")
     else:
         if not np.array_equal(a, b):
             idx = np.argwhere(a != b)

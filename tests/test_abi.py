@@ -125,3 +125,18 @@ def test_cpp_manager_headless_builds_and_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     r = subprocess.run([exe, "CUDA", "2", "1", T.SCENE], capture_output=True, text=True)
     assert r.returncode != 0 and "device" in r.stderr.lower()
+
+
+def test_caller_written_against_mgr_hpp_compiles_and_out_of_scope_parts_throw(tmp_path):
+    """tests/mgr_hpp_caller.cpp names every public Manager method with the
+    reference's signature (src/mgr.hpp:54-157, incl. Manager(cfg, VizState*),
+    vizStep, getWorldContext, setExploreAction, setCoarsePvPAction) and runs
+    without a GPU: a non-null VizState and ExecMode::CPU are refused."""
+    exe = str(tmp_path / "mgr_caller")
+    pkg = T.PKG
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(T.ROOT, "include"),
+                    os.path.join(T.ROOT, "tests", "mgr_hpp_caller.cpp"), "-o", exe, "-L", pkg, "-lmpenv",
+                    f"-Wl,-rpath,{pkg}"], check=True)
+    r = subprocess.run([exe, T.SCENE], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "mgr.hpp caller ok" in r.stdout

@@ -81,6 +81,70 @@ def test_every_world_of_the_bench_window_matches_oracle(ts, W, warmup, steps, ev
     o.close()
 
 
+COMBAT = [
+    # team_size, worlds, steps, compare every
+    (6, 16384, 120, 20),   # C3
+    (3, 4096, 300, 25),    # C2
+]
+
+
+@pytest.mark.parametrize("ts,W,steps,every", COMBAT, ids=["C3_6v6x16384", "C2_3v3x4096"])
+def test_every_world_in_the_combat_regime_matches_oracle(ts, W, steps, every):
+    """bench.py --actions combat, world by world: every step the device
+    aim-bot (mpenv_combat_actions mode 1: fire at the first visible
+    opponent, else turn and run toward the zone, reload an empty magazine)
+    rewrites the tape row from the engine's observations; the same actions
+    must come out of its numpy twin (seek_combat_actions) over the ORACLE's
+    observations, and the oracle then steps the whole batch with them.  Every
+    STEP_OUTPUT and debug export of every world is compared byte for byte
+    (floats by bit pattern), so respawn scoring (utils.cpp:734-948), kill
+    bookkeeping and last-known updates are checked at full batch."""
+    t_start = time.time()
+    N = 2 * ts
+    A = W * N
+    e = T.Engine(W, ts)
+    e.set_world_groups(2)  # as bench.py's timed pass
+    o = T.Oracle(W, ts)
+    for sim in (e, o):
+        sim.put_ctrl([0, 1, 1])
+        sim.init()
+    ring = T.mpenv_tape.tape_ring(SEED, 0, A, RING)
+    dev_ring = e.mem.upload(ring)
+    dev_acts = e.mem.upload(np.zeros((A, 6), np.int32))
+    threads = T.usable_cpus()
+    e.enable_stats(True)
+
+    def compare_all(where):
+        for n in ALL:
+            T.compare(e.get(n), o.get(n), f"{n} @ {where}")
+
+    compare_all("init")
+    t_oracle = 0.0
+    acts = np.empty((A, 6), np.int32)
+    for s in range(steps):
+        e.combat_actions(dev_ring + (s % RING) * A * 24, dev_acts, 1)
+        e.mem.d2h(dev_acts, acts.nbytes, acts)
+        twin = T.seek_combat_actions(o, s, base=ring[s % RING])
+        T.compare(acts, twin, f"combat actions @ step {s}")
+        e.copy_actions(dev_acts)
+        e.step()
+        t_oracle += o.lib.oracle_run_threaded(o.h, 1, threads, twin.ctypes.data, 1)
+        if (s + 1) % every == 0 or s == steps - 1:
+            compare_all(f"step {s}")
+        else:
+            for n in ("REWARD", "DONE", "HP", "ALIVE", "SELF_OBSERVATION"):
+                T.compare(e.get(n), o.get(n), f"{n} @ step {s}")
+    st = e.read_stats()
+    e.mem.free(dev_ring)
+    e.mem.free(dev_acts)
+    print(f"\n{ts}v{ts} x {W} combat: {steps} steps, every world compared ({len(ALL)} exports every {every} "
+          f"steps); {st['shot_rays']} shots, {st['hit_agents']} agents hit, {st['kills']} kills; oracle "
+          f"{t_oracle:.1f} s on {threads} threads, test {time.time() - t_start:.1f} s")
+    assert st["kills"] > 0 and st["hit_agents"] > 0
+    e.close()
+    o.close()
+
+
 C4_SHARDS, C4_WORLDS, C4_TS, C4_STEPS = 8, 16384, 6, 300
 
 

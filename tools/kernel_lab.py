@@ -80,8 +80,15 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
     lib.mpenv_copy_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     per = ring[0].nbytes
 
+    lib.mpenv_combat_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    combat = os.environ.get("LAB_ACTIONS", "tape") == "combat"
+
     def step(s):
-        lib.mpenv_copy_actions(h, C.c_void_p(dptr.value + (s % 16) * per), None)
+        if combat:
+            # bench.py --actions combat: the device aim-bot over the tape
+            lib.mpenv_combat_actions(h, C.c_void_p(dptr.value + (s % 16) * per), None, 1, None)
+        else:
+            lib.mpenv_copy_actions(h, C.c_void_p(dptr.value + (s % 16) * per), None)
         lib.mpenv_step(h)
 
     lib.mpenv_set_world_groups.argtypes = [C.c_void_p, C.c_int32]

@@ -99,8 +99,17 @@ def main(tag, src):
                "per_kernel": {k: v.get("hbm_bytes_per_launch") for k, v in ks.items()},
                "valu_insts_per_launch": {k: v.get("sq_insts_valu") for k, v in ks.items()},
                "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per whole-batch launch, separate --pmc passes"}
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
+    # one entry per workload (bench.py picks the one it runs)
+    path = os.path.join(prof, "pmc_traffic.json")
+    try:
+        allw = json.load(open(path))
+    except (OSError, ValueError):
+        allw = {}
+    if "workloads" not in allw:
+        allw = {"workloads": {allw["workload"]: allw} if "workload" in allw else {}}
+    allw["workloads"][traffic["workload"]] = traffic
+    with open(path, "w") as f:
+        json.dump(allw, f, indent=1)
     for k, v in ks.items():
         print(k, v)
 

@@ -10,13 +10,14 @@
 # Outputs under gpurun_out/prof_<tag>/; tools/pmc_summary.py condenses them.
 set -o pipefail
 TAG=${1:-r02}
-PMC_ARGS=${PMC_ARGS:---steps 200 --warmup 100 --world-groups 1 --no-profile-pass --cpu-baseline off}
+# BENCH_ARGS: extra bench.py flags for every pass (e.g. "--actions combat")
+PMC_ARGS="${PMC_ARGS:---steps 200 --warmup 100 --world-groups 1 --no-profile-pass --cpu-baseline off} $BENCH_ARGS"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 bench.py --cpu-baseline off > $OUT/trace_bench.json && \
+    python3 bench.py --cpu-baseline off $BENCH_ARGS > $OUT/trace_bench.json && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- \
     python3 bench.py $PMC_ARGS > $OUT/fetch_bench.json && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- \
