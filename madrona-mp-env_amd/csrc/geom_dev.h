@@ -487,7 +487,25 @@ __device__ __forceinline__ bool rayTriRot(const MP_LDS lf4 *p, float o0, float o
 // kExit: stop as soon as a hit at t <= exit_at is found (t_out is then
 // that hit, not necessarily the closest; callers that only compare the
 // closest hit with exit_at get the same answer).
-template <bool kExit, bool kPerm = false, int kNodeQ = 4, bool kRot = false, bool kOctImage = false>
+// kLex (lidar, DESIGN.md §2 definition 12): the order-independent closest
+// hit -- the smallest t = fl(T * fl(1 / det)) over every triangle the ray
+// hits.  Boxes and triangles are tested against t_best * (1 + 2^-20)
+// (kLexRelax), which keeps every triangle whose t ties or beats t_best:
+// t <= t_best implies T <= fl(fl(t_best * kLexRelax) * det) for the two
+// roundings of t, and such a triangle's box is entered below that bound.
+// Hits at t = -0 and +0 (an origin on a vertex or edge) are ordered -0
+// first: lexLessD compares bit patterns as signed integers, the total order
+// of {-0} and [+0, inf].  Boxes are entered when t_near <= t_far + |t_far| *
+// 2^-16 + 2^-8: a child box quantised at its node's boundary has no margin,
+// and a ray aimed exactly at such a vertex can miss it by slab rounding while
+// hitting the triangle; with the slack the traversal visits every triangle a
+// brute-force loop would find nearer than the bound (the oracle applies the
+// same rule; tests/test_lidar_order.py checks it against brute force).
+constexpr float kLexRelax = 1.00000095367431640625f; // 1 + 2^-20
+constexpr float kBoxSlackRel = 1.52587890625e-5f, kBoxSlackAbs = 0.00390625f;
+__device__ __forceinline__ bool lexLessD(float a, float b) { return __float_as_int(a) < __float_as_int(b); }
+
+template <bool kExit, bool kPerm = false, int kNodeQ = 4, bool kRot = false, bool kOctImage = false, bool kLex = false>
 __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
                                              float t_max0, float exit_at, int *exit_tri = nullptr)
 {
@@ -524,7 +542,8 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
         rsw = tx.kx != kx0;
     }
 
-    float t_max = t_max0;
+    float t_max = kLex ? t_max0 * kLexRelax : t_max0; // kLex: the relaxed bound of t_best
+    float t_best = t_max0;
     bool ray_hit = false;
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
@@ -571,7 +590,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
 #else
             const float t_far = fmin_(fmin_(t_far_x, t_far_y), fmin_(t_far_z, t_max));
 #endif
-            if (t_near <= t_far) {
+            if (t_near <= (kLex ? fmaf(fabsf(t_far), kBoxSlackRel, t_far + kBoxSlackAbs) : t_far)) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;
                     const int ntri = (int)((node.triSize >> (8 * i)) & 0xffu);
@@ -603,12 +622,22 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                             h = rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t);
 #endif
                         }
+                        if constexpr (kLex) {
+                            if (h && lexLessD(hit_t, t_best)) {
+                                t_best = hit_t;
+                                t_max = t_best * kLexRelax;
+                                leaf_tmax = t_max;
+                                ray_hit = true;
+                            }
+                            continue;
+                        }
                         if (h) {
                             hit_tri = true;
                             leaf_tmax = hit_t;
                             if constexpr (kExit) hit_k = k;
                         }
                     }
+                    if (kLex) continue;
                     if (hit_tri) {
                         ray_hit = true;
                         t_max = hit_t;
@@ -626,7 +655,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
             }
         }
     }
-    t_out = t_max;
+    t_out = kLex ? t_best : t_max;
     return ray_hit;
 }
 

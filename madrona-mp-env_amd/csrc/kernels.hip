@@ -3452,7 +3452,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // capsules.  World / agent indices are formed after the traversal,
         // from an opaque copy of g (nothing but the ray lives across it).
         float tb;
-        const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ, kLidarRot, true>(ob, ray_o, dir, tb, kFltMax, 0.f);
+        const bool bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ, kLidarRot, true, true>(ob, ray_o, dir, tb, kFltMax, 0.f);
         // The lane id again (volatile) and the ray's indices from it: integer
         // work only, so they need not live across the traversal (at 64 VGPRs
         // they were spilled to scratch).  Shuffles below address lanes from

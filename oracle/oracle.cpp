@@ -241,9 +241,10 @@ struct Oracle {
     struct ZOBB { Vec3 pMin, pMax; float rotation; } subZones[8]; // level_gen.cpp:282-326
     std::vector<int32_t> astar;  // [T][T] (buildAStarLookup, built by the oracle)
     std::vector<int32_t> navAdj; // [T][3]
-    // Lidar child visit order (cfg.lidar_octant_order): per ray octant and
-    // node, the slot visited k-th (octantOrder()).
-    bool lidarOctant = false;
+    // Lidar closest-hit rule (cfg.lidar_octant_order: kLidarSlot / kLidarOctant /
+    // kLidarLex, bvhTraceRay); octOrder: per ray octant and node, the slot
+    // visited k-th (octantOrder()).
+    int lidarOrder = 0;
     std::vector<int8_t> octOrder; // [8][numNodes][4]
     int numNavTris = 0;
     std::vector<Vec3> verts;
@@ -362,7 +363,32 @@ int g_slabFma = 1;
 inline float slabT(float q, float dq, float oq) { return g_slabFma ? fma_(q, dq, oq) : q * dq + oq; }
 
 // mesh_bvh.inl:110-208 (MeshBVH::traceRay) + 360-431 (traceRayLeaf)
-bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_max = kFltMax, bool octant = false)
+// Lidar closest-hit rules (cfg.lidar_octant_order; DESIGN.md §2 definition 12):
+//   kLidarSlot   -- mesh_bvh.inl:160-204 as written: slots in order, each
+//                   accepted hit tightens t_max (the reference);
+//   kLidarOctant -- the round-2/3 octant child order (same acceptance);
+//   kLidarLex    -- order-independent: the smallest t = fl(T * fl(1 / det))
+//                   of the watertight test over every triangle the ray hits
+//                   (which triangle attains it is not observable), -0 below
+//                   +0 (an origin on a vertex or edge hits at t = -0 or +0:
+//                   lexLess compares the bit patterns as signed integers,
+//                   the total order of {-0} and [+0, inf]).  Boxes and triangles are tested
+//                   against t_best * (1 + 2^-20), so no triangle whose t ties
+//                   or beats the current best is ever pruned, whatever the
+//                   visit order (the product's fan lists rely on that).
+enum { kLidarSlot = 0, kLidarOctant = 1, kLidarLex = 2 };
+constexpr float kLexRelax = 1.00000095367431640625f; // 1 + 2^-20
+// kLidarLex box test: t_near <= fma(|t_far|, 2^-16, t_far + 2^-8) (as the engine).  A child box
+// quantised at its node's boundary has no margin (qMin clamps at 0), so a
+// ray aimed exactly at such a vertex can miss the box by slab rounding
+// although it hits the triangle; the slack keeps those boxes, so the
+// traversal visits every triangle a brute-force loop would find nearer than
+// the bound (tests/test_lidar_order.py checks equality with brute force).
+constexpr float kBoxSlackRel = 1.52587890625e-5f, kBoxSlackAbs = 0.00390625f;
+inline bool lexLess(float a, float b) { return (int32_t)f2u(a) < (int32_t)f2u(b); }
+
+bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_max = kFltMax, bool octant = false,
+                 bool lex = false)
 {
     // octant: visit each node's child slots in the order octantOrder()
     // defines for the ray's direction signs (the lidar's documented child
@@ -376,6 +402,8 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
     int sp = 0;
     stack[sp++] = 0;
     bool ray_hit = false;
+    float t_best = t_max; // kLidarLex: the smallest t so far
+    if (lex) t_max = t_best * kLexRelax;
     while (sp > 0) {
         int32_t node_idx = stack[--sp];
         const Node &node = o.nodes[node_idx];
@@ -403,9 +431,23 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
                                  fmax_(fmin_(t_near_y, t_far_y), fmax_(fmin_(t_near_z, t_far_z), 0.f)));
             float t_far = fmin_(fmax_(t_far_x, t_near_x),
                                 fmin_(fmax_(t_far_y, t_near_y), fmin_(fmax_(t_far_z, t_near_z), t_max)));
-            if (t_near <= t_far) {
+            if (t_near <= (lex ? fma_(fabs_(t_far), kBoxSlackRel, t_far + kBoxSlackAbs) : t_far)) {
                 if (node.children[i] & 0x80000000) {
                     int32_t leaf_idx = node.children[i] & ~0x80000000;
+                    if (lex) {
+                        for (int k = 0; k < node.triSize[i]; k++) {
+                            const int tri = leaf_idx + k;
+                            float t = 0.f;
+                            if (rayTriangleIntersection(o.verts[tri * 3 + 0], o.verts[tri * 3 + 1],
+                                                        o.verts[tri * 3 + 2], tx, ray_o, t_max, &t) &&
+                                lexLess(t, t_best)) {
+                                t_best = t;
+                                ray_hit = true;
+                                t_max = t_best * kLexRelax;
+                            }
+                        }
+                        continue;
+                    }
                     // traceRayLeaf
                     bool hit_tri = false;
                     float hit_t = 0.f;
@@ -429,7 +471,7 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
             }
         }
     }
-    *t_hit = t_max;
+    *t_hit = lex ? t_best : t_max;
     return ray_hit;
 }
 
@@ -617,11 +659,11 @@ struct HitResult {
 };
 
 // utils.cpp:10-72 traceRayAgainstWorld
-HitResult traceRayAgainstWorld(const Oracle &o, int w, Vec3 org, Vec3 d, bool octant = false)
+HitResult traceRayAgainstWorld(const Oracle &o, int w, Vec3 org, Vec3 d, int order = kLidarSlot)
 {
     float min_hit_t = kFltMax;
     float t_bvh;
-    bool hit = bvhTraceRay(o, org, d, &t_bvh, kFltMax, octant);
+    bool hit = bvhTraceRay(o, org, d, &t_bvh, kFltMax, order == kLidarOctant, order == kLidarLex);
     if (hit) min_hit_t = t_bvh;
     int hit_entity = -1;
     for (int j = 0; j < o.N; j++) {
@@ -2524,7 +2566,7 @@ void pvpLidar(Oracle &o, int w, int i)
         float x = -cosf_(theta);
         float y = sinf_(theta);
         Vec3 dir = normalize(x * right + y * fwd);
-        HitResult h = traceRayAgainstWorld(o, w, ray_o, dir, o.lidarOctant);
+        HitResult h = traceRayAgainstWorld(o, w, ray_o, dir, o.lidarOrder);
         if (h.hit) {
             bool wall = h.entity == -1;
             bool tm = !wall && o.agent(w, h.entity).team == ag.team;
@@ -3233,7 +3275,7 @@ void *oracle_create(const oracle_config *cfg)
         for (int i = 0; i < cfg->num_bvh_verts; i++)
             o->verts[i] = v3(cfg->bvh_verts[3 * i], cfg->bvh_verts[3 * i + 1], cfg->bvh_verts[3 * i + 2]);
         if (o->simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) addMiddleSpawnCells(*o);
-        o->lidarOctant = cfg->lidar_octant_order != 0;
+        o->lidarOrder = cfg->lidar_octant_order;
         o->octOrder = octantOrder(o->nodes);
         {
             // bots' navmesh and A* table, built here from navmesh.bin
@@ -3534,14 +3576,33 @@ float oracle_sphere_cast(void *h, const float *org, const float *d, float r, flo
 
 void oracle_set_slab_fma(int32_t on) { g_slabFma = on ? 1 : 0; }
 
-void oracle_trace_ray_batch(void *h, int32_t n, const float *org, const float *d, int32_t octant, float *t_out,
+void oracle_trace_ray_batch(void *h, int32_t n, const float *org, const float *d, int32_t order, float *t_out,
                             int32_t *hit_out)
 {
     Oracle &o = *static_cast<Oracle *>(h);
+    const int ntri = (int)o.verts.size() / 3;
     for (int32_t k = 0; k < n; k++) {
         float t = 0.f;
-        hit_out[k] = bvhTraceRay(o, v3(org[3 * k], org[3 * k + 1], org[3 * k + 2]),
-                                 v3(d[3 * k], d[3 * k + 1], d[3 * k + 2]), &t, kFltMax, octant != 0) ? 1 : 0;
+        const Vec3 ro = v3(org[3 * k], org[3 * k + 1], org[3 * k + 2]), rd = v3(d[3 * k], d[3 * k + 1], d[3 * k + 2]);
+        if (order == 3) {
+            // brute force under the kLidarLex rule: the smallest t over
+            // every triangle, each tested with t_max = FLT_MAX
+            const RayTxfm tx = computeRayIsectTxfm(rd, v3(1.f / rd.x, 1.f / rd.y, 1.f / rd.z));
+            float tb = kFltMax;
+            int ib = -1;
+            for (int tri = 0; tri < ntri; tri++) {
+                float th = 0.f;
+                if (rayTriangleIntersection(o.verts[tri * 3], o.verts[tri * 3 + 1], o.verts[tri * 3 + 2], tx, ro,
+                                            kFltMax, &th) && lexLess(th, tb)) {
+                    tb = th;
+                    ib = tri;
+                }
+            }
+            hit_out[k] = ib >= 0 ? 1 : 0;
+            t_out[k] = tb;
+            continue;
+        }
+        hit_out[k] = bvhTraceRay(o, ro, rd, &t, kFltMax, order == kLidarOctant, order == kLidarLex) ? 1 : 0;
         t_out[k] = t;
     }
 }

@@ -33,9 +33,11 @@ typedef struct oracle_config {
     int32_t task_type;
     /* RewardMode::Flank (train_flank, mgr.cpp:1746-1750) */
     int32_t train_flank;
-    /* Lidar child visit order: 0 = slot order (mesh_bvh.inl:160-204 as
-     * written), 1 = the octant order the product's k_lidar uses (DESIGN.md
-     * §2); closest hits differ only at exact coplanar ties. */
+    /* Lidar closest-hit rule: 0 = slot order (mesh_bvh.inl:160-204 as
+     * written), 1 = the round-3 octant child order, 2 = the smallest t
+     * over every hit triangle -- order-independent, the
+     * rule the product's k_lidar follows (DESIGN.md §2 definition 12);
+     * closest hits differ only between near-coplanar overlapping triangles. */
     int32_t lidar_octant_order;
 } oracle_config;
 
@@ -86,9 +88,10 @@ float oracle_sphere_cast(void *h, const float *o, const float *d, float r,
 /* Analysis hook (DESIGN.md §2 definition 13): ray-slab products fused (1,
  * the shared definition) or multiplied then added (0). Process-wide. */
 void oracle_set_slab_fma(int32_t on);
-/* n closest-hit queries (MeshBVH::traceRay, slot order or octant order):
- * o, d [n][3]; t_out, hit_out [n]. */
-void oracle_trace_ray_batch(void *h, int32_t n, const float *o, const float *d, int32_t octant, float *t_out,
+/* n closest-hit queries (MeshBVH::traceRay): order 0 slot order, 1 octant
+ * order, 2 the smallest-t rule over the BVH, 3 the same rule by brute
+ * force over every triangle; o, d [n][3]; t_out, hit_out [n]. */
+void oracle_trace_ray_batch(void *h, int32_t n, const float *o, const float *d, int32_t order, float *t_out,
                             int32_t *hit_out);
 /* n casts of MeshBVH::sphereCast with its t_max argument (mesh_bvh.inl:743-747;
  * t_max null = FLT_MAX): o, d, n_out [n][3]; normals are (0,0,0) on a miss. */

@@ -292,13 +292,13 @@ class Oracle:
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
                  world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None, flank=False,
-                 lidar_order="octant"):
+                 lidar_order="lex"):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
                            world_id_offset, scene.encode(), self.nodes.ctypes.data,
                            len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3, task,
-                           int(flank), 1 if lidar_order == "octant" else 0)
+                           int(flank), {"slot": 0, "octant": 1, "lex": 2}[lidar_order])
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
         if curriculum:

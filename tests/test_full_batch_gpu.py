@@ -122,6 +122,8 @@ def test_every_world_in_the_combat_regime_matches_oracle(ts, W, steps, every):
     t_oracle = 0.0
     acts = np.empty((A, 6), np.int32)
     for s in range(steps):
+        if s % 5 == 0:  # progress (a long GPU test must not look hung)
+            print(f"  step {s}: oracle {t_oracle:.0f} s, test {time.time() - t_start:.0f} s", flush=True)
         e.combat_actions(dev_ring + (s % RING) * A * 24, dev_acts, 1)
         e.mem.d2h(dev_acts, acts.nbytes, acts)
         twin = T.seek_combat_actions(o, s, base=ring[s % RING])

@@ -1,21 +1,87 @@
-"""The lidar's child visit order.
+"""The lidar's closest-hit rule (DESIGN.md §2 definition 12).
 
-The product's k_lidar walks each node's children in the octant order of
-scene.h octantNodeImages; the oracle follows it when lidar_order="octant"
-(the default, so GPU parity stays bit-exact) and follows the slot order of
-mesh_bvh.inl:160-204 as written when lidar_order="slot".  Closest hits can
-only differ where two distinct coplanar triangles tie (simple_map holds
-overlapping coplanar faces): this pins that the difference is at most one
-ulp of lidar depth and never reaches a discrete channel or another output.
-"""
+The reference walks MeshBVH children in slot order (mesh_bvh.inl:160-204)
+and each accepted hit tightens t_max in the watertight test's scaled form
+(T <= t_max * det), so where two distinct near-coplanar triangles give hits
+one ulp apart, the triangle visited first can win.  The product's k_lidar
+follows an order-independent rule instead: the smallest t = fl(T * fl(1/det))
+over every triangle the ray hits (the oracle's lidar_order="lex", the
+default).  Pinned here: (1) the oracle's BVH traversal under that rule
+equals a brute-force minimum over all 252 triangles on lidar fans from
+rollouts (tape and combat), on random rays, on rays aimed exactly at every
+vertex and edge midpoint and on near-axis rays from on or near vertices
+(-0 ranks below +0); (2) against the reference's slot order the
+rule moves at most one ulp of depth on a few rays and never a discrete
+channel or any other output."""
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
+import numpy as np
+
+import mpenv_testlib as T
+
+sys.path.insert(0, os.path.join(T.ROOT, "tools"))
 import lidar_order_check  # noqa: E402
+from dump_lidar_rays import rays_for  # noqa: E402
 
 
-def test_octant_order_matches_slot_order_up_to_coplanar_ties():
+def _trace(o, org, d, order):
+    n = len(org)
+    org = np.ascontiguousarray(org, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    t = np.zeros(n, np.float32)
+    h = np.zeros(n, np.int32)
+    o.lib.oracle_trace_ray_batch(o.h, n, T.fptr(org), T.fptr(d), order, T.fptr(t), h.ctypes.data)
+    return t, h
+
+
+def _rollout_rays(combat, W=8, steps=(40, 120)):
+    o = T.Oracle(W, 6)
+    o.put_ctrl([0, 1, 1])
+    o.init()
+    out = []
+    for s in range(max(steps) + 1):
+        o.set_actions(T.seek_combat_actions(o, s) if combat else T.mpenv_tape.tape_actions(1234, s, 0, W * 12))
+        o.step()
+        if s in steps:
+            out.append(rays_for(o.get("DEBUG_AGENT_F32"), o.get("DEBUG_AGENT_I32")))
+    o.close()
+    r = np.concatenate(out)
+    return r[:, :3], r[:, 3:]
+
+
+def test_smallest_t_rule_over_the_bvh_equals_brute_force():
+    o = T.Oracle(1, 1)
+    rng = np.random.default_rng(3)
+    sets = [_rollout_rays(False), _rollout_rays(True)]
+    org = rng.uniform([-1500, -1500, -50], [1500, 1500, 300], (20000, 3))
+    d = rng.normal(size=(20000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    sets.append((org, d))
+    sets.append(T.edge_aimed_rays(o.verts, 6, seed=11))
+    # near-axis rays from on or near vertices (origins on a vertex hit at
+    # t = -0 or +0; axis-aligned rays meet zero-margin box faces)
+    V = o.verts.reshape(-1, 3)
+    n = 20000
+    org = V[rng.integers(0, len(V), n)] + rng.normal(size=(n, 3)) * rng.choice([0, 1e-3, 1, 30], size=(n, 1))
+    d = np.zeros((n, 3))
+    d[np.arange(n), rng.integers(0, 3, n)] = rng.choice([-1, 1], n)
+    d += rng.normal(size=(n, 3)) * rng.choice([0, 0, 1e-6, 1e-2], size=(n, 1))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    sets.append((org, d))
+    total = hits = 0
+    for org, d in sets:
+        t2, h2 = _trace(o, org, d, 2)
+        t3, h3 = _trace(o, org, d, 3)
+        assert np.array_equal(h2, h3)
+        assert np.array_equal(t2.view(np.uint32), t3.view(np.uint32))
+        total += len(org)
+        hits += int(h2.sum())
+    assert total > 70000 and hits > 30000
+    o.close()
+
+
+def test_smallest_t_rule_matches_slot_order_up_to_near_coplanar_ties():
     rays, diff, max_ulp, disc, other = lidar_order_check.main(W=24, steps=150, ts=6)
     assert rays == 24 * 12 * 80 * 150
     assert max_ulp <= 1

@@ -4,6 +4,8 @@ order -- per 4-agent unit: each agent's 64 forward rays, then the 4 agents'
 tools/trav_stats.cpp; sim.cpp:3324-3506 ray construction, float32 numpy).
 
     python tools/dump_lidar_rays.py OUT.f32 [worlds] [step ...]
+    DUMP_ACTIONS=combat ...   the zone-seeking aim-bot over the tape (bench.py
+                              --actions combat; mpenv_testlib.seek_combat_actions)
 """
 import os
 import sys
@@ -66,7 +68,10 @@ if __name__ == "__main__":
     o.init()
     allr = []
     for s in range(max(steps) + 1):
-        o.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, W * 12))
+        if os.environ.get("DUMP_ACTIONS") == "combat":
+            o.set_actions(T.seek_combat_actions(o, s))
+        else:
+            o.set_actions(T.mpenv_tape.tape_actions(1234, s, 0, W * 12))
         o.step()
         if s in steps:
             allr.append(rays_for(o.get("DEBUG_AGENT_F32"), o.get("DEBUG_AGENT_I32")))

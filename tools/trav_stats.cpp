@@ -341,6 +341,181 @@ static void traceWavePacket(const float *rays, size_t r0, size_t n, int mode, PK
     }
 }
 
+// Per-fan candidate lists (forward waves only: one agent's 64 rays, two
+// sheets of 32 rays from one xy origin at two heights, each sheet in the
+// plane spanned by the aim frame's right and forward axes).  Cull per
+// (triangle, sheet): back faces (the sheet origin behind the triangle's
+// plane: rayTri accepts one winding only), triangles with no point within
+// `eps` of the sheet plane, then the angular span (seen from the sheet
+// origin) of the triangle's band |s| <= eps gives the candidate rays (plus
+// `delta` rad each side); the exact distance from the origin to the
+// triangle bounds any hit's t from below.  Entries (triangle, sheet, 32-ray
+// mask, bound) are walked in lockstep in one of three orders -- sorted by
+// bound, bucketed by bound (counting sort on log2 buckets), or unsorted --
+// an entry costs a full triangle test when some ray of its mask still has
+// t > bound (order-independent closest hit: the minimum of (t, triangle)),
+// else a skip.  Compared with brute force over every triangle.
+struct FanStats {
+    double waves = 0, entries = 0, walked = 0, full = 0, laneTests = 0;
+    double wrong = 0, bigLists = 0;
+    double planeTests = 0, straddle = 0; // per (triangle, sheet): after the back-face cull, after the band test
+};
+static int g_frontSign = 0; // +1 / -1: the origin side rayTri accepts; 0: no back-face cull
+
+static double closestDist(const double *a, const double *b, const double *c) // RTCD 5.1.5, p = origin
+{
+    auto dot = [](const double *x, const double *y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+    double ab[3], ac[3], ap[3], bp[3], cp[3], r[3];
+    for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ap[k] = -a[k]; bp[k] = -b[k]; cp[k] = -c[k]; }
+    auto len = [&](const double *x) { return std::sqrt(dot(x, x)); };
+    double d1 = dot(ab, ap), d2 = dot(ac, ap);
+    if (d1 <= 0 && d2 <= 0) return len(a);
+    double d3 = dot(ab, bp), d4 = dot(ac, bp);
+    if (d3 >= 0 && d4 <= d3) return len(b);
+    double vc = d1 * d4 - d3 * d2;
+    if (vc <= 0 && d1 >= 0 && d3 <= 0) { double v = d1 / (d1 - d3); for (int k = 0; k < 3; k++) r[k] = a[k] + v * ab[k]; return len(r); }
+    double d5 = dot(ab, cp), d6 = dot(ac, cp);
+    if (d6 >= 0 && d5 <= d6) return len(c);
+    double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0 && d2 >= 0 && d6 <= 0) { double w = d2 / (d2 - d6); for (int k = 0; k < 3; k++) r[k] = a[k] + w * ac[k]; return len(r); }
+    double va = d3 * d6 - d5 * d4;
+    if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+        double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        for (int k = 0; k < 3; k++) r[k] = b[k] + w * (c[k] - b[k]);
+        return len(r);
+    }
+    double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
+    for (int k = 0; k < 3; k++) r[k] = a[k] + ab[k] * v + ac[k] * w;
+    return len(r);
+}
+
+static void fanWave(const float *rays, size_t r0, int order, FanStats &fs)
+{
+    const double kPi = 3.14159265358979323846;
+    const double eps = 0.05, delta = 1e-3;
+    double R[3], F[3], N[3], O[2][3];
+    {
+        const float *d0 = &rays[6 * r0 + 3], *d31 = &rays[6 * (r0 + 31) + 3];
+        for (int k = 0; k < 3; k++) {
+            F[k] = (d0[k] + d31[k]) / (2.0 * std::sin(kPi / 8));
+            R[k] = (d31[k] - d0[k]) / (2.0 * std::cos(kPi / 8));
+        }
+        N[0] = R[1] * F[2] - R[2] * F[1]; N[1] = R[2] * F[0] - R[0] * F[2]; N[2] = R[0] * F[1] - R[1] * F[0];
+        for (int h = 0; h < 2; h++)
+            for (int k = 0; k < 3; k++) O[h][k] = rays[6 * (r0 + 32 * h) + k];
+    }
+    struct Ent { int tri, sheet; uint32_t mask; double nearB; };
+    std::vector<Ent> ents;
+    const int ntri = (int)(verts.size() / 9);
+    const double step = 0.75 * kPi / 31, off = 0.125 * kPi;
+    for (int t = 0; t < ntri; t++) {
+        const float *tv = &verts[t * 9];
+        double e1[3], e2[3], tn[3];
+        for (int k = 0; k < 3; k++) { e1[k] = tv[3 + k] - tv[k]; e2[k] = tv[6 + k] - tv[k]; }
+        tn[0] = e1[1] * e2[2] - e1[2] * e2[1]; tn[1] = e1[2] * e2[0] - e1[0] * e2[2]; tn[2] = e1[0] * e2[1] - e1[1] * e2[0];
+        const double tnl = std::sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
+        for (int h = 0; h < 2; h++) {
+            double v[3][3], s[3];
+            for (int i = 0; i < 3; i++) {
+                for (int k = 0; k < 3; k++) v[i][k] = tv[3 * i + k] - O[h][k];
+                s[i] = v[i][0] * N[0] + v[i][1] * N[1] + v[i][2] * N[2];
+            }
+            if (g_frontSign != 0) {
+                const double so = -(tn[0] * v[0][0] + tn[1] * v[0][1] + tn[2] * v[0][2]);
+                if (so * g_frontSign < -1e-3 * tnl) continue;
+            }
+            fs.planeTests++;
+            if ((s[0] > eps && s[1] > eps && s[2] > eps) || (s[0] < -eps && s[1] < -eps && s[2] < -eps)) continue;
+            fs.straddle++;
+            // the band |s| <= eps: vertices inside it, edge crossings of s = +-eps
+            double pts[9][2];
+            int np = 0;
+            auto addP = [&](const double *p) {
+                pts[np][0] = p[0] * R[0] + p[1] * R[1] + p[2] * R[2];
+                pts[np][1] = p[0] * F[0] + p[1] * F[1] + p[2] * F[2];
+                np++;
+            };
+            for (int i = 0; i < 3; i++) {
+                if (std::fabs(s[i]) <= eps) addP(v[i]);
+                const int j = (i + 1) % 3;
+                for (double bnd : { eps, -eps }) {
+                    if ((s[i] - bnd) * (s[j] - bnd) < 0) {
+                        const double a = (s[i] - bnd) / (s[i] - s[j]);
+                        double p[3];
+                        for (int k = 0; k < 3; k++) p[k] = v[i][k] + (v[j][k] - v[i][k]) * a;
+                        addP(p);
+                    }
+                }
+            }
+            if (np == 0) continue;
+            double lo = 0, hi = 0;
+            bool full = false;
+            const double a0 = std::atan2(pts[0][1], -pts[0][0]);
+            for (int p = 0; p < np; p++) {
+                if (pts[p][0] * pts[p][0] + pts[p][1] * pts[p][1] < 1.0) full = true;
+                double d = std::atan2(pts[p][1], -pts[p][0]) - a0;
+                while (d > kPi) d -= 2 * kPi;
+                while (d <= -kPi) d += 2 * kPi;
+                lo = std::min(lo, d);
+                hi = std::max(hi, d);
+            }
+            if (hi - lo >= kPi - 1e-3) full = true;
+            uint32_t m = 0;
+            for (int x = 0; x < 32; x++) {
+                const double th = off + step * x;
+                for (double wrap : { -2 * kPi, 0.0, 2 * kPi })
+                    if (full || (th + wrap >= a0 + lo - delta && th + wrap <= a0 + hi + delta)) m |= 1u << x;
+            }
+            if (!m) continue;
+            const double nb = closestDist(v[0], v[1], v[2]);
+            ents.push_back({ t, h, m, std::max(0.0, nb * (1 - 1e-5) - 0.01) });
+        }
+    }
+    if (order == 0) {
+        std::stable_sort(ents.begin(), ents.end(), [](const Ent &a, const Ent &b) { return a.nearB < b.nearB; });
+    } else if (order == 1) {
+        // counting sort on 16 buckets: log2 of the bound (bucket 0: < 64 units)
+        auto bk = [](double nb) { return nb < 64 ? 0 : std::min(15, 1 + (int)std::floor(std::log2(nb / 64) * 2)); };
+        std::stable_sort(ents.begin(), ents.end(), [&](const Ent &a, const Ent &b) { return bk(a.nearB) < bk(b.nearB); });
+    }
+    fs.waves++;
+    fs.entries += ents.size();
+    if (ents.size() > 64) fs.bigLists++;
+    float tl[64];
+    int il[64];
+    for (int l = 0; l < 64; l++) { tl[l] = 3.4e38f; il[l] = -1; }
+    for (size_t ci = 0; ci < ents.size(); ci++) {
+        bool anyLater = false;
+        for (size_t cj = ci; cj < ents.size() && !anyLater; cj++)
+            for (int x = 0; x < 32; x++)
+                if (((ents[cj].mask >> x) & 1) && ents[cj].nearB < tl[32 * ents[cj].sheet + x]) { anyLater = true; break; }
+        if (!anyLater) break;
+        fs.walked++;
+        const Ent &c = ents[ci];
+        bool act = false;
+        for (int x = 0; x < 32; x++) {
+            const int l = 32 * c.sheet + x;
+            if (!((c.mask >> x) & 1) || !(c.nearB < tl[l])) continue;
+            act = true;
+            fs.laneTests++;
+            float th;
+            if (tri(&verts[c.tri * 9], &rays[6 * (r0 + l)], &rays[6 * (r0 + l) + 3], 3.4e38f, th) &&
+                (th < tl[l] || (th == tl[l] && c.tri < il[l]))) { tl[l] = th; il[l] = c.tri; }
+        }
+        if (act) fs.full++;
+    }
+    // brute force: min (t, triangle) over every triangle
+    for (int l = 0; l < 64; l++) {
+        float tb = 3.4e38f;
+        int ib = -1;
+        for (int t = 0; t < ntri; t++) {
+            float th;
+            if (tri(&verts[t * 9], &rays[6 * (r0 + l)], &rays[6 * (r0 + l) + 3], 3.4e38f, th) && (th < tb || (th == tb && t < ib))) { tb = th; ib = t; }
+        }
+        if (tb != tl[l] || ib != il[l]) fs.wrong++;
+    }
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3) {
@@ -378,6 +553,62 @@ int main(int argc, char **argv)
         printf("packet (64 consecutive rays): union nodes/wave %.2f, union tris/wave %.2f\n", un / waves, ut / waves);
     }
     buildOctOrder();
+    if (getenv("TRAV_FAN")) {
+        // forward waves only (dump_lidar_rays order: 4 forward waves, then 1 rear)
+        // which side of a triangle does an accepted hit come from?
+        {
+            long pos = 0, neg = 0;
+            for (size_t r = 0; r < n; r += 7) {
+                Stats one;
+                trace(&rays[6 * r], &rays[6 * r + 3], 2, one);
+                if (g_lastTri < 0) continue;
+                const float *tv = &verts[g_lastTri * 9], *o = &rays[6 * r];
+                const double e1[3] = { tv[3] - tv[0], tv[4] - tv[1], tv[5] - tv[2] };
+                const double e2[3] = { tv[6] - tv[0], tv[7] - tv[1], tv[8] - tv[2] };
+                const double nn[3] = { e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0] };
+                const double so = nn[0] * (o[0] - tv[0]) + nn[1] * (o[1] - tv[1]) + nn[2] * (o[2] - tv[2]);
+                (so > 0 ? pos : neg)++;
+            }
+            printf("accepted hits: origin on the +normal side %ld, on the -normal side %ld\n", pos, neg);
+            g_frontSign = getenv("TRAV_FAN_NOBF") ? 0 : (pos > neg ? 1 : -1);
+        }
+        for (int order = 0; order < 3; order++) {
+            FanStats fs;
+            double octNode = 0, octTri = 0;
+            size_t nf = 0;
+            for (size_t w0 = 0; w0 + 64 <= n; w0 += 64) {
+                if ((w0 / 64) % 5 == 4) continue;
+                fanWave(rays.data(), w0, order, fs);
+                nf += 64;
+                if (order) continue;
+                double mp = 0;
+                std::vector<Stats> lanes;
+                for (size_t r = w0; r < w0 + 64; r++) {
+                    Stats one;
+                    trace(&rays[6 * r], &rays[6 * r + 3], 2, one);
+                    lanes.push_back(one);
+                    mp = std::max(mp, one.pops);
+                }
+                octNode += mp;
+                for (int it = 0; it < (int)mp; it++)
+                    for (int i = 0; i < 4; i++) {
+                        int m = 0;
+                        for (auto &L : lanes)
+                            if (it < (int)L.slotTris.size()) m = std::max(m, L.slotTris[it][i]);
+                        octTri += m;
+                    }
+            }
+            printf("fan lists, %s: per forward wave: (tri, sheet) entries %.1f (lists > 64: %.3f), walked %.1f, "
+                   "lockstep full tests %.1f, lane tests/ray %.2f | per sheet: front-facing %.1f, in the band %.1f | "
+                   "closest hits differing from brute force %.0f of %zu",
+                   order == 0 ? "sorted  " : order == 1 ? "bucketed" : "unsorted", fs.entries / fs.waves,
+                   fs.bigLists / fs.waves, fs.walked / fs.waves, fs.full / fs.waves, fs.laneTests / nf,
+                   fs.planeTests / fs.waves / 2, fs.straddle / fs.waves / 2, fs.wrong, nf);
+            if (!order) printf(" | octant BVH lockstep: node iters %.2f, tri tests %.2f", octNode / fs.waves, octTri / fs.waves);
+            printf("\n");
+        }
+        return 0;
+    }
     for (int ftb = 0; ftb < 4; ftb++) {
         Stats st;
         double wave_pops = 0, wave_tris = 0, simt_slot = 0, simt_merged = 0;
