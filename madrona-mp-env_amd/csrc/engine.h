@@ -223,6 +223,10 @@ struct SceneDev {
     // |e12|^2, 0 -- computed on the host with the same mpenv_core.h
     // expressions the traversal would evaluate (bit-identical).
     const float *triPre;
+    // Per triangle, k_lidar's fan-list cull data (manager.cpp): unit normal
+    // of (b - a) x (c - a), its plane offset, bounding-sphere centre and
+    // radius (8 floats).
+    const float *triAux;
     int32_t numNodes;
     int32_t numVerts;
     mp::AABB worldBounds;

@@ -186,10 +186,17 @@ __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
     const float *src_v = sc.verts;
     float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
     if constexpr (kLidarRot) {
+        // The .w slots carry the fan-list cull data (SceneDev::triAux) of
+        // triangle t = v / 3, vertex slot i = v % 3: copy 2 (x, y, z) the
+        // unit normal's component i; copy 0 the plane offset, the bounding
+        // radius, the centre's x; copy 1 the centre's y and z (fanTraceD).
         for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
             const int r = k / sc.numVerts, v = k - r * sc.numVerts;
             const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
-            dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r], 0.f);
+            const int t = v / 3, i = v - 3 * t;
+            const int ai = r == 2 ? i : r == 0 ? (i == 0 ? 3 : i == 1 ? 7 : 4) : (i == 0 ? 5 : i == 1 ? 6 : -1);
+            dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r],
+                                   ai >= 0 ? sc.triAux[8 * t + ai] : 0.f);
         }
     } else {
         for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
@@ -199,6 +206,31 @@ __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
     LBVH b;
     b.nodes = (const MP_LDS BVHNode *)(smem);
     b.verts = (const MP_LDS float *)(smem + (size_t)node_q * 16);
+    b.pre = nullptr;
+    b.snodes = nullptr;
+    b.stats = nullptr;
+    b.rotStride = sc.numVerts;
+    return b;
+}
+
+// k_lidar_fan's LDS image: the three rotated vertex copies only (with the
+// fan-list cull data in their .w slots, stageBVHOct), no node images.
+__device__ __forceinline__ LBVH stageBVHRot(char *smem, const SceneDev &sc)
+{
+    float4 *dst_v = reinterpret_cast<float4 *>(smem);
+    const float *src_v = sc.verts;
+    for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
+        const int r = k / sc.numVerts, v = k - r * sc.numVerts;
+        const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
+        const int t = v / 3, i = v - 3 * t;
+        const int ai = r == 2 ? i : r == 0 ? (i == 0 ? 3 : i == 1 ? 7 : 4) : (i == 0 ? 5 : i == 1 ? 6 : -1);
+        dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r],
+                               ai >= 0 ? sc.triAux[8 * t + ai] : 0.f);
+    }
+    __syncthreads();
+    LBVH b;
+    b.nodes = nullptr;
+    b.verts = (const MP_LDS float *)(smem);
     b.pre = nullptr;
     b.snodes = nullptr;
     b.stats = nullptr;
@@ -665,6 +697,296 @@ __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::
     return bvhTraceRayT<false>(b, ray_o, ray_d, t_out, t_max0, 0.f);
 }
 
+// Orders one wave's LDS writes before other lanes' reads of them (and those
+// reads before the next overwrite): a wavefront-scope release/acquire fence
+// pair around a wave barrier.  The wave's DS instructions execute in issue
+// order, so this constrains the compiler only.
+__device__ __forceinline__ void waveSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------ fan lists
+// k_lidar's forward fans without the BVH (tools/trav_stats.cpp
+// TRAV_FAN model).  A forward wave traces one agent's 64 rays: two sheets
+// (lanes 0-31 / 32-63) of 32 rays from one origin each, every ray of a sheet
+// in the plane through that origin spanned by the aim frame's right R and
+// forward F axes (normal N = R x F).  The closest hit under the lidar's
+// smallest-t rule (bvhTraceRayT kLex) is found from a per-wave candidate list:
+//   1. cull (lane = triangle, 4 rounds over <= 255 triangles): the sheet
+//      origin on the front side of the triangle's plane (rayTri accepts
+//      hits from the +n side of (b - a) x (c - a) only) and some vertex
+//      within kFanBand of the sheet plane band; survivors' ids + sheet bits
+//      go to an LDS list (ballot + mbcnt);
+//   2. masks (lane = survivor): per sheet, the triangle's strip inside the
+//      band |N.(p - O)| <= kFanBand is a quadrilateral between the two
+//      edges that cross the plane; its angular span seen from the origin,
+//      widened by kFanDelta, gives the sheet's candidate rays (a fan slot
+//      mask); strips near the origin, wrapping past pi, with a vertex inside
+//      the band or nearly parallel to the sheet (sin < kFanSinMin) take all
+//      32 rays.  Lower bound of any hit's t: the larger of the distance to
+//      the triangle's plane and to its bounding sphere;
+//   3. walk (lane = ray): entries in 8 log2 buckets of their bound; an entry
+//      runs the watertight test on the lanes in its mask whose current t is
+//      not below the bound, with the relaxed kLex acceptance.
+// Every cull is conservative (a ray of a sheet stays within 1e-7 t of the
+// plane, far inside the band; hit points lie in the strip; the float
+// rounding of angles and bounds is far below kFanDelta and the bound's
+// margin), so the result equals the smallest t over all triangles -- the
+// value the BVH path (and the oracle) computes.
+constexpr float kFanBand = 0.05f, kFanTol = 0.05f, kFanDelta = 2e-3f, kFanSinMin = 0.1f;
+constexpr float kFanNearR2 = 16.f; // strip points nearer than 4 units: every ray
+constexpr int kFanListCap = 256;   // u16 list entries per wave (triangle id | sheet bits << 8)
+
+// atan2 to ~1e-5 rad (minimax atan on [0, 1]); cull use only
+__device__ __forceinline__ float fanAtan2(float y, float x)
+{
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+    const float q = a * a;
+    float r = fmaf(fmaf(fmaf(fmaf(fmaf(-0.01172120f, q, 0.05265332f), q, -0.11643287f), q, 0.19354346f), q,
+                        -0.33262347f), q, 0.99997726f) * a;
+    if (ay > ax) r = 1.57079637f - r;
+    if (x < 0.f) r = 3.14159274f - r;
+    return y < 0.f ? -r : r;
+}
+
+// Fan slots x (theta_x = 0.75 pi x / 31 + pi / 8, sim.cpp:3324-3506) with
+// theta_x in [a, b] modulo 2 pi (b - a < 2 pi).
+__device__ __forceinline__ uint32_t fanSlotMask(float a, float b)
+{
+    constexpr float kOff = 0.392699082f, kInvStep = 31.f / 2.35619449f;
+    uint32_t m = 0;
+#pragma unroll
+    for (int sh = -1; sh <= 1; sh++) {
+        const float o = (float)sh * 6.28318531f - kOff;
+        const float lo = fmaxf(ceilf((a + o) * kInvStep), 0.f);
+        const float hi = fminf(floorf((b + o) * kInvStep), 31.f);
+        if (lo <= hi) {
+            const uint32_t l = (uint32_t)lo, h = (uint32_t)hi;
+            m |= (h == 31u ? 0xffffffffu : ((2u << h) - 1u)) & ~((1u << l) - 1u);
+        }
+    }
+    return m;
+}
+
+// One sheet's candidate mask for a survivor: sv / uv / wv = N.v, R.v, F.v of
+// the three vertices, c = N.O, (uO, wO) = (R.O, F.O).
+__device__ __forceinline__ uint32_t fanSheetMaskD(const float sv[3], const float uv[3], const float wv[3], float c,
+                                                  float uO, float wO, float sinT)
+{
+    const float s0 = sv[0] - c, s1 = sv[1] - c, s2 = sv[2] - c;
+    const bool p0 = s0 > 0.f, p1 = s1 > 0.f, p2 = s2 > 0.f;
+    if (sinT < kFanSinMin || fabsf(s0) <= kFanBand || fabsf(s1) <= kFanBand || fabsf(s2) <= kFanBand ||
+        (p0 == p1 && p1 == p2))
+        return 0xffffffffu;
+    // the lone vertex (on its own side of the plane) and the other two
+    const int L = p0 == p1 ? 2 : (p0 == p2 ? 1 : 0);
+    const int A = L == 2 ? 0 : L + 1, B = L == 0 ? 2 : (L == 1 ? 0 : 1);
+    auto pick = [](const float v[3], int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); };
+    const float sl = pick(sv, L) - c, ul = pick(uv, L) - uO, wl = pick(wv, L) - wO;
+    float pu[4], pw[4];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int o = e ? B : A;
+        const float so = pick(sv, o) - c, uo = pick(uv, o) - uO, wo = pick(wv, o) - wO;
+        const float inv = 1.f / (sl - so);
+#pragma unroll
+        for (int bi = 0; bi < 2; bi++) {
+            const float a = (sl - (bi ? -kFanBand : kFanBand)) * inv; // in (0, 1)
+            pu[2 * e + bi] = fmaf(a, uo - ul, ul);
+            pw[2 * e + bi] = fmaf(a, wo - wl, wl);
+        }
+    }
+    // angular extremes of the quad seen from the origin, by cross products
+    // (exact ordering inside a half-plane), then their two angles
+    bool full = false;
+    float lu = pu[0], lw = pw[0], hu = pu[0], hw = pw[0];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        full = full || fmaf(pu[k], pu[k], pw[k] * pw[k]) < kFanNearR2;
+        // angle phi = atan2(w, -u): q is counter-clockwise of p iff
+        // cross((-u_p, w_p), (-u_q, w_q)) = u_q w_p - u_p w_q > 0
+        if (k) {
+            if (fmaf(pu[k], lw, -(lu * pw[k])) < 0.f) { lu = pu[k]; lw = pw[k]; }
+            if (fmaf(pu[k], hw, -(hu * pw[k])) > 0.f) { hu = pu[k]; hw = pw[k]; }
+        }
+    }
+    // every point between the extremes (else the quad is not inside a
+    // half-plane seen from the origin: all rays)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float tol = 1e-5f * (fabsf(pu[k]) + fabsf(pw[k])) * (fabsf(lu) + fabsf(lw) + fabsf(hu) + fabsf(hw));
+        full = full || fmaf(pu[k], lw, -(lu * pw[k])) < -tol || fmaf(hu, pw[k], -(pu[k] * hw)) < -tol;
+    }
+    if (full) return 0xffffffffu;
+    const float a0 = fanAtan2(lw, -lu);
+    float a1 = fanAtan2(hw, -hu);
+    if (a1 < a0) a1 += 6.28318548f;
+    if (a1 - a0 >= 3.13159274f) return 0xffffffffu;
+    return fanSlotMask(a0 - kFanDelta, a1 + kFanDelta);
+}
+
+// Lower bound of the distance from o to triangle t (aux: plane offset and
+// bounding sphere from the .w slots), with a margin for rounding.
+__device__ __forceinline__ float fanNearD(float sf, float cx, float cy, float cz, float rad, float ox, float oy,
+                                          float oz)
+{
+    const float dx = ox - cx, dy = oy - cy, dz = oz - cz;
+    const float cd = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz))) - rad;
+    return fmaxf(0.f, fmaf(fmaxf(fabsf(sf), cd), 0.99999f, -0.05f));
+}
+
+// mkRay(o, d): the lane's ray, formed only once the walk starts (so it is not
+// live across the cull); returned in ray_o / ray_d.
+template <class MkRay>
+__device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uint16_t *list, float ox, float oy,
+                                          float z0, float z1, mp::Vec3 R, mp::Vec3 F, MkRay mkRay,
+                                          mp::Vec3 &ray_o, mp::Vec3 &ray_d, float &t_out)
+{
+    using namespace mp;
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    // the frame is wave-uniform: keep it in SGPRs (readfirstlane), not in
+    // 20-odd VGPRs that would hold the same value in every lane
+    auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    auto uni3 = [&](Vec3 v) { return v3(uni(v.x), uni(v.y), uni(v.z)); };
+    ox = uni(ox); oy = uni(oy); z0 = uni(z0); z1 = uni(z1);
+    R = uni3(R); F = uni3(F);
+    const Vec3 N = uni3(cross(R, F));
+    const float dz = uni(z1 - z0);
+    const float c0 = uni(fmaf(N.x, ox, fmaf(N.y, oy, N.z * z0))), c1 = uni(fmaf(N.z, dz, c0));
+    const MP_LDS lf4 *vp = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + 2 * b.rotStride; // (x, y, z, n_i)
+    const MP_LDS lf4 *v0 = reinterpret_cast<const MP_LDS lf4 *>(b.verts);                  // .w: d, r, cx
+    const MP_LDS lf4 *v1 = v0 + b.rotStride;                                                // .w: cy, cz
+    // 1. cull
+    uint32_t count = 0;
+#pragma unroll 1
+    for (int base = 0; base < numTris; base += 64) {
+        const int t = base + (int)lane;
+        uint32_t fl = 0;
+        if (t < numTris) {
+            const lf4 A = vp[3 * t], B = vp[3 * t + 1], C = vp[3 * t + 2];
+            const float dT = v0[3 * t].w;
+            const float sf0 = fmaf(A.w, ox, fmaf(B.w, oy, fmaf(C.w, z0, -dT)));
+            const float sf1 = fmaf(C.w, dz, sf0);
+            const float sa = fmaf(N.x, A.x, fmaf(N.y, A.y, N.z * A.z));
+            const float sb = fmaf(N.x, B.x, fmaf(N.y, B.y, N.z * B.z));
+            const float sc = fmaf(N.x, C.x, fmaf(N.y, C.y, N.z * C.z));
+            const float smin = fminf(sa, fminf(sb, sc)), smax = fmaxf(sa, fmaxf(sb, sc));
+            if (sf0 >= -kFanTol && smin <= c0 + kFanBand && smax >= c0 - kFanBand) fl |= 1u;
+            if (sf1 >= -kFanTol && smin <= c1 + kFanBand && smax >= c1 - kFanBand) fl |= 2u;
+        }
+        const uint64_t m = __ballot(fl != 0u);
+        if (fl) {
+            const uint32_t pos = count + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (pos < (uint32_t)kFanListCap) list[pos] = (uint16_t)(t | (fl << 8));
+        }
+        count += (uint32_t)__popcll(m);
+    }
+    waveSync();
+    const Vec3 oh0 = v3(ox, oy, z0);
+    const float uO0 = uni(dot(R, oh0)), wO0 = uni(dot(F, oh0));
+    const float uO1 = uni(fmaf(R.z, dz, uO0)), wO1 = uni(fmaf(F.z, dz, wO0));
+    float t_best = kFltMax, t_relax = kFltMax * kLexRelax;
+    // Phases 2-3 per chunk of 128 survivors (one chunk but for rare wide
+    // views; the smallest-t result does not depend on the walk order).
+    uint32_t ch = 0;
+    do {
+    // 2. masks, one or two survivors per lane (slot s holds list entry ch + 64 s + lane)
+    // entry registers per slot: triangle | bucket << 8 (bucket 8: none), the
+    // two sheet masks, the two bounds as bf16 rounded down (still bounds)
+    uint32_t eTB0 = 8u << 8, eLo0 = 0u, eHi0 = 0u, eNN0 = 0u; // bucket 8: not walked
+    uint32_t eTB1 = 8u << 8, eLo1 = 0u, eHi1 = 0u, eNN1 = 0u;
+    // one slot, and within it one sheet, at a time (rolled loops: the
+    // unrolled form interleaves four mask computations and needs ~85 VGPRs)
+#pragma unroll 1
+    for (int sl = 0; sl < 2; sl++) {
+        const uint32_t j = ch + (uint32_t)sl * 64u + lane;
+        uint32_t eTB = 8u << 8, eLo = 0u, eHi = 0u, eNN = 0u;
+        if (j < count) {
+            const uint32_t e = list[j];
+            const int t = (int)(e & 0xffu);
+            const uint32_t fl = e >> 8;
+            const lf4 A = vp[3 * t], B = vp[3 * t + 1], C = vp[3 * t + 2];
+            const float sv[3] = { fmaf(N.x, A.x, fmaf(N.y, A.y, N.z * A.z)), fmaf(N.x, B.x, fmaf(N.y, B.y, N.z * B.z)),
+                                  fmaf(N.x, C.x, fmaf(N.y, C.y, N.z * C.z)) };
+            const float uv[3] = { fmaf(R.x, A.x, fmaf(R.y, A.y, R.z * A.z)), fmaf(R.x, B.x, fmaf(R.y, B.y, R.z * B.z)),
+                                  fmaf(R.x, C.x, fmaf(R.y, C.y, R.z * C.z)) };
+            const float wv[3] = { fmaf(F.x, A.x, fmaf(F.y, A.y, F.z * A.z)), fmaf(F.x, B.x, fmaf(F.y, B.y, F.z * B.z)),
+                                  fmaf(F.x, C.x, fmaf(F.y, C.y, F.z * C.z)) };
+            const float cosT = fabsf(fmaf(A.w, N.x, fmaf(B.w, N.y, C.w * N.z)));
+            const float sinT = sqrtf(fmaxf(0.f, fmaf(-cosT, cosT, 1.f)));
+            const float sf0 = fmaf(A.w, ox, fmaf(B.w, oy, fmaf(C.w, z0, -v0[3 * t].w)));
+            uint32_t m0 = 0u, m1 = 0u;
+            float n0 = 0.f, n1 = 0.f;
+#pragma unroll 1
+            for (int h = 0; h < 2; h++) {
+                const uint32_t m = ((fl >> h) & 1u) ? fanSheetMaskD(sv, uv, wv, h ? c1 : c0, h ? uO1 : uO0,
+                                                                    h ? wO1 : wO0, sinT)
+                                                    : 0u;
+                const float n = fanNearD(h ? fmaf(C.w, dz, sf0) : sf0, v0[3 * t + 2].w, v1[3 * t].w,
+                                         v1[3 * t + 1].w, v0[3 * t + 1].w, ox, oy, h ? z1 : z0);
+                if (h) { m1 = m; n1 = n; } else { m0 = m; n0 = n; }
+            }
+            const float key = m0 ? (m1 ? fminf(n0, n1) : n0) : n1;
+            eLo = m0; eHi = m1;
+            // n >= 0: truncating to the upper 16 bits rounds toward zero
+            eNN = (__float_as_uint(n0) >> 16) | (__float_as_uint(n1) & 0xffff0000u);
+            // bucket: 0 below 32 units, then one per octave up to 7
+            const int ex = (int)((__float_as_uint(key) >> 23) & 0xffu) - 127;
+            eTB = (uint32_t)t | (((m0 | m1) ? (uint32_t)min(max(ex - 4, 0), 7) : 8u) << 8);
+        }
+        if (sl) { eTB1 = eTB; eLo1 = eLo; eHi1 = eHi; eNN1 = eNN; }
+        else { eTB0 = eTB; eLo0 = eLo; eHi0 = eHi; eNN0 = eNN; }
+    }
+    // 3. walk
+    mkRay(ray_o, ray_d);
+    const bool upper = lane >= 32u;
+    const uint32_t x = lane & 31u;
+    const Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
+    const RayTxfmD tx = rayTxfm(ray_d, inv_d);
+    const int kx0 = tx.kz == 2 ? 0 : tx.kz + 1, ky0 = kx0 == 2 ? 0 : kx0 + 1;
+    const MP_LDS lf4 *vrot = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + tx.kz * b.rotStride;
+    const float ro0 = comp(ray_o, kx0), ro1 = comp(ray_o, ky0), roz = comp(ray_o, tx.kz);
+    const bool rsw = tx.kx != kx0;
+    const int nslots = count > ch + 64u ? 2 : 1;
+    for (uint32_t bk = 0; bk < 8u; bk++) {
+        for (int sl = 0; sl < nslots; sl++) {
+            const uint32_t sTB = sl ? eTB1 : eTB0, sLo = sl ? eLo1 : eLo0, sHi = sl ? eHi1 : eHi0;
+            const uint32_t sNN = sl ? eNN1 : eNN0;
+            uint64_t m = __ballot((sTB >> 8) == bk);
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1ull;
+                // entry j's fields (wave-uniform), then this lane's sheet half
+                const int tri = __builtin_amdgcn_readlane((int)sTB, j) & 0xff;
+                const uint32_t mLo = (uint32_t)__builtin_amdgcn_readlane((int)sLo, j);
+                const uint32_t mHi = (uint32_t)__builtin_amdgcn_readlane((int)sHi, j);
+                const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)sNN, j);
+                const uint32_t mm = upper ? mHi : mLo;
+                const float nb = __uint_as_float(upper ? (nn & 0xffff0000u) : (nn << 16));
+                const bool act = ((mm >> x) & 1u) && !(t_best < nb);
+                if (__ballot(act) == 0ull) continue;
+                if (act) {
+                    float th;
+                    if (rayTriRot(vrot + tri * 3, ro0, ro1, roz, rsw, tx, t_relax, th) && lexLessD(th, t_best)) {
+                        t_best = th;
+                        t_relax = th * kLexRelax;
+                    }
+                }
+            }
+        }
+    }
+    ch += 128u;
+    } while (ch < count);
+    t_out = t_best;
+}
+
 // Out-of-line traversal for the ray-query test hook.
 struct RayHitD {
     float t;
@@ -1037,16 +1359,6 @@ __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, cons
     return h;
 }
 
-// Orders one wave's LDS writes before other lanes' reads of them (and those
-// reads before the next overwrite): a wavefront-scope release/acquire fence
-// pair around a wave barrier.  The wave's DS instructions execute in issue
-// order, so this constrains the compiler only.
-__device__ __forceinline__ void waveSync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // traceRayAgainstWorld(org, d).entity == target (utils.cpp:10-72, as
 // isAgentVisible uses it, utils.cpp:218) without the full closest-hit

@@ -435,7 +435,12 @@ static void fanWave(const float *rays, size_t r0, int order, FanStats &fs)
                 pts[np][1] = p[0] * F[0] + p[1] * F[1] + p[2] * F[2];
                 np++;
             };
-            for (int i = 0; i < 3; i++) {
+            // TRAV_FAN_TRI: the angular span of the whole projected triangle
+            // (3 vertices) instead of its band strip
+            static const bool triSpan = getenv("TRAV_FAN_TRI") != nullptr;
+            if (triSpan)
+                for (int i = 0; i < 3; i++) addP(v[i]);
+            for (int i = 0; i < 3 && !triSpan; i++) {
                 if (std::fabs(s[i]) <= eps) addP(v[i]);
                 const int j = (i + 1) % 3;
                 for (double bnd : { eps, -eps }) {
@@ -450,6 +455,41 @@ static void fanWave(const float *rays, size_t r0, int order, FanStats &fs)
             if (np == 0) continue;
             double lo = 0, hi = 0;
             bool full = false;
+            // TRAV_FAN_MID: the cut segment of the sheet's own plane (s = 0),
+            // widened by the band's reach along the triangle, eps / sin of
+            // the angle between the planes (+0.5), seen from its distance;
+            // a triangle in the band that does not cross the plane, or a
+            // near-parallel one (sin < 0.1), takes every ray
+            static const bool midSeg = getenv("TRAV_FAN_MID") != nullptr;
+            double widen = 0;
+            if (midSeg) {
+                const double cosT = std::fabs(tn[0] * N[0] + tn[1] * N[1] + tn[2] * N[2]) / tnl;
+                const double sinT = std::sqrt(std::max(0.0, 1 - cosT * cosT));
+                np = 0;
+                for (int i = 0; i < 3; i++) {
+                    const int j = (i + 1) % 3;
+                    if (s[i] == 0) addP(v[i]);
+                    if ((s[i] < 0 && s[j] > 0) || (s[i] > 0 && s[j] < 0)) {
+                        const double a = s[i] / (s[i] - s[j]);
+                        double p[3];
+                        for (int k = 0; k < 3; k++) p[k] = v[i][k] + (v[j][k] - v[i][k]) * a;
+                        addP(p);
+                    }
+                }
+                if (np < 2 || sinT < 0.1) {
+                    full = true;
+                    np = np ? np : 1;
+                    if (!np) pts[0][0] = pts[0][1] = 1;
+                } else {
+                    const double e = eps / sinT + 0.5;
+                    const double ex = pts[1][0] - pts[0][0], ey = pts[1][1] - pts[0][1], L = ex * ex + ey * ey;
+                    double tt = L > 0 ? -(pts[0][0] * ex + pts[0][1] * ey) / L : 0;
+                    tt = std::min(1.0, std::max(0.0, tt));
+                    const double cx = pts[0][0] + tt * ex, cy = pts[0][1] + tt * ey, dseg = std::sqrt(cx * cx + cy * cy);
+                    if (dseg < e + 16) full = true;
+                    else widen = std::asin(e / dseg);
+                }
+            }
             const double a0 = std::atan2(pts[0][1], -pts[0][0]);
             for (int p = 0; p < np; p++) {
                 if (pts[p][0] * pts[p][0] + pts[p][1] * pts[p][1] < 1.0) full = true;
@@ -464,13 +504,64 @@ static void fanWave(const float *rays, size_t r0, int order, FanStats &fs)
             for (int x = 0; x < 32; x++) {
                 const double th = off + step * x;
                 for (double wrap : { -2 * kPi, 0.0, 2 * kPi })
-                    if (full || (th + wrap >= a0 + lo - delta && th + wrap <= a0 + hi + delta)) m |= 1u << x;
+                    if (full || (th + wrap >= a0 + lo - delta - widen && th + wrap <= a0 + hi + delta + widen)) m |= 1u << x;
             }
             if (!m) continue;
-            const double nb = closestDist(v[0], v[1], v[2]);
+            double nb = closestDist(v[0], v[1], v[2]);
+            if (getenv("TRAV_FAN_CHEAPNB")) {
+                // max(distance to the triangle's plane, distance to its bounding sphere)
+                double c[3], r2 = 0;
+                for (int k = 0; k < 3; k++) c[k] = (v[0][k] + v[1][k] + v[2][k]) / 3;
+                for (int i = 0; i < 3; i++) {
+                    double d2 = 0;
+                    for (int k = 0; k < 3; k++) d2 += (v[i][k] - c[k]) * (v[i][k] - c[k]);
+                    r2 = std::max(r2, d2);
+                }
+                const double pd = std::fabs(tn[0] * v[0][0] + tn[1] * v[0][1] + tn[2] * v[0][2]) / tnl;
+                const double cd = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) - std::sqrt(r2);
+                nb = std::max(pd, cd);
+            }
             ents.push_back({ t, h, m, std::max(0.0, nb * (1 - 1e-5) - 0.01) });
         }
     }
+    fs.waves++;
+    float tl[64];
+    int il[64];
+    for (int l = 0; l < 64; l++) { tl[l] = 3.4e38f; il[l] = -1; }
+    if (order >= 3) {
+        // one entry per triangle: both sheets' masks (64 lanes) and bounds;
+        // 3: 8 log2 buckets of the smaller bound, 4: sorted by it.  Every
+        // entry is walked (no termination test); an entry with no lane
+        // still above its bound is a skip.
+        struct M { int tri; uint64_t mask; double nb[2]; double key; };
+        std::vector<M> ms;
+        for (const Ent &e : ents) {
+            if (ms.empty() || ms.back().tri != e.tri) ms.push_back({ e.tri, 0ull, { 1e30, 1e30 }, 1e30 });
+            ms.back().mask |= (uint64_t)e.mask << (32 * e.sheet);
+            ms.back().nb[e.sheet] = e.nearB;
+            ms.back().key = std::min(ms.back().key, e.nearB);
+        }
+        auto bk = [](double nb) { return nb < 32 ? 0 : std::min(7, 1 + (int)std::floor(std::log2(nb / 32))); };
+        if (order == 3)
+            std::stable_sort(ms.begin(), ms.end(), [&](const M &a, const M &b) { return bk(a.key) < bk(b.key); });
+        else
+            std::stable_sort(ms.begin(), ms.end(), [](const M &a, const M &b) { return a.key < b.key; });
+        fs.entries += ms.size();
+        if (ms.size() > 64) fs.bigLists++;
+        for (const M &c : ms) {
+            fs.walked++;
+            bool act = false;
+            for (int l = 0; l < 64; l++) {
+                if (!((c.mask >> l) & 1) || !(c.nb[l >> 5] < tl[l])) continue;
+                act = true;
+                fs.laneTests++;
+                float th;
+                if (tri(&verts[c.tri * 9], &rays[6 * (r0 + l)], &rays[6 * (r0 + l) + 3], 3.4e38f, th) &&
+                    (th < tl[l] || (th == tl[l] && c.tri < il[l]))) { tl[l] = th; il[l] = c.tri; }
+            }
+            if (act) fs.full++;
+        }
+    } else {
     if (order == 0) {
         std::stable_sort(ents.begin(), ents.end(), [](const Ent &a, const Ent &b) { return a.nearB < b.nearB; });
     } else if (order == 1) {
@@ -478,12 +569,8 @@ static void fanWave(const float *rays, size_t r0, int order, FanStats &fs)
         auto bk = [](double nb) { return nb < 64 ? 0 : std::min(15, 1 + (int)std::floor(std::log2(nb / 64) * 2)); };
         std::stable_sort(ents.begin(), ents.end(), [&](const Ent &a, const Ent &b) { return bk(a.nearB) < bk(b.nearB); });
     }
-    fs.waves++;
     fs.entries += ents.size();
     if (ents.size() > 64) fs.bigLists++;
-    float tl[64];
-    int il[64];
-    for (int l = 0; l < 64; l++) { tl[l] = 3.4e38f; il[l] = -1; }
     for (size_t ci = 0; ci < ents.size(); ci++) {
         bool anyLater = false;
         for (size_t cj = ci; cj < ents.size() && !anyLater; cj++)
@@ -503,6 +590,7 @@ static void fanWave(const float *rays, size_t r0, int order, FanStats &fs)
                 (th < tl[l] || (th == tl[l] && c.tri < il[l]))) { tl[l] = th; il[l] = c.tri; }
         }
         if (act) fs.full++;
+    }
     }
     // brute force: min (t, triangle) over every triangle
     for (int l = 0; l < 64; l++) {
@@ -572,7 +660,7 @@ int main(int argc, char **argv)
             printf("accepted hits: origin on the +normal side %ld, on the -normal side %ld\n", pos, neg);
             g_frontSign = getenv("TRAV_FAN_NOBF") ? 0 : (pos > neg ? 1 : -1);
         }
-        for (int order = 0; order < 3; order++) {
+        for (int order = 0; order < 5; order++) {
             FanStats fs;
             double octNode = 0, octTri = 0;
             size_t nf = 0;
@@ -601,7 +689,7 @@ int main(int argc, char **argv)
             printf("fan lists, %s: per forward wave: (tri, sheet) entries %.1f (lists > 64: %.3f), walked %.1f, "
                    "lockstep full tests %.1f, lane tests/ray %.2f | per sheet: front-facing %.1f, in the band %.1f | "
                    "closest hits differing from brute force %.0f of %zu",
-                   order == 0 ? "sorted  " : order == 1 ? "bucketed" : "unsorted", fs.entries / fs.waves,
+                   order == 0 ? "sorted  " : order == 1 ? "bucketed" : order == 2 ? "unsorted" : order == 3 ? "merged, 8 buckets, walk all" : "merged, sorted, walk all", fs.entries / fs.waves,
                    fs.bigLists / fs.waves, fs.walked / fs.waves, fs.full / fs.waves, fs.laneTests / nf,
                    fs.planeTests / fs.waves / 2, fs.straddle / fs.waves / 2, fs.wrong, nf);
             if (!order) printf(" | octant BVH lockstep: node iters %.2f, tri tests %.2f", octNode / fs.waves, octTri / fs.waves);
