@@ -47,17 +47,21 @@ TAPE_SEED = 1234
 #            w (8); explore tile cache (tile, 64-bit word) r+w (24);
 #            rewardCoefs r (4)                                      = 300
 #   k_vis  : pos 12 + aim rot 16 + pose 4 + alive 4 r; mask w 1   = 37
-#   k_obs  : state r ~124; self 172 + teammates 640 + opponents 768 +
-#            last-known 768 w, last-known 768 r; positions 12+60+72 w,
-#            last-known pos 72 r+w (144); masks 24 + filters 4 w; vis 1 r;
-#            full-team player 112 + enemy 132 + last-known 96 w  = 3893
+#   k_obs  : state r ~124; self 172 + teammates 640 + opponents 768 w;
+#            positions 12+60+72 w; masks 24 + filters 4 w; vis 1 r;
+#            full-team player 112 + enemy 132 + last-known 96 w  = 2213,
+#            plus 140 B (a 128-B row + its 12-B position) per last-known row
+#            written (when the team knows the opponent, or it died), counted
+#            per step by the workload counter lk_rows (rounds 1-3 charged
+#            every row every step, read and written: 3,893 B)
 #   k_lidar: pos 12 + rot 16 + aim rot 16 + pose 4 r; 80 rays x 16 B w;
 #            previous rays 80 x 16 B r + full-team copy 80 x 16 B w = 3888
 # plus per world-step: 32 singleton columns x 4 B r+w (256), full-team
 # reward/done 16 w and the live breadcrumbs r+w (32 B each; 18.8 per world
 # at steady state under the tape, oracle rollout of 256 worlds, steps
 # 100-1100: 1,203 B) in k_sim; full-team global 2 x 64 w in k_obs.
-KERNEL_BYTES_PER_AGENT = {"k_move": 184, "k_sim": 300, "k_vis": 37, "k_obs": 3893, "k_lidar": 3888}
+KERNEL_BYTES_PER_AGENT = {"k_move": 184, "k_sim": 300, "k_vis": 37, "k_obs": 2213, "k_lidar": 3888}
+LK_ROW_BYTES = 140  # k_obs, per last-known row written (counter lk_rows)
 KERNEL_BYTES_PER_WORLD = {"k_move": 0, "k_sim": 1475, "k_vis": 0, "k_obs": 128, "k_lidar": 0}
 
 
@@ -75,12 +79,14 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline timed budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPUs this process may use")
-    ap.add_argument("--exchange", choices=["auto", "none", "gather", "local"], default="auto",
-                    help="learner exchange over RCCL (named in config.parallelism): gather = every shipped "
-                         "trainInterface output to rank 0 each step, overlapped with the next step "
-                         "(config C4 as named; the default for N>1); local = each rank's learner keeps "
-                         "its shard, a gradient-sized all-reduce every --update-every steps; none = "
-                         "simulators only (the default at N=1)")
+    ap.add_argument("--exchange", choices=["auto", "none", "gather", "wire", "local"], default="auto",
+                    help="learner exchange over RCCL (named in config.parallelism): wire = every "
+                         "trainInterface output to rank 0 each step in the compact wire format, rebuilt "
+                         "there bit for bit (config C4 as named; the default for N>1; at N=1 a loopback: "
+                         "pack + unpack into a shadow on the same GPU); gather = the same outputs as "
+                         "exported (3,924 B per agent); local = each rank's learner keeps its shard, a "
+                         "gradient-sized all-reduce every --update-every steps; none = simulators only "
+                         "(the default at N=1)")
     ap.add_argument("--gather", action="store_true", help="alias of --exchange gather")
     ap.add_argument("--grad-mb", type=float, default=16.0, help="local exchange: all-reduced gradient MB")
     ap.add_argument("--update-every", type=int, default=50,
@@ -281,7 +287,7 @@ def main():
     dev = torch.device("cuda", gpu)
     exchange = "gather" if args.gather else args.exchange
     if exchange == "auto":
-        exchange = "gather" if world_size > 1 and not args.share_device else "none"
+        exchange = "wire" if world_size > 1 and not args.share_device else "none"
     xgroup = None
     if world_size > 1:
         # Control plane (barriers, max-over-ranks time) on gloo: the step has
@@ -334,9 +340,21 @@ def main():
     ring = torch.from_numpy(mpenv_tape.tape_ring(TAPE_SEED, offset * N, A, RING)).to(dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    learner = make_exchange(exchange, sim, group=xgroup, grad_bytes=int(args.grad_mb * (1 << 20)),
-                            update_every=args.update_every) if exchange == "local" else \
-        make_exchange(exchange, sim, group=xgroup)
+    def make_shadow(r):
+        # the learner's copy of rank r's engine: same configuration, rank r's
+        # worlds (wire.hip rebuilds r's outputs into it)
+        return m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=gpu, num_worlds=W, rand_seed=5,
+                            auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                            team_size=ts, num_pbt_policies=0, policy_history_size=0,
+                            scene_path=args.scene, world_id_offset=r * W)
+
+    if exchange == "local":
+        learner = make_exchange(exchange, sim, group=xgroup, grad_bytes=int(args.grad_mb * (1 << 20)),
+                                update_every=args.update_every)
+    elif exchange == "wire":
+        learner = make_exchange(exchange, sim, group=xgroup, make_shadow=make_shadow)
+    else:
+        learner = make_exchange(exchange, sim, group=xgroup)
 
     policy = make_policy(sim, args.policy_hidden, dev) if args.actions == "policy" else None
     stream_ptrs = None
@@ -459,6 +477,8 @@ def main():
     }
     if learner is not None:
         result["exchange_bytes_per_step"] = learner.bytes_per_step()
+        if exchange in ("wire", "gather"):
+            result["exchange_bytes_per_agent"] = round(result["exchange_bytes_per_step"]["sent_per_rank"] / A, 1)
     if stream_ptrs is not None:
         result["config"]["path"] = "gpuStreamStep (mgr.cpp:614-645)"
         result["stream_copy_bytes_per_step"] = stream_bytes
@@ -467,12 +487,13 @@ def main():
         steps = args.steps
         dom = max(timings, key=lambda k: timings[k][0])
         dom_ms = timings[dom][0]
-        alg = KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W
+        lk_bytes = LK_ROW_BYTES * counts.get("lk_rows", 0) / steps  # k_obs's conditional rows, per step
+        alg = KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W + (lk_bytes if dom == "k_obs" else 0)
         achieved = alg / (dom_ms * 1e-3) / 1e9
         prof = load_profile(args.traffic, workload)
         traffic = prof.get("per_kernel", {}).get(dom)
         valu = prof.get("valu_insts_per_launch", {}).get(dom)
-        step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W
+        step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W + lk_bytes
         kern_ms = sum(v[0] for v in timings.values())
         result["roofline"] = {
             "bound": KERNEL_BOUND[dom],
@@ -489,6 +510,10 @@ def main():
             # the limiter of the ray kernels: VALU issue (PMC instructions
             # per launch from profiles/, same workload) over the launch time
             "valu_issue": None if not valu else {
+                "window": f"PMC instructions from {os.path.basename(args.traffic)} (tag {prof.get('tag')}: its "
+                          f"profile pass, one world group); launch time from this run's profile pass "
+                          f"(steps {args.warmup}..{args.warmup + args.steps - 1})",
+                "same_window": prof.get("bench_window") == [args.warmup, args.steps],
                 "insts_per_launch": valu,
                 "achieved_per_s": round(valu / (dom_ms * 1e-3), 1),
                 "peak_per_s": VALU_PEAK,
@@ -498,7 +523,11 @@ def main():
         }
         result["kernels_ms"] = {k: round(v[0], 4) for k, v in timings.items()}
         result["step_hbm"] = {
-            "algorithmic_bytes_per_step": step_bytes,
+            "note": "sum of the kernels' algorithmic bytes (state each kernel reads counted per kernel); "
+                    "survey_8d_bytes_per_step = SURVEY.md 8(d)'s whole-step definition, A x 4,468 + W x 512",
+            "algorithmic_bytes_per_step": round(step_bytes),
+            "survey_8d_bytes_per_step": 4468 * A + 512 * W,
+            "lk_rows_per_step": round(counts.get("lk_rows", 0) / steps, 1),
             "kernel_ms_per_step": round(kern_ms, 4),
             "achieved_GBps_over_kernels": round(step_bytes / (kern_ms * 1e-3) / 1e9, 2),
         }

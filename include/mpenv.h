@@ -380,6 +380,29 @@ int mpenv_combat_actions(mpenv_manager *mgr, const int32_t *tape_device, int32_t
 int mpenv_debug_trace_rays(mpenv_manager *mgr, const float *o_device, const float *d_device, int32_t n,
                            int32_t mode, float *t_device, int32_t *hit_device, void *hip_stream);
 
+/* Extension, the learner exchange's compact wire format (DESIGN.md §6;
+ * replaces shipping the trainInterface outputs of mgr.cpp:2383-2431 as they
+ * are exported, 3,924 B per agent, with ~477 B per agent + 160 B per world).
+ * pack: one message of this step's outputs into dst (device memory of
+ * mpenv_wire_bytes bytes), asynchronous on hip_stream; keyframe != 0 also
+ * carries the last-known rows (the first message of an exchange).
+ * unpack: on the learner, into a manager of the same configuration (the
+ * sender's shadow): the message's state, lidar and rewards, then the
+ * observation system over them, so every trainInterface output of the
+ * shadow equals the sender's bit for bit.  A message for another
+ * configuration, of the other kind, or one whose values did not fit the
+ * packed fields is not unpacked and raises the error word that
+ * mpenv_wire_error returns (and clears; it synchronises the device). */
+int mpenv_wire_bytes(mpenv_manager *mgr, int32_t keyframe, int64_t *bytes);
+int mpenv_wire_pack(mpenv_manager *mgr, void *dst_device, int32_t keyframe, void *hip_stream);
+int mpenv_wire_unpack(mpenv_manager *mgr, const void *src_device, int32_t keyframe, void *hip_stream);
+int mpenv_wire_error(mpenv_manager *mgr, uint32_t *out);
+
+/* Measurement hook: how many times the Step graph has been captured (the
+ * graph is re-captured whenever a kernel argument struct changes: world
+ * groups, stats or timing buffers; every other step replays it). */
+int mpenv_graph_captures(mpenv_manager *mgr, int64_t *out);
+
 /* Extension: step the worlds as `groups` contiguous ranges on concurrent
  * HIP streams (fork/join on the step stream; results identical for any
  * split).  Default: 2 for >= 3072 worlds, else 1; env MPENV_WORLD_GROUPS
@@ -417,8 +440,9 @@ int mpenv_enable_kernel_timing(mpenv_manager *mgr, int32_t enable);
  * [0] alive agents at k_move, [1] (viewer, opponent) pairs both alive,
  * [2] visibility rays traced, [3] visibility rays that saw their target,
  * [4] sphere casts, [5] shot rays, [6] agents that took damage, [7] agents
- * killed.  read_stats copies min(n, 8) counters
- * and returns the number of counters (8). */
+ * killed, [8] last-known observation rows written by the observation
+ * system.  read_stats copies min(n, 9) counters and returns the number of
+ * counters (9). */
 int mpenv_enable_stats(mpenv_manager *mgr, int32_t enable);
 int mpenv_read_stats(mpenv_manager *mgr, uint64_t *out, int32_t n);
 

@@ -26,7 +26,7 @@ LIB = os.path.join(PKG, "libmpenv.so")
 EXT = os.path.join(PKG, "madrona_mp_env" + sysconfig.get_config_var("EXT_SUFFIX"))
 ORACLE_LIB = os.path.join(ORACLE, "_build", "liboracle.so")
 
-LIB_SOURCES = ["kernels.hip", "manager.cpp", "scene.cpp", "navmesh.cpp"]
+LIB_SOURCES = ["kernels.hip", "wire.hip", "manager.cpp", "scene.cpp", "navmesh.cpp"]
 LIB_HEADERS = ["mpenv_core.h", "engine.h", "geom_dev.h", "scene.h"]
 
 

@@ -170,10 +170,11 @@ enum StatId {
     kStatShots = 5,       // fireSystem rays (k_sim)
     kStatHits = 6,        // agents that took damage (applyDmgSystem)
     kStatKills = 7,       // agents killed (alive -> hp <= 0)
+    kStatLkRows = 8,      // last-known rows k_obs wrote (knows / cleared on death)
 #if defined(MPENV_LAB_PHASE_T)
-    kNumStats = 24, // lab: k_sim phase cycles in slots 8..
+    kNumStats = 25, // lab: k_sim phase cycles in slots 9..
 #else
-    kNumStats = 8,
+    kNumStats = 9,
 #endif
 };
 
@@ -301,5 +302,10 @@ int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, fl
 int launchFillActions(const DevState &s, const int32_t *src6, void *stream);
 int launchCombatActions(const DevState &s, const int32_t *tape6, int32_t *out6, int32_t mode, void *stream);
 int computeSceneFrames(SceneTables *d_tab, void *stream); // fills zoneFrame / goalFrame in place
+
+// Learner-exchange wire format (wire.hip)
+int64_t wireBytes(const DevState &s, bool keyframe);
+int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOffset, void *stream);
+int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, void *stream);
 
 } // namespace mpenv

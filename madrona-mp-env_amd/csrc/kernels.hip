@@ -2414,7 +2414,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     auto PT = [&]() {
         if (threadIdx.x == 0 && S.stats) {
             const uint64_t t = clock64();
-            atomicAdd(&S.stats[8 + pt_k], (unsigned long long)(t - pt_prev));
+            atomicAdd(&S.stats[9 + pt_k], (unsigned long long)(t - pt_prev));
             pt_prev = t;
         }
         pt_k++;
@@ -2776,10 +2776,9 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
         const float len = length(to_test);
         to_test = to_test / len;
-#ifndef MPENV_VIS_OCC
-#define MPENV_VIS_OCC 1
-#endif
-        uint16_t *occ = MPENV_VIS_OCC ? S.visOcc + (g * T + k) * 4 + p : nullptr;
+        // the occluder hint (geom_dev.h visibleRayD) stores triangle ids as
+        // u16 with 0xffff = none: off for scenes of 65,535 triangles or more
+        uint16_t *occ = sc.numVerts / 3 < 0xffff ? S.visOcc + (g * T + k) * 4 + p : nullptr;
         const bool seen = visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target, occ,
                                       (uint32_t)(sc.numVerts / 3));
         if (seen) atomicOr(&masks[(int)(g - agent0)], 1u << k);
@@ -3320,6 +3319,7 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
         flushRowsWave(S.oppObs, 6, k, gw0, S.A, wbuf, lane);
         // the rows are still staged (stride kObsRowPad): the last-known copy
         ws.flush4<kOtherObs / 4, kObsRowPad>(S.lkObs, lk_write ? (g * 6 + k) * kOtherObs : -1, !lk_keep);
+        if (S.stats) statAdd(S.stats + kStatLkRows, lk_write ? 1u : 0u);
         for (int q = 0; q < 3; q++) prow[3 * k + q] = opos[q];
         {
             float lpos[3];

@@ -147,11 +147,21 @@ struct mpenv_manager {
     hipGraph_t stepGraph = nullptr;
     hipGraphExec_t stepExec = nullptr;
     std::vector<char> graphKey;
+    // recorded after every hipGraphLaunch on the launch's stream: a
+    // re-capture waits on it before destroying the previous exec (its last
+    // launch may still run on a caller stream the manager does not own)
+    hipEvent_t graphDoneEv = nullptr;
+    int64_t graphCaptures = 0; // mpenv_graph_captures
+    uint32_t *wireErr = nullptr; // device word raised by a rejected wire message (wire.hip)
 
     ~mpenv_manager()
     {
         if (stream) (void)hipStreamSynchronize(stream);
         for (hipStream_t gs : gstreams) (void)hipStreamSynchronize(gs);
+        if (graphDoneEv) {
+            (void)hipEventSynchronize(graphDoneEv);
+            (void)hipEventDestroy(graphDoneEv);
+        }
         if (stepExec) (void)hipGraphExecDestroy(stepExec);
         if (stepGraph) (void)hipGraphDestroy(stepGraph);
         if (capStream) (void)hipStreamDestroy(capStream);
@@ -284,6 +294,7 @@ struct mpenv_manager {
         }
         std::vector<char> key = argKey();
         if (!stepExec || key != graphKey) {
+            if (graphDoneEv) HIP_CHECK(hipEventSynchronize(graphDoneEv));
             if (stepExec) HIP_CHECK(hipGraphExecDestroy(stepExec));
             if (stepGraph) HIP_CHECK(hipGraphDestroy(stepGraph));
             stepExec = nullptr;
@@ -304,8 +315,11 @@ struct mpenv_manager {
             HIP_CHECK(hipStreamEndCapture(capStream, &stepGraph));
             HIP_CHECK(hipGraphInstantiate(&stepExec, stepGraph, nullptr, nullptr, 0));
             graphKey = std::move(key);
+            graphCaptures++;
         }
         HIP_CHECK(hipGraphLaunch(stepExec, st));
+        if (!graphDoneEv) HIP_CHECK(hipEventCreateWithFlags(&graphDoneEv, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(graphDoneEv, st));
     }
 
     void launchStepDirect(hipStream_t st)
@@ -678,6 +692,8 @@ static void allocState(mpenv_manager &m)
     S.dmg = m.alloc<float>(A * kMaxTeamSize);
     S.dmgStride = (int64_t)A;
     S.visMask = m.alloc<uint8_t>(A);
+    m.wireErr = m.alloc<uint32_t>(1);
+    HIP_CHECK(hipMemsetAsync(m.wireErr, 0, sizeof(uint32_t), m.stream));
     S.visOcc = m.alloc<uint16_t>((size_t)A * S.T * 4);
     HIP_CHECK(hipMemsetAsync(S.visOcc, 0xff, sizeof(uint16_t) * (size_t)A * S.T * 4, m.stream));
     S.exploreBits = m.alloc<uint64_t>(A * kExploreTiles);
@@ -1074,6 +1090,53 @@ int mpenv_debug_trace_rays(mpenv_manager *m, const float *o, const float *d, int
     hipStream_t st = stream ? (hipStream_t)stream : m->stream;
     if (launchTraceRays(m->sc, o, d, n, mode, t_out, hit_out, st) || hipStreamSynchronize(st) != hipSuccess)
         return fail(MPENV_ERR_HIP, "trace-ray launch failed");
+    return MPENV_OK;
+}
+
+// Learner exchange wire format (wire.hip)
+int mpenv_wire_bytes(mpenv_manager *m, int32_t keyframe, int64_t *bytes)
+{
+    if (!m || !bytes) return fail(MPENV_ERR_INVALID, "null argument");
+    *bytes = wireBytes(m->S, keyframe != 0);
+    return MPENV_OK;
+}
+
+int mpenv_wire_pack(mpenv_manager *m, void *dst, int32_t keyframe, void *stream)
+{
+    if (!m || !dst) return fail(MPENV_ERR_INVALID, "null argument");
+    if (launchWirePack(m->S, static_cast<char *>(dst), keyframe != 0, m->sc.worldOffset,
+                       stream ? stream : (void *)m->stream))
+        return fail(MPENV_ERR_HIP, "wire pack launch failed");
+    return MPENV_OK;
+}
+
+int mpenv_wire_unpack(mpenv_manager *m, const void *src, int32_t keyframe, void *stream)
+{
+    if (!m || !src) return fail(MPENV_ERR_INVALID, "null argument");
+    void *st = stream ? stream : (void *)m->stream;
+    if (launchWireUnpack(m->S, static_cast<const char *>(src), keyframe != 0, m->wireErr, st) ||
+        launchObservations(m->S, m->sc, st))
+        return fail(MPENV_ERR_HIP, "wire unpack launch failed");
+    return MPENV_OK;
+}
+
+int mpenv_wire_error(mpenv_manager *m, uint32_t *out)
+{
+    if (!m || !out) return fail(MPENV_ERR_INVALID, "null argument");
+    try {
+        HIP_CHECK(hipDeviceSynchronize());
+        HIP_CHECK(hipMemcpy(out, m->wireErr, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemset(m->wireErr, 0, sizeof(uint32_t)));
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_graph_captures(mpenv_manager *m, int64_t *out)
+{
+    if (!m || !out) return fail(MPENV_ERR_INVALID, "null argument");
+    *out = m->graphCaptures;
     return MPENV_OK;
 }
 

@@ -239,18 +239,38 @@ PYBIND11_MODULE(madrona_mp_env, m)
             for (size_t k = 0; k < bufs.size(); k++) b[k] = reinterpret_cast<void *>(bufs[k]);
             check(mpenv_gpu_stream_step(s.h->mgr, reinterpret_cast<void *>(stream), b.data()));
         }, py::arg("stream"), py::arg("buffers"))
+        // the learner exchange's compact wire format (include/mpenv.h
+        // mpenv_wire_*): sizes, pack into / unpack from device buffers
+        .def("wire_bytes", [](PySimManager &s, bool keyframe) {
+            int64_t b = 0;
+            check(mpenv_wire_bytes(s.h->mgr, keyframe ? 1 : 0, &b));
+            return b;
+        }, py::arg("keyframe") = false)
+        .def("wire_pack", [](PySimManager &s, uintptr_t dst, bool keyframe, uintptr_t stream) {
+            check(mpenv_wire_pack(s.h->mgr, reinterpret_cast<void *>(dst), keyframe ? 1 : 0,
+                                  reinterpret_cast<void *>(stream)));
+        }, py::arg("dst"), py::arg("keyframe") = false, py::arg("stream") = 0)
+        .def("wire_unpack", [](PySimManager &s, uintptr_t src, bool keyframe, uintptr_t stream) {
+            check(mpenv_wire_unpack(s.h->mgr, reinterpret_cast<const void *>(src), keyframe ? 1 : 0,
+                                    reinterpret_cast<void *>(stream)));
+        }, py::arg("src"), py::arg("keyframe") = false, py::arg("stream") = 0)
+        .def("wire_error", [](PySimManager &s) {
+            uint32_t e = 0;
+            check(mpenv_wire_error(s.h->mgr, &e));
+            return e;
+        })
         .def("set_world_groups", [](PySimManager &s, int32_t g) { check(mpenv_set_world_groups(s.h->mgr, g)); })
         .def("world_groups", [](PySimManager &s) { int32_t g = 0; check(mpenv_world_groups(s.h->mgr, &g)); return g; })
         .def("enable_kernel_timing", [](PySimManager &s, bool on) { check(mpenv_enable_kernel_timing(s.h->mgr, on)); })
         .def("enable_stats", [](PySimManager &s, bool on) { check(mpenv_enable_stats(s.h->mgr, on)); })
         .def("read_stats", [](PySimManager &s) {
-            uint64_t v[8] = {};
-            int n = mpenv_read_stats(s.h->mgr, v, 8);
+            uint64_t v[9] = {};
+            int n = mpenv_read_stats(s.h->mgr, v, 9);
             if (n < 0) check(n);
-            static const char *names[8] = { "alive_agents", "los_pairs", "los_rays", "los_seen",
-                                            "sphere_casts", "shot_rays", "hit_agents", "kills" };
+            static const char *names[9] = { "alive_agents", "los_pairs", "los_rays", "los_seen",
+                                            "sphere_casts", "shot_rays", "hit_agents", "kills", "lk_rows" };
             py::dict d;
-            for (int k = 0; k < 8; k++) d[py::str(names[k])] = v[k];
+            for (int k = 0; k < 9; k++) d[py::str(names[k])] = v[k];
             return d;
         })
         .def("kernel_timings", [](PySimManager &s) {

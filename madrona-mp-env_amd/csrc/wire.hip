@@ -1,0 +1,308 @@
+// wire.hip — the learner exchange's compact wire format.
+//
+// mpenv_wire_pack turns one step of a shard's trainInterface outputs
+// (mgr.cpp:2383-2431, 3,924 B per agent as exported) into a message of
+// ~477 B per agent + 160 B per world; mpenv_wire_unpack, on the learner,
+// rebuilds every output bit for bit into a shadow manager of the same
+// configuration:
+//   * lidar as the f32 depth of each ray plus its class in two bit-planes
+//     (none / wall / teammate / opponent), 340 B per agent instead of 1,280:
+//     pvpLidarSystem writes (min(t, maxDist), wall, teammate, opponent) or
+//     (-1, 0, 0, 0) (sim.cpp:3324-3506), so the class decides the three
+//     one-hot channels;
+//   * the observation rows (self, teammates, opponents, positions, masks,
+//     filters) are not shipped: the message carries the agent and world
+//     state they are computed from and the shadow runs the same k_obs on it,
+//     so the rows come out of the same device code on the same inputs;
+//   * the last-known rows are the one piece of history k_obs reads: the
+//     shadow keeps its own copy, clears a world's rows when that world's
+//     episode counter moves (resetPersistentEntities is the only other
+//     writer, level_gen.cpp:330-370) and k_obs updates them as on the
+//     sender; a keyframe message carries them once (the first message of an
+//     exchange, which may start mid-episode);
+//   * small integer fields are packed into one word; the pack kernel flags
+//     any value outside its packed range (or a lidar ray off the pattern
+//     above) in the header and unpack then refuses the message.
+// Columns are structure-of-arrays blocks, 256-B aligned, so both kernels
+// read and write coalesced rows (thread = agent, ray or world).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "engine.h"
+#include "mpenv_core.h"
+
+namespace mpenv {
+
+using namespace mp;
+
+constexpr uint32_t kWireMagic = 0x3157504du; // "MPW1"
+constexpr uint32_t kWireVersion = 1;
+constexpr uint32_t kWireKeyframe = 1u, kWireOverflow = 2u;
+
+// agent f32 columns, agent i32 columns, world i32 columns (order = wire order)
+#define MP_WIRE_AF(X) \
+    X(px) X(py) X(pz) X(vx) X(vy) X(vz) X(rw) X(rx) X(ry) X(rz) X(ayaw) X(apitch) X(dyv) X(dpv) X(firedT)
+#define MP_WIRE_AI(X) X(transRem) X(wasShot) X(autohealSteps)
+#define MP_WIRE_WI(X) \
+    X(curStep) X(filtMatched0) X(filtMatched1) X(curZone) X(controlling) X(contested) X(captured) \
+    X(stepsUntilPoint) X(zoneSteps) X(episodeCounter)
+#define MP_COUNT(n) +1
+constexpr int kWireAF = 0 MP_WIRE_AF(MP_COUNT);
+constexpr int kWireAI = 0 MP_WIRE_AI(MP_COUNT);
+constexpr int kWireWI = 0 MP_WIRE_WI(MP_COUNT);
+#undef MP_COUNT
+
+struct WireHeader {
+    uint32_t magic, version, flags, worldOffset;
+    int32_t W, N, T, pad;
+    int64_t A, bytes;
+    uint32_t reserved[8];
+};
+static_assert(sizeof(WireHeader) == 80, "wire header");
+
+struct WireLayout {
+    int64_t af[kWireAF], hp, alive, reward; // f32 [A]
+    int64_t ai[kWireAI], done, mag;         // i32 [A] (mag: [A][2])
+    int64_t packed;                         // u32 [A]: curPose | tgtPose << 8 | weapon << 16 | flags << 24
+    int64_t vis;                            // u8 [A]
+    int64_t coefs;                          // f32 [A][9]
+    int64_t depth;                          // f32 [A * 80]
+    int64_t plane[2];                       // u32 [ceil(A * 80 / 32)]
+    int64_t wi[kWireWI], match;             // i32 [W], [W][30]
+    int64_t lkObs, lkPos;                   // keyframes: f32 [A][6][32], [A][6][3]
+    int64_t total;
+};
+
+__host__ __device__ inline WireLayout wireLayout(int64_t A, int64_t W, bool keyframe)
+{
+    WireLayout L {};
+    int64_t off = 256; // header
+    auto take = [&](int64_t bytes) {
+        const int64_t o = off;
+        off += (bytes + 255) / 256 * 256;
+        return o;
+    };
+    for (int k = 0; k < kWireAF; k++) L.af[k] = take(A * 4);
+    L.hp = take(A * 4);
+    L.alive = take(A * 4);
+    L.reward = take(A * 4);
+    for (int k = 0; k < kWireAI; k++) L.ai[k] = take(A * 4);
+    L.done = take(A * 4);
+    L.mag = take(A * 8);
+    L.packed = take(A * 4);
+    L.vis = take(A);
+    L.coefs = take(A * 36);
+    L.depth = take(A * kLidarRays * 4);
+    const int64_t words = (A * kLidarRays + 31) / 32;
+    L.plane[0] = take(words * 4);
+    L.plane[1] = take(words * 4);
+    for (int k = 0; k < kWireWI; k++) L.wi[k] = take(W * 4);
+    L.match = take(W * 120);
+    L.lkObs = keyframe ? take(A * 6 * kOtherObs * 4) : -1;
+    L.lkPos = keyframe ? take(A * 18 * 4) : -1;
+    L.total = off;
+    return L;
+}
+
+// ------------------------------------------------------------------ pack
+// thread = agent: state columns (and, for a keyframe, the last-known rows)
+__global__ void k_wire_pack_agents(DevState S, char *dst, WireLayout L)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= S.A) return;
+    int k = 0;
+#define MP_PUT_F(n) reinterpret_cast<float *>(dst + L.af[k++])[g] = S.n[g];
+    MP_WIRE_AF(MP_PUT_F)
+#undef MP_PUT_F
+    k = 0;
+#define MP_PUT_I(n) reinterpret_cast<int32_t *>(dst + L.ai[k++])[g] = S.n[g];
+    MP_WIRE_AI(MP_PUT_I)
+#undef MP_PUT_I
+    reinterpret_cast<float *>(dst + L.hp)[g] = S.hp[g];
+    reinterpret_cast<float *>(dst + L.alive)[g] = S.alive[g];
+    reinterpret_cast<float *>(dst + L.reward)[g] = S.reward[g];
+    reinterpret_cast<int32_t *>(dst + L.done)[g] = S.done[g];
+    reinterpret_cast<int2 *>(dst + L.mag)[g] = make_int2(S.magazine[2 * g], S.magazine[2 * g + 1]);
+    const int32_t cp = S.curPose[g], tp = S.tgtPose[g], wp = S.weapon[g], fl = S.flags[g];
+    const bool fits = ((uint32_t)cp | (uint32_t)tp | (uint32_t)wp | (uint32_t)fl) < 256u;
+    reinterpret_cast<uint32_t *>(dst + L.packed)[g] =
+        (uint32_t)cp | ((uint32_t)tp << 8) | ((uint32_t)wp << 16) | ((uint32_t)fl << 24);
+    reinterpret_cast<uint8_t *>(dst + L.vis)[g] = S.visMask[g];
+    for (int c = 0; c < 9; c++) reinterpret_cast<float *>(dst + L.coefs)[g * 9 + c] = S.rewardCoefs[g * 9 + c];
+    if (L.lkObs >= 0) {
+        const float4 *src = reinterpret_cast<const float4 *>(S.lkObs + g * 6 * kOtherObs);
+        float4 *o = reinterpret_cast<float4 *>(dst + L.lkObs) + g * 6 * kOtherObs / 4;
+        for (int q = 0; q < 6 * kOtherObs / 4; q++) o[q] = src[q];
+        for (int q = 0; q < 18; q++) reinterpret_cast<float *>(dst + L.lkPos)[g * 18 + q] = S.lkPos[g * 18 + q];
+    }
+    if (!fits) atomicOr(&reinterpret_cast<WireHeader *>(dst)->flags, kWireOverflow);
+}
+
+// thread = lidar ray (agent * 80 + ray, forward rays first): the depth, and
+// the class in two bit-planes (one ballot per plane per 64 rays)
+__global__ void k_wire_pack_lidar(DevState S, char *dst, WireLayout L)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nr = S.A * kLidarRays;
+    uint32_t c = 0;
+    bool ok = true;
+    if (r < nr) {
+        const int64_t g = r / kLidarRays;
+        const int k = (int)(r - g * kLidarRays);
+        const float4 v = k < kFwdRays ? reinterpret_cast<const float4 *>(S.fwdLidar)[g * kFwdRays + k]
+                                      : reinterpret_cast<const float4 *>(S.rearLidar)[g * kRearRays + k - kFwdRays];
+        reinterpret_cast<float *>(dst + L.depth)[r] = v.x;
+        const uint32_t y = __float_as_uint(v.y), z = __float_as_uint(v.z), w = __float_as_uint(v.w);
+        const uint32_t one = 0x3f800000u;
+        if (y == one && z == 0u && w == 0u) c = 1;
+        else if (y == 0u && z == one && w == 0u) c = 2;
+        else if (y == 0u && z == 0u && w == one) c = 3;
+        else ok = y == 0u && z == 0u && w == 0u && __float_as_uint(v.x) == 0xbf800000u; // (-1, 0, 0, 0)
+    }
+    const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c >> 1);
+    const int lane = threadIdx.x & 63;
+    const int64_t word = (r - lane) / 32; // first of the wave's two words
+    const int64_t words = (nr + 31) / 32;
+    if (lane < 4) {
+        const int p = lane >> 1, h = lane & 1;
+        const uint64_t b = p ? b1 : b0;
+        if (word + h < words) reinterpret_cast<uint32_t *>(dst + L.plane[p])[word + h] = (uint32_t)(b >> (32 * h));
+    }
+    if (!ok) atomicOr(&reinterpret_cast<WireHeader *>(dst)->flags, kWireOverflow);
+}
+
+// thread = world: world columns, episode results; thread 0 the header
+// (launched first: the agent and lidar kernels may then raise the overflow bit)
+__global__ void k_wire_pack_worlds(DevState S, char *dst, WireLayout L, uint32_t worldOffset)
+{
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w == 0) {
+        WireHeader *h = reinterpret_cast<WireHeader *>(dst);
+        h->magic = kWireMagic;
+        h->version = kWireVersion;
+        h->flags = L.lkObs >= 0 ? kWireKeyframe : 0u;
+        h->worldOffset = worldOffset;
+        h->W = S.W; h->N = S.N; h->T = S.T; h->pad = 0;
+        h->A = S.A;
+        h->bytes = L.total;
+    }
+    if (w >= S.W) return;
+    int k = 0;
+#define MP_PUT_W(n) reinterpret_cast<int32_t *>(dst + L.wi[k++])[w] = S.n[w];
+    MP_WIRE_WI(MP_PUT_W)
+#undef MP_PUT_W
+    for (int c = 0; c < 30; c++) reinterpret_cast<int32_t *>(dst + L.match)[w * 30 + c] = S.matchResult[w * 30 + c];
+}
+
+// ---------------------------------------------------------------- unpack
+// Every unpack kernel checks the header first: a message for another
+// configuration, of the other kind (keyframe or not), or one the pack kernels
+// flagged is not unpacked; *err is raised (mpenv_wire_error).
+__device__ __forceinline__ bool wireOk(const DevState &S, const char *src, const WireLayout &L, uint32_t *err)
+{
+    const WireHeader *h = reinterpret_cast<const WireHeader *>(src);
+    const bool ok = h->magic == kWireMagic && h->version == kWireVersion && h->W == S.W && h->N == S.N &&
+                    h->A == S.A && h->bytes == L.total && !(h->flags & kWireOverflow) &&
+                    ((h->flags & kWireKeyframe) != 0) == (L.lkObs >= 0);
+    if (!ok && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 1u);
+    return ok;
+}
+
+// thread = world: world columns; a world whose episode counter moved since
+// the last message had its agents' last-known rows cleared by the reset on
+// the sender (resetAgentD / resetPersistentEntitiesD): the same here.
+__global__ void k_wire_unpack_worlds(DevState S, const char *src, WireLayout L, uint32_t *err)
+{
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (!wireOk(S, src, L, err) || w >= S.W) return;
+    const int32_t ep = reinterpret_cast<const int32_t *>(src + L.wi[kWireWI - 1])[w];
+    if (ep != S.episodeCounter[w] && L.lkObs < 0) {
+        for (int64_t g = w * S.N; g < (w + 1) * S.N; g++) {
+            float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
+            for (int q = 0; q < 6 * kOtherObs / 4; q++) lk[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = 0; q < 18; q++) S.lkPos[g * 18 + q] = -1000.f;
+        }
+    }
+    int k = 0;
+#define MP_GET_W(n) S.n[w] = reinterpret_cast<const int32_t *>(src + L.wi[k++])[w];
+    MP_WIRE_WI(MP_GET_W)
+#undef MP_GET_W
+    for (int c = 0; c < 30; c++) S.matchResult[w * 30 + c] = reinterpret_cast<const int32_t *>(src + L.match)[w * 30 + c];
+}
+
+__global__ void k_wire_unpack_agents(DevState S, const char *src, WireLayout L, uint32_t *err)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (!wireOk(S, src, L, err) || g >= S.A) return;
+    int k = 0;
+#define MP_GET_F(n) S.n[g] = reinterpret_cast<const float *>(src + L.af[k++])[g];
+    MP_WIRE_AF(MP_GET_F)
+#undef MP_GET_F
+    k = 0;
+#define MP_GET_I(n) S.n[g] = reinterpret_cast<const int32_t *>(src + L.ai[k++])[g];
+    MP_WIRE_AI(MP_GET_I)
+#undef MP_GET_I
+    S.hp[g] = reinterpret_cast<const float *>(src + L.hp)[g];
+    S.alive[g] = reinterpret_cast<const float *>(src + L.alive)[g];
+    S.reward[g] = reinterpret_cast<const float *>(src + L.reward)[g];
+    S.done[g] = reinterpret_cast<const int32_t *>(src + L.done)[g];
+    const int2 mg = reinterpret_cast<const int2 *>(src + L.mag)[g];
+    S.magazine[2 * g] = mg.x;
+    S.magazine[2 * g + 1] = mg.y;
+    const uint32_t p = reinterpret_cast<const uint32_t *>(src + L.packed)[g];
+    S.curPose[g] = (int32_t)(p & 0xffu);
+    S.tgtPose[g] = (int32_t)((p >> 8) & 0xffu);
+    S.weapon[g] = (int32_t)((p >> 16) & 0xffu);
+    S.flags[g] = (int32_t)(p >> 24);
+    S.visMask[g] = reinterpret_cast<const uint8_t *>(src + L.vis)[g];
+    for (int c = 0; c < 9; c++) S.rewardCoefs[g * 9 + c] = reinterpret_cast<const float *>(src + L.coefs)[g * 9 + c];
+    if (L.lkObs >= 0) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(src + L.lkObs) + g * 6 * kOtherObs / 4;
+        float4 *lk = reinterpret_cast<float4 *>(S.lkObs + g * 6 * kOtherObs);
+        for (int q = 0; q < 6 * kOtherObs / 4; q++) lk[q] = s4[q];
+        for (int q = 0; q < 18; q++) S.lkPos[g * 18 + q] = reinterpret_cast<const float *>(src + L.lkPos)[g * 18 + q];
+    }
+}
+
+__global__ void k_wire_unpack_lidar(DevState S, const char *src, WireLayout L, uint32_t *err)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (!wireOk(S, src, L, err) || r >= S.A * kLidarRays) return;
+    const float d = reinterpret_cast<const float *>(src + L.depth)[r];
+    const uint32_t b0 = (reinterpret_cast<const uint32_t *>(src + L.plane[0])[r >> 5] >> (r & 31)) & 1u;
+    const uint32_t b1 = (reinterpret_cast<const uint32_t *>(src + L.plane[1])[r >> 5] >> (r & 31)) & 1u;
+    const uint32_t c = b0 | (b1 << 1);
+    const float4 v = make_float4(d, c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f, c == 3 ? 1.f : 0.f);
+    const int64_t g = r / kLidarRays;
+    const int k = (int)(r - g * kLidarRays);
+    if (k < kFwdRays) reinterpret_cast<float4 *>(S.fwdLidar)[g * kFwdRays + k] = v;
+    else reinterpret_cast<float4 *>(S.rearLidar)[g * kRearRays + k - kFwdRays] = v;
+}
+
+static int checkW(hipError_t e) { return e == hipSuccess ? 0 : -1; }
+static unsigned grid(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+int64_t wireBytes(const DevState &s, bool keyframe) { return wireLayout(s.A, s.W, keyframe).total; }
+
+int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOffset, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const WireLayout L = wireLayout(s.A, s.W, keyframe);
+    hipLaunchKernelGGL(k_wire_pack_worlds, dim3(grid(s.W)), dim3(256), 0, st, s, dst, L, worldOffset);
+    hipLaunchKernelGGL(k_wire_pack_agents, dim3(grid(s.A)), dim3(256), 0, st, s, dst, L);
+    hipLaunchKernelGGL(k_wire_pack_lidar, dim3(grid(s.A * kLidarRays)), dim3(256), 0, st, s, dst, L);
+    return checkW(hipGetLastError());
+}
+
+int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const WireLayout L = wireLayout(s.A, s.W, keyframe);
+    hipLaunchKernelGGL(k_wire_unpack_worlds, dim3(grid(s.W)), dim3(256), 0, st, s, src, L, err);
+    hipLaunchKernelGGL(k_wire_unpack_agents, dim3(grid(s.A)), dim3(256), 0, st, s, src, L, err);
+    hipLaunchKernelGGL(k_wire_unpack_lidar, dim3(grid(s.A * kLidarRays)), dim3(256), 0, st, s, src, L, err);
+    return checkW(hipGetLastError());
+}
+
+} // namespace mpenv

@@ -115,6 +115,11 @@ class LearnerGather:
     at construction), e.g.
     SimManager.train_interface()["outputs"] as torch tensors, or
     `from_sim(sim)`.
+
+    Construction is a collective call: every rank of `group` must construct
+    its LearnerGather at the same point (the layout check is an
+    all_gather_object over the group), and with an RCCL group each rank must
+    have called torch.cuda.set_device first.
     """
 
     NOT_SHIPPED = NOT_SHIPPED
@@ -249,7 +254,8 @@ class LearnerLocal:
         self.ws = dist.get_world_size(group)
         self.update_every = max(1, int(update_every))
         dev = next(iter(self.sources.values())).device
-        self.grad = torch.ones(max(1, grad_bytes // 4), dtype=torch.float32, device=dev)
+        # zeros: a SUM all-reduce keeps them finite however many updates run
+        self.grad = torch.zeros(max(1, grad_bytes // 4), dtype=torch.float32, device=dev)
         self.layout, self.nbytes = flat_layout(self.sources)
         self.pending = None
         self.k = 0
@@ -282,14 +288,152 @@ class LearnerLocal:
         self.drain()
 
 
+class LearnerWire:
+    """Per-step learner exchange in the compact wire format (csrc/wire.hip,
+    include/mpenv.h mpenv_wire_*): every rank packs one
+    message of its step's outputs (~477 B per agent + 160 B per world
+    instead of the 3,924 B per agent LearnerGather ships) into a 2-slot ring
+    on the step stream and sends it to the learner rank `dst`; the learner
+    receives each peer's message into its slot and unpacks it into that
+    peer's shadow manager (a SimManager of the same configuration), whose
+    own observation kernel rebuilds every trainInterface output bit for bit.
+    The first message of each sender is a keyframe (it also carries the
+    last-known rows).  Unpacking lags one step: `submit()` posts this
+    step's transfers and unpacks the previous slot's messages, so the
+    transfers overlap a whole step; `drain()` finishes both.
+
+    On `dst`, `outputs()` returns {name: [world_size, rows, ...]} stacked from
+    the learner's own engine (rank dst) and the shadows, in rank order
+    (global world order, as LearnerGather), after `drain()`.
+
+    pack(dst_ptr, keyframe, stream) / unpack(r, src_ptr, keyframe, stream) /
+    nbytes(keyframe) default to the SimManager's wire_* methods and
+    make_shadow(r) builds the shadow of rank r; the CPU tests substitute
+    byte-level stand-ins.  Construction is a collective call (the message
+    sizes are checked across the group); with RCCL, set the device first.
+
+    One rank (world_size 1, bench.py --exchange wire at N = 1): loopback --
+    the rank packs its own message and unpacks it into its own shadow each
+    step, so the line carries the per-message pack and unpack cost a learner
+    pays for each peer (nothing crosses xGMI).
+    """
+
+    NOT_SHIPPED = NOT_SHIPPED
+    mode = "wire"
+
+    def __init__(self, sim, make_shadow=None, dst: int = 0, group=None, slots: int = 2, pack=None, unpack=None,
+                 nbytes=None, device=None):
+        import torch
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.dst = dst
+        self.rank = dist.get_rank(group)
+        self.ws = dist.get_world_size(group)
+        self.sim = sim
+        self._nbytes = nbytes or (lambda kf: sim.wire_bytes(kf))
+        self._pack = pack or (lambda ptr, kf, st: sim.wire_pack(ptr, kf, st))
+        self.shadows = {}
+        self.loopback = self.ws == 1
+        if self.rank == dst and make_shadow is not None:
+            self.shadows = {r: make_shadow(r) for r in range(self.ws) if r != dst or self.loopback}
+        self._unpack = unpack or (lambda r, ptr, kf, st: self.shadows[r].wire_unpack(ptr, kf, st))
+        self.nb, self.nk = int(self._nbytes(False)), int(self._nbytes(True))
+        sizes = [None] * self.ws
+        dist.all_gather_object(sizes, (self.nb, self.nk), group=group)
+        if any(x != (self.nb, self.nk) for x in sizes):
+            raise ValueError(f"LearnerWire: message sizes differ across ranks: {sizes}")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.slots = slots
+        if self.rank == dst:
+            self.bufs = [[torch.empty(self.nk, dtype=torch.uint8, device=dev) for _ in range(self.ws)]
+                         for _ in range(slots)]
+        else:
+            self.bufs = [[torch.empty(self.nk, dtype=torch.uint8, device=dev)] for _ in range(slots)]
+        self.pending = [None] * slots
+        self.unpacked = [True] * slots
+        self.keyframe = [True] * slots  # the kind of message in each slot
+        self.k = 0
+
+    def bytes_per_step(self) -> dict:
+        return {"sent_per_rank": self.nb, "learner_ingress": self.nb * (self.ws - 1), "keyframe": self.nk}
+
+    def _peer(self, r):
+        return self.dist.get_global_rank(self.group, r) if self.group is not None else r
+
+    def _finish(self, slot, stream_ptr):
+        """Wait for a slot's transfers and (learner) unpack its messages."""
+        if self.pending[slot] is not None:
+            for w in self.pending[slot]:
+                w.wait()
+            self.pending[slot] = None
+        if self.rank == self.dst and not self.unpacked[slot]:
+            for r in range(self.ws):
+                if r != self.dst:
+                    self._unpack(r, self.bufs[slot][r].data_ptr(), self.keyframe[slot], stream_ptr or 0)
+            self.unpacked[slot] = True
+
+    def submit(self, stream_ptr=None):
+        dist = self.dist
+        slot = self.k % self.slots
+        kf = self.k == 0
+        self.k += 1
+        self._finish(slot, stream_ptr)  # the slot's previous round is done before it is reused
+        n = self.nk if kf else self.nb
+        self.keyframe[slot] = kf
+        if self.loopback:
+            buf = self.bufs[slot][0].data_ptr()
+            self._pack(buf, kf, stream_ptr or 0)
+            self._unpack(0, buf, kf, stream_ptr or 0)
+            return slot
+        if self.rank == self.dst:
+            ops = [dist.P2POp(dist.irecv, self.bufs[slot][r][:n], self._peer(r), self.group)
+                   for r in range(self.ws) if r != self.dst]
+            self.unpacked[slot] = False
+        else:
+            self._pack(self.bufs[slot][0].data_ptr(), kf, stream_ptr or 0)
+            ops = [dist.P2POp(dist.isend, self.bufs[slot][0][:n], self._peer(self.dst), self.group)]
+        self.pending[slot] = dist.batch_isend_irecv(ops) if ops else None
+        # the previous slot's messages have had a whole step to arrive
+        prev = (slot - 1) % self.slots
+        if self.slots > 1 and self.k > 1:
+            self._finish(prev, stream_ptr)
+        return slot
+
+    def drain(self, stream_ptr=None):
+        for i in range(self.slots):
+            self._finish((self.k + i) % self.slots, stream_ptr)
+
+    def outputs(self):
+        """{name: [world_size, rows, ...]} on dst (own engine + shadows)."""
+        import torch
+
+        if self.rank != self.dst:
+            return {}
+        self.drain()
+        own = LearnerGather.from_sim(self.sim)
+        if self.loopback:  # the shadow's rebuild of the rank's own outputs
+            own = LearnerGather.from_sim(self.shadows[0])
+        parts = {r: (own if r == self.dst else LearnerGather.from_sim(self.shadows[r])) for r in range(self.ws)}
+        return {n: torch.stack([parts[r][n] for r in range(self.ws)]) for n in own if n not in NOT_SHIPPED}
+
+    def close(self):
+        self.drain()
+
+
 def make_exchange(mode: str, sim, group=None, **kw):
     """The learner exchange a multi-GPU run names in config.parallelism:
     "none" (simulators only), "gather" (LearnerGather: every shipped output
-    to one learner rank each step) or "local" (LearnerLocal)."""
+    to one learner rank each step, as exported), "wire" (LearnerWire: the
+    same outputs in the compact wire format, rebuilt on the learner; needs
+    make_shadow=) or "local" (LearnerLocal)."""
     if mode == "none":
         return None
     if mode == "gather":
         return LearnerGather(sim, dst=0, group=group)
+    if mode == "wire":
+        return LearnerWire(sim, dst=0, group=group, **kw)
     if mode == "local":
         return LearnerLocal(sim, group=group, **kw)
     raise ValueError(f"unknown exchange {mode!r}")

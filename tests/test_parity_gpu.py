@@ -659,6 +659,29 @@ def test_step_graph_replay_equals_direct_launches(monkeypatch):
                     _, _, shape = g.desc(n)
                     k = shape[0] // W
                     T.compare(g.get_rows(n, w0 * k, (w0 + 2) * k), o.get(n), f"{n} worlds {w0}.. @ {s}")
+    # one capture per argument change and none otherwise: steps 0 (first),
+    # 8 (3 groups), 16 (stats on), 20 (stats off + 1 group), 28 (2 groups);
+    # the timed steps 34-37 bypass the graph and 38 replays the step-28 graph
+    import ctypes as C
+    n_cap = C.c_int64(-1)
+    g.lib.mpenv_graph_captures.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+    assert g.lib.mpenv_graph_captures(g.h, C.byref(n_cap)) == 0
+    assert n_cap.value == 5, n_cap.value
+    # a re-capture right after an asynchronous launch (the previous exec may
+    # still run): groups 2 -> 3 with no sync between, then both engines agree
+    g.lib.mpenv_step_async.argtypes = [C.c_void_p, C.c_void_p]
+    acts = T.mpenv_tape.tape_actions(1234, steps, 0, W * N)
+    for e in (ref, g):
+        e.set_actions(acts)
+    ref.step()
+    assert g.lib.mpenv_step_async(g.h, None) == 0
+    g.set_world_groups(3)
+    acts = T.mpenv_tape.tape_actions(1234, steps + 1, 0, W * N)
+    for e in (ref, g):
+        e.set_actions(acts)
+        e.step()
+    for n in T.STEP_OUTPUTS:
+        T.compare(g.get(n), ref.get(n), f"{n} graph vs direct after an async re-capture")
 
 
 def test_logs_record_and_events_match_oracle(tmp_path):

@@ -222,3 +222,67 @@ def test_learner_gather_rejects_non_contiguous_sources():
     t = torch.zeros(8, 4)[:, :2]
     with pytest.raises(ValueError, match="contiguous"):
         LearnerGather.__init__(object.__new__(LearnerGather), {"x": t})
+
+
+# ---- LearnerWire transport (the compact wire format's exchange): byte-level
+# stand-ins for pack / unpack, three ranks on gloo.  Every message of every
+# sender must reach the learner's unpack in order, the first as a keyframe,
+# each sized as its kind, with its bytes intact.
+WIRE_NB, WIRE_NK, WIRE_STEPS = 1000, 1600, 7
+
+
+def _wire_bytes(rank, step, keyframe):
+    n = WIRE_NK if keyframe else WIRE_NB
+    return (np.arange(n, dtype=np.int64) * 7 + rank * 131 + step * 17 + (5 if keyframe else 0)).astype(np.uint8)
+
+
+def _wire_worker(rank, world_size, port, result_path):
+    import ctypes as C
+
+    from mpenv_dist import LearnerWire
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        step = [0]
+        seen = []
+
+        def pack(ptr, keyframe, stream):
+            b = _wire_bytes(rank, step[0], keyframe)
+            C.memmove(ptr, b.ctypes.data, len(b))
+
+        def unpack(r, ptr, keyframe, stream):
+            n = WIRE_NK if keyframe else WIRE_NB
+            seen.append((r, bool(keyframe), bytes((C.c_uint8 * n).from_address(ptr))))
+
+        lw = LearnerWire(None, dst=0, pack=pack, unpack=unpack,
+                         nbytes=lambda kf: WIRE_NK if kf else WIRE_NB, device=torch.device("cpu"))
+        assert lw.bytes_per_step() == {"sent_per_rank": WIRE_NB, "learner_ingress": WIRE_NB * (world_size - 1),
+                                       "keyframe": WIRE_NK}
+        for s in range(WIRE_STEPS):
+            step[0] = s
+            lw.submit()
+        lw.drain()
+        if rank == 0:
+            import pickle  # our own file, written and read by this test only
+
+            with open(result_path, "wb") as f:
+                pickle.dump(seen, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_learner_wire_transport_three_ranks(tmp_path):
+    import pickle  # reads the file _wire_worker wrote above
+
+    path = str(tmp_path / "wire.pkl")
+    mp.spawn(_wire_worker, args=(3, _free_port(), path), nprocs=3, join=True)
+    with open(path, "rb") as f:
+        seen = pickle.load(f)
+    for r in (1, 2):
+        msgs = [(kf, b) for rr, kf, b in seen if rr == r]
+        assert len(msgs) == WIRE_STEPS
+        for s, (kf, b) in enumerate(msgs):
+            assert kf == (s == 0)
+            assert b == _wire_bytes(r, s, kf).tobytes(), (r, s)

@@ -1,0 +1,123 @@
+"""The learner exchange's compact wire format (csrc/wire.hip).
+
+unpack(pack(x)) on a shadow manager of the sender's configuration must give
+every trainInterface output (mgr.cpp:2383-2431) bit for bit: the lidar from
+depth + class bit-planes, the observation rows from the shipped state through
+the shadow's own k_obs, the last-known rows from the shadow's history
+(cleared when a world's episode counter moves, carried once by a keyframe).
+Driven at the full C3 batch with the device aim-bot (kills, respawns and
+last-known updates) and triggered resets (episode counters move), from the
+first step and from a keyframe mid-episode; plus the rejections."""
+import ctypes as C
+import time
+
+import numpy as np
+import pytest
+
+import mpenv_testlib as T
+
+pytestmark = pytest.mark.gpu
+
+RING = 64
+SEED = 1234
+
+
+def _lib():
+    lib = T.lib_mpenv()
+    lib.mpenv_wire_bytes.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]
+    lib.mpenv_wire_pack.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    lib.mpenv_wire_unpack.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    lib.mpenv_wire_error.argtypes = [C.c_void_p, C.POINTER(C.c_uint32)]
+    return lib
+
+
+def _bytes(e, keyframe):
+    n = C.c_int64()
+    assert e.lib.mpenv_wire_bytes(e.h, int(keyframe), C.byref(n)) == 0
+    return n.value
+
+
+def _error(e):
+    v = C.c_uint32(99)
+    assert e.lib.mpenv_wire_error(e.h, C.byref(v)) == 0
+    return v.value
+
+
+def _ship(e, sh, buf, keyframe):
+    assert e.lib.mpenv_wire_pack(e.h, buf, int(keyframe), None) == 0
+    assert sh.lib.mpenv_wire_unpack(sh.h, buf, int(keyframe), None) == 0
+
+
+def _compare(e, sh, where):
+    e.mem.hip.hipDeviceSynchronize()
+    for n, ex in T.TRAIN_OUTPUTS.items():
+        T.compare(sh.get(ex), e.get(ex), f"{n} (shadow vs sender) @ {where}")
+
+
+def test_wire_roundtrip_full_batch_combat_and_resets():
+    ts, W, steps = 6, 16384, 100
+    N = 2 * ts
+    A = W * N
+    t0 = time.time()
+    _lib()
+    e = T.Engine(W, ts)
+    sh = T.Engine(W, ts)        # the learner's shadow of e, shipped from step 0
+    late = T.Engine(W, ts)      # a shadow joining at step 50 with a keyframe
+    e.put_ctrl([0, 1, 1])
+    e.init()
+    nb, nk = _bytes(e, False), _bytes(e, True)
+    assert nb < 500 * A and nk > nb
+    buf = e.mem.upload(np.zeros(nk, np.uint8))
+    ring = e.mem.upload(T.mpenv_tape.tape_ring(SEED, 0, A, RING))
+    _ship(e, sh, buf, True)
+    assert _error(sh) == 0
+    _compare(e, sh, "init")
+    e.enable_stats(True)
+    rng = np.random.default_rng(3)
+    for s in range(steps):
+        if s in (30, 60):  # episode counters move: the shadow must clear last-known rows
+            for w in rng.choice(W, 64, replace=False):
+                e.trigger_reset(int(w))
+        e.combat_actions(ring + (s % RING) * A * 24, None, 1)
+        e.step()
+        _ship(e, sh, buf, False)
+        if s == 50:
+            _ship(e, late, buf, True)  # keyframe: last-known rows included
+        elif s > 50:
+            assert late.lib.mpenv_wire_unpack(late.h, buf, 0, None) == 0
+        if s % 10 == 9 or s == steps - 1:
+            _compare(e, sh, f"step {s}")
+            if s > 50:
+                _compare(e, late, f"step {s} (keyframe at 50)")
+            print(f"  step {s}: shadows equal, test {time.time() - t0:.0f} s", flush=True)
+    assert _error(sh) == 0 and _error(late) == 0
+    st = e.read_stats()
+    assert st["kills"] > 0
+    lk = e.get("OPPONENT_LAST_KNOWN_OBSERVATIONS")
+    assert (lk != 0).any()
+    print(f"\nwire: {nb / A:.1f} B per agent ({nb / 1e6:.1f} MB per C3 message, keyframe {nk / 1e6:.1f} MB) "
+          f"against {sum(e.get(x).nbytes for x in T.TRAIN_OUTPUTS.values()) / A:.1f} B exported; "
+          f"{steps} combat steps, {st['kills']} kills, resets at 30 and 60; test {time.time() - t0:.1f} s")
+    e.mem.free(buf)
+    e.mem.free(ring)
+
+
+def test_wire_rejects_foreign_or_mismatched_messages():
+    _lib()
+    a = T.Engine(64, 3)
+    b = T.Engine(32, 3)
+    for x in (a, b):
+        x.put_ctrl([0, 1, 1])
+        x.init()
+    buf = a.mem.upload(np.zeros(_bytes(a, True), np.uint8))
+    assert a.lib.mpenv_wire_pack(a.h, buf, 0, None) == 0
+    # another configuration
+    assert b.lib.mpenv_wire_unpack(b.h, buf, 0, None) == 0
+    assert _error(b) == 1
+    # a plain message unpacked as a keyframe
+    assert a.lib.mpenv_wire_unpack(a.h, buf, 1, None) == 0
+    assert _error(a) == 1
+    # the right kind is accepted again
+    assert a.lib.mpenv_wire_unpack(a.h, buf, 0, None) == 0
+    assert _error(a) == 0
+    a.mem.free(buf)
