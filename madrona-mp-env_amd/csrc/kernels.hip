@@ -3997,7 +3997,7 @@ int launchLidar(const DevState &s, const SceneDev &sc, void *stream)
         return check(hipGetLastError());
     };
     const int64_t units = (s.A + 3) / 4;
-    if (!lidarFanScene(sc)) return launch(k_lidar, lidarTasks(s.A), bvhLdsBytesOct(sc));
+    if (!sc.lidarFan || !lidarFanScene(sc)) return launch(k_lidar, lidarTasks(s.A), bvhLdsBytesOct(sc));
     const size_t fanLds = (size_t)sc.numVerts * 16 * 3 + (size_t)kLidarWaves * kFanListCap * sizeof(uint16_t);
     if (launch(k_lidar_fan, units * 4, fanLds)) return -1;
     return launch(k_lidar_rear, units, bvhLdsBytesOct(sc));

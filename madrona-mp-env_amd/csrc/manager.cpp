@@ -558,6 +558,8 @@ static void buildSceneDev(mpenv_manager &m)
         float *d_aux = m.alloc<float>(aux.size());
         m.upload(d_aux, aux.data(), sizeof(float) * aux.size());
         sc.triAux = d_aux;
+        sc.lidarFan = 1;
+        if (const char *e = std::getenv("MPENV_LIDAR_FAN")) sc.lidarFan = std::atoi(e) != 0;
     }
     {
         // the sphere-cast radius is always consts::agentRadius (k_move)

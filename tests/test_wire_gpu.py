@@ -44,8 +44,12 @@ def _error(e):
 
 
 def _ship(e, sh, buf, keyframe):
+    # pack on the sender's stream, unpack on the shadow's: the device sync
+    # in between stands in for the transfer's completion
     assert e.lib.mpenv_wire_pack(e.h, buf, int(keyframe), None) == 0
+    e.mem.hip.hipDeviceSynchronize()
     assert sh.lib.mpenv_wire_unpack(sh.h, buf, int(keyframe), None) == 0
+    e.mem.hip.hipDeviceSynchronize()  # read before anything packs into buf again
 
 
 def _compare(e, sh, where):
@@ -55,7 +59,7 @@ def _compare(e, sh, where):
 
 
 def test_wire_roundtrip_full_batch_combat_and_resets():
-    ts, W, steps = 6, 16384, 100
+    ts, W, steps = 6, 16384, 300
     N = 2 * ts
     A = W * N
     t0 = time.time()
@@ -75,20 +79,21 @@ def test_wire_roundtrip_full_batch_combat_and_resets():
     e.enable_stats(True)
     rng = np.random.default_rng(3)
     for s in range(steps):
-        if s in (30, 60):  # episode counters move: the shadow must clear last-known rows
+        if s in (30, 200):  # episode counters move: the shadow must clear last-known rows
             for w in rng.choice(W, 64, replace=False):
                 e.trigger_reset(int(w))
         e.combat_actions(ring + (s % RING) * A * 24, None, 1)
         e.step()
         _ship(e, sh, buf, False)
-        if s == 50:
+        if s == 150:
             _ship(e, late, buf, True)  # keyframe: last-known rows included
-        elif s > 50:
+        elif s > 150:
             assert late.lib.mpenv_wire_unpack(late.h, buf, 0, None) == 0
-        if s % 10 == 9 or s == steps - 1:
+        e.mem.hip.hipDeviceSynchronize()  # unpacks done before the next pack overwrites buf
+        if s % 25 == 24 or s == steps - 1:
             _compare(e, sh, f"step {s}")
-            if s > 50:
-                _compare(e, late, f"step {s} (keyframe at 50)")
+            if s > 150:
+                _compare(e, late, f"step {s} (keyframe at 150)")
             print(f"  step {s}: shadows equal, test {time.time() - t0:.0f} s", flush=True)
     assert _error(sh) == 0 and _error(late) == 0
     st = e.read_stats()
@@ -97,7 +102,8 @@ def test_wire_roundtrip_full_batch_combat_and_resets():
     assert (lk != 0).any()
     print(f"\nwire: {nb / A:.1f} B per agent ({nb / 1e6:.1f} MB per C3 message, keyframe {nk / 1e6:.1f} MB) "
           f"against {sum(e.get(x).nbytes for x in T.TRAIN_OUTPUTS.values()) / A:.1f} B exported; "
-          f"{steps} combat steps, {st['kills']} kills, resets at 30 and 60; test {time.time() - t0:.1f} s")
+          f"{steps} combat steps, {st['kills']} kills, {st['lk_rows']} last-known rows written, resets at 30 "
+          f"and 200, keyframe shadow from 150; test {time.time() - t0:.1f} s")
     e.mem.free(buf)
     e.mem.free(ring)
 
@@ -111,6 +117,7 @@ def test_wire_rejects_foreign_or_mismatched_messages():
         x.init()
     buf = a.mem.upload(np.zeros(_bytes(a, True), np.uint8))
     assert a.lib.mpenv_wire_pack(a.h, buf, 0, None) == 0
+    a.mem.hip.hipDeviceSynchronize()
     # another configuration
     assert b.lib.mpenv_wire_unpack(b.h, buf, 0, None) == 0
     assert _error(b) == 1
