@@ -307,6 +307,20 @@ int launchFillActions(const DevState &s, const int32_t *src6, void *stream);
 int launchCombatActions(const DevState &s, const int32_t *tape6, int32_t *out6, int32_t mode, void *stream);
 int computeSceneFrames(SceneTables *d_tab, void *stream); // fills zoneFrame / goalFrame in place
 
+// Batched device copies (wire.hip): up to kMaxCopySegs segments in one
+// launch; src == nullptr zero-fills.  Pointers must be 16-B aligned.
+constexpr int kMaxCopySegs = 32;
+struct CopySeg {
+    const void *src;
+    void *dst;
+    int64_t bytes;
+};
+struct CopyBatch {
+    CopySeg seg[kMaxCopySegs];
+    int n;
+};
+int launchCopyBatch(const CopyBatch &b, void *stream);
+
 // Learner-exchange wire format (wire.hip)
 int64_t wireBytes(const DevState &s, bool keyframe);
 int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOffset, void *stream);

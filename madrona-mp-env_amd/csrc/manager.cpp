@@ -1038,21 +1038,40 @@ int mpenv_train_interface_entry(int32_t is_output, int32_t idx, const char **nam
     return MPENV_OK;
 }
 
+// cudaCopyStepInputs / cudaCopyStepOutputs (mgr.cpp:614-645): every
+// trainInterface input from the caller's buffers, or every output into
+// them, as one batched copy launch (the agent maps are never written by the
+// step and stay all zeros, so their copies are zero fills); a segment whose
+// pointers are not 16-B aligned falls back to hipMemcpyAsync.
 static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs, bool outputs)
 {
+    CopyBatch b {};
+    auto add = [&](const void *src, void *dst, size_t bytes) {
+        if (((uintptr_t)src | (uintptr_t)dst) & 15u) {
+            if (src) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+            else HIP_CHECK(hipMemsetAsync(dst, 0, bytes, st));
+            return;
+        }
+        if (b.n == kMaxCopySegs) {
+            if (launchCopyBatch(b, st)) throw std::runtime_error("copy launch failed");
+            b.n = 0;
+        }
+        b.seg[b.n++] = CopySeg { src, dst, (int64_t)bytes };
+    };
     int k = 0;
     for (int i = 0; i < kNumTIInputs; i++, k++) {
-        if (!inputs) continue;
+        if (!inputs || !buffers[k]) continue;
         TensorDesc d;
         m->exportDesc(kTIInputs[i].id, d);
-        if (buffers[k]) HIP_CHECK(hipMemcpyAsync(d.ptr, buffers[k], d.bytes(), hipMemcpyDeviceToDevice, st));
+        add(buffers[k], d.ptr, d.bytes());
     }
     for (int i = 0; i < kNumTIOutputs; i++, k++) {
-        if (!outputs) continue;
+        if (!outputs || !buffers[k]) continue;
         TensorDesc d;
         m->exportDesc(kTIOutputs[i].id, d);
-        if (buffers[k]) HIP_CHECK(hipMemcpyAsync(buffers[k], d.ptr, d.bytes(), hipMemcpyDeviceToDevice, st));
+        add(kTIOutputs[i].id == MPENV_EXPORT_AGENT_MAP ? nullptr : d.ptr, buffers[k], d.bytes());
     }
+    if (launchCopyBatch(b, st)) throw std::runtime_error("copy launch failed");
     return 0;
 }
 

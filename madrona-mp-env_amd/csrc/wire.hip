@@ -27,6 +27,7 @@
 // read and write coalesced rows (thread = agent, ray or world).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "engine.h"
@@ -280,6 +281,25 @@ __global__ void k_wire_unpack_lidar(DevState S, const char *src, WireLayout L, u
     else reinterpret_cast<float4 *>(S.rearLidar)[g * kRearRays + k - kFwdRays] = v;
 }
 
+// ------------------------------------------------------------ batch copy
+// gpuStreamStep's input and output copies (mgr.cpp:614-645) as one launch
+// per direction: blockIdx.y = segment, 16-B vectors grid-strided over it
+// (hipMemcpyAsync per tensor ran at ~1 TB/s for the 2.4 GB of a C3 step);
+// src == nullptr writes zeros (the agent maps, never written by the step).
+__global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b)
+{
+    const CopySeg sg = b.seg[blockIdx.y];
+    const int64_t n16 = sg.bytes / 16;
+    const uint4 *src = static_cast<const uint4 *>(sg.src);
+    uint4 *dst = static_cast<uint4 *>(sg.dst);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src ? src[i] : make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == 0 && threadIdx.x < (sg.bytes & 15)) {
+        const int64_t o = n16 * 16 + threadIdx.x;
+        static_cast<uint8_t *>(sg.dst)[o] = src ? static_cast<const uint8_t *>(sg.src)[o] : 0;
+    }
+}
+
 static int checkW(hipError_t e) { return e == hipSuccess ? 0 : -1; }
 static unsigned grid(int64_t n) { return (unsigned)((n + 255) / 256); }
 
@@ -292,6 +312,16 @@ int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOf
     hipLaunchKernelGGL(k_wire_pack_worlds, dim3(grid(s.W)), dim3(256), 0, st, s, dst, L, worldOffset);
     hipLaunchKernelGGL(k_wire_pack_agents, dim3(grid(s.A)), dim3(256), 0, st, s, dst, L);
     hipLaunchKernelGGL(k_wire_pack_lidar, dim3(grid(s.A * kLidarRays)), dim3(256), 0, st, s, dst, L);
+    return checkW(hipGetLastError());
+}
+
+int launchCopyBatch(const CopyBatch &b, void *stream)
+{
+    if (b.n <= 0) return 0;
+    int64_t most = 0;
+    for (int k = 0; k < b.n; k++) most = b.seg[k].bytes > most ? b.seg[k].bytes : most;
+    const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>((most / 16 + 255) / 256, 1), 1024);
+    hipLaunchKernelGGL(k_copy_batch, dim3(gx, (unsigned)b.n), dim3(256), 0, (hipStream_t)stream, b);
     return checkW(hipGetLastError());
 }
 

@@ -527,7 +527,7 @@ def test_gpu_stream_step_buffers_abi():
         stream.synchronize()
         for (io, nm, ename), b in zip(names, bufs):
             if io == 1:
-                np.testing.assert_array_equal(b.cpu().numpy(), o.get(ename), err_msg=f"{nm} @ {s}")
+                T.compare(b.cpu().numpy(), o.get(ename), f"{nm} @ {s}")
 
 
 _edge_aimed_rays = T.edge_aimed_rays
