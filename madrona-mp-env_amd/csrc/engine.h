@@ -171,11 +171,7 @@ enum StatId {
     kStatHits = 6,        // agents that took damage (applyDmgSystem)
     kStatKills = 7,       // agents killed (alive -> hp <= 0)
     kStatLkRows = 8,      // last-known rows k_obs wrote (knows / cleared on death)
-#if defined(MPENV_LAB_PHASE_T)
-    kNumStats = 25, // lab: k_sim phase cycles in slots 9..
-#else
     kNumStats = 9,
-#endif
 };
 
 struct ZOBBDev {

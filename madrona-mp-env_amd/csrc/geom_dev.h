@@ -28,7 +28,7 @@ struct LBVH {
     const MP_LDS float *pre; // sphere-casting kernels only (stageBVHSphere)
     const MP_LDS float *snodes; // sphere-cast node image (stageBVHSphere), else null
     unsigned long long *stats;  // workload counters (DevState::stats), null = off
-    int32_t rotStride;          // stageBVHOct with kLidarRot: float4s per rotated vertex copy
+    int32_t rotStride;          // stageBVHOct / stageBVHRot: float4s per rotated vertex copy
 };
 
 // Workload counter add, one atomic per wave: the active lanes' values
@@ -52,11 +52,9 @@ constexpr float kSphereR = 15.f;  // consts::agentRadius: the radius of every k_
 // of every node sits in one bank, so lanes at different nodes conflict (PMC:
 // 44% of k_move's LDS cycles are conflict cycles); an odd stride puts node
 // k's field in bank (k + field) mod 32, but k_move does not get faster (it
-// waits on its cast chain, not on LDS).
-#ifndef MPENV_SNODE_STRIDE
-#define MPENV_SNODE_STRIDE 32 // 33: no measurable change (k_move 0.2182 vs 0.2181 ms, r03e lab)
-#endif
-constexpr int kSNodeFloats = MPENV_SNODE_STRIDE;
+// waits on its cast chain, not on LDS: stride 33 measured 0.2182 vs 0.2181
+// ms, round 3).
+constexpr int kSNodeFloats = 32;
 
 // Byte stack: push shifts left by 8 across a 128-bit register pair.
 struct ByteStack {
@@ -157,24 +155,14 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
 }
 
 // k_lidar's LDS image: the 8 octant node images (scene.h octantNodeImages,
-// 8 x numNodes nodes) then the vertices as float4 (three rotated copies with
-// kLidarRot).  The traversal of a ray
-// reads image (d.x < 0) | (d.y < 0) << 1 | (d.z < 0) << 2.  Each node takes
-// kOctNodeQ 16-B slots: 4 = packed 64-B nodes; 5 = one pad slot, so the
-// slots of nodes k and k' sit in different LDS bank groups whenever
-// k != k' (mod 16) (with 64-B nodes only k mod 4 decides the bank group of a
-// ds_read_b128, and divergent lanes reading distinct nodes conflict).
-#ifndef MPENV_OCT_NODE_Q
-#define MPENV_OCT_NODE_Q 4
-#endif
-constexpr int kOctNodeQ = MPENV_OCT_NODE_Q;
-
-// kLidarRot: the vertices three times, copy r as (v[r+1], v[r+2], v[r]) (mod
-// 3), for rayTriRot; else once as (x, y, z).
-#ifndef MPENV_LIDAR_ROT
-#define MPENV_LIDAR_ROT 1 // 0: one (x, y, z) copy and per-component gathers (k_lidar 0.730 -> 0.744 ms, r03y lab)
-#endif
-constexpr bool kLidarRot = MPENV_LIDAR_ROT != 0;
+// 8 x numNodes nodes) then the vertices as float4 (three rotated copies).
+// The traversal of a ray reads image (d.x < 0) | (d.y < 0) << 1 | (d.z < 0) << 2.  Each node takes
+// kOctNodeQ = 4 16-B slots (packed 64-B nodes; a fifth pad slot, which moves
+// nodes k != k' (mod 16) to different LDS bank groups, measured no faster in
+// round 2).  The vertices follow three times, copy r as (v[r+1], v[r+2],
+// v[r]) (mod 3), for rayTriRot (one (x, y, z) copy with per-component
+// gathers: k_lidar 0.730 -> 0.744 ms, round 3).
+constexpr int kOctNodeQ = 4;
 
 __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
 {
@@ -185,22 +173,17 @@ __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
         dst_n[(k >> 2) * kOctNodeQ + (k & 3)] = src_n[k];
     const float *src_v = sc.verts;
     float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
-    if constexpr (kLidarRot) {
-        // The .w slots carry the fan-list cull data (SceneDev::triAux) of
-        // triangle t = v / 3, vertex slot i = v % 3: copy 2 (x, y, z) the
-        // unit normal's component i; copy 0 the plane offset, the bounding
-        // radius, the centre's x; copy 1 the centre's y and z (fanTraceD).
-        for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
-            const int r = k / sc.numVerts, v = k - r * sc.numVerts;
-            const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
-            const int t = v / 3, i = v - 3 * t;
-            const int ai = r == 2 ? i : r == 0 ? (i == 0 ? 3 : i == 1 ? 7 : 4) : (i == 0 ? 5 : i == 1 ? 6 : -1);
-            dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r],
-                                   ai >= 0 ? sc.triAux[8 * t + ai] : 0.f);
-        }
-    } else {
-        for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
-            dst_v[k] = make_float4(src_v[3 * k], src_v[3 * k + 1], src_v[3 * k + 2], 0.f);
+    // The .w slots carry the fan-list cull data (SceneDev::triAux) of
+    // triangle t = v / 3, vertex slot i = v % 3: copy 2 (x, y, z) the unit
+    // normal's component i; copy 0 the plane offset, the bounding radius, the
+    // centre's x; copy 1 the centre's y and z (fanTraceD).
+    for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
+        const int r = k / sc.numVerts, v = k - r * sc.numVerts;
+        const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
+        const int t = v / 3, i = v - 3 * t;
+        const int ai = r == 2 ? i : r == 0 ? (i == 0 ? 3 : i == 1 ? 7 : 4) : (i == 0 ? 5 : i == 1 ? 6 : -1);
+        dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r],
+                               ai >= 0 ? sc.triAux[8 * t + ai] : 0.f);
     }
     __syncthreads();
     LBVH b;
@@ -357,103 +340,6 @@ __device__ __forceinline__ bool rayTri(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, co
     return true;
 }
 
-// rayTri with one data-dependent branch (the accepted hit's division) plus
-// the rare f64 edge fallback: the rejection tests are folded into one
-// predicate instead of nested early returns, so a wave whose lanes reject
-// at different tests runs no extra exec-mask rounds.  Every value is
-// computed exactly as in rayTri (T and det of a rejected lane are computed
-// and dropped), so the accepted set and out_t are identical.
-__device__ __forceinline__ bool rayTriFlat(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, const RayTxfmD &tx, mp::Vec3 org,
-                                           float t_max, float &out_t)
-{
-    using namespace mp;
-    const Vec3 A = ta - org, B = tb - org, C = tc - org;
-    const float Az_ = comp(A, tx.kz), Bz_ = comp(B, tx.kz), Cz_ = comp(C, tx.kz);
-    const float Ax = fma_(-tx.Sx, Az_, comp(A, tx.kx));
-    const float Ay = fma_(-tx.Sy, Az_, comp(A, tx.ky));
-    const float Bx = fma_(-tx.Sx, Bz_, comp(B, tx.kx));
-    const float By = fma_(-tx.Sy, Bz_, comp(B, tx.ky));
-    const float Cx = fma_(-tx.Sx, Cz_, comp(C, tx.kx));
-    const float Cy = fma_(-tx.Sy, Cz_, comp(C, tx.ky));
-    float U = fma_(Cx, By, -(Cy * Bx));
-    float V = fma_(Ax, Cy, -(Ay * Cx));
-    float W = fma_(Bx, Ay, -(By * Ax));
-    bool ok = !(U < 0.0f || V < 0.0f || W < 0.0f);
-    if (ok && (U == 0.0f || V == 0.0f || W == 0.0f)) {
-        double CxBy = (double)Cx * (double)By;
-        double CyBx = (double)Cy * (double)Bx;
-        U = (float)(CxBy - CyBx);
-        double AxCy = (double)Ax * (double)Cy;
-        double AyCx = (double)Ay * (double)Cx;
-        V = (float)(AxCy - AyCx);
-        double BxAy = (double)Bx * (double)Ay;
-        double ByAx = (double)By * (double)Ax;
-        W = (float)(BxAy - ByAx);
-        ok = !(U < 0.0f || V < 0.0f || W < 0.0f);
-    }
-    const float det = U + V + W;
-    const float Az = tx.Sz * Az_;
-    const float Bz = tx.Sz * Bz_;
-    const float Cz = tx.Sz * Cz_;
-    const float T = fma_(U, Az, fma_(V, Bz, W * Cz));
-    ok = ok && det != 0.f && !(T < 0.0f || T > t_max * det);
-    if (ok) out_t = T * (1.0f / det);
-    return ok;
-}
-
-// rayTri with the vertex components read in the ray's (kx, ky, kz) order
-// straight from LDS (per-lane byte offsets ko = 4 * k) instead of selected
-// from full vertices: comp(ta - org, k) == ta[k] - org[k] exactly, so
-// every value equals rayTri's bit for bit.  orgP = (org[kx], org[ky],
-// org[kz]).
-struct RayPermD {
-    uint32_t kox, koy, koz; // byte offsets of the permuted components
-    float ox, oy, oz;       // origin in permuted order
-};
-
-__device__ __forceinline__ bool rayTriPermD(const LBVH &b, int tri, const RayTxfmD &tx, const RayPermD &rp,
-                                            float t_max, float &out_t)
-{
-    using namespace mp;
-    const MP_LDS char *base = reinterpret_cast<const MP_LDS char *>(b.verts) + tri * 48;
-    auto ld = [&](int v, uint32_t ko) { return *reinterpret_cast<const MP_LDS float *>(base + v * 16 + ko); };
-    const float Akx = ld(0, rp.kox) - rp.ox, Aky = ld(0, rp.koy) - rp.oy, Az_ = ld(0, rp.koz) - rp.oz;
-    const float Bkx = ld(1, rp.kox) - rp.ox, Bky = ld(1, rp.koy) - rp.oy, Bz_ = ld(1, rp.koz) - rp.oz;
-    const float Ckx = ld(2, rp.kox) - rp.ox, Cky = ld(2, rp.koy) - rp.oy, Cz_ = ld(2, rp.koz) - rp.oz;
-    const float Ax = fma_(-tx.Sx, Az_, Akx);
-    const float Ay = fma_(-tx.Sy, Az_, Aky);
-    const float Bx = fma_(-tx.Sx, Bz_, Bkx);
-    const float By = fma_(-tx.Sy, Bz_, Bky);
-    const float Cx = fma_(-tx.Sx, Cz_, Ckx);
-    const float Cy = fma_(-tx.Sy, Cz_, Cky);
-    float U = fma_(Cx, By, -(Cy * Bx));
-    float V = fma_(Ax, Cy, -(Ay * Cx));
-    float W = fma_(Bx, Ay, -(By * Ax));
-    if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
-    if (U == 0.0f || V == 0.0f || W == 0.0f) {
-        double CxBy = (double)Cx * (double)By;
-        double CyBx = (double)Cy * (double)Bx;
-        U = (float)(CxBy - CyBx);
-        double AxCy = (double)Ax * (double)Cy;
-        double AyCx = (double)Ay * (double)Cx;
-        V = (float)(AxCy - AyCx);
-        double BxAy = (double)Bx * (double)Ay;
-        double ByAx = (double)By * (double)Ax;
-        W = (float)(BxAy - ByAx);
-        if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
-    }
-    float det = U + V + W;
-    if (det == 0.f) return false;
-    const float Az = tx.Sz * Az_;
-    const float Bz = tx.Sz * Bz_;
-    const float Cz = tx.Sz * Cz_;
-    const float T = fma_(U, Az, fma_(V, Bz, W * Cz));
-    if (T < 0.0f || T > t_max * det) return false;
-    const float rcpDet = 1.0f / det;
-    out_t = T * rcpDet;
-    return true;
-}
-
 // rayTri over a rotated vertex copy: the LDS image holds every vertex three
 // times, copy kz as (v[kz+1], v[kz+2], v[kz]) (indices mod 3), so the ray's
 // copy yields each vertex already in (kx0, ky0, kz) order with kx0 = kz + 1,
@@ -507,10 +393,6 @@ __device__ __forceinline__ bool rayTriRot(const MP_LDS lf4 *p, float o0, float o
     return true;
 }
 
-#ifndef MPENV_TRI_FLAT
-#define MPENV_TRI_FLAT 0
-#endif
-
 // MeshBVH::traceRay (mesh_bvh.inl:110-208) over the LDS-resident BVH.
 // Returns hit flag; *t_out = closest hit t when hit.
 // t_max0 < FLT_MAX: only hits up to about t_max0 are sought (boxes entered
@@ -537,7 +419,7 @@ constexpr float kLexRelax = 1.00000095367431640625f; // 1 + 2^-20
 constexpr float kBoxSlackRel = 1.52587890625e-5f, kBoxSlackAbs = 0.00390625f;
 __device__ __forceinline__ bool lexLessD(float a, float b) { return __float_as_int(a) < __float_as_int(b); }
 
-template <bool kExit, bool kPerm = false, int kNodeQ = 4, bool kRot = false, bool kOctImage = false, bool kLex = false>
+template <bool kExit, int kNodeQ = 4, bool kRot = false, bool kOctImage = false, bool kLex = false>
 __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
                                              float t_max0, float exit_at, int *exit_tri = nullptr)
 {
@@ -555,11 +437,6 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
     // and t(qMax) otherwise -- the reference's six fminf/fmaxf give the same
     // values (mesh_bvh.inl:165-183).
     const bool negX = rayXInv < 0.f, negY = rayYInv < 0.f, negZ = rayZInv < 0.f;
-    RayPermD rp;
-    if constexpr (kPerm) {
-        rp.kox = 4u * (uint32_t)tx.kx; rp.koy = 4u * (uint32_t)tx.ky; rp.koz = 4u * (uint32_t)tx.kz;
-        rp.ox = comp(ray_o, tx.kx); rp.oy = comp(ray_o, tx.ky); rp.oz = comp(ray_o, tx.kz);
-    }
 
     // kRot: the ray's rotated vertex copy and the origin in its order
     const MP_LDS lf4 *vrot = nullptr;
@@ -609,19 +486,13 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
             const float t_far_y = fma_(qb(farY, i), dirQuantY, originQuantY);
             const float t_far_z = fma_(qb(farZ, i), dirQuantZ, originQuantZ);
             const float t_near = fmax_(fmax_(t_near_x, t_near_y), fmax_(t_near_z, 0.f));
-#ifndef MPENV_SLAB_ASM_MIN
-#define MPENV_SLAB_ASM_MIN 1 // 0: fmin_ (k_lidar 0.6944 vs 0.6847 ms, r03zm lab)
-#endif
-#if MPENV_SLAB_ASM_MIN
-            // the same minimum (no operand is NaN; a -0 / +0 choice only
-            // meets the `<=` below) without the per-use canonicalisation
-            // the compiler inserts for the loop-carried t_max
+            // fmin_ of the four (no operand is NaN; a -0 / +0 choice only
+            // meets the `<=` below) without the per-use canonicalisation the
+            // compiler inserts for the loop-carried t_max (k_lidar 0.6944 ->
+            // 0.6847 ms, round 3)
             float t_far;
             asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
                 : "=&v"(t_far) : "v"(t_far_x), "v"(t_far_y), "v"(t_far_z), "v"(t_max));
-#else
-            const float t_far = fmin_(fmin_(t_far_x, t_far_y), fmin_(t_far_z, t_max));
-#endif
             if (t_near <= (kLex ? fmaf(fabsf(t_far), kBoxSlackRel, t_far + kBoxSlackAbs) : t_far)) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;
@@ -630,29 +501,19 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                     float hit_t = 0.f;
                     float leaf_tmax = t_max;
                     int hit_k = 0;
-#ifdef MPENV_LAB_NO_TRI
-                    for (int k = 0; k < 0; k++) {
-#else
                     // Leaves hold at most 2 triangles (scene.cpp Builder):
                     // the unrolled pair runs without a loop counter
                     // (k_lidar -3%, k_vis -3%, identical outputs).
 #pragma unroll
                     for (int k = 0; k < 2; k++) {
                         if (k >= ntri) break;
-#endif
                         bool h;
                         if constexpr (kRot) {
                             h = rayTriRot(vrot + (leaf + k) * 3, ro0, ro1, roz, rsw, tx, leaf_tmax, hit_t);
-                        } else if constexpr (kPerm) {
-                            h = rayTriPermD(b, leaf + k, tx, rp, leaf_tmax, hit_t);
                         } else {
                             Vec3 a, bb, c;
                             loadTri(b, leaf + k, a, bb, c);
-#if MPENV_TRI_FLAT
-                            h = rayTriFlat(a, bb, c, tx, ray_o, leaf_tmax, hit_t);
-#else
                             h = rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t);
-#endif
                         }
                         if constexpr (kLex) {
                             if (h && lexLessD(hit_t, t_best)) {
@@ -755,33 +616,38 @@ __device__ __forceinline__ float fanAtan2(float y, float x)
 }
 
 // Fan slots x (theta_x = 0.75 pi x / 31 + pi / 8, sim.cpp:3324-3506) with
-// theta_x in [a, b] modulo 2 pi (b - a < 2 pi).
+// theta_x in [a, b], for a > -pi - 1 and b < a + pi + 1: the fan's range
+// [pi/8, 7pi/8] shifted by -2 pi ends below -pi - 1 and shifted by +2 pi
+// starts above 2 pi + 1 -- neither copy can meet such an interval.
 __device__ __forceinline__ uint32_t fanSlotMask(float a, float b)
 {
     constexpr float kOff = 0.392699082f, kInvStep = 31.f / 2.35619449f;
-    uint32_t m = 0;
-#pragma unroll
-    for (int sh = -1; sh <= 1; sh++) {
-        const float o = (float)sh * 6.28318531f - kOff;
-        const float lo = fmaxf(ceilf((a + o) * kInvStep), 0.f);
-        const float hi = fminf(floorf((b + o) * kInvStep), 31.f);
-        if (lo <= hi) {
-            const uint32_t l = (uint32_t)lo, h = (uint32_t)hi;
-            m |= (h == 31u ? 0xffffffffu : ((2u << h) - 1u)) & ~((1u << l) - 1u);
-        }
-    }
-    return m;
+    const float lo = fmaxf(ceilf((a - kOff) * kInvStep), 0.f);
+    const float hi = fminf(floorf((b - kOff) * kInvStep), 31.f);
+    if (!(lo <= hi)) return 0u;
+    const uint32_t l = (uint32_t)lo, h = (uint32_t)hi;
+    return (h == 31u ? 0xffffffffu : ((2u << h) - 1u)) & ~((1u << l) - 1u);
 }
 
+// The plane distance below which a strip may surround the origin: a strip
+// point p projecting onto the origin lies within kFanBand of it, so |sf| <=
+// kFanBand; above kFanNearPlane the projected quad misses the origin by more
+// than sqrt(kFanNearPlane^2 - kFanBand^2) ~ 0.5 units, lies inside an open
+// half-plane seen from it, and the cross-product order of its corners is a
+// total order (rounding flips it only for corners within ~1e-6 rad of
+// opposite, i.e. a quad passing within ~1e-6 |p| of the origin).
+constexpr float kFanNearPlane = 0.5f;
+
 // One sheet's candidate mask for a survivor: sv / uv / wv = N.v, R.v, F.v of
-// the three vertices, c = N.O, (uO, wO) = (R.O, F.O).
+// the three vertices, c = N.O, (uO, wO) = (R.O, F.O), sfAbs = the origin's
+// distance to the triangle's plane.
 __device__ __forceinline__ uint32_t fanSheetMaskD(const float sv[3], const float uv[3], const float wv[3], float c,
-                                                  float uO, float wO, float sinT)
+                                                  float uO, float wO, float sinT, float sfAbs)
 {
     const float s0 = sv[0] - c, s1 = sv[1] - c, s2 = sv[2] - c;
     const bool p0 = s0 > 0.f, p1 = s1 > 0.f, p2 = s2 > 0.f;
-    if (sinT < kFanSinMin || fabsf(s0) <= kFanBand || fabsf(s1) <= kFanBand || fabsf(s2) <= kFanBand ||
-        (p0 == p1 && p1 == p2))
+    if (sinT < kFanSinMin || sfAbs <= kFanNearPlane || fabsf(s0) <= kFanBand || fabsf(s1) <= kFanBand ||
+        fabsf(s2) <= kFanBand || (p0 == p1 && p1 == p2))
         return 0xffffffffu;
     // the lone vertex (on its own side of the plane) and the other two
     const int L = p0 == p1 ? 2 : (p0 == p2 ? 1 : 0);
@@ -793,7 +659,9 @@ __device__ __forceinline__ uint32_t fanSheetMaskD(const float sv[3], const float
     for (int e = 0; e < 2; e++) {
         const int o = e ? B : A;
         const float so = pick(sv, o) - c, uo = pick(uv, o) - uO, wo = pick(wv, o) - wO;
-        const float inv = 1.f / (sl - so);
+        // |sl - so| > 2 kFanBand: the 1-ulp reciprocal moves a corner by
+        // ~1e-7 of the edge, far inside kFanDelta at >= 4 units
+        const float inv = __builtin_amdgcn_rcpf(sl - so);
 #pragma unroll
         for (int bi = 0; bi < 2; bi++) {
             const float a = (sl - (bi ? -kFanBand : kFanBand)) * inv; // in (0, 1)
@@ -802,7 +670,7 @@ __device__ __forceinline__ uint32_t fanSheetMaskD(const float sv[3], const float
         }
     }
     // angular extremes of the quad seen from the origin, by cross products
-    // (exact ordering inside a half-plane), then their two angles
+    // (a total order inside the half-plane, see kFanNearPlane)
     bool full = false;
     float lu = pu[0], lw = pw[0], hu = pu[0], hw = pw[0];
 #pragma unroll
@@ -814,13 +682,6 @@ __device__ __forceinline__ uint32_t fanSheetMaskD(const float sv[3], const float
             if (fmaf(pu[k], lw, -(lu * pw[k])) < 0.f) { lu = pu[k]; lw = pw[k]; }
             if (fmaf(pu[k], hw, -(hu * pw[k])) > 0.f) { hu = pu[k]; hw = pw[k]; }
         }
-    }
-    // every point between the extremes (else the quad is not inside a
-    // half-plane seen from the origin: all rays)
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const float tol = 1e-5f * (fabsf(pu[k]) + fabsf(pw[k])) * (fabsf(lu) + fabsf(lw) + fabsf(hu) + fabsf(hw));
-        full = full || fmaf(pu[k], lw, -(lu * pw[k])) < -tol || fmaf(hu, pw[k], -(pu[k] * hw)) < -tol;
     }
     if (full) return 0xffffffffu;
     const float a0 = fanAtan2(lw, -lu);
@@ -836,7 +697,7 @@ __device__ __forceinline__ float fanNearD(float sf, float cx, float cy, float cz
                                           float oz)
 {
     const float dx = ox - cx, dy = oy - cy, dz = oz - cz;
-    const float cd = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz))) - rad;
+    const float cd = __builtin_amdgcn_sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz))) - rad; // 1 ulp
     return fmaxf(0.f, fmaf(fmaxf(fabsf(sf), cd), 0.99999f, -0.05f));
 }
 
@@ -920,16 +781,17 @@ __device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uin
             const float wv[3] = { fmaf(F.x, A.x, fmaf(F.y, A.y, F.z * A.z)), fmaf(F.x, B.x, fmaf(F.y, B.y, F.z * B.z)),
                                   fmaf(F.x, C.x, fmaf(F.y, C.y, F.z * C.z)) };
             const float cosT = fabsf(fmaf(A.w, N.x, fmaf(B.w, N.y, C.w * N.z)));
-            const float sinT = sqrtf(fmaxf(0.f, fmaf(-cosT, cosT, 1.f)));
+            const float sinT = __builtin_amdgcn_sqrtf(fmaxf(0.f, fmaf(-cosT, cosT, 1.f)));
             const float sf0 = fmaf(A.w, ox, fmaf(B.w, oy, fmaf(C.w, z0, -v0[3 * t].w)));
             uint32_t m0 = 0u, m1 = 0u;
             float n0 = 0.f, n1 = 0.f;
 #pragma unroll 1
             for (int h = 0; h < 2; h++) {
+                const float sf = h ? fmaf(C.w, dz, sf0) : sf0;
                 const uint32_t m = ((fl >> h) & 1u) ? fanSheetMaskD(sv, uv, wv, h ? c1 : c0, h ? uO1 : uO0,
-                                                                    h ? wO1 : wO0, sinT)
+                                                                    h ? wO1 : wO0, sinT, fabsf(sf))
                                                     : 0u;
-                const float n = fanNearD(h ? fmaf(C.w, dz, sf0) : sf0, v0[3 * t + 2].w, v1[3 * t].w,
+                const float n = fanNearD(sf, v0[3 * t + 2].w, v1[3 * t].w,
                                          v1[3 * t + 1].w, v0[3 * t + 1].w, ox, oy, h ? z1 : z0);
                 if (h) { m1 = m; n1 = n; } else { m0 = m; n0 = n; }
             }
@@ -1130,51 +992,14 @@ struct SphereHit {
 // t_max0: MeshBVH::sphereCast's own t_max argument (mesh_bvh.inl:743-747):
 // the search starts with hit_t = t_max0 and returns it when nothing is
 // nearer.
-#ifdef MPENV_LAB_WORK
-// kernel_lab only: per-thread sphere-cast work (casts, nodes popped, triangle
-// tests) of the last k_move, indexed by global thread id; read by
-// mpenv_lab_work (kernels.hip).
-// Rows 3..10: nodes popped per cast site (MP_LAB_SITE before each call).
-constexpr int kLabWorkMax = 1 << 18;
-constexpr int kLabWorkRows = 11;
-__device__ uint32_t g_labWork[kLabWorkRows][kLabWorkMax];
-__device__ uint32_t g_labSite[kLabWorkMax];
-__device__ __forceinline__ void labWorkAdd(int k, uint32_t v)
-{
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid < (uint32_t)kLabWorkMax) {
-        g_labWork[k][tid] += v;
-        if (k == 1) g_labWork[3 + (g_labSite[tid] & 7u)][tid] += v;
-    }
-}
-__device__ __forceinline__ void labSite(uint32_t s)
-{
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid < (uint32_t)kLabWorkMax) g_labSite[tid] = s;
-}
-#define MP_LAB_WORK(k, v) labWorkAdd(k, v)
-#define MP_LAB_SITE(s) labSite(s)
-#else
-#define MP_LAB_WORK(k, v) ((void)0)
-#define MP_LAB_SITE(s) ((void)0)
-#endif
 
 __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r,
                                                  float t_max0 = mp::kFltMax)
 {
-    MP_LAB_WORK(0, 1u);
     using namespace mp;
     Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
     Vec3 closest = v3(0.f, 0.f, 0.f);
     float hit_t = t_max0;
-#ifdef MPENV_LAB_NO_SPHERE
-    if (ray_o.x != 12345.f) {
-        SphereHit h0;
-        h0.t = t_max0;
-        h0.n = closest;
-        return h0;
-    }
-#endif
     // sphereCastNodeCheck (mesh_bvh.inl:817-855) with the slab ends chosen
     // once per cast from the sign of inv_d: per axis b_min is the child's
     // (min - r) or (max + r) end, exactly as the per-child selects pick it;
@@ -1193,7 +1018,6 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
     bsPush(st, 0);
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
-        MP_LAB_WORK(1, 1u);
         const MP_LDS float *nd = b.snodes + node_idx * kSNodeFloats;
 #pragma unroll 1
         for (int i = 0; i < 4; i++) {
@@ -1210,7 +1034,6 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
                     const int ntri = (int)__float_as_uint(nd[28 + i]);
                     Vec3 leaf_n = v3(0.f, 0.f, 0.f);
                     float leaf_t = hit_t;
-                    MP_LAB_WORK(2, (uint32_t)ntri);
                     for (int k = 0; k < ntri; k++) {
                         Vec3 a, bb, c;
                         loadTri(b, leaf + k, a, bb, c);
@@ -1257,7 +1080,6 @@ __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, cons
                                               const float *__restrict__ pz, int64_t g0, int N, mp::Vec3 org,
                                               mp::Vec3 d, int self, bool hit, float min_t, uint32_t capMask = ~0u);
 
-template <bool kPerm = false, int kNodeQ = 4>
 __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__restrict__ px,
                                                 const float *__restrict__ py, const float *__restrict__ pz,
                                                 int64_t g0, int N, mp::Vec3 org, mp::Vec3 d, int self = -1,
@@ -1266,16 +1088,8 @@ __device__ __forceinline__ WorldHit traceWorldD(const LBVH &b, const float *__re
     using namespace mp;
     float min_t = kFltMax;
     float tb;
-#ifdef MPENV_LAB_NO_BVH
-    bool hit = false;
-    tb = 0.f;
-#else
-    bool hit = bvhTraceRayT<false, kPerm, kNodeQ>(b, org, d, tb, mp::kFltMax, 0.f);
-#endif
+    const bool hit = bvhTraceRayT<false>(b, org, d, tb, mp::kFltMax, 0.f);
     if (hit) min_t = tb;
-#ifdef MPENV_LAB_NO_CAPSULE
-    N = 0;
-#endif
     return capsulesD(px, py, pz, g0, N, org, d, self, hit, min_t, capMask);
 }
 
@@ -1326,9 +1140,7 @@ __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, cons
     const float dxy2 = d.x * d.x + d.y * d.y;
     const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
     for (int j = 0; j < N; j++) {
-#ifndef MPENV_LAB_NO_SELF_SKIP
         if (j == self) continue;
-#endif
         Vec3 co = v3(px[g0 + j], py[g0 + j], pz[g0 + j]);
         co.z += kCapsuleRadius;
         Vec3 tr = org - co;

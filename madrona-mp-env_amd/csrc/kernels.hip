@@ -463,12 +463,9 @@ __device__ __forceinline__ bool castPathQuirkFreeD(const SceneDev &sc, Vec3 o, V
 
 // The cast's hit if nearer than `near_b`, else t = kFltMax: for callers to
 // which every hit at or beyond near_b acts like no hit.  Horizontal d.
-#ifndef MPENV_LAB_MOVE_SKIP
-#define MPENV_LAB_MOVE_SKIP 0 // kernel_lab only: cut parts of k_move to time them (wrong results)
-#endif
 __device__ __forceinline__ SphereHit castNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
 {
-    if (!(MPENV_LAB_MOVE_SKIP & 2) && !castPathQuirkFreeD(sc, o, d, near_b)) return bvhSphereCastD(bvh, o, d, kSphereR);
+    if (!castPathQuirkFreeD(sc, o, d, near_b)) return bvhSphereCastD(bvh, o, d, kSphereR);
     SphereHit h = bvhSphereCastD(bvh, o, d, kSphereR, near_b);
     if (!(h.t < near_b)) h.t = kFltMax;
     return h;
@@ -478,9 +475,9 @@ __device__ __forceinline__ SphereHit castNearD(const LBVH &bvh, const SceneDev &
 // path guard is the cell of 2o).
 __device__ __forceinline__ float castFirstNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
 {
-    if ((MPENV_LAB_MOVE_SKIP & 4) || castQuirkFreeD(sc, o)) {
+    if (castQuirkFreeD(sc, o)) {
         const float t = bvhSphereCastD(bvh, o, d, kSphereR, near_b).t;
-        if ((MPENV_LAB_MOVE_SKIP & 4) || t < near_b) return t;
+        if (t < near_b) return t;
     }
     return bvhSphereCastD(bvh, o, d, kSphereR).t;
 }
@@ -504,10 +501,6 @@ __device__ __forceinline__ int nthSetBitD(uint64_t m, int n)
     return pos;
 }
 
-#ifndef MPENV_MOVE_COOP_STUCK
-#define MPENV_MOVE_COOP_STUCK 1
-#endif
-
 // The "stuck" fallback's four horizontal casts (sim.cpp:962-984), for the
 // lanes of the wave with `need` set: their 4·k casts are dealt one per lane
 // across the whole wave (rounds of 64) instead of four in a row on the
@@ -523,13 +516,12 @@ __device__ __forceinline__ void stuckCastsD(const LBVH &bvh, bool need, Vec3 x, 
     const uint64_t act = __ballot(1);
     const uint64_t m = __ballot(need);
     if (m == 0ull) return;
-    if (!MPENV_MOVE_COOP_STUCK || act != ~0ull) {
+    if (act != ~0ull) {
         if (need) {
             for (int dir = 0; dir < 4; dir++) {
                 const Vec3 dv = rotate2DD(v_norm, (float)dir * 3.14159f * 0.5f);
                 Vec3 ray_o = x - dv * r * 2.0f;
                 ray_o.z += low_check;
-                MP_LAB_SITE(5);
                 hd4[dir] = bvhSphereCastD(bvh, ray_o, dv, r).t;
             }
         }
@@ -549,7 +541,6 @@ __device__ __forceinline__ void stuckCastsD(const LBVH &bvh, bool need, Vec3 x, 
             const Vec3 dv = rotate2DD(v3(vx, vy, vz), (float)(t & 3) * 3.14159f * 0.5f);
             Vec3 ray_o = v3(ox, oy, oz) - dv * r * 2.0f;
             ray_o.z += lc;
-            MP_LAB_SITE(5);
             hd = bvhSphereCastD(bvh, ray_o, dv, r).t;
         }
 #pragma unroll
@@ -595,10 +586,9 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         Vec3 ray_o = x;
         ray_o.z += top;
         Vec3 normal = v3(0.f, 0.f, 0.f);
-        if (!(MPENV_LAB_MOVE_SKIP & 1)) {
+        {
             // the ground below, wherever it is (a bounded first try gains
             // nothing here: the downward cast prunes at the floor anyway)
-            MP_LAB_SITE(0);
             SphereHit h = bvhSphereCastD(bvh, ray_o, -kUp, r);
             if (h.t < kFltMax) normal = h.n;
         }
@@ -613,7 +603,6 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         ray_o.z += low_check;
         float low_dist;
         {
-            MP_LAB_SITE(1);
             SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
             low_dist = h.t;
             if (h.t < kFltMax) normal = h.n;
@@ -622,7 +611,6 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         bool high_hit = false;
         if (pose != kProne) {
             ray_o.z = x.z + top;
-            MP_LAB_SITE(2);
             SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
             high_dist = h.t;
             if (high_dist < low_dist) {
@@ -643,7 +631,6 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
             ray_o.z += high_hit ? top : low_check;
             float max_move = move_dist - low_dist;
             // only min(slide - buffer, max_move) is used
-            MP_LAB_SITE(3);
             float slide = castNearD(bvh, sc, ray_o, slide_dir, (max_move + buffer) + kCastSlack).t;
             slide = fmaxD(0.0f, slide - buffer);
             slide = fminD(slide, max_move);
@@ -653,10 +640,9 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         ground_check = hit_pos;
         ground_check.z += top;
         // min(ground_dist, top) is used, and whether there is ground at all
-        MP_LAB_SITE(4);
         ground_dist = castFirstNearD(bvh, sc, ground_check, -kUp, 2.f * top + 10.f);
         if (ground_dist == kFltMax) break;
-        stuck_path = !(MPENV_LAB_MOVE_SKIP & 8) && (ground_dist <= 0.0f || stuck);
+        stuck_path = (ground_dist <= 0.0f || stuck);
         cont = true;
     } while (false);
 
@@ -678,7 +664,6 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
                 hit_pos = x + dv * (fminD(furthest - r * 2.0f, -buffer));
                 ground_check = hit_pos;
                 ground_check.z += top;
-                MP_LAB_SITE(6);
                 ground_dist = bvhSphereCastD(bvh, ground_check, -kUp, r).t;
                 if (ground_dist == kFltMax) break;
             }
@@ -702,7 +687,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
 // sim.cpp:1041-1104 fallSystem + updateMoveStatePostFallSystem
 __device__ void fallD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
 {
-    if ((MPENV_LAB_MOVE_SKIP & 16) || S.alive[g] == 0.f) return;
+    if (S.alive[g] == 0.f) return;
     const float fall_rate = 386.08858267717f;
     const float cast_offset = c::kAgentRadius;
     Vec3 pos = ldPos(S, g);
@@ -710,7 +695,6 @@ __device__ void fallD(const DevState &S, const SceneDev &sc, const LBVH &bvh, in
     ray_o.z += c::kAgentRadius + cast_offset;
     // min(ground - cast_offset, fall_rate * dt) is used, and whether there
     // is ground at all
-    MP_LAB_SITE(7);
     float ground = castFirstNearD(bvh, sc, ray_o, -kUp, 2.f * (cast_offset + fall_rate * c::kDeltaT) + 10.f);
     if (ground == kFltMax || ground < cast_offset) return;
     float fall = fminD(ground - cast_offset, fall_rate * c::kDeltaT);
@@ -1571,10 +1555,8 @@ __device__ void accumulateCrumbsD(const DevState &S, int w, int i)
     S.bcPenalty[g] = total;
 }
 
-#ifndef MPENV_CRUMB_CHUNK
-#define MPENV_CRUMB_CHUNK 4
-#endif
-// In chunks of MPENV_CRUMB_CHUNK crumbs loaded before any is written back: the world lane
+constexpr int kCrumbChunk = 4;
+// In chunks of kCrumbChunk crumbs loaded before any is written back: the world lane
 // waits for one round of loads per chunk instead of per crumb, and the
 // compaction only ever writes to slots at or below the chunk being read.
 __device__ void decayCrumbsD(const DevState &S, int w)
@@ -1591,7 +1573,7 @@ __device__ void decayCrumbsD(const DevState &S, int w)
             m += 1;
         }
     };
-    constexpr int CK = MPENV_CRUMB_CHUNK;
+    constexpr int CK = kCrumbChunk;
     #pragma unroll 1
     for (int k0 = 0; k0 < n; k0 += CK) {
         // past the end: re-read the last crumb (unused)
@@ -2222,18 +2204,11 @@ constexpr int kBlock = 256;
 // step kernels index worlds / agents by block, so neighbouring blocks share
 // cache lines of the per-world and per-agent columns.  Renumbered, each XCD
 // runs one contiguous range of blocks (bijective for any grid size).
-#ifndef MPENV_XCD_REMAP
-#define MPENV_XCD_REMAP 1
-#endif
 __device__ __forceinline__ uint32_t xcdBlockId()
 {
-#if MPENV_XCD_REMAP
     const uint32_t nwg = gridDim.x, orig = blockIdx.x;
     const uint32_t xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
     return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
-#else
-    return blockIdx.x;
-#endif
 }
 
 // Persistent-entity setup + the Sim constructor's initWorld(ctx, true)
@@ -2317,60 +2292,21 @@ __global__ void __launch_bounds__(64) k_reset_only(DevState S, SceneDev sc)
 // Step graph part 1 (sim.cpp:5299-5320 up to updateMoveStatePostFall): the
 // per-agent systems, which read no other agent's state.  Lane = agent, no
 // barriers, so sphere-cast latency overlaps across the whole grid.
-#ifndef MPENV_MOVE_WPE
-#define MPENV_MOVE_WPE 3
-#endif
-#ifdef MPENV_LAB_WAVE_HIST
-// kernel_lab only: per-wave timeline of the kernel MPENV_LAB_WAVE_HIST
-// names (1 k_move, 2 k_sim, 3 k_obs, 4 k_vis): lane 0 of each wave stores
-// its start / end on the 100 MHz wall clock in its own slot (no atomics:
-// same-address atomics from thousands of waves would stretch the tail they
-// measure); mpenv_lab_wave reads and clears them.
-constexpr int kLabWaves = 1 << 16;
-__device__ uint64_t g_labWaveT[kLabWaves][2];
-__device__ __forceinline__ void labWaveEnd(const DevState &S, uint64_t wt0, uint64_t wt1)
-{
-    (void)S;
-    (void)wt1;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if ((threadIdx.x & 63) == 0 && wave < (uint32_t)kLabWaves) {
-        g_labWaveT[wave][0] = wt0;
-        g_labWaveT[wave][1] = wall_clock64();
-    }
-}
-#define MP_WAVE_T0(id) const uint64_t labWt0 = wall_clock64()
-#define MP_WAVE_T1(id)                                                                                             \
-    do {                                                                                                           \
-        if (MPENV_LAB_WAVE_HIST == (id)) labWaveEnd(S, labWt0, labWt0);                                            \
-    } while (0)
-#else
-#define MP_WAVE_T0(id) ((void)0)
-#define MP_WAVE_T1(id) ((void)0)
-#endif
 // apw: agents per wave (64, or fewer on small batches: a wave runs the
 // longest of its lanes' sphere-cast chains, so when the batch leaves SIMDs
 // idle, fewer agents per wave shorten every wave; launchMove picks it).
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPENV_MOVE_WPE))) k_move(DevState S, SceneDev sc, int apw)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) k_move(DevState S, SceneDev sc, int apw)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-#ifdef MPENV_LAB_WAVE_HIST
-    const uint64_t wt0 = wall_clock64();
-#endif
     LBVH bvh = stageBVHSphere(smem, sc);
     bvh.stats = S.stats;
-#ifdef MPENV_LAB_WAVE_HIST
-    const uint64_t wt1 = wall_clock64();
-    bvh.stats = nullptr; // the timeline only: no per-cast counters
-#endif
     [&]() {
         const int lane = threadIdx.x & 63;
         if (lane >= apw) return;
         const int64_t wave = ((int64_t)xcdBlockId() * blockDim.x + threadIdx.x) >> 6;
         const int64_t g = wave * apw + lane;
         if (g >= S.A) return;
-#ifndef MPENV_LAB_WAVE_HIST
         if (S.stats) statAdd(S.stats + kStatAliveAgents, S.alive[g] != 0.f ? 1u : 0u);
-#endif
         planAStarD(S, sc, g);
         if (sc.replayOn) return; // pvpReplayLogic replaces the gameplay systems (sim.cpp:5587-5605)
         applyBotActionsD(S, g);
@@ -2379,50 +2315,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MPE
         applyVelocityD(S, sc, bvh, g);
         fallD(S, sc, bvh, g);
     }();
-#ifdef MPENV_LAB_WAVE_HIST
-    if (MPENV_LAB_WAVE_HIST == 1) labWaveEnd(S, wt0, wt1);
-#endif
 }
 
 // Step graph part 2 (fireSystem onward): per-world phases.  A workgroup
 // holds floor(kSimBlock / N) whole worlds, lane = agent, phases separated
 // by workgroup barriers.
 constexpr int kSimBlock = 128;
-// kernel_lab only: skip k_sim phases to time them (wrong results by design)
-#ifndef MPENV_LAB_SIM_SKIP
-#define MPENV_LAB_SIM_SKIP 0
-#endif
 
 __device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
 
 // 4 waves/SIMD (128 VGPRs, at the price of ~420 B/lane of scratch spills):
 // k_sim alone 0.196 -> 0.139 ms -- every wave of a C3 launch resident,
 // which hides the per-world phases' latency better than the spills cost.
-#ifndef MPENV_SIM_WPE
-#define MPENV_SIM_WPE 4
-#endif
-#define MP_SIM_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_SIM_WPE)))
+#define MP_SIM_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 // flatten: every phase inlined (an outlined call needs a stack frame in
 // scratch for the whole kernel and spills around the call).
 __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)) k_sim(DevState S, SceneDev sc)
 {
-    MP_WAVE_T0(2);
-#ifdef MPENV_LAB_PHASE_T
-    // lab: per-block phase durations (thread 0, after each barrier)
-    uint64_t pt_prev = clock64();
-    int pt_k = 0;
-    auto PT = [&]() {
-        if (threadIdx.x == 0 && S.stats) {
-            const uint64_t t = clock64();
-            atomicAdd(&S.stats[9 + pt_k], (unsigned long long)(t - pt_prev));
-            pt_prev = t;
-        }
-        pt_k++;
-    };
-#define MP_PT() PT()
-#else
-#define MP_PT() ((void)0)
-#endif
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const LBVH bvh = stageBVH(smem, sc);
@@ -2446,23 +2355,17 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         if (act) replayAgentD(S, w, i);
         if (wlane) S.curStep[w] = S.replayLog[w].cur_step;
         __syncthreads();
-    MP_PT();
         if (wlane) zoneSystemD(S, sc, w);
         __syncthreads();
-    MP_PT();
     } else {
-        if (!(MPENV_LAB_SIM_SKIP & 1) && act) fireD(S, sc, bvh, w, i);
+        if (act) fireD(S, sc, bvh, w, i);
         __syncthreads();
-    MP_PT();
-        if (!(MPENV_LAB_SIM_SKIP & 2048) && act) applyDmgD(S, g);
+        if (act) applyDmgD(S, g);
         __syncthreads();
-    MP_PT();
-        if (!(MPENV_LAB_SIM_SKIP & 2) && wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
+        if (wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
         __syncthreads();
-    MP_PT();
         if (act) autoHealD(S, g);
         __syncthreads();
-    MP_PT();
         {
             __shared__ int zoneCz[kSimBlock];
             __shared__ uint8_t zoneIn[kSimBlock];
@@ -2480,11 +2383,10 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             if (act) {
                 zoneIn[threadIdx.x] = zoneInD(S, sc, zoneCz[wl], g) ? 1 : 0;
                 if (sc.recordOn) recordAgentD(S, w, i);
-                if (!(MPENV_LAB_SIM_SKIP & 256)) leaveBreadcrumbAgentD(S, w, g);
+                leaveBreadcrumbAgentD(S, w, g);
             }
             if (wlane && sc.recordOn) S.recordLog[w].cur_step = S.curStep[w];
             __syncthreads();
-    MP_PT();
             if (wlane) {
                 int na = 0, nb = 0;
                 #pragma unroll 1
@@ -2495,15 +2397,14 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
                 }
                 zonePostD(S, w, zp, na, nb);
                 if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
-                if (!(MPENV_LAB_SIM_SKIP & 256)) appendCrumbsD(S, w);
+                appendCrumbsD(S, w);
             }
         }
         __syncthreads();
-    MP_PT();
         // accumulateBreadcrumbPenalties shares its agent phase with the
         // match-info / goal-region reads below (each lane reads its own
         // agent and the crumbs, which nothing in that phase writes)
-        if (!(MPENV_LAB_SIM_SKIP & 512) && act) accumulateCrumbsD(S, w, i);
+        if (act) accumulateCrumbsD(S, w, i);
     }
     // zoneMatchInfoSystem's per-agent reads, one lane per agent (the world
     // lane would otherwise walk them serially)
@@ -2514,23 +2415,18 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         goalDistAgentD(S, sc, w, i, ldPos(S, g), &goalDist[threadIdx.x * 6]);
     }
     __syncthreads();
-    MP_PT();
     if (wlane) {
-        if (!(MPENV_LAB_SIM_SKIP & 256) && !sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem
-        MP_PT(); // (lab: thread 0 is world 0's lane)
-        if (!(MPENV_LAB_SIM_SKIP & 8)) zoneMatchInfoD(S, sc, w, &matchBits[wl * N]);
-        MP_PT();
-        if (!(MPENV_LAB_SIM_SKIP & 16)) goalRegionsD(S, sc, w, &goalDist[wl * N * 6]);
+        if (!sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem // (lab: thread 0 is world 0's lane)
+        zoneMatchInfoD(S, sc, w, &matchBits[wl * N]);
+        goalRegionsD(S, sc, w, &goalDist[wl * N * 6]);
     }
     __syncthreads();
-    MP_PT();
     if (act) {
-        if (!(MPENV_LAB_SIM_SKIP & 1024)) exploreVisitedD(S, w, g);
+        exploreVisitedD(S, w, g);
         if (sc.flank && sc.task == MPENV_TASK_ZONE) flankRewardD(S, sc, bvh, w, i);
-        else if (!(MPENV_LAB_SIM_SKIP & 64)) zoneRewardD(S, sc, w, i);
+        else zoneRewardD(S, sc, w, i);
     }
     __syncthreads();
-    MP_PT();
     if (wlane) {
         // pvpTeamRewardSystem (sim.cpp:4292-4313)
         float tr[2] = { 0.f, 0.f };
@@ -2547,7 +2443,6 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         S.teamRew1[w] = tr[1];
     }
     __syncthreads();
-    MP_PT();
     if (act) {
         // pvpFinalRewardSystem (sim.cpp:4315-4339) + doneSystem (4712-4717)
         const int team = i / S.T;
@@ -2561,7 +2456,6 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     RandKey *pre = S.resetKeys + ((int64_t)w * N) * (kPreDraws + 1);
     if (act && resetDueD(S, sc, w)) resetPreD(S, sc, w, i, pre + i * (kPreDraws + 1));
     __syncthreads();
-    MP_PT();
     if (wlane) {
         // fullTeamDoneRewardSystem (sim.cpp:4720-4747)
         for (int t = 0; t < 2; t++) {
@@ -2574,9 +2468,8 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             S.ftReward[(int64_t)w * 2 + t] = r;
             S.ftDone[(int64_t)w * 2 + t] = done ? 1 : 0;
         }
-        if (!(MPENV_LAB_SIM_SKIP & 128)) resetSystemD(S, sc, w, pre);
+        resetSystemD(S, sc, w, pre);
     }
-    MP_WAVE_T1(2);
 }
 
 // utils.cpp:169-184 inFrustum
@@ -2677,14 +2570,8 @@ __device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &
     S.reward[g] = r;
 }
 
-#ifdef MPENV_VIS_WPE
-#define MP_VIS_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_VIS_WPE)))
-#else
-#define MP_VIS_ATTR
-#endif
-__global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev sc)
+__global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
 {
-    MP_WAVE_T0(4);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ uint16_t rays[kVisMaxRays]; // (lane << 2) | point
     __shared__ uint32_t masks[kBlock]; // per agent of the block (<= 4 waves x 64/T)
@@ -2792,7 +2679,6 @@ __global__ void __launch_bounds__(kBlock) MP_VIS_ATTR k_vis(DevState S, SceneDev
         const bool valid = wl < apw * T && g < S.A;
         if (valid && wl % T == 0) S.visMask[g] = (uint8_t)masks[(int)(g - agent0)];
     }
-    MP_WAVE_T1(4);
 }
 
 __device__ __forceinline__ Vec3 normalizedPosD(const SceneDev &sc, Vec3 p) // sim.cpp:2693-2718
@@ -2909,24 +2795,9 @@ constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B align
 constexpr int kObsSpanPad = 44;            // rowBuf floats per lane: >= kObsRowPad and the 43-float self obs
 constexpr int kPosPad = 19;                // posBuf floats per lane: 6 slots x 3, odd stride
 
-// Observation stores: plain, or nontemporal (MPENV_OBS_NT=1: the streamed
-// outputs, ~1.2 GB per C3 step, bypass the L2's normal allocation).
-#ifndef MPENV_OBS_NT
-#define MPENV_OBS_NT 0
-#endif
-__device__ __forceinline__ void ntStore(float *p, float v) { __builtin_nontemporal_store(v, p); }
-__device__ __forceinline__ void ntStore(float4 *p, float4 v)
-{
-    __builtin_nontemporal_store(lf4{ v.x, v.y, v.z, v.w }, reinterpret_cast<lf4 *>(p));
-}
-template <typename V> __device__ __forceinline__ void obsStore(V *p, V v)
-{
-#if MPENV_OBS_NT
-    ntStore(p, v);
-#else
-    *p = v;
-#endif
-}
+// Observation stores: plain (nontemporal stores for the ~1.2 GB per C3
+// step were measured no faster, round 2).
+template <typename V> __device__ __forceinline__ void obsStore(V *p, V v) { *p = v; }
 
 
 // Flushes the wave's staged 32-float rows (lane l's row at buf + l *
@@ -2978,19 +2849,13 @@ struct WaveStage {
     }
     template <int n, int P> __device__ __forceinline__ void flush(float *dst, int64_t off, bool zero = false) const
     {
-#ifdef MPENV_LAB_NO_DWORD_FLUSH
-        if (off != -12345) return; // lab: every dword-flushed row dropped (upper bound of their cost)
-#endif
         // which rows exist / are zeros: wave-wide bit masks (lane r = row r)
         const uint64_t wbits = __ballot(off >= 0), zbits = __ballot(zero);
         offs[lane] = off;
         waveSync();
         // the m live lanes (a tail wave's lanes past A have returned) share
         // the m x n staged floats
-#ifndef MPENV_FLUSH_UNROLL
-#define MPENV_FLUSH_UNROLL 1
-#endif
-#pragma unroll MPENV_FLUSH_UNROLL
+#pragma unroll 1
         for (int j = 0; j < n; j++) {
             const int c = lane + m * j;
             const int r = c / n, col = c - r * n;
@@ -3155,17 +3020,8 @@ __device__ __forceinline__ void fullTeamSlotD(const DevState &S, const SceneDev 
     storeVec(&S.ftGlobal[mine * MPENV_FT_GLOBAL_DIM], gob, MPENV_FT_GLOBAL_DIM);
 }
 
-#ifndef MPENV_OBS_NOUNROLL
-#define MPENV_OBS_NOUNROLL 0
-#endif
-#ifdef MPENV_OBS_WPE
-#define MP_OBS_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_OBS_WPE)))
-#else
-#define MP_OBS_ATTR
-#endif
-__global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev sc)
+__global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
 {
-    MP_WAVE_T0(3);
     // per wave: observation rows (stride kObsRowPad) or a whole self-obs
     // span (stride 43); position rows of the slot loops (stride kPosPad)
     __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsSpanPad];
@@ -3266,9 +3122,6 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
     // teammate / opponent rows are built in place in the lane's LDS row
     float *row = wbuf + lane * kObsRowPad;
     // teammates
-#if MPENV_OBS_NOUNROLL
-#pragma unroll 1
-#endif
     for (int k = 0; k < kMaxTeamSize - 1; k++) {
         float *tob = row;
         float tpos[3];
@@ -3287,9 +3140,6 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
     wp.flushSpan<15, kPosPad>(S.tmPos + gw0 * 15);
 
     // opponents (+ last known)
-#if MPENV_OBS_NOUNROLL
-#pragma unroll 1
-#endif
     for (int k = 0; k < kMaxTeamSize; k++) {
         float *oob = row;
         float opos[3];
@@ -3329,10 +3179,7 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
     }
     wp.flushSpan<18, kPosPad>(S.oppPos + gw0 * 18);
 
-#ifndef MPENV_LAB_OBS_NO_FT
     fullTeamSlotD(S, sc, w, g, team, off, ws);
-#endif
-    MP_WAVE_T1(3);
 }
 
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray.  Rays are dealt to
@@ -3346,36 +3193,18 @@ __global__ void __launch_bounds__(kBlock) MP_OBS_ATTR k_obs(DevState S, SceneDev
 // consecutive task quads: up to kLidarIters (amortises the BVH staging) on
 // big batches, fewer on small ones so the grid still spreads over the CUs
 // (at 64 worlds 1v1 a fixed 8 put the whole lidar on 5 CUs).
-#ifndef MPENV_LIDAR_ITERS
-#define MPENV_LIDAR_ITERS 4 // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 ms (k_lidar alone, C3)
-#endif
-constexpr int kLidarIters = MPENV_LIDAR_ITERS;
-// 1: rear fans cull capsules per 16-lane group (positions by ds_bpermute); 0: capsulesD
-// per ray (with the rotated vertex copies k_lidar 0.7302 vs 0.7375 ms, r03y lab; through
-// a per-wave LDS slot table instead of ds_bpermute: no gain, dropped)
-#ifndef MPENV_LIDAR_REARCULL
-#define MPENV_LIDAR_REARCULL 1
-#endif
-#ifndef MPENV_LIDAR_NT
-#define MPENV_LIDAR_NT 0 // 1: the full-team lidar copy (written, never read here) as a nontemporal store
-#endif
+constexpr int kLidarIters = 4; // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 ms (k_lidar alone, C3, round 2)
 // 1024-thread blocks: the 8 octant node images + the three rotated vertex
 // copies (31 + 36 KB on simple_map) are staged once per 16 waves, so 2
 // blocks per CU (8 waves per SIMD) fit the 160 KB of LDS.
-#ifndef MPENV_LIDAR_BLOCK
-#define MPENV_LIDAR_BLOCK 1024
-#endif
-constexpr int kLidarBlock = MPENV_LIDAR_BLOCK;
+constexpr int kLidarBlock = 1024;
 constexpr int kLidarWaves = kLidarBlock / 64;
 
 __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A + 3) / 4) * 5; }
 
 // 8 waves per SIMD (64 VGPRs, a few bytes of spill outside the traversal
 // loop): latency-bound LDS traversal gains more from occupancy (-7%).
-#ifndef MPENV_LIDAR_WPE
-#define MPENV_LIDAR_WPE 8
-#endif
-#define MP_LIDAR_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_LIDAR_WPE)))
+#define MP_LIDAR_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 
 // Lidar task sets: kLidarAll -- every task (5 per 4-agent unit: 4 forward
 // fans, then the unit's rear fans) through the BVH; kLidarFan -- the
@@ -3388,7 +3217,7 @@ __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A +
 // 64 that 8 waves per SIMD need).
 enum { kLidarAll = 0, kLidarFan = 1, kLidarRear = 2 };
 
-__device__ __host__ __forceinline__ bool lidarFanScene(const SceneDev &sc) { return kLidarRot && sc.numVerts / 3 <= 255; }
+__device__ __host__ __forceinline__ bool lidarFanScene(const SceneDev &sc) { return sc.numVerts / 3 <= 255; }
 
 template <int kMode>
 __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc, int iters, char *smem)
@@ -3432,9 +3261,6 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             sub = 4u;
         }
         const bool fwd = sub < 4u;
-#ifdef MPENV_LAB_NO_REAR
-        if (!fwd) continue;
-#endif
         // The ray of lane `ln`: a tail unit's lanes past A trace a copy of
         // the last agent's rays and store nothing.
         auto rayIndex = [&](uint32_t ln, uint32_t &g, bool &valid, uint32_t &kk) {
@@ -3464,13 +3290,6 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
         uint32_t g, kk;
         bool valid;
         Vec3 ray_o, dir;
-#ifndef MPENV_LIDAR_PERM
-#define MPENV_LIDAR_PERM 0
-#endif
-
-#ifndef MPENV_LIDAR_WAVECULL
-#define MPENV_LIDAR_WAVECULL 1
-#endif
         // The BVH first (one traversal for both fan kinds), then the world's
         // capsules.  World / agent indices are formed after the traversal,
         // from an opaque copy of g (nothing but the ray lives across it).
@@ -3506,7 +3325,7 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             LBVH ob = bvh;
             ob.nodes = reinterpret_cast<const MP_LDS BVHNode *>(reinterpret_cast<const MP_LDS uint4 *>(bvh.nodes) +
                                                                  rayOctant(dir) * sc.numNodes * kOctNodeQ);
-            bhit = bvhTraceRayT<false, MPENV_LIDAR_PERM != 0, kOctNodeQ, kLidarRot, true, true>(ob, ray_o, dir, tb,
+            bhit = bvhTraceRayT<false, kOctNodeQ, true, true, true>(ob, ray_o, dir, tb,
                                                                                                kFltMax, 0.f);
         }
         // The lane id again (volatile) and the ray's indices from it: integer
@@ -3522,7 +3341,7 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
         const uint32_t i = g - w * N;
         const int64_t g0 = (int64_t)w * N;
         WorldHit hw;
-        if (MPENV_LIDAR_WAVECULL && fwd) {
+        if (fwd) {
             // Forward fan (one agent, one xy origin per wave): the BVH first,
             // then only the capsules some ray of the wave could hit before
             // its BVH hit.  Any point of capsule j lies within r of its
@@ -3575,7 +3394,7 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             hw.hit = hit;
             hw.t = min_t;
             hw.entity = ent;
-        } else if (MPENV_LIDAR_REARCULL) {
+        } else {
             // Rear fans: the same cull per 16-lane group (one agent, one xy
             // origin per group; N <= 12 capsules).  Lane q*16 + j < q*16 + N
             // loads capsule j of group q's world; the wave walks the union
@@ -3626,8 +3445,6 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             hw.hit = hit;
             hw.t = min_t;
             hw.entity = ent;
-        } else {
-            hw = capsulesD(S.px, S.py, S.pz, g0, (int)N, ray_o, dir, (int)i, bhit, bhit ? tb : kFltMax);
         }
         if (!valid) continue;
         const bool second = i >= T; // team of the casting agent
@@ -3649,16 +3466,7 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
         // fullTeamObservationsSystem copies the lidar before this system
         // overwrites it (sim.cpp:5283-5310): the previous value moves into
         // the team interface's slot.
-#ifndef MPENV_LAB_NO_FT_LIDAR
-        const float4 prev = *dst;
-#if MPENV_LIDAR_NT
-        ntStore(tdst, prev);
-#else
-        *tdst = prev;
-#endif
-#else
-        (void)tdst;
-#endif
+        *tdst = *dst;
         *dst = out;
     }
 }
@@ -3682,36 +3490,6 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar_rear(DevSta
 }
 
 static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
-
-#ifdef MPENV_LAB_WAVE_HIST
-// kernel_lab only: copy out (and clear) the per-wave start / end stamps,
-// [n][2] u64 (zeros for waves that did not run).
-extern "C" int mpenv_lab_wave(uint64_t *out, int32_t n)
-{
-    n = n < kLabWaves ? n : kLabWaves;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_labWaveT), sizeof(uint64_t) * 2 * n, 0, hipMemcpyDeviceToHost) !=
-        hipSuccess)
-        return -1;
-    static uint64_t zeros[kLabWaves * 2];
-    return check(hipMemcpyToSymbol(HIP_SYMBOL(g_labWaveT), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice));
-}
-#endif
-
-#ifdef MPENV_LAB_WORK
-// kernel_lab only: copy out (and clear) the per-thread sphere-cast work
-// counters, [11][n] u32 (casts, nodes popped, triangle tests, nodes per cast site 0..7).
-extern "C" int mpenv_lab_work(uint32_t *out, int32_t n)
-{
-    n = n < kLabWorkMax ? n : kLabWorkMax;
-    for (int k = 0; k < kLabWorkRows; k++) {
-        if (hipMemcpyFromSymbol(out + (size_t)k * n, HIP_SYMBOL(g_labWork), sizeof(uint32_t) * n,
-                                sizeof(uint32_t) * kLabWorkMax * k, hipMemcpyDeviceToHost) != hipSuccess)
-            return -1;
-    }
-    static uint32_t zeros[kLabWorkRows * kLabWorkMax];
-    return check(hipMemcpyToSymbol(HIP_SYMBOL(g_labWork), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice));
-}
-#endif
 
 // Debug/test hook: closest-hit BVH queries for caller rays (mode 0 = the
 // traversal inlined into the step kernels, 1 = its out-of-line copy).
@@ -3904,7 +3682,7 @@ size_t bvhLdsBytesSphere(const SceneDev &sc)
 
 size_t bvhLdsBytesOct(const SceneDev &sc)
 {
-    return (size_t)sc.numNodes * 16 * kOctNodeQ * 8 + (size_t)sc.numVerts * 16 * (kLidarRot ? 3 : 1);
+    return (size_t)sc.numNodes * 16 * kOctNodeQ * 8 + (size_t)sc.numVerts * 16 * 3;
 }
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
@@ -3932,11 +3710,8 @@ int launchMove(const DevState &s, const SceneDev &sc, void *stream)
     // (the 24 KB LDS image per block would otherwise cap occupancy).
     // Agents per wave: 64 once the batch fills ~1.5 waves per SIMD (1,536
     // waves on 256 CUs), else the power of two (>= 8) that gets closest.
-#ifndef MPENV_MOVE_TARGET_WAVES
-#define MPENV_MOVE_TARGET_WAVES 1536
-#endif
     int apw = 64;
-    while (apw > 8 && (s.A + apw - 1) / apw < MPENV_MOVE_TARGET_WAVES) apw >>= 1;
+    while (apw > 8 && (s.A + apw - 1) / apw < 1536) apw >>= 1;
     const int64_t waves = (s.A + apw - 1) / apw;
     const int bs = waves < 64 * 4 ? 64 : kBlock;
     const int64_t threads = waves * 64;

@@ -140,3 +140,28 @@ def test_caller_written_against_mgr_hpp_compiles_and_out_of_scope_parts_throw(tm
     r = subprocess.run([exe, T.SCENE], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert "mgr.hpp caller ok" in r.stdout
+
+
+def test_product_kernels_carry_no_lab_switches_and_lab_patches_apply(tmp_path):
+    """Only the shipped configuration is in csrc/ (no lab hooks or dropped
+    variants behind compile-time switches); the lab overlay under tools/lab/
+    still applies to it, so kernel_lab variants keep building."""
+    import shutil
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "madrona-mp-env_amd", "csrc")
+    switch = re.compile(r"^\s*#\s*(if|ifdef|ifndef|elif)\b.*\bMPENV_", re.M)
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h", ".cpp")):
+            text = open(os.path.join(csrc, f)).read()
+            assert not switch.search(text), f"compile-time MPENV_ switch left in {f}"
+            assert "MPENV_LAB" not in text and "MP_LAB_" not in text, f"lab hook left in {f}"
+    lab = os.path.join(root, "tools", "lab")
+    patches = sorted(p for p in os.listdir(lab) if p.endswith(".patch"))
+    assert "lab_hooks.patch" in patches
+    for p in patches:
+        work = tmp_path / p
+        shutil.copytree(csrc, work)
+        r = subprocess.run(["patch", "-s", "-p1", "-d", str(work), "-i", os.path.join(lab, p)],
+                           capture_output=True, text=True)
+        assert r.returncode == 0 and "fuzz" not in r.stdout, (p, r.stdout, r.stderr)

@@ -3,8 +3,23 @@ their step kernels on the C3 workload (development tool; variants that
 switch parts of a kernel off give wrong results by design and are never
 used outside this tool).
 
-  python tools/kernel_lab.py build NAME [-DFOO=1 ...]   (here, cross-compiles)
+  python tools/kernel_lab.py build NAME [--patch tools/lab/X.patch ...] [-DFOO=1 ...]
+                                                        (here, cross-compiles)
   python tools/kernel_lab.py run NAME [NAME ...]        (on the GPU box)
+
+Instrumentation and switched-off parts live in patches under tools/lab/
+(the overlay): a build copies csrc/ into lab/NAME/src, applies the patches
+there and compiles that copy, so no lab hook sits in the shipped sources.
+
+  tools/lab/lab_hooks.patch   the round-1..3 switches: -DMPENV_LAB_MOVE_SKIP=,
+                              _SIM_SKIP=, _PHASE_T, _WAVE_HIST=k, _WORK, _NO_TRI,
+                              _NO_BVH, _NO_CAPSULE, _NO_REAR, _NO_FT_LIDAR, ...,
+                              and the dropped variants (MPENV_LIDAR_PERM,
+                              MPENV_TRI_FLAT, MPENV_OBS_NT, MPENV_*_WPE, ...)
+  tools/lab/fan_phases.patch  k_lidar_fan per-phase wave cycles and work counts
+                              (read back through mpenv_lab_fan)
+e.g. build phase --patch tools/lab/lab_hooks.patch -DMPENV_LAB_PHASE_T
+(tests/test_abi.py checks that every patch still applies to csrc/).
 """
 import ctypes as C
 import json
@@ -20,16 +35,30 @@ sys.path.insert(0, PKG)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def build(name, defines):
+def build(name, args):
+    import shutil
+
     import build_native as B
 
     out = os.path.join(LAB, name)
     os.makedirs(out, exist_ok=True)
-    common = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{B.CSRC}",
+    patches, defines = [], []
+    it = iter(args)
+    for a in it:
+        if a == "--patch":
+            patches.append(os.path.abspath(next(it)))
+        else:
+            defines.append(a)
+    src_dir = os.path.join(out, "src")
+    shutil.rmtree(src_dir, ignore_errors=True)
+    shutil.copytree(B.CSRC, src_dir)
+    for pf in patches:
+        subprocess.run(["patch", "-s", "-p1", "-d", src_dir, "-i", pf], check=True)
+    common = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{src_dir}",
               f"-I{B.INCLUDE}"] + list(defines)
     objs = []
     for src in B.LIB_SOURCES:
-        s = os.path.join(B.CSRC, src)
+        s = os.path.join(src_dir, src)
         o = os.path.join(out, src + ".o")
         if src.endswith(".hip"):
             cmd = [B.HIPCC, "-x", "hip", f"--offload-arch={B.ARCH}", "-c", s, "-o", o] + common
@@ -40,7 +69,8 @@ def build(name, defines):
         objs.append(o)
     subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o",
                     os.path.join(out, "libmpenv.so")] + objs, check=True)
-    json.dump({"defines": defines}, open(os.path.join(out, "variant.json"), "w"))
+    json.dump({"defines": defines, "patches": [os.path.relpath(p, ROOT) for p in patches]},
+              open(os.path.join(out, "variant.json"), "w"))
     print("built", name, defines)
 
 
@@ -142,7 +172,7 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
             open(os.path.join(ROOT, "gpurun_out", f"dump_{label or name}_{eid}.bin"), "wb").write(bytes(buf))
     phases = None
     if os.environ.get("LAB_STATS"):
-        # lab builds with -DMPENV_LAB_PHASE_T: k_sim per-phase block cycles
+        # lab_hooks.patch builds with -DMPENV_LAB_PHASE_T: k_sim per-phase block cycles
         lib.mpenv_enable_stats.argtypes = [C.c_void_p, C.c_int32]
         lib.mpenv_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
         lib.mpenv_enable_stats(h, 1)
@@ -155,7 +185,7 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
         phases = [round(st[k] / ns / 1e6, 2) for k in range(9, n)]
     timeline = None
     if hasattr(lib, "mpenv_lab_wave"):
-        # -DMPENV_LAB_WAVE_HIST=k: per-wave start / end of one kernel in one
+        # lab_hooks.patch with -DMPENV_LAB_WAVE_HIST=k: per-wave start / end of one kernel in one
         # step (100 MHz wall clock), the default world groups
         import numpy as np
 
@@ -183,7 +213,7 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
                                                    for f in (0.1, 0.25, 0.5, 0.75, 0.9)]}
     work = None
     if hasattr(lib, "mpenv_lab_work"):
-        # -DMPENV_LAB_WORK: per-thread sphere-cast work of one step's k_move
+        # lab_hooks.patch with -DMPENV_LAB_WORK: per-thread sphere-cast work of one step's k_move
         import numpy as np
 
         nthr = 1 << 18
@@ -206,7 +236,27 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
                         "wave_max_pct": [round(float(np.percentile(wmax, q)), 1) for q in (10, 50, 90, 99, 100)],
                         "lane_pct": [round(float(np.percentile(wv[k], q)), 1) for q in (50, 90, 99, 99.9, 100)],
                         "lanes_active": round(float((wv[k] > 0).mean()), 4)}
-    print(json.dumps({"variant": label or name, "work": work, "timeline": timeline, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
+    fan = None
+    if hasattr(lib, "mpenv_lab_fan"):
+        # tools/lab/fan_phases.patch: per forward-fan task, mean wave cycles
+        # per phase and mean work counts (each read: the last launch's
+        # per-wave sums; 5 steps)
+        import numpy as np
+
+        lib.mpenv_lab_fan.argtypes = [C.c_void_p, C.c_int32]
+        acc = np.zeros(10, np.float64)
+        fb = np.zeros(10, np.uint64)
+        for s in range(5):
+            step(s)
+            hip.hipDeviceSynchronize()
+            assert lib.mpenv_lab_fan(fb.ctypes.data, 10) == 0
+            acc += fb
+        nt = max(acc[5], 1.0)
+        fan = {k: round(float(acc[i]) / nt, 2) for i, k in enumerate(
+            ("cyc_pre", "cyc_cull", "cyc_masks", "cyc_walk", "cyc_post", "tasks", "survivors", "entries_walked",
+             "entries_tested", "lane_tests")) if i != 5}
+        fan["tasks_per_step"] = nt / 5
+    print(json.dumps({"variant": label or name, "fan": fan, "work": work, "timeline": timeline, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
                       "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
                       "digest": dig.hexdigest()[:16], "per_export": pex}), flush=True)
 
