@@ -540,6 +540,7 @@ def main():
             "los_pairs": round(counts["los_pairs"] / steps, 1),
             "los_rays": round(counts["los_rays"] / steps, 1),
             "los_seen": round(counts["los_seen"] / steps, 1),
+            "los_traced": round(counts.get("los_traced", 0) / steps, 1),
             "lidar_rays": 80 * A,
             "shot_rays": round(counts["shot_rays"] / steps, 1),
             "hit_agents": round(counts["hit_agents"] / steps, 1),

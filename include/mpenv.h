@@ -438,11 +438,13 @@ int mpenv_enable_kernel_timing(mpenv_manager *mgr, int32_t enable);
 /* Measurement hook (no reference counterpart): per-step workload counters
  * accumulated by the step kernels while enabled (enabling zeroes them):
  * [0] alive agents at k_move, [1] (viewer, opponent) pairs both alive,
- * [2] visibility rays traced, [3] visibility rays that saw their target,
- * [4] sphere casts, [5] shot rays, [6] agents that took damage, [7] agents
- * killed, [8] last-known observation rows written by the observation
- * system.  read_stats copies min(n, 9) counters and returns the number of
- * counters (9). */
+ * [2] visibility rays after the view / frustum tests, [3] visibility rays
+ * that saw their target, [4] sphere casts, [5] shot rays, [6] agents that
+ * took damage, [7] agents killed, [8] last-known observation rows written by
+ * the observation system, [9] visibility rays that needed a BVH traversal
+ * (not decided by the target-capsule test or the occluder hint).
+ * read_stats copies min(n, 10) counters and returns the number of counters
+ * (10). */
 int mpenv_enable_stats(mpenv_manager *mgr, int32_t enable);
 int mpenv_read_stats(mpenv_manager *mgr, uint64_t *out, int32_t n);
 

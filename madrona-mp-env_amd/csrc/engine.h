@@ -171,7 +171,8 @@ enum StatId {
     kStatHits = 6,        // agents that took damage (applyDmgSystem)
     kStatKills = 7,       // agents killed (alive -> hp <= 0)
     kStatLkRows = 8,      // last-known rows k_obs wrote (knows / cleared on death)
-    kNumStats = 9,
+    kStatLosTraced = 9,   // LOS rays that needed a BVH traversal (not decided by the target test or hint)
+    kNumStats = 10,
 };
 
 struct ZOBBDev {

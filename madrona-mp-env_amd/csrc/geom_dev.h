@@ -701,6 +701,14 @@ __device__ __forceinline__ float fanNearD(float sf, float cx, float cy, float cz
     return fmaxf(0.f, fmaf(fmaxf(fabsf(sf), cd), 0.99999f, -0.05f));
 }
 
+// The fan's wedge in the sheet plane, widened: directions at angles
+// [pi/8 - 0.01, 7pi/8 + 0.01] (cos / sin of the lower edge; the upper edge is
+// its mirror image).  A triangle whose three vertices all lie more than
+// kFanWedgeTol outside one edge line cannot hold a hit of the sheet (a hit
+// point lies on a ray of the sheet, inside the wedge, and the projected
+// triangle is the hull of its projected vertices).
+constexpr float kFanWedgeC = 0.92766011f, kFanWedgeS = 0.37342566f, kFanWedgeTol = 0.01f;
+
 // mkRay(o, d): the lane's ray, formed only once the walk starts (so it is not
 // live across the cull); returned in ray_o / ray_d.
 template <class MkRay>
@@ -720,6 +728,14 @@ __device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uin
     const Vec3 N = uni3(cross(R, F));
     const float dz = uni(z1 - z0);
     const float c0 = uni(fmaf(N.x, ox, fmaf(N.y, oy, N.z * z0))), c1 = uni(fmaf(N.z, dz, c0));
+    // wedge edge normals (G1: inside where G1.(p - O) >= 0; G2 likewise)
+    const Vec3 G1 = uni3(v3(fmaf(kFanWedgeC, F.x, kFanWedgeS * R.x), fmaf(kFanWedgeC, F.y, kFanWedgeS * R.y),
+                            fmaf(kFanWedgeC, F.z, kFanWedgeS * R.z)));
+    const Vec3 G2 = uni3(v3(fmaf(kFanWedgeC, F.x, -kFanWedgeS * R.x), fmaf(kFanWedgeC, F.y, -kFanWedgeS * R.y),
+                            fmaf(kFanWedgeC, F.z, -kFanWedgeS * R.z)));
+    const float k10 = uni(fmaf(G1.x, ox, fmaf(G1.y, oy, G1.z * z0)) - kFanWedgeTol);
+    const float k20 = uni(fmaf(G2.x, ox, fmaf(G2.y, oy, G2.z * z0)) - kFanWedgeTol);
+    const float k11 = uni(fmaf(G1.z, dz, k10)), k21 = uni(fmaf(G2.z, dz, k20));
     const MP_LDS lf4 *vp = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + 2 * b.rotStride; // (x, y, z, n_i)
     const MP_LDS lf4 *v0 = reinterpret_cast<const MP_LDS lf4 *>(b.verts);                  // .w: d, r, cx
     const MP_LDS lf4 *v1 = v0 + b.rotStride;                                                // .w: cy, cz
@@ -738,8 +754,16 @@ __device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uin
             const float sb = fmaf(N.x, B.x, fmaf(N.y, B.y, N.z * B.z));
             const float sc = fmaf(N.x, C.x, fmaf(N.y, C.y, N.z * C.z));
             const float smin = fminf(sa, fminf(sb, sc)), smax = fmaxf(sa, fmaxf(sb, sc));
-            if (sf0 >= -kFanTol && smin <= c0 + kFanBand && smax >= c0 - kFanBand) fl |= 1u;
-            if (sf1 >= -kFanTol && smin <= c1 + kFanBand && smax >= c1 - kFanBand) fl |= 2u;
+            const float g1 = fmaxf(fmaf(G1.x, A.x, fmaf(G1.y, A.y, G1.z * A.z)),
+                                   fmaxf(fmaf(G1.x, B.x, fmaf(G1.y, B.y, G1.z * B.z)),
+                                         fmaf(G1.x, C.x, fmaf(G1.y, C.y, G1.z * C.z))));
+            const float g2 = fmaxf(fmaf(G2.x, A.x, fmaf(G2.y, A.y, G2.z * A.z)),
+                                   fmaxf(fmaf(G2.x, B.x, fmaf(G2.y, B.y, G2.z * B.z)),
+                                         fmaf(G2.x, C.x, fmaf(G2.y, C.y, G2.z * C.z))));
+            if (sf0 >= -kFanTol && smin <= c0 + kFanBand && smax >= c0 - kFanBand && g1 >= k10 && g2 >= k20)
+                fl |= 1u;
+            if (sf1 >= -kFanTol && smin <= c1 + kFanBand && smax >= c1 - kFanBand && g1 >= k11 && g2 >= k21)
+                fl |= 2u;
         }
         const uint64_t m = __ballot(fl != 0u);
         if (fl) {
@@ -754,59 +778,61 @@ __device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uin
     const float uO0 = uni(dot(R, oh0)), wO0 = uni(dot(F, oh0));
     const float uO1 = uni(fmaf(R.z, dz, uO0)), wO1 = uni(fmaf(F.z, dz, wO0));
     float t_best = kFltMax, t_relax = kFltMax * kLexRelax;
-    // Phases 2-3 per chunk of 128 survivors (one chunk but for rare wide
+    const uint32_t h = lane & 1u; // phase 2: the lane's sheet
+    // Phases 2-3 per chunk of 64 survivors (one chunk but for rare wide
     // views; the smallest-t result does not depend on the walk order).
     uint32_t ch = 0;
     do {
-    // 2. masks, one or two survivors per lane (slot s holds list entry ch + 64 s + lane)
-    // entry registers per slot: triangle | bucket << 8 (bucket 8: none), the
-    // two sheet masks, the two bounds as bf16 rounded down (still bounds)
-    uint32_t eTB0 = 8u << 8, eLo0 = 0u, eHi0 = 0u, eNN0 = 0u; // bucket 8: not walked
+    // 2. masks: lane pair (2k, 2k + 1) takes survivor ch + 32 p + k in pass
+    // p, one sheet per lane, then the even lane holds the entry: triangle |
+    // bucket << 8 (bucket 8: none), the two sheet masks, the two bounds as
+    // bf16 rounded down (still bounds)
+    uint32_t eTB0 = 8u << 8, eLo0 = 0u, eHi0 = 0u, eNN0 = 0u;
     uint32_t eTB1 = 8u << 8, eLo1 = 0u, eHi1 = 0u, eNN1 = 0u;
-    // one slot, and within it one sheet, at a time (rolled loops: the
-    // unrolled form interleaves four mask computations and needs ~85 VGPRs)
+    const int npass = count > ch + 32u ? 2 : 1;
 #pragma unroll 1
-    for (int sl = 0; sl < 2; sl++) {
-        const uint32_t j = ch + (uint32_t)sl * 64u + lane;
-        uint32_t eTB = 8u << 8, eLo = 0u, eHi = 0u, eNN = 0u;
+    for (int ps = 0; ps < npass; ps++) {
+        const uint32_t j = ch + (uint32_t)ps * 32u + (lane >> 1);
+        uint32_t m = 0u, t = 0u;
+        float n = 0.f;
         if (j < count) {
             const uint32_t e = list[j];
-            const int t = (int)(e & 0xffu);
-            const uint32_t fl = e >> 8;
-            const lf4 A = vp[3 * t], B = vp[3 * t + 1], C = vp[3 * t + 2];
-            const float sv[3] = { fmaf(N.x, A.x, fmaf(N.y, A.y, N.z * A.z)), fmaf(N.x, B.x, fmaf(N.y, B.y, N.z * B.z)),
-                                  fmaf(N.x, C.x, fmaf(N.y, C.y, N.z * C.z)) };
-            const float uv[3] = { fmaf(R.x, A.x, fmaf(R.y, A.y, R.z * A.z)), fmaf(R.x, B.x, fmaf(R.y, B.y, R.z * B.z)),
-                                  fmaf(R.x, C.x, fmaf(R.y, C.y, R.z * C.z)) };
-            const float wv[3] = { fmaf(F.x, A.x, fmaf(F.y, A.y, F.z * A.z)), fmaf(F.x, B.x, fmaf(F.y, B.y, F.z * B.z)),
-                                  fmaf(F.x, C.x, fmaf(F.y, C.y, F.z * C.z)) };
-            const float cosT = fabsf(fmaf(A.w, N.x, fmaf(B.w, N.y, C.w * N.z)));
-            const float sinT = __builtin_amdgcn_sqrtf(fmaxf(0.f, fmaf(-cosT, cosT, 1.f)));
-            const float sf0 = fmaf(A.w, ox, fmaf(B.w, oy, fmaf(C.w, z0, -v0[3 * t].w)));
-            uint32_t m0 = 0u, m1 = 0u;
-            float n0 = 0.f, n1 = 0.f;
-#pragma unroll 1
-            for (int h = 0; h < 2; h++) {
-                const float sf = h ? fmaf(C.w, dz, sf0) : sf0;
-                const uint32_t m = ((fl >> h) & 1u) ? fanSheetMaskD(sv, uv, wv, h ? c1 : c0, h ? uO1 : uO0,
-                                                                    h ? wO1 : wO0, sinT, fabsf(sf))
-                                                    : 0u;
-                const float n = fanNearD(sf, v0[3 * t + 2].w, v1[3 * t].w,
-                                         v1[3 * t + 1].w, v0[3 * t + 1].w, ox, oy, h ? z1 : z0);
-                if (h) { m1 = m; n1 = n; } else { m0 = m; n0 = n; }
+            t = e & 0xffu;
+            if ((e >> (8u + h)) & 1u) {
+                const lf4 A = vp[3 * t], B = vp[3 * t + 1], C = vp[3 * t + 2];
+                const float sv[3] = { fmaf(N.x, A.x, fmaf(N.y, A.y, N.z * A.z)),
+                                      fmaf(N.x, B.x, fmaf(N.y, B.y, N.z * B.z)),
+                                      fmaf(N.x, C.x, fmaf(N.y, C.y, N.z * C.z)) };
+                const float uv[3] = { fmaf(R.x, A.x, fmaf(R.y, A.y, R.z * A.z)),
+                                      fmaf(R.x, B.x, fmaf(R.y, B.y, R.z * B.z)),
+                                      fmaf(R.x, C.x, fmaf(R.y, C.y, R.z * C.z)) };
+                const float wv[3] = { fmaf(F.x, A.x, fmaf(F.y, A.y, F.z * A.z)),
+                                      fmaf(F.x, B.x, fmaf(F.y, B.y, F.z * B.z)),
+                                      fmaf(F.x, C.x, fmaf(F.y, C.y, F.z * C.z)) };
+                const float cosT = fabsf(fmaf(A.w, N.x, fmaf(B.w, N.y, C.w * N.z)));
+                const float sinT = __builtin_amdgcn_sqrtf(fmaxf(0.f, fmaf(-cosT, cosT, 1.f)));
+                const float oz = h ? z1 : z0;
+                const float sf = fmaf(A.w, ox, fmaf(B.w, oy, fmaf(C.w, oz, -v0[3 * t].w)));
+                m = fanSheetMaskD(sv, uv, wv, h ? c1 : c0, h ? uO1 : uO0, h ? wO1 : wO0, sinT, fabsf(sf));
+                n = fanNearD(sf, v0[3 * t + 2].w, v1[3 * t].w, v1[3 * t + 1].w, v0[3 * t + 1].w, ox, oy, oz);
             }
-            const float key = m0 ? (m1 ? fminf(n0, n1) : n0) : n1;
-            eLo = m0; eHi = m1;
-            // n >= 0: truncating to the upper 16 bits rounds toward zero
-            eNN = (__float_as_uint(n0) >> 16) | (__float_as_uint(n1) & 0xffff0000u);
-            // bucket: 0 below 32 units, then one per octave up to 7
-            const int ex = (int)((__float_as_uint(key) >> 23) & 0xffu) - 127;
-            eTB = (uint32_t)t | (((m0 | m1) ? (uint32_t)min(max(ex - 4, 0), 7) : 8u) << 8);
         }
-        if (sl) { eTB1 = eTB; eLo1 = eLo; eHi1 = eHi; eNN1 = eNN; }
-        else { eTB0 = eTB; eLo0 = eLo; eHi0 = eHi; eNN0 = eNN; }
+        // the partner lane's sheet (DPP quad_perm [1, 0, 3, 2])
+        const uint32_t mo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false);
+        const float no = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(n), 0xB1, 0xF, 0xF, false));
+        const uint32_t m0 = h ? mo : m, m1 = h ? m : mo;
+        const float n0 = h ? no : n, n1 = h ? n : no;
+        const float key = m0 ? (m1 ? fminf(n0, n1) : n0) : n1;
+        // n >= 0: truncating to the upper 16 bits rounds toward zero
+        const uint32_t eNN = (__float_as_uint(n0) >> 16) | (__float_as_uint(n1) & 0xffff0000u);
+        // bucket: 0 below 32 units, then one per octave up to 7
+        const int ex = (int)((__float_as_uint(key) >> 23) & 0xffu) - 127;
+        const uint32_t eTB = t | (((m0 | m1) && !h && j < count ? (uint32_t)min(max(ex - 4, 0), 7) : 8u) << 8);
+        if (ps) { eTB1 = eTB; eLo1 = m0; eHi1 = m1; eNN1 = eNN; }
+        else { eTB0 = eTB; eLo0 = m0; eHi0 = m1; eNN0 = eNN; }
     }
-    // 3. walk
+    // 3. walk, nearest bucket first; stops once no ray's t reaches the next
+    // bucket's lower edge (16 << bk units)
     mkRay(ray_o, ray_d);
     const bool upper = lane >= 32u;
     const uint32_t x = lane & 31u;
@@ -816,9 +842,9 @@ __device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uin
     const MP_LDS lf4 *vrot = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + tx.kz * b.rotStride;
     const float ro0 = comp(ray_o, kx0), ro1 = comp(ray_o, ky0), roz = comp(ray_o, tx.kz);
     const bool rsw = tx.kx != kx0;
-    const int nslots = count > ch + 64u ? 2 : 1;
     for (uint32_t bk = 0; bk < 8u; bk++) {
-        for (int sl = 0; sl < nslots; sl++) {
+        if (bk && __ballot(!(t_best < (float)(16u << bk))) == 0ull) break;
+        for (int sl = 0; sl < npass; sl++) {
             const uint32_t sTB = sl ? eTB1 : eTB0, sLo = sl ? eLo1 : eLo0, sHi = sl ? eHi1 : eHi0;
             const uint32_t sNN = sl ? eNN1 : eNN0;
             uint64_t m = __ballot((sTB >> 8) == bk);
@@ -844,7 +870,7 @@ __device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uin
             }
         }
     }
-    ch += 128u;
+    ch += 64u;
     } while (ch < count);
     t_out = t_best;
 }
@@ -1190,16 +1216,22 @@ __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, cons
 // current t_max is always accepted), so testing the hint first returns the
 // same answer; on a miss the full search runs and records its occluder.
 // numTris bounds the hint (any stale or foreign value is merely a miss).
-__device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restrict__ px,
-                                            const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
-                                            int N, mp::Vec3 org, mp::Vec3 d, int target,
-                                            uint16_t *occ = nullptr, uint32_t numTris = 0)
+// visibleRayD's two parts.  visibleQuickD: the decisions that need no
+// traversal -- true when the target capsule is missed (t_c == 0) or the
+// occluder hint is hit at t <= t_c (both mean "not visible"); otherwise t_c
+// is returned for visibleFullD, the BVH search and the capsule loop.  k_vis
+// runs the first part on every candidate ray and the second on the
+// unresolved ones only, compacted (the answer per ray is the same).
+__device__ __forceinline__ bool visibleQuickD(const LBVH &b, const float *__restrict__ px,
+                                              const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
+                                              mp::Vec3 org, mp::Vec3 d, int target, const uint16_t *occ,
+                                              uint32_t numTris, float &t_c)
 {
     using namespace mp;
     Vec3 ct = v3(px[g0 + target], py[g0 + target], pz[g0 + target]);
     ct.z += kCapsuleRadius;
-    const float t_c = intersectRayZOriginCapsule(org - ct, d, kCapsuleRadius, kCapsuleSegment);
-    if (t_c == 0) return false;
+    t_c = intersectRayZOriginCapsule(org - ct, d, kCapsuleRadius, kCapsuleSegment);
+    if (t_c == 0) return true;
     if (occ) {
         const uint32_t hint = *occ;
         if (hint < numTris) {
@@ -1208,9 +1240,18 @@ __device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restri
             Vec3 a, bb, c;
             loadTri(b, (int)hint, a, bb, c);
             float th;
-            if (rayTri(a, bb, c, tx, org, t_c * 1.001f, th) && th <= t_c) return false;
+            if (rayTri(a, bb, c, tx, org, t_c * 1.001f, th) && th <= t_c) return true;
         }
     }
+    return false;
+}
+
+__device__ __forceinline__ bool visibleFullD(const LBVH &b, const float *__restrict__ px,
+                                             const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
+                                             int N, mp::Vec3 org, mp::Vec3 d, int target, float t_c,
+                                             uint16_t *occ = nullptr)
+{
+    using namespace mp;
     float min_t = kFltMax;
     float tb;
     int occ_tri = -1;
@@ -1250,6 +1291,16 @@ __device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restri
         }
     }
     return ent == target;
+}
+
+__device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restrict__ px,
+                                            const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
+                                            int N, mp::Vec3 org, mp::Vec3 d, int target,
+                                            uint16_t *occ = nullptr, uint32_t numTris = 0)
+{
+    float t_c;
+    if (visibleQuickD(b, px, py, pz, g0, org, d, target, occ, numTris, t_c)) return false;
+    return visibleFullD(b, px, py, pz, g0, N, org, d, target, t_c, occ);
 }
 
 } // namespace mpenv

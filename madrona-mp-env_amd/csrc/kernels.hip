@@ -2573,10 +2573,14 @@ __device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &
 __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ uint16_t rays[kVisMaxRays]; // (lane << 2) | point
+    __shared__ uint16_t rays[kVisMaxRays];  // (lane << 2) | point
+    __shared__ uint16_t rays2[kVisMaxRays]; // phase B2: indices into rays
     __shared__ uint32_t masks[kBlock]; // per agent of the block (<= 4 waves x 64/T)
-    __shared__ uint32_t nrays;
-    if (threadIdx.x == 0) nrays = 0;
+    __shared__ uint32_t nrays, nrays2;
+    if (threadIdx.x == 0) {
+        nrays = 0;
+        nrays2 = 0;
+    }
     masks[threadIdx.x] = 0;
     const LBVH bvh = stageBVH(smem, sc); // barrier
     const int T = S.T, N = S.N;
@@ -2644,30 +2648,58 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
     }
     __syncthreads();
 
-    // ---- phase B: trace the compacted rays
+    // ---- phase B: the compacted rays.  B1 decides what needs no traversal
+    // (target capsule missed, occluder hint hit); the rest are compacted
+    // again so B2's traversals run in dense waves (a wave of mixed rays
+    // otherwise idles all but its few traversing lanes).
     const uint32_t total = nrays;
-    for (uint32_t r = threadIdx.x; r < total; r += kBlock) {
+    const uint32_t numTris = (uint32_t)(sc.numVerts / 3);
+    // the occluder hint stores triangle ids as u16 with 0xffff = none: off
+    // for scenes of 65,535 triangles or more
+    const bool hints = numTris < 0xffffu;
+    auto rayOf = [&](uint32_t r, int64_t &g, int &k, int &p, int64_t &g0, int &target, Vec3 &org, Vec3 &dir) {
         const uint32_t d = rays[r];
-        const int lane = (int)(d >> 2), p = (int)(d & 3);
+        const int lane = (int)(d >> 2);
+        p = (int)(d & 3);
         const int lwl = lane & 63;
-        const int64_t g = ((((int64_t)xcdBlockId() * blockDim.x + lane) >> 6) * apw) + lwl / T;
-        const int k = lwl % T;
+        g = ((((int64_t)xcdBlockId() * blockDim.x + lane) >> 6) * apw) + lwl / T;
+        k = lwl % T;
         const int w = (int)(g / N);
         const int i = (int)(g - (int64_t)w * N);
-        const int64_t g0 = (int64_t)w * N;
-        const int target = ((i / T) ^ 1) * T + k;
-        Vec3 org = ldPos(S, g);
+        g0 = (int64_t)w * N;
+        target = ((i / T) ^ 1) * T + k;
+        org = ldPos(S, g);
         org.z += viewHeightD(S.curPose[g]);
         const Quat aim_rot = ldAimRot(S, g);
         const Vec3 delta_right = rotateVec(aim_rot, kRight) * 0.9f * c::kAgentRadius;
         Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
         const float len = length(to_test);
-        to_test = to_test / len;
-        // the occluder hint (geom_dev.h visibleRayD) stores triangle ids as
-        // u16 with 0xffff = none: off for scenes of 65,535 triangles or more
-        uint16_t *occ = sc.numVerts / 3 < 0xffff ? S.visOcc + (g * T + k) * 4 + p : nullptr;
-        const bool seen = visibleRayD(bvh, S.px, S.py, S.pz, g0, N, org, to_test, target, occ,
-                                      (uint32_t)(sc.numVerts / 3));
+        dir = to_test / len;
+    };
+    for (uint32_t r = threadIdx.x; r < total; r += kBlock) {
+        int64_t g, g0;
+        int k, p, target;
+        Vec3 org, dir;
+        rayOf(r, g, k, p, g0, target, org, dir);
+        float t_c;
+        if (!visibleQuickD(bvh, S.px, S.py, S.pz, g0, org, dir, target,
+                           hints ? S.visOcc + (g * T + k) * 4 + p : nullptr, numTris, t_c))
+            rays2[atomicAdd(&nrays2, 1u)] = (uint16_t)r;
+    }
+    __syncthreads();
+    const uint32_t total2 = nrays2;
+    if (S.stats && threadIdx.x == 0) atomicAdd(S.stats + kStatLosTraced, (unsigned long long)total2);
+    for (uint32_t q = threadIdx.x; q < total2; q += kBlock) {
+        int64_t g, g0;
+        int k, p, target;
+        Vec3 org, dir;
+        rayOf(rays2[q], g, k, p, g0, target, org, dir);
+        // t_c again (the same bits as in B1)
+        Vec3 ct = v3(S.px[g0 + target], S.py[g0 + target], S.pz[g0 + target]);
+        ct.z += kCapsuleRadius;
+        const float t_c = intersectRayZOriginCapsule(org - ct, dir, kCapsuleRadius, kCapsuleSegment);
+        const bool seen = visibleFullD(bvh, S.px, S.py, S.pz, g0, N, org, dir, target, t_c,
+                                       hints ? S.visOcc + (g * T + k) * 4 + p : nullptr);
         if (seen) atomicOr(&masks[(int)(g - agent0)], 1u << k);
         if (S.stats) statAdd(S.stats + kStatLosSeen, seen ? 1u : 0u);
     }
@@ -3219,6 +3251,17 @@ enum { kLidarAll = 0, kLidarFan = 1, kLidarRear = 2 };
 
 __device__ __host__ __forceinline__ bool lidarFanScene(const SceneDev &sc) { return sc.numVerts / 3 <= 255; }
 
+// Maximum over the lane's DPP row (16 lanes) of non-negative float bit
+// patterns compared as signed ints (the float order; -0 sorts lowest): the
+// exact float maximum of the row's hit distances, without LDS round trips.
+__device__ __forceinline__ int rowMaxBits16(int v)
+{
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // quad_perm [1, 0, 3, 2]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));  // quad_perm [2, 3, 0, 1]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false)); // row_ror:4
+    return max(v, __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false)); // row_ror:8
+}
+
 template <int kMode>
 __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc, int iters, char *smem)
 {
@@ -3354,9 +3397,9 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             // once; the per-ray loop reads the survivors' bases from those
             // lanes (readlane) in ascending j, so ties resolve as before.
             float min_t = bhit ? tb : kFltMax;
-            float mx = min_t;
-#pragma unroll
-            for (int sh = 32; sh >= 1; sh >>= 1) mx = fmaxf(mx, shflLane(mx, lane ^ (uint32_t)sh));
+            const int rm = rowMaxBits16(__float_as_int(min_t));
+            const float mx = __int_as_float(max(max(__builtin_amdgcn_readlane(rm, 0), __builtin_amdgcn_readlane(rm, 16)),
+                                                max(__builtin_amdgcn_readlane(rm, 32), __builtin_amdgcn_readlane(rm, 48))));
             float cx = 0.f, cy = 0.f, cz = 0.f;
             bool keep = false;
             if (lane < N) {
@@ -3403,9 +3446,7 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             // group kept -- per ray the same capsules in the same order as
             // capsulesD minus those no ray of the group can reach.
             float min_t = bhit ? tb : kFltMax;
-            float mx = min_t;
-#pragma unroll
-            for (int sh = 8; sh >= 1; sh >>= 1) mx = fmaxf(mx, shflLane(mx, lane ^ (uint32_t)sh));
+            const float mx = __int_as_float(rowMaxBits16(__float_as_int(min_t)));
             const uint32_t gb = lane & 48u, jl = lane & 15u;
             float cx = 0.f, cy = 0.f, cz = 0.f;
             bool keep = false;

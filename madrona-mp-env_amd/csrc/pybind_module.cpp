@@ -264,13 +264,14 @@ PYBIND11_MODULE(madrona_mp_env, m)
         .def("enable_kernel_timing", [](PySimManager &s, bool on) { check(mpenv_enable_kernel_timing(s.h->mgr, on)); })
         .def("enable_stats", [](PySimManager &s, bool on) { check(mpenv_enable_stats(s.h->mgr, on)); })
         .def("read_stats", [](PySimManager &s) {
-            uint64_t v[9] = {};
-            int n = mpenv_read_stats(s.h->mgr, v, 9);
+            uint64_t v[10] = {};
+            int n = mpenv_read_stats(s.h->mgr, v, 10);
             if (n < 0) check(n);
-            static const char *names[9] = { "alive_agents", "los_pairs", "los_rays", "los_seen",
-                                            "sphere_casts", "shot_rays", "hit_agents", "kills", "lk_rows" };
+            static const char *names[10] = { "alive_agents", "los_pairs", "los_rays", "los_seen",
+                                             "sphere_casts", "shot_rays", "hit_agents", "kills", "lk_rows",
+                                             "los_traced" };
             py::dict d;
-            for (int k = 0; k < 9; k++) d[py::str(names[k])] = v[k];
+            for (int k = 0; k < 10; k++) d[py::str(names[k])] = v[k];
             return d;
         })
         .def("kernel_timings", [](PySimManager &s) {

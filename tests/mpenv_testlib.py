@@ -463,10 +463,10 @@ class Engine:
     def read_stats(self):
         """Workload counters (include/mpenv.h mpenv_read_stats)."""
         self.lib.mpenv_read_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
-        v = np.zeros(9, np.uint64)
-        assert self.lib.mpenv_read_stats(self.h, v.ctypes.data, 9) >= 0, self.lib.mpenv_last_error().decode()
+        v = np.zeros(10, np.uint64)
+        assert self.lib.mpenv_read_stats(self.h, v.ctypes.data, 10) >= 0, self.lib.mpenv_last_error().decode()
         names = ("alive_agents", "los_pairs", "los_rays", "los_seen", "sphere_casts", "shot_rays",
-                 "hit_agents", "kills", "lk_rows")
+                 "hit_agents", "kills", "lk_rows", "los_traced")
         return dict(zip(names, (int(x) for x in v)))
 
     def copy_actions(self, dev_ptr):

@@ -162,6 +162,6 @@ def test_product_kernels_carry_no_lab_switches_and_lab_patches_apply(tmp_path):
     for p in patches:
         work = tmp_path / p
         shutil.copytree(csrc, work)
-        r = subprocess.run(["patch", "-s", "-p1", "-d", str(work), "-i", os.path.join(lab, p)],
+        r = subprocess.run(["patch", "-p1", "-d", str(work), "-i", os.path.join(lab, p)],
                            capture_output=True, text=True)
         assert r.returncode == 0 and "fuzz" not in r.stdout, (p, r.stdout, r.stderr)

@@ -182,7 +182,7 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
         st = (C.c_uint64 * 64)()
         n = lib.mpenv_read_stats(h, st, 64)
         lib.mpenv_enable_stats(h, 0)
-        phases = [round(st[k] / ns / 1e6, 2) for k in range(9, n)]
+        phases = [round(st[k] / ns / 1e6, 2) for k in range(10, n)]
     timeline = None
     if hasattr(lib, "mpenv_lab_wave"):
         # lab_hooks.patch with -DMPENV_LAB_WAVE_HIST=k: per-wave start / end of one kernel in one
