@@ -3458,6 +3458,9 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             const uint64_t cm = __ballot(keep);
             uint32_t um = (uint32_t)((cm | (cm >> 16) | (cm >> 32) | (cm >> 48)) & 0xffffu);
             const uint32_t mine = (uint32_t)(cm >> gb) & 0xffffu;
+            // the four agents in one world (always for 6v6: 4 divides N):
+            // every group holds the same capsules, read from group 0's lanes
+            const bool oneWorld = __ballot(w != (uint32_t)__builtin_amdgcn_readfirstlane((int)w)) == 0ull;
             bool hit = bhit;
             int ent = -1;
             const float dxy2 = dir.x * dir.x + dir.y * dir.y;
@@ -3465,8 +3468,15 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
             while (um) {
                 const int j = __builtin_ctz(um);
                 um &= um - 1u;
-                const int src = (int)gb + j;
-                Vec3 co = v3(shflLane(cx, (uint32_t)src), shflLane(cy, (uint32_t)src), shflLane(cz, (uint32_t)src));
+                Vec3 co;
+                if (oneWorld) {
+                    co = v3(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), j)),
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), j)),
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), j)));
+                } else {
+                    const uint32_t src = gb + (uint32_t)j;
+                    co = v3(shflLane(cx, src), shflLane(cy, src), shflLane(cz, src));
+                }
                 if (!((mine >> j) & 1u)) continue;
                 co.z += kCapsuleRadius;
                 const Vec3 tr = ray_o - co;

@@ -244,18 +244,22 @@ def time_one(name, worlds=int(os.environ.get("LAB_WORLDS", 16384)), team=int(os.
         import numpy as np
 
         lib.mpenv_lab_fan.argtypes = [C.c_void_p, C.c_int32]
-        acc = np.zeros(10, np.float64)
-        fb = np.zeros(10, np.uint64)
+        acc = np.zeros(13, np.float64)
+        fb = np.zeros(13, np.uint64)
         for s in range(5):
             step(s)
             hip.hipDeviceSynchronize()
-            assert lib.mpenv_lab_fan(fb.ctypes.data, 10) == 0
+            assert lib.mpenv_lab_fan(fb.ctypes.data, 13) == 0
             acc += fb
         nt = max(acc[5], 1.0)
         fan = {k: round(float(acc[i]) / nt, 2) for i, k in enumerate(
             ("cyc_pre", "cyc_cull", "cyc_masks", "cyc_walk", "cyc_post", "tasks", "survivors", "entries_walked",
              "entries_tested", "lane_tests")) if i != 5}
         fan["tasks_per_step"] = nt / 5
+        nr = max(acc[12], 1.0)
+        fan["rear_cyc_trace"] = round(float(acc[10]) / nr, 2)
+        fan["rear_cyc_post"] = round(float(acc[11]) / nr, 2)
+        fan["rear_tasks_per_step"] = nr / 5
     print(json.dumps({"variant": label or name, "fan": fan, "work": work, "timeline": timeline, "ms_per_step": round(1e3 * el_groups / steps, 4), "phases_mcyc": phases,
                       "ms_per_step_1group": round(1e3 * el / steps, 4), "kernels_1group": res,
                       "digest": dig.hexdigest()[:16], "per_export": pex}), flush=True)

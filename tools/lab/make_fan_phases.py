@@ -25,9 +25,10 @@ def edit_geom(g):
 // lab overlay (tools/lab/fan_phases.patch): per-wave phase cycles and work
 // counts of the forward-fan tasks, summed over the wave's tasks in `lab`
 // (0 pre, 1 cull, 2 masks, 3 walk, 4 post, 5 tasks, 6 survivors, 7 entries
-// walked, 8 entries tested, 9 lane tests) and stored per wave at the end of
-// the kernel (no atomics: contention would stretch what is measured).
-constexpr int kLabFanWaves = 1 << 17, kLabFanK = 10;
+// walked, 8 entries tested, 9 lane tests; k_lidar_rear: 10 pre + traversal,
+// 11 post, 12 tasks) and stored per wave at the end of the kernel (no
+// atomics: contention would stretch what is measured).
+constexpr int kLabFanWaves = 1 << 17, kLabFanK = 13;
 static __device__ unsigned long long g_labFan[kLabFanWaves][kLabFanK];
 """, "kFanListCap")
     g = sub(g, r"(mp::Vec3 &ray_o, mp::Vec3 &ray_d, float &t_out)\)\n\{\n    using namespace mp;\n",
@@ -50,26 +51,30 @@ def edit_kernels(k):
                r"(    for \(int it = 0; it < iters; it\+\+\) \{\n)",
             r"\1    uint64_t lab[kLabFanK] = {};\n\2        const uint64_t lab_t0 = clock64();\n"
             r"        uint64_t lab_t2 = 0;\n", "lidar task loop")
-    k = sub(k, r"(        if \(task >= ntasks\) break;\n)", r"\1        if (kMode == kLidarFan) lab[5]++;\n",
-            "task bound")
+    k = sub(k, r"(        if \(task >= ntasks\) break;\n)",
+            r"\1        if (kMode == kLidarFan) lab[5]++;\n        if (kMode == kLidarRear) lab[12]++;\n", "task bound")
+    k = sub(k, r"(bhit = bvhTraceRayT<[^;]*;\n        \}\n)",
+            r"\1        if (kMode == kLidarRear) { lab_t2 = clock64(); lab[10] += lab_t2 - lab_t0; }\n", "rear trace")
     k = sub(k, r"(\n(\s*)fanTraceD\()", r"\n\2lab[0] += clock64() - lab_t0;\1", "fanTraceD call")
     k = sub(k, r"(ray_o, dir, tb)\);", r"\1, lab);", "fanTraceD args")
     k = sub(k, r"(bhit = __float_as_int\(tb\) != __float_as_int\(kFltMax\);\n)",
             r"\1            lab_t2 = clock64();\n", "after fanTraceD")
     k = sub(k, r"        if \(!valid\) continue;\n",
-            "        if (!valid) { if (kMode == kLidarFan) lab[4] += clock64() - lab_t2; continue; }\n", "valid")
+            "        if (!valid) { if (kMode != kLidarAll) lab[kMode == kLidarFan ? 4 : 11] += clock64() - lab_t2; "
+            "continue; }\n", "valid")
     k = sub(k, r"(        \*dst = out;\n)(    \}\n\})",
-            r"""\1        if (kMode == kLidarFan) lab[4] += clock64() - lab_t2;
+            r"""\1        if (kMode != kLidarAll) lab[kMode == kLidarFan ? 4 : 11] += clock64() - lab_t2;
     }
-    if (kMode == kLidarFan) {
+    if (kMode != kLidarAll) {
         const uint32_t gw = blockIdx.x * kLidarWaves + wave;
         if ((threadIdx.x & 63) == 0 && gw < (uint32_t)kLabFanWaves)
-            for (int q = 0; q < kLabFanK; q++) g_labFan[gw][q] = lab[q];
+            for (int q = kMode == kLidarFan ? 0 : 10; q < (kMode == kLidarFan ? 10 : kLabFanK); q++)
+                g_labFan[gw][q] = lab[q];
     }
 }""", "task end")
     k = sub(k, r"(static int check\(hipError_t e\) \{ return e == hipSuccess \? 0 : -1; \}\n)", r"""\1
-// lab overlay: the per-wave sums of the last k_lidar_fan launch, summed over
-// waves into out[0..9] (the per-wave slots are cleared)
+// lab overlay: the per-wave sums of the last k_lidar_fan / k_lidar_rear
+// launches, summed over waves into out[0..12] (the per-wave slots are cleared)
 extern "C" int mpenv_lab_fan(uint64_t *out, int32_t n)
 {
     static unsigned long long h[kLabFanWaves][kLabFanK];
