@@ -82,14 +82,16 @@ def test_every_world_of_the_bench_window_matches_oracle(ts, W, warmup, steps, ev
 
 
 COMBAT = [
-    # team_size, worlds, steps, compare every
-    (6, 16384, 120, 20),   # C3
-    (3, 4096, 300, 25),    # C2
+    # team_size, worlds, steps, compare every, kills required (C3's teams
+    # first meet near the zone: 120 steps see ~25 agents hit and no kill
+    # yet; C2's 300 steps ~700 kills)
+    (6, 16384, 120, 20, False),   # C3
+    (3, 4096, 300, 25, True),     # C2
 ]
 
 
-@pytest.mark.parametrize("ts,W,steps,every", COMBAT, ids=["C3_6v6x16384", "C2_3v3x4096"])
-def test_every_world_in_the_combat_regime_matches_oracle(ts, W, steps, every):
+@pytest.mark.parametrize("ts,W,steps,every,need_kills", COMBAT, ids=["C3_6v6x16384", "C2_3v3x4096"])
+def test_every_world_in_the_combat_regime_matches_oracle(ts, W, steps, every, need_kills):
     """bench.py --actions combat, world by world: every step the device
     aim-bot (mpenv_combat_actions mode 1: fire at the first visible
     opponent, else turn and run toward the zone, reload an empty magazine)
@@ -142,7 +144,9 @@ def test_every_world_in_the_combat_regime_matches_oracle(ts, W, steps, every):
     print(f"\n{ts}v{ts} x {W} combat: {steps} steps, every world compared ({len(ALL)} exports every {every} "
           f"steps); {st['shot_rays']} shots, {st['hit_agents']} agents hit, {st['kills']} kills; oracle "
           f"{t_oracle:.1f} s on {threads} threads, test {time.time() - t_start:.1f} s")
-    assert st["kills"] > 0 and st["hit_agents"] > 0
+    assert st["hit_agents"] > 0 and st["shot_rays"] > 0
+    if need_kills:
+        assert st["kills"] > 0
     e.close()
     o.close()
 
