@@ -221,14 +221,6 @@ struct SceneDev {
     // |e12|^2, 0 -- computed on the host with the same mpenv_core.h
     // expressions the traversal would evaluate (bit-identical).
     const float *triPre;
-    // Per triangle, k_lidar's fan-list cull data (manager.cpp): unit normal
-    // of (b - a) x (c - a), its plane offset, bounding-sphere centre and
-    // radius (8 floats).
-    const float *triAux;
-    // k_lidar's forward fans through the candidate lists (k_lidar_fan) when
-    // the scene allows (<= 255 triangles); 0: through the BVH (k_lidar).
-    // MPENV_LIDAR_FAN=0 at creation; the same answer either way.
-    int32_t lidarFan;
     int32_t numNodes;
     int32_t numVerts;
     mp::AABB worldBounds;

@@ -28,7 +28,7 @@ struct LBVH {
     const MP_LDS float *pre; // sphere-casting kernels only (stageBVHSphere)
     const MP_LDS float *snodes; // sphere-cast node image (stageBVHSphere), else null
     unsigned long long *stats;  // workload counters (DevState::stats), null = off
-    int32_t rotStride;          // stageBVHOct / stageBVHRot: float4s per rotated vertex copy
+    int32_t rotStride;          // stageBVHOct: float4s per rotated vertex copy
 };
 
 // Workload counter add, one atomic per wave: the active lanes' values
@@ -173,47 +173,15 @@ __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
         dst_n[(k >> 2) * kOctNodeQ + (k & 3)] = src_n[k];
     const float *src_v = sc.verts;
     float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
-    // The .w slots carry the fan-list cull data (SceneDev::triAux) of
-    // triangle t = v / 3, vertex slot i = v % 3: copy 2 (x, y, z) the unit
-    // normal's component i; copy 0 the plane offset, the bounding radius, the
-    // centre's x; copy 1 the centre's y and z (fanTraceD).
     for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
         const int r = k / sc.numVerts, v = k - r * sc.numVerts;
         const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
-        const int t = v / 3, i = v - 3 * t;
-        const int ai = r == 2 ? i : r == 0 ? (i == 0 ? 3 : i == 1 ? 7 : 4) : (i == 0 ? 5 : i == 1 ? 6 : -1);
-        dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r],
-                               ai >= 0 ? sc.triAux[8 * t + ai] : 0.f);
+        dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r], 0.f);
     }
     __syncthreads();
     LBVH b;
     b.nodes = (const MP_LDS BVHNode *)(smem);
     b.verts = (const MP_LDS float *)(smem + (size_t)node_q * 16);
-    b.pre = nullptr;
-    b.snodes = nullptr;
-    b.stats = nullptr;
-    b.rotStride = sc.numVerts;
-    return b;
-}
-
-// k_lidar_fan's LDS image: the three rotated vertex copies only (with the
-// fan-list cull data in their .w slots, stageBVHOct), no node images.
-__device__ __forceinline__ LBVH stageBVHRot(char *smem, const SceneDev &sc)
-{
-    float4 *dst_v = reinterpret_cast<float4 *>(smem);
-    const float *src_v = sc.verts;
-    for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
-        const int r = k / sc.numVerts, v = k - r * sc.numVerts;
-        const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
-        const int t = v / 3, i = v - 3 * t;
-        const int ai = r == 2 ? i : r == 0 ? (i == 0 ? 3 : i == 1 ? 7 : 4) : (i == 0 ? 5 : i == 1 ? 6 : -1);
-        dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r],
-                               ai >= 0 ? sc.triAux[8 * t + ai] : 0.f);
-    }
-    __syncthreads();
-    LBVH b;
-    b.nodes = nullptr;
-    b.verts = (const MP_LDS float *)(smem);
     b.pre = nullptr;
     b.snodes = nullptr;
     b.stats = nullptr;
@@ -401,25 +369,7 @@ __device__ __forceinline__ bool rayTriRot(const MP_LDS lf4 *p, float o0, float o
 // kExit: stop as soon as a hit at t <= exit_at is found (t_out is then
 // that hit, not necessarily the closest; callers that only compare the
 // closest hit with exit_at get the same answer).
-// kLex (lidar, DESIGN.md §2 definition 12): the order-independent closest
-// hit -- the smallest t = fl(T * fl(1 / det)) over every triangle the ray
-// hits.  Boxes and triangles are tested against t_best * (1 + 2^-20)
-// (kLexRelax), which keeps every triangle whose t ties or beats t_best:
-// t <= t_best implies T <= fl(fl(t_best * kLexRelax) * det) for the two
-// roundings of t, and such a triangle's box is entered below that bound.
-// Hits at t = -0 and +0 (an origin on a vertex or edge) are ordered -0
-// first: lexLessD compares bit patterns as signed integers, the total order
-// of {-0} and [+0, inf].  Boxes are entered when t_near <= t_far + |t_far| *
-// 2^-16 + 2^-8: a child box quantised at its node's boundary has no margin,
-// and a ray aimed exactly at such a vertex can miss it by slab rounding while
-// hitting the triangle; with the slack the traversal visits every triangle a
-// brute-force loop would find nearer than the bound (the oracle applies the
-// same rule; tests/test_lidar_order.py checks it against brute force).
-constexpr float kLexRelax = 1.00000095367431640625f; // 1 + 2^-20
-constexpr float kBoxSlackRel = 1.52587890625e-5f, kBoxSlackAbs = 0.00390625f;
-__device__ __forceinline__ bool lexLessD(float a, float b) { return __float_as_int(a) < __float_as_int(b); }
-
-template <bool kExit, int kNodeQ = 4, bool kRot = false, bool kOctImage = false, bool kLex = false>
+template <bool kExit, int kNodeQ = 4, bool kRot = false, bool kOctImage = false>
 __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
                                              float t_max0, float exit_at, int *exit_tri = nullptr)
 {
@@ -451,8 +401,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
         rsw = tx.kx != kx0;
     }
 
-    float t_max = kLex ? t_max0 * kLexRelax : t_max0; // kLex: the relaxed bound of t_best
-    float t_best = t_max0;
+    float t_max = t_max0;
     bool ray_hit = false;
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
@@ -493,7 +442,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
             float t_far;
             asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
                 : "=&v"(t_far) : "v"(t_far_x), "v"(t_far_y), "v"(t_far_z), "v"(t_max));
-            if (t_near <= (kLex ? fmaf(fabsf(t_far), kBoxSlackRel, t_far + kBoxSlackAbs) : t_far)) {
+            if (t_near <= t_far) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;
                     const int ntri = (int)((node.triSize >> (8 * i)) & 0xffu);
@@ -515,22 +464,12 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
                             loadTri(b, leaf + k, a, bb, c);
                             h = rayTri(a, bb, c, tx, ray_o, leaf_tmax, hit_t);
                         }
-                        if constexpr (kLex) {
-                            if (h && lexLessD(hit_t, t_best)) {
-                                t_best = hit_t;
-                                t_max = t_best * kLexRelax;
-                                leaf_tmax = t_max;
-                                ray_hit = true;
-                            }
-                            continue;
-                        }
                         if (h) {
                             hit_tri = true;
                             leaf_tmax = hit_t;
                             if constexpr (kExit) hit_k = k;
                         }
                     }
-                    if (kLex) continue;
                     if (hit_tri) {
                         ray_hit = true;
                         t_max = hit_t;
@@ -548,7 +487,7 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
             }
         }
     }
-    t_out = kLex ? t_best : t_max;
+    t_out = t_max;
     return ray_hit;
 }
 
@@ -567,312 +506,6 @@ __device__ __forceinline__ void waveSync()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// ------------------------------------------------------------ fan lists
-// k_lidar's forward fans without the BVH (tools/trav_stats.cpp
-// TRAV_FAN model).  A forward wave traces one agent's 64 rays: two sheets
-// (lanes 0-31 / 32-63) of 32 rays from one origin each, every ray of a sheet
-// in the plane through that origin spanned by the aim frame's right R and
-// forward F axes (normal N = R x F).  The closest hit under the lidar's
-// smallest-t rule (bvhTraceRayT kLex) is found from a per-wave candidate list:
-//   1. cull (lane = triangle, 4 rounds over <= 255 triangles): the sheet
-//      origin on the front side of the triangle's plane (rayTri accepts
-//      hits from the +n side of (b - a) x (c - a) only) and some vertex
-//      within kFanBand of the sheet plane band; survivors' ids + sheet bits
-//      go to an LDS list (ballot + mbcnt);
-//   2. masks (lane = survivor): per sheet, the triangle's strip inside the
-//      band |N.(p - O)| <= kFanBand is a quadrilateral between the two
-//      edges that cross the plane; its angular span seen from the origin,
-//      widened by kFanDelta, gives the sheet's candidate rays (a fan slot
-//      mask); strips near the origin, wrapping past pi, with a vertex inside
-//      the band or nearly parallel to the sheet (sin < kFanSinMin) take all
-//      32 rays.  Lower bound of any hit's t: the larger of the distance to
-//      the triangle's plane and to its bounding sphere;
-//   3. walk (lane = ray): entries in 8 log2 buckets of their bound; an entry
-//      runs the watertight test on the lanes in its mask whose current t is
-//      not below the bound, with the relaxed kLex acceptance.
-// Every cull is conservative (a ray of a sheet stays within 1e-7 t of the
-// plane, far inside the band; hit points lie in the strip; the float
-// rounding of angles and bounds is far below kFanDelta and the bound's
-// margin), so the result equals the smallest t over all triangles -- the
-// value the BVH path (and the oracle) computes.
-constexpr float kFanBand = 0.05f, kFanTol = 0.05f, kFanDelta = 2e-3f, kFanSinMin = 0.1f;
-constexpr float kFanNearR2 = 16.f; // strip points nearer than 4 units: every ray
-constexpr int kFanListCap = 256;   // u16 list entries per wave (triangle id | sheet bits << 8)
-
-// atan2 to ~1e-5 rad (minimax atan on [0, 1]); cull use only
-__device__ __forceinline__ float fanAtan2(float y, float x)
-{
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float a = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
-    const float q = a * a;
-    float r = fmaf(fmaf(fmaf(fmaf(fmaf(-0.01172120f, q, 0.05265332f), q, -0.11643287f), q, 0.19354346f), q,
-                        -0.33262347f), q, 0.99997726f) * a;
-    if (ay > ax) r = 1.57079637f - r;
-    if (x < 0.f) r = 3.14159274f - r;
-    return y < 0.f ? -r : r;
-}
-
-// Fan slots x (theta_x = 0.75 pi x / 31 + pi / 8, sim.cpp:3324-3506) with
-// theta_x in [a, b], for a > -pi - 1 and b < a + pi + 1: the fan's range
-// [pi/8, 7pi/8] shifted by -2 pi ends below -pi - 1 and shifted by +2 pi
-// starts above 2 pi + 1 -- neither copy can meet such an interval.
-__device__ __forceinline__ uint32_t fanSlotMask(float a, float b)
-{
-    constexpr float kOff = 0.392699082f, kInvStep = 31.f / 2.35619449f;
-    const float lo = fmaxf(ceilf((a - kOff) * kInvStep), 0.f);
-    const float hi = fminf(floorf((b - kOff) * kInvStep), 31.f);
-    if (!(lo <= hi)) return 0u;
-    const uint32_t l = (uint32_t)lo, h = (uint32_t)hi;
-    return (h == 31u ? 0xffffffffu : ((2u << h) - 1u)) & ~((1u << l) - 1u);
-}
-
-// The plane distance below which a strip may surround the origin: a strip
-// point p projecting onto the origin lies within kFanBand of it, so |sf| <=
-// kFanBand; above kFanNearPlane the projected quad misses the origin by more
-// than sqrt(kFanNearPlane^2 - kFanBand^2) ~ 0.5 units, lies inside an open
-// half-plane seen from it, and the cross-product order of its corners is a
-// total order (rounding flips it only for corners within ~1e-6 rad of
-// opposite, i.e. a quad passing within ~1e-6 |p| of the origin).
-constexpr float kFanNearPlane = 0.5f;
-
-// One sheet's candidate mask for a survivor: sv / uv / wv = N.v, R.v, F.v of
-// the three vertices, c = N.O, (uO, wO) = (R.O, F.O), sfAbs = the origin's
-// distance to the triangle's plane.
-__device__ __forceinline__ uint32_t fanSheetMaskD(const float sv[3], const float uv[3], const float wv[3], float c,
-                                                  float uO, float wO, float sinT, float sfAbs)
-{
-    const float s0 = sv[0] - c, s1 = sv[1] - c, s2 = sv[2] - c;
-    const bool p0 = s0 > 0.f, p1 = s1 > 0.f, p2 = s2 > 0.f;
-    if (sinT < kFanSinMin || sfAbs <= kFanNearPlane || fabsf(s0) <= kFanBand || fabsf(s1) <= kFanBand ||
-        fabsf(s2) <= kFanBand || (p0 == p1 && p1 == p2))
-        return 0xffffffffu;
-    // the lone vertex (on its own side of the plane) and the other two
-    const int L = p0 == p1 ? 2 : (p0 == p2 ? 1 : 0);
-    const int A = L == 2 ? 0 : L + 1, B = L == 0 ? 2 : (L == 1 ? 0 : 1);
-    auto pick = [](const float v[3], int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); };
-    const float sl = pick(sv, L) - c, ul = pick(uv, L) - uO, wl = pick(wv, L) - wO;
-    float pu[4], pw[4];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-        const int o = e ? B : A;
-        const float so = pick(sv, o) - c, uo = pick(uv, o) - uO, wo = pick(wv, o) - wO;
-        // |sl - so| > 2 kFanBand: the 1-ulp reciprocal moves a corner by
-        // ~1e-7 of the edge, far inside kFanDelta at >= 4 units
-        const float inv = __builtin_amdgcn_rcpf(sl - so);
-#pragma unroll
-        for (int bi = 0; bi < 2; bi++) {
-            const float a = (sl - (bi ? -kFanBand : kFanBand)) * inv; // in (0, 1)
-            pu[2 * e + bi] = fmaf(a, uo - ul, ul);
-            pw[2 * e + bi] = fmaf(a, wo - wl, wl);
-        }
-    }
-    // angular extremes of the quad seen from the origin, by cross products
-    // (a total order inside the half-plane, see kFanNearPlane)
-    bool full = false;
-    float lu = pu[0], lw = pw[0], hu = pu[0], hw = pw[0];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        full = full || fmaf(pu[k], pu[k], pw[k] * pw[k]) < kFanNearR2;
-        // angle phi = atan2(w, -u): q is counter-clockwise of p iff
-        // cross((-u_p, w_p), (-u_q, w_q)) = u_q w_p - u_p w_q > 0
-        if (k) {
-            if (fmaf(pu[k], lw, -(lu * pw[k])) < 0.f) { lu = pu[k]; lw = pw[k]; }
-            if (fmaf(pu[k], hw, -(hu * pw[k])) > 0.f) { hu = pu[k]; hw = pw[k]; }
-        }
-    }
-    if (full) return 0xffffffffu;
-    const float a0 = fanAtan2(lw, -lu);
-    float a1 = fanAtan2(hw, -hu);
-    if (a1 < a0) a1 += 6.28318548f;
-    if (a1 - a0 >= 3.13159274f) return 0xffffffffu;
-    return fanSlotMask(a0 - kFanDelta, a1 + kFanDelta);
-}
-
-// Lower bound of the distance from o to triangle t (aux: plane offset and
-// bounding sphere from the .w slots), with a margin for rounding.
-__device__ __forceinline__ float fanNearD(float sf, float cx, float cy, float cz, float rad, float ox, float oy,
-                                          float oz)
-{
-    const float dx = ox - cx, dy = oy - cy, dz = oz - cz;
-    const float cd = __builtin_amdgcn_sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz))) - rad; // 1 ulp
-    return fmaxf(0.f, fmaf(fmaxf(fabsf(sf), cd), 0.99999f, -0.05f));
-}
-
-// The fan's wedge in the sheet plane, widened: directions at angles
-// [pi/8 - 0.01, 7pi/8 + 0.01] (cos / sin of the lower edge; the upper edge is
-// its mirror image).  A triangle whose three vertices all lie more than
-// kFanWedgeTol outside one edge line cannot hold a hit of the sheet (a hit
-// point lies on a ray of the sheet, inside the wedge, and the projected
-// triangle is the hull of its projected vertices).
-constexpr float kFanWedgeC = 0.92766011f, kFanWedgeS = 0.37342566f, kFanWedgeTol = 0.01f;
-
-// mkRay(o, d): the lane's ray, formed only once the walk starts (so it is not
-// live across the cull); returned in ray_o / ray_d.
-template <class MkRay>
-__device__ __forceinline__ void fanTraceD(const LBVH &b, int numTris, MP_LDS uint16_t *list, float ox, float oy,
-                                          float z0, float z1, mp::Vec3 R, mp::Vec3 F, MkRay mkRay,
-                                          mp::Vec3 &ray_o, mp::Vec3 &ray_d, float &t_out)
-{
-    using namespace mp;
-    uint32_t lane;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    // the frame is wave-uniform: keep it in SGPRs (readfirstlane), not in
-    // 20-odd VGPRs that would hold the same value in every lane
-    auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-    auto uni3 = [&](Vec3 v) { return v3(uni(v.x), uni(v.y), uni(v.z)); };
-    ox = uni(ox); oy = uni(oy); z0 = uni(z0); z1 = uni(z1);
-    R = uni3(R); F = uni3(F);
-    const Vec3 N = uni3(cross(R, F));
-    const float dz = uni(z1 - z0);
-    const float c0 = uni(fmaf(N.x, ox, fmaf(N.y, oy, N.z * z0))), c1 = uni(fmaf(N.z, dz, c0));
-    // wedge edge normals (G1: inside where G1.(p - O) >= 0; G2 likewise)
-    const Vec3 G1 = uni3(v3(fmaf(kFanWedgeC, F.x, kFanWedgeS * R.x), fmaf(kFanWedgeC, F.y, kFanWedgeS * R.y),
-                            fmaf(kFanWedgeC, F.z, kFanWedgeS * R.z)));
-    const Vec3 G2 = uni3(v3(fmaf(kFanWedgeC, F.x, -kFanWedgeS * R.x), fmaf(kFanWedgeC, F.y, -kFanWedgeS * R.y),
-                            fmaf(kFanWedgeC, F.z, -kFanWedgeS * R.z)));
-    const float k10 = uni(fmaf(G1.x, ox, fmaf(G1.y, oy, G1.z * z0)) - kFanWedgeTol);
-    const float k20 = uni(fmaf(G2.x, ox, fmaf(G2.y, oy, G2.z * z0)) - kFanWedgeTol);
-    const float k11 = uni(fmaf(G1.z, dz, k10)), k21 = uni(fmaf(G2.z, dz, k20));
-    const MP_LDS lf4 *vp = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + 2 * b.rotStride; // (x, y, z, n_i)
-    const MP_LDS lf4 *v0 = reinterpret_cast<const MP_LDS lf4 *>(b.verts);                  // .w: d, r, cx
-    const MP_LDS lf4 *v1 = v0 + b.rotStride;                                                // .w: cy, cz
-    // 1. cull
-    uint32_t count = 0;
-#pragma unroll 1
-    for (int base = 0; base < numTris; base += 64) {
-        const int t = base + (int)lane;
-        uint32_t fl = 0;
-        if (t < numTris) {
-            const lf4 A = vp[3 * t], B = vp[3 * t + 1], C = vp[3 * t + 2];
-            const float dT = v0[3 * t].w;
-            const float sf0 = fmaf(A.w, ox, fmaf(B.w, oy, fmaf(C.w, z0, -dT)));
-            const float sf1 = fmaf(C.w, dz, sf0);
-            const float sa = fmaf(N.x, A.x, fmaf(N.y, A.y, N.z * A.z));
-            const float sb = fmaf(N.x, B.x, fmaf(N.y, B.y, N.z * B.z));
-            const float sc = fmaf(N.x, C.x, fmaf(N.y, C.y, N.z * C.z));
-            const float smin = fminf(sa, fminf(sb, sc)), smax = fmaxf(sa, fmaxf(sb, sc));
-            const float g1 = fmaxf(fmaf(G1.x, A.x, fmaf(G1.y, A.y, G1.z * A.z)),
-                                   fmaxf(fmaf(G1.x, B.x, fmaf(G1.y, B.y, G1.z * B.z)),
-                                         fmaf(G1.x, C.x, fmaf(G1.y, C.y, G1.z * C.z))));
-            const float g2 = fmaxf(fmaf(G2.x, A.x, fmaf(G2.y, A.y, G2.z * A.z)),
-                                   fmaxf(fmaf(G2.x, B.x, fmaf(G2.y, B.y, G2.z * B.z)),
-                                         fmaf(G2.x, C.x, fmaf(G2.y, C.y, G2.z * C.z))));
-            if (sf0 >= -kFanTol && smin <= c0 + kFanBand && smax >= c0 - kFanBand && g1 >= k10 && g2 >= k20)
-                fl |= 1u;
-            if (sf1 >= -kFanTol && smin <= c1 + kFanBand && smax >= c1 - kFanBand && g1 >= k11 && g2 >= k21)
-                fl |= 2u;
-        }
-        const uint64_t m = __ballot(fl != 0u);
-        if (fl) {
-            const uint32_t pos = count + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (pos < (uint32_t)kFanListCap) list[pos] = (uint16_t)(t | (fl << 8));
-        }
-        count += (uint32_t)__popcll(m);
-    }
-    waveSync();
-    const Vec3 oh0 = v3(ox, oy, z0);
-    const float uO0 = uni(dot(R, oh0)), wO0 = uni(dot(F, oh0));
-    const float uO1 = uni(fmaf(R.z, dz, uO0)), wO1 = uni(fmaf(F.z, dz, wO0));
-    float t_best = kFltMax, t_relax = kFltMax * kLexRelax;
-    const uint32_t h = lane & 1u; // phase 2: the lane's sheet
-    // Phases 2-3 per chunk of 64 survivors (one chunk but for rare wide
-    // views; the smallest-t result does not depend on the walk order).
-    uint32_t ch = 0;
-    do {
-    // 2. masks: lane pair (2k, 2k + 1) takes survivor ch + 32 p + k in pass
-    // p, one sheet per lane, then the even lane holds the entry: triangle |
-    // bucket << 8 (bucket 8: none), the two sheet masks, the two bounds as
-    // bf16 rounded down (still bounds)
-    uint32_t eTB0 = 8u << 8, eLo0 = 0u, eHi0 = 0u, eNN0 = 0u;
-    uint32_t eTB1 = 8u << 8, eLo1 = 0u, eHi1 = 0u, eNN1 = 0u;
-    const int npass = count > ch + 32u ? 2 : 1;
-#pragma unroll 1
-    for (int ps = 0; ps < npass; ps++) {
-        const uint32_t j = ch + (uint32_t)ps * 32u + (lane >> 1);
-        uint32_t m = 0u, t = 0u;
-        float n = 0.f;
-        if (j < count) {
-            const uint32_t e = list[j];
-            t = e & 0xffu;
-            if ((e >> (8u + h)) & 1u) {
-                const lf4 A = vp[3 * t], B = vp[3 * t + 1], C = vp[3 * t + 2];
-                const float sv[3] = { fmaf(N.x, A.x, fmaf(N.y, A.y, N.z * A.z)),
-                                      fmaf(N.x, B.x, fmaf(N.y, B.y, N.z * B.z)),
-                                      fmaf(N.x, C.x, fmaf(N.y, C.y, N.z * C.z)) };
-                const float uv[3] = { fmaf(R.x, A.x, fmaf(R.y, A.y, R.z * A.z)),
-                                      fmaf(R.x, B.x, fmaf(R.y, B.y, R.z * B.z)),
-                                      fmaf(R.x, C.x, fmaf(R.y, C.y, R.z * C.z)) };
-                const float wv[3] = { fmaf(F.x, A.x, fmaf(F.y, A.y, F.z * A.z)),
-                                      fmaf(F.x, B.x, fmaf(F.y, B.y, F.z * B.z)),
-                                      fmaf(F.x, C.x, fmaf(F.y, C.y, F.z * C.z)) };
-                const float cosT = fabsf(fmaf(A.w, N.x, fmaf(B.w, N.y, C.w * N.z)));
-                const float sinT = __builtin_amdgcn_sqrtf(fmaxf(0.f, fmaf(-cosT, cosT, 1.f)));
-                const float oz = h ? z1 : z0;
-                const float sf = fmaf(A.w, ox, fmaf(B.w, oy, fmaf(C.w, oz, -v0[3 * t].w)));
-                m = fanSheetMaskD(sv, uv, wv, h ? c1 : c0, h ? uO1 : uO0, h ? wO1 : wO0, sinT, fabsf(sf));
-                n = fanNearD(sf, v0[3 * t + 2].w, v1[3 * t].w, v1[3 * t + 1].w, v0[3 * t + 1].w, ox, oy, oz);
-            }
-        }
-        // the partner lane's sheet (DPP quad_perm [1, 0, 3, 2])
-        const uint32_t mo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false);
-        const float no = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(n), 0xB1, 0xF, 0xF, false));
-        const uint32_t m0 = h ? mo : m, m1 = h ? m : mo;
-        const float n0 = h ? no : n, n1 = h ? n : no;
-        const float key = m0 ? (m1 ? fminf(n0, n1) : n0) : n1;
-        // n >= 0: truncating to the upper 16 bits rounds toward zero
-        const uint32_t eNN = (__float_as_uint(n0) >> 16) | (__float_as_uint(n1) & 0xffff0000u);
-        // bucket: 0 below 32 units, then one per octave up to 7
-        const int ex = (int)((__float_as_uint(key) >> 23) & 0xffu) - 127;
-        const uint32_t eTB = t | (((m0 | m1) && !h && j < count ? (uint32_t)min(max(ex - 4, 0), 7) : 8u) << 8);
-        if (ps) { eTB1 = eTB; eLo1 = m0; eHi1 = m1; eNN1 = eNN; }
-        else { eTB0 = eTB; eLo0 = m0; eHi0 = m1; eNN0 = eNN; }
-    }
-    // 3. walk, nearest bucket first; stops once no ray's t reaches the next
-    // bucket's lower edge (16 << bk units)
-    mkRay(ray_o, ray_d);
-    const bool upper = lane >= 32u;
-    const uint32_t x = lane & 31u;
-    const Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
-    const RayTxfmD tx = rayTxfm(ray_d, inv_d);
-    const int kx0 = tx.kz == 2 ? 0 : tx.kz + 1, ky0 = kx0 == 2 ? 0 : kx0 + 1;
-    const MP_LDS lf4 *vrot = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + tx.kz * b.rotStride;
-    const float ro0 = comp(ray_o, kx0), ro1 = comp(ray_o, ky0), roz = comp(ray_o, tx.kz);
-    const bool rsw = tx.kx != kx0;
-    for (uint32_t bk = 0; bk < 8u; bk++) {
-        if (bk && __ballot(!(t_best < (float)(16u << bk))) == 0ull) break;
-        for (int sl = 0; sl < npass; sl++) {
-            const uint32_t sTB = sl ? eTB1 : eTB0, sLo = sl ? eLo1 : eLo0, sHi = sl ? eHi1 : eHi0;
-            const uint32_t sNN = sl ? eNN1 : eNN0;
-            uint64_t m = __ballot((sTB >> 8) == bk);
-            while (m) {
-                const int j = __builtin_ctzll(m);
-                m &= m - 1ull;
-                // entry j's fields (wave-uniform), then this lane's sheet half
-                const int tri = __builtin_amdgcn_readlane((int)sTB, j) & 0xff;
-                const uint32_t mLo = (uint32_t)__builtin_amdgcn_readlane((int)sLo, j);
-                const uint32_t mHi = (uint32_t)__builtin_amdgcn_readlane((int)sHi, j);
-                const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)sNN, j);
-                const uint32_t mm = upper ? mHi : mLo;
-                const float nb = __uint_as_float(upper ? (nn & 0xffff0000u) : (nn << 16));
-                const bool act = ((mm >> x) & 1u) && !(t_best < nb);
-                if (__ballot(act) == 0ull) continue;
-                if (act) {
-                    float th;
-                    if (rayTriRot(vrot + tri * 3, ro0, ro1, roz, rsw, tx, t_relax, th) && lexLessD(th, t_best)) {
-                        t_best = th;
-                        t_relax = th * kLexRelax;
-                    }
-                }
-            }
-        }
-    }
-    ch += 64u;
-    } while (ch < count);
-    t_out = t_best;
 }
 
 // Out-of-line traversal for the ray-query test hook.

@@ -3238,19 +3238,6 @@ __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A +
 // loop): latency-bound LDS traversal gains more from occupancy (-7%).
 #define MP_LIDAR_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 
-// Lidar task sets: kLidarAll -- every task (5 per 4-agent unit: 4 forward
-// fans, then the unit's rear fans) through the BVH; kLidarFan -- the
-// forward fans only, through per-wave candidate lists (geom_dev.h
-// fanTraceD; task = unit * 4 + agent); kLidarRear -- the rear fans only,
-// through the BVH (task = unit).  Scenes of up to 255 triangles run
-// k_lidar_fan + k_lidar_rear, larger ones k_lidar.  Separate kernels give
-// the two traversals their own register allocation: together, the BVH
-// loop carried the candidate walk's live values (86 VGPRs, spills at the
-// 64 that 8 waves per SIMD need).
-enum { kLidarAll = 0, kLidarFan = 1, kLidarRear = 2 };
-
-__device__ __host__ __forceinline__ bool lidarFanScene(const SceneDev &sc) { return sc.numVerts / 3 <= 255; }
-
 // Maximum over the lane's DPP row (16 lanes) of non-negative float bit
 // patterns compared as signed ints (the float order; -0 sorts lowest): the
 // exact float maximum of the row's hit distances, without LDS round trips.
@@ -3262,9 +3249,9 @@ __device__ __forceinline__ int rowMaxBits16(int v)
     return max(v, __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false)); // row_ror:8
 }
 
-template <int kMode>
-__device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc, int iters, char *smem)
+__global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S, SceneDev sc, int iters)
 {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     // Ray-fan directions (sim.cpp:3324-3506): theta depends only on the ray
     // slot, so the 32 forward + 8 rear (-cos, sin) pairs are computed once
     // per workgroup with the same sinf_/cosf_ and read from LDS.
@@ -3278,31 +3265,15 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
         const float theta = range * (float(x) / float(width - 1)) + offset;
         fan[threadIdx.x] = make_float2(-cosf_(theta), sinf_(theta));
     }
-    // k_lidar_fan: the rotated vertex copies with the cull data, then the
-    // per-wave candidate lists; the others: octant node images + copies
-    const LBVH bvh = kMode == kLidarFan ? stageBVHRot(smem, sc) : stageBVHOct(smem, sc); // ends with __syncthreads
-    const int numTris = sc.numVerts / 3;
-    MP_LDS uint16_t *fanList = reinterpret_cast<MP_LDS uint16_t *>(
-        reinterpret_cast<MP_LDS char *>(const_cast<MP_LDS float *>(bvh.verts)) + (size_t)sc.numVerts * 16 * 3);
+    const LBVH bvh = stageBVHOct(smem, sc); // ends with __syncthreads
     const uint32_t N = (uint32_t)S.N, T = (uint32_t)S.T;
     const uint32_t A = (uint32_t)S.A;
-    const uint32_t units = (A + 3u) / 4u;
-    const uint32_t ntasks = kMode == kLidarAll ? (uint32_t)lidarTasks(S.A) : kMode == kLidarFan ? units * 4u : units;
+    const uint32_t ntasks = (uint32_t)lidarTasks(S.A);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int it = 0; it < iters; it++) {
         const uint32_t task = (xcdBlockId() * iters + it) * kLidarWaves + wave; // wave-uniform
         if (task >= ntasks) break;
-        uint32_t unit, sub;
-        if (kMode == kLidarAll) {
-            unit = task / 5u;
-            sub = task - unit * 5u;
-        } else if (kMode == kLidarFan) {
-            unit = task >> 2;
-            sub = task & 3u;
-        } else {
-            unit = task;
-            sub = 4u;
-        }
+        const uint32_t unit = task / 5u, sub = task - unit * 5u;
         const bool fwd = sub < 4u;
         // The ray of lane `ln`: a tail unit's lanes past A trace a copy of
         // the last agent's rays and store nothing.
@@ -3338,38 +3309,14 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
         // from an opaque copy of g (nothing but the ray lives across it).
         float tb;
         bool bhit;
-        // Forward fans: the per-wave candidate lists (geom_dev.h fanTraceD);
-        // rear fans (and scenes of more than 255 triangles): the BVH.  Both
-        // give the smallest-t closest hit.
-        if (kMode == kLidarFan) {
-            // one agent per forward wave: its aim frame and sheet origins
-            const uint32_t gu = min(unit * 4u + sub, A - 1u);
-            const Quat qa = ldAimRot(S, gu);
-            const float top = viewHeightD(S.curPose[gu]) + c::kAgentRadius;
-            const float pz = S.pz[gu];
-            const float z0 = pz + (c::kAgentRadius + (top - 2.f * c::kAgentRadius) * 0.f);
-            const float z1 = pz + (c::kAgentRadius + (top - 2.f * c::kAgentRadius) * 1.f);
-            // the lane's own ray is formed only for the walk (fewer live registers)
-            fanTraceD(bvh, numTris, fanList + wave * kFanListCap, S.px[gu], S.py[gu], z0, z1,
-                               rotateVec(qa, kRight), rotateVec(qa, kFwd),
-                               [&](Vec3 &o, Vec3 &d) {
-                                   uint32_t l2;
-                                   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0"
-                                                : "=v"(l2));
-                                   makeRay(l2, g, valid, kk, o, d);
-                               },
-                      ray_o, dir, tb);
-            bhit = __float_as_int(tb) != __float_as_int(kFltMax);
-        }
-        if (kMode != kLidarFan) {
+        {
             makeRay(lane, g, valid, kk, ray_o, dir);
             // the ray's octant image: same nodes and leaves, near-first slot
             // order (scene.h octantNodeImages)
             LBVH ob = bvh;
             ob.nodes = reinterpret_cast<const MP_LDS BVHNode *>(reinterpret_cast<const MP_LDS uint4 *>(bvh.nodes) +
                                                                  rayOctant(dir) * sc.numNodes * kOctNodeQ);
-            bhit = bvhTraceRayT<false, kOctNodeQ, true, true, true>(ob, ray_o, dir, tb,
-                                                                                               kFltMax, 0.f);
+            bhit = bvhTraceRayT<false, kOctNodeQ, true, true>(ob, ray_o, dir, tb, kFltMax, 0.f);
         }
         // The lane id again (volatile) and the ray's indices from it: integer
         // work only, so they need not live across the traversal (at 64 VGPRs
@@ -3520,24 +3467,6 @@ __device__ __forceinline__ void lidarBody(const DevState &S, const SceneDev &sc,
         *tdst = *dst;
         *dst = out;
     }
-}
-
-__global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S, SceneDev sc, int iters)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    lidarBody<kLidarAll>(S, sc, iters, smem);
-}
-
-__global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar_fan(DevState S, SceneDev sc, int iters)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    lidarBody<kLidarFan>(S, sc, iters, smem);
-}
-
-__global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar_rear(DevState S, SceneDev sc, int iters)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    lidarBody<kLidarRear>(S, sc, iters, smem);
 }
 
 static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
@@ -3815,18 +3744,13 @@ int computeZoneGoalTris(const SceneDev &sc, int32_t *dev_scratch, int32_t *host_
 int launchLidar(const DevState &s, const SceneDev &sc, void *stream)
 {
     // ~1024 blocks before the iterations grow past 1
-    auto launch = [&](void (*kern)(DevState, SceneDev, int), int64_t tasks, size_t lds) {
-        const int iters = (int)std::max<int64_t>(1, std::min<int64_t>(kLidarIters, tasks / (kLidarWaves * 1024)));
-        const int64_t per_block = (int64_t)kLidarWaves * iters;
-        const int blocks = (int)((tasks + per_block - 1) / per_block);
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(kLidarBlock), lds, (hipStream_t)stream, s, sc, iters);
-        return check(hipGetLastError());
-    };
-    const int64_t units = (s.A + 3) / 4;
-    if (!sc.lidarFan || !lidarFanScene(sc)) return launch(k_lidar, lidarTasks(s.A), bvhLdsBytesOct(sc));
-    const size_t fanLds = (size_t)sc.numVerts * 16 * 3 + (size_t)kLidarWaves * kFanListCap * sizeof(uint16_t);
-    if (launch(k_lidar_fan, units * 4, fanLds)) return -1;
-    return launch(k_lidar_rear, units, bvhLdsBytesOct(sc));
+    const int64_t tasks = lidarTasks(s.A);
+    const int iters = (int)std::max<int64_t>(1, std::min<int64_t>(kLidarIters, tasks / (kLidarWaves * 1024)));
+    const int64_t per_block = (int64_t)kLidarWaves * iters;
+    const int blocks = (int)((tasks + per_block - 1) / per_block);
+    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(kLidarBlock), bvhLdsBytesOct(sc), (hipStream_t)stream, s, sc,
+                       iters);
+    return check(hipGetLastError());
 }
 
 int launchDebugGather(const DevState &s, float *af, int32_t *ai, int32_t *wi, float *wf, uint32_t *explore,

@@ -523,45 +523,6 @@ static void buildSceneDev(mpenv_manager &m)
         sc.triPre = d_pre;
     }
     {
-        // k_lidar fan lists (geom_dev.h fanTraceD): per triangle the unit
-        // normal n of (b - a) x (c - a) (an accepted ray hit comes from the
-        // +n side), its plane offset n.a, and a bounding sphere (centroid,
-        // radius rounded up) -- cull data only, computed in double; every
-        // use carries a margin far above their rounding.
-        const size_t nt = s.bvhVerts.size() / 3;
-        std::vector<float> aux(std::max<size_t>(nt, 1) * 8, 0.f);
-        for (size_t t = 0; t < nt; t++) {
-            double v[3][3];
-            for (int i = 0; i < 3; i++) {
-                v[i][0] = s.bvhVerts[3 * t + i].x;
-                v[i][1] = s.bvhVerts[3 * t + i].y;
-                v[i][2] = s.bvhVerts[3 * t + i].z;
-            }
-            const double e1[3] = { v[1][0] - v[0][0], v[1][1] - v[0][1], v[1][2] - v[0][2] };
-            const double e2[3] = { v[2][0] - v[0][0], v[2][1] - v[0][1], v[2][2] - v[0][2] };
-            double n[3] = { e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0] };
-            const double nl = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-            for (int k = 0; k < 3; k++) n[k] = nl > 0 ? n[k] / nl : 0.0;
-            double c[3], r2 = 0;
-            for (int k = 0; k < 3; k++) c[k] = (v[0][k] + v[1][k] + v[2][k]) / 3.0;
-            for (int i = 0; i < 3; i++) {
-                double d2 = 0;
-                for (int k = 0; k < 3; k++) d2 += (v[i][k] - c[k]) * (v[i][k] - c[k]);
-                r2 = std::max(r2, d2);
-            }
-            float *o = &aux[8 * t];
-            o[0] = (float)n[0]; o[1] = (float)n[1]; o[2] = (float)n[2];
-            o[3] = (float)(n[0] * v[0][0] + n[1] * v[0][1] + n[2] * v[0][2]);
-            o[4] = (float)c[0]; o[5] = (float)c[1]; o[6] = (float)c[2];
-            o[7] = (float)(std::sqrt(r2) * (1.0 + 1e-6) + 1e-3);
-        }
-        float *d_aux = m.alloc<float>(aux.size());
-        m.upload(d_aux, aux.data(), sizeof(float) * aux.size());
-        sc.triAux = d_aux;
-        sc.lidarFan = 1;
-        if (const char *e = std::getenv("MPENV_LIDAR_FAN")) sc.lidarFan = std::atoi(e) != 0;
-    }
-    {
         // the sphere-cast radius is always consts::agentRadius (k_move)
         const QuirkGrid q = quirkGrid(s.bvhVerts, 15.f, 2.f, 16.f);
         uint32_t *d_q = m.alloc<uint32_t>(std::max<size_t>(q.bits.size(), 1));

@@ -292,7 +292,7 @@ class Oracle:
 
     def __init__(self, num_worlds, team_size, rand_seed=5, sim_flags=0, auto_reset=True,
                  world_id_offset=0, scene=SCENE, task=TASK_ZONE, curriculum=None, flank=False,
-                 lidar_order="lex"):
+                 lidar_order="octant"):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,

@@ -162,6 +162,10 @@ def test_product_kernels_carry_no_lab_switches_and_lab_patches_apply(tmp_path):
     for p in patches:
         work = tmp_path / p
         shutil.copytree(csrc, work)
-        r = subprocess.run(["patch", "-p1", "-d", str(work), "-i", os.path.join(lab, p)],
-                           capture_output=True, text=True)
-        assert r.returncode == 0 and "fuzz" not in r.stdout, (p, r.stdout, r.stderr)
+        # a patch may build on others ("# requires: a.patch b.patch" first line)
+        first = open(os.path.join(lab, p)).readline()
+        chain = first.split(":", 1)[1].split() if first.startswith("# requires:") else []
+        for q in chain + [p]:
+            r = subprocess.run(["patch", "-p1", "-d", str(work), "-i", os.path.join(lab, q)],
+                               capture_output=True, text=True)
+            assert r.returncode == 0 and "fuzz" not in r.stdout, (p, q, r.stdout, r.stderr)

@@ -4,15 +4,16 @@ The reference walks MeshBVH children in slot order (mesh_bvh.inl:160-204)
 and each accepted hit tightens t_max in the watertight test's scaled form
 (T <= t_max * det), so where two distinct near-coplanar triangles give hits
 one ulp apart, the triangle visited first can win.  The product's k_lidar
-follows an order-independent rule instead: the smallest t = fl(T * fl(1/det))
-over every triangle the ray hits (the oracle's lidar_order="lex", the
-default).  Pinned here: (1) the oracle's BVH traversal under that rule
-equals a brute-force minimum over all 252 triangles on lidar fans from
-rollouts (tape and combat), on random rays, on rays aimed exactly at every
-vertex and edge midpoint and on near-axis rays from on or near vertices
-(-0 ranks below +0); (2) against the reference's slot order the
-rule moves at most one ulp of depth on a few rays and never a discrete
-channel or any other output."""
+walks children in the per-octant order (the oracle's lidar_order="octant",
+the default).  Pinned here: (1) on lidar fans from rollouts (tape and
+combat) and random rays that order's closest hit is within one ulp of a
+brute-force minimum over all 252 triangles, with the same hit flags; the
+order-independent smallest-t rule the round-4 candidate lists needed
+(lidar_order="lex", tools/lab/fan_lists.patch) equals the brute force
+exactly, also on rays aimed at every vertex and edge midpoint and near-axis
+rays from on or near vertices; (2) against the reference's slot order the
+octant order moves at most one ulp of depth on a few rays and never a
+discrete channel or any other output."""
 import os
 import sys
 
@@ -50,6 +51,28 @@ def _rollout_rays(combat, W=8, steps=(40, 120)):
     return r[:, :3], r[:, 3:]
 
 
+def test_octant_order_is_within_one_ulp_of_brute_force():
+    o = T.Oracle(1, 1)
+    rng = np.random.default_rng(5)
+    sets = [_rollout_rays(False), _rollout_rays(True)]
+    org = rng.uniform([-1500, -1500, -50], [1500, 1500, 300], (20000, 3))
+    d = rng.normal(size=(20000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    sets.append((org, d))
+    total = hits = off = 0
+    for org, d in sets:
+        t1, h1 = _trace(o, org, d, 1)
+        t3, h3 = _trace(o, org, d, 3)
+        assert np.array_equal(h1, h3)
+        ulp = np.abs(t1.view(np.int32).astype(np.int64) - t3.view(np.int32).astype(np.int64))[h1 != 0]
+        assert ulp.max(initial=0) <= 1
+        off += int((ulp > 0).sum())
+        total += len(org)
+        hits += int(h1.sum())
+    assert total > 30000 and hits > 20000 and off <= total * 1e-3
+    o.close()
+
+
 def test_smallest_t_rule_over_the_bvh_equals_brute_force():
     o = T.Oracle(1, 1)
     rng = np.random.default_rng(3)
@@ -81,7 +104,7 @@ def test_smallest_t_rule_over_the_bvh_equals_brute_force():
     o.close()
 
 
-def test_smallest_t_rule_matches_slot_order_up_to_near_coplanar_ties():
+def test_octant_order_matches_slot_order_up_to_near_coplanar_ties():
     rays, diff, max_ulp, disc, other = lidar_order_check.main(W=24, steps=150, ts=6)
     assert rays == 24 * 12 * 80 * 150
     assert max_ulp <= 1

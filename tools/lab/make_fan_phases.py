@@ -1,7 +1,10 @@
-"""Regenerates tools/lab/fan_phases.patch from the current csrc/ (the
+"""Regenerates tools/lab/fan_phases.patch from csrc/ + fan_lists.patch (the
 fan-phase timers sit inside fanTraceD, so the patch is rebuilt whenever that
 function changes): per-wave phase cycles and work counts of k_lidar_fan,
-read back through mpenv_lab_fan (tools/kernel_lab.py prints them)."""
+read back through mpenv_lab_fan (tools/kernel_lab.py prints them).
+
+  python tools/kernel_lab.py build fanph --patch tools/lab/fan_lists.patch \
+      --patch tools/lab/fan_phases.patch"""
 import os
 import re
 import shutil
@@ -95,14 +98,17 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         a, b = os.path.join(td, "a"), os.path.join(td, "b")
         shutil.copytree(CSRC, a)
-        shutil.copytree(CSRC, b)
+        lists = os.path.join(ROOT, "tools", "lab", "fan_lists.patch")
+        subprocess.run(["patch", "-s", "-p1", "-d", a, "-i", lists], check=True)
+        shutil.copytree(a, b)
         for f, fn in (("geom_dev.h", edit_geom), ("kernels.hip", edit_kernels)):
             p = os.path.join(b, f)
             text = fn(open(p).read())
             open(p, "w").write(text)
         out = subprocess.run(["diff", "-ru", "a", "b"], cwd=td, capture_output=True, text=True).stdout
         out = re.sub(r"^(---|\+\+\+) (a|b)/(\S+)\t[^\n]*", r"\1 \2/\3", out, flags=re.M)
-        open(os.path.join(ROOT, "tools", "lab", "fan_phases.patch"), "w").write(out)
+        open(os.path.join(ROOT, "tools", "lab", "fan_phases.patch"), "w").write(
+            "# requires: fan_lists.patch\n" + out)
     print("wrote tools/lab/fan_phases.patch")
 
 

@@ -1,7 +1,7 @@
 """Closest-hit lidar under two rules (oracle, CPU): slot order as
-mesh_bvh.inl:160-204 is written, and the order-independent smallest-t rule
-the product's k_lidar follows (DESIGN.md §2 definition 12; or the round-3
-octant child order with LIDAR_B=octant).  Reports
+mesh_bvh.inl:160-204 is written, and the octant child order the product's
+k_lidar follows (DESIGN.md §2 definition 12; or the order-independent
+smallest-t rule with LIDAR_B=lex).  Reports
 how many rays differ, by how many ulps, and whether any discrete channel
 (wall / teammate / opponent one-hot) or any other output differs.
 
@@ -18,7 +18,7 @@ import mpenv_testlib as T  # noqa: E402
 
 def main(W=64, steps=300, ts=6):
     A = W * 2 * ts
-    sims = [T.Oracle(W, ts, lidar_order=o) for o in ("slot", os.environ.get("LIDAR_B", "lex"))]
+    sims = [T.Oracle(W, ts, lidar_order=o) for o in ("slot", os.environ.get("LIDAR_B", "octant"))]
     for o in sims:
         o.put_ctrl([0, 1, 1])
         o.init()
