@@ -367,17 +367,19 @@ def main():
         if stream_ptrs is not None:
             # gpuStreamStep: inputs from the caller's buffers (the step's
             # actions straight from the ring), the step, outputs copied out
+            # -- the whole step (no step_async after it)
             sim.gpu_stream_step(sptr, stream_ptrs[s % RING])
-        elif policy is not None:
-            # actions from the observations the previous step left (no tape)
-            sim.copy_actions(policy(), sptr)
-        elif args.actions == "combat":
-            # the aim-bot reads the previous step's observations and writes
-            # the step inputs directly (replaces the input copy)
-            sim.combat_actions(ring[s % RING].data_ptr(), 0, 1, sptr)
         else:
-            sim.copy_actions(ring[s % RING].data_ptr(), sptr)
-        sim.step_async(sptr)
+            if policy is not None:
+                # actions from the observations the previous step left (no tape)
+                sim.copy_actions(policy(), sptr)
+            elif args.actions == "combat":
+                # the aim-bot reads the previous step's observations and writes
+                # the step inputs directly (replaces the input copy)
+                sim.combat_actions(ring[s % RING].data_ptr(), 0, 1, sptr)
+            else:
+                sim.copy_actions(ring[s % RING].data_ptr(), sptr)
+            sim.step_async(sptr)
         if learner is not None:
             learner.submit(sptr)
 
