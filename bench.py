@@ -179,7 +179,8 @@ def load_profile(path, workload):
     except (OSError, ValueError):
         return {}
     if "workloads" in d:
-        return d["workloads"].get(workload, {})
+        e = d["workloads"].get(workload, {})
+        return dict(e, by_window=e.get("by_window", {}))
     return d if d.get("workload") == workload else {}
 
 
@@ -493,6 +494,8 @@ def main():
         alg = KERNEL_BYTES_PER_AGENT[dom] * A + KERNEL_BYTES_PER_WORLD[dom] * W + (lk_bytes if dom == "k_obs" else 0)
         achieved = alg / (dom_ms * 1e-3) / 1e9
         prof = load_profile(args.traffic, workload)
+        # the PMC pass of this very window when one was collected
+        prof = prof.get("by_window", {}).get(f"{args.warmup}x{args.steps}", prof)
         traffic = prof.get("per_kernel", {}).get(dom)
         valu = prof.get("valu_insts_per_launch", {}).get(dom)
         step_bytes = sum(KERNEL_BYTES_PER_AGENT.values()) * A + sum(KERNEL_BYTES_PER_WORLD.values()) * W + lk_bytes

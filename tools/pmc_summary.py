@@ -121,7 +121,16 @@ def main(tag, src):
         allw = {}
     if "workloads" not in allw:
         allw = {"workloads": {allw["workload"]: allw} if "workload" in allw else {}}
-    allw["workloads"][traffic["workload"]] = traffic
+    # per workload: every measured window under by_window ("WARMUPxSTEPS",
+    # bench.py prefers the one it runs), the longest one at the top level
+    prev = allw["workloads"].get(traffic["workload"], {})
+    by_window = dict(prev.get("by_window", {}))
+    if "bench_window" in prev and "per_kernel" in prev:
+        pw = prev["bench_window"]
+        by_window.setdefault(f"{pw[0]}x{pw[1]}", {k: v for k, v in prev.items() if k != "by_window"})
+    by_window[f"{warm}x{steps}"] = traffic
+    top = max(by_window.values(), key=lambda e: e["bench_window"][1])
+    allw["workloads"][traffic["workload"]] = dict(top, by_window=by_window)
     with open(path, "w") as f:
         json.dump(allw, f, indent=1)
     for k, v in ks.items():
