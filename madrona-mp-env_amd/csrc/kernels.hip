@@ -3231,6 +3231,9 @@ constexpr int kLidarIters = 4; // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 m
 // blocks per CU (8 waves per SIMD) fit the 160 KB of LDS.
 constexpr int kLidarBlock = 1024;
 constexpr int kLidarWaves = kLidarBlock / 64;
+constexpr int kLidarStageMax = 96, kLidarStageCols = 12; // k_lidar's per-block agent stage
+static_assert(4 * ((kLidarIters * kLidarWaves) / 5 + 2) + 2 * (2 * kMaxTeamSize - 1) <= kLidarStageMax,
+              "k_lidar agent stage");
 
 __device__ __host__ __forceinline__ int64_t lidarTasks(int64_t A) { return ((A + 3) / 4) * 5; }
 
@@ -3265,10 +3268,39 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         const float theta = range * (float(x) / float(width - 1)) + offset;
         fan[threadIdx.x] = make_float2(-cosf_(theta), sinf_(theta));
     }
-    const LBVH bvh = stageBVHOct(smem, sc); // ends with __syncthreads
     const uint32_t N = (uint32_t)S.N, T = (uint32_t)S.T;
     const uint32_t A = (uint32_t)S.A;
     const uint32_t ntasks = (uint32_t)lidarTasks(S.A);
+    // The agents this block's tasks read -- the rays' origins and frames and
+    // every capsule of their worlds -- staged in LDS with the BVH: whole
+    // worlds around the block's task range (<= 14 units of 4 agents plus a
+    // partial world at each end: <= 78 agents, N <= 12), so no task waits
+    // on HBM for them.
+    __shared__ float agentStage[kLidarStageCols][kLidarStageMax];
+    const uint32_t t0 = xcdBlockId() * (uint32_t)iters * kLidarWaves;
+    const uint32_t t1 = min(ntasks, t0 + (uint32_t)iters * kLidarWaves);
+    uint32_t s0 = 0, ns = 0;
+    if (t0 < t1) {
+        const uint32_t a_lo = (t0 / 5u) * 4u, a_hi = min(A, ((t1 - 1u) / 5u) * 4u + 4u);
+        s0 = (a_lo / N) * N;
+        ns = ((a_hi - 1u) / N + 1u) * N - s0;
+        for (uint32_t k = threadIdx.x; k < ns; k += blockDim.x) {
+            const uint32_t g = s0 + k;
+            agentStage[0][k] = S.px[g];
+            agentStage[1][k] = S.py[g];
+            agentStage[2][k] = S.pz[g];
+            agentStage[3][k] = S.aw[g];
+            agentStage[4][k] = S.ax[g];
+            agentStage[5][k] = S.ay[g];
+            agentStage[6][k] = S.az[g];
+            agentStage[7][k] = S.rw[g];
+            agentStage[8][k] = S.rx[g];
+            agentStage[9][k] = S.ry[g];
+            agentStage[10][k] = S.rz[g];
+            agentStage[11][k] = viewHeightD(S.curPose[g]);
+        }
+    }
+    const LBVH bvh = stageBVHOct(smem, sc); // ends with __syncthreads
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int it = 0; it < iters; it++) {
         const uint32_t task = (xcdBlockId() * iters + it) * kLidarWaves + wave; // wave-uniform
@@ -3286,11 +3318,13 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         auto makeRay = [&](uint32_t ln, uint32_t &g, bool &valid, uint32_t &kk, Vec3 &ray_o, Vec3 &dir) {
             rayIndex(ln, g, valid, kk);
             const uint32_t h = fwd ? (kk >> 5) : (kk >> 3), x = fwd ? (kk & 31u) : (kk & 7u);
-            const Quat q = fwd ? ldAimRot(S, g) : ldRot(S, g);
+            const uint32_t k = g - s0, qc = fwd ? 3u : 7u;
+            const Quat q = quat(agentStage[qc][k], agentStage[qc + 1u][k], agentStage[qc + 2u][k],
+                                agentStage[qc + 3u][k]);
             const Vec3 dir_fwd = rotateVec(q, kFwd);
             const Vec3 dir_right = rotateVec(q, kRight);
-            const float top = viewHeightD(S.curPose[g]) + c::kAgentRadius;
-            ray_o = ldPos(S, g);
+            const float top = agentStage[11][k] + c::kAgentRadius;
+            ray_o = v3(agentStage[0][k], agentStage[1][k], agentStage[2][k]);
             ray_o.z += c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(h) / float(2 - 1));
             const float2 cs = fan[fwd ? x : 32 + x];
             dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
@@ -3350,7 +3384,8 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             float cx = 0.f, cy = 0.f, cz = 0.f;
             bool keep = false;
             if (lane < N) {
-                cx = S.px[g0 + lane]; cy = S.py[g0 + lane]; cz = S.pz[g0 + lane];
+                const uint32_t k = (uint32_t)(g0 - s0) + lane;
+                cx = agentStage[0][k]; cy = agentStage[1][k]; cz = agentStage[2][k];
                 const float dx = cx - ray_o.x, dy = cy - ray_o.y;
                 keep = lane != i && !(sqrtf(dx * dx + dy * dy) - c::kAgentRadius * 1.01f - 1.f > mx);
             }
@@ -3398,7 +3433,8 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             float cx = 0.f, cy = 0.f, cz = 0.f;
             bool keep = false;
             if (jl < N) {
-                cx = S.px[g0 + jl]; cy = S.py[g0 + jl]; cz = S.pz[g0 + jl];
+                const uint32_t k = (uint32_t)(g0 - s0) + jl;
+                cx = agentStage[0][k]; cy = agentStage[1][k]; cz = agentStage[2][k];
                 const float dx = cx - ray_o.x, dy = cy - ray_o.y;
                 keep = jl != i && !(sqrtf(dx * dx + dy * dy) - c::kAgentRadius * 1.01f - 1.f > mx);
             }
