@@ -855,13 +855,13 @@ __device__ __forceinline__ WorldHit capsulesD(const float *__restrict__ px, cons
 // is returned for visibleFullD, the BVH search and the capsule loop.  k_vis
 // runs the first part on every candidate ray and the second on the
 // unresolved ones only, compacted (the answer per ray is the same).
-__device__ __forceinline__ bool visibleQuickD(const LBVH &b, const float *__restrict__ px,
-                                              const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
-                                              mp::Vec3 org, mp::Vec3 d, int target, const uint16_t *occ,
-                                              uint32_t numTris, float &t_c)
+// capsule(j): the base of the world's agent j's capsule (its position).
+template <class CapsuleFn>
+__device__ __forceinline__ bool visibleQuickD(const LBVH &b, CapsuleFn capsule, mp::Vec3 org, mp::Vec3 d, int target,
+                                              const uint16_t *occ, uint32_t numTris, float &t_c)
 {
     using namespace mp;
-    Vec3 ct = v3(px[g0 + target], py[g0 + target], pz[g0 + target]);
+    Vec3 ct = capsule(target);
     ct.z += kCapsuleRadius;
     t_c = intersectRayZOriginCapsule(org - ct, d, kCapsuleRadius, kCapsuleSegment);
     if (t_c == 0) return true;
@@ -879,10 +879,9 @@ __device__ __forceinline__ bool visibleQuickD(const LBVH &b, const float *__rest
     return false;
 }
 
-__device__ __forceinline__ bool visibleFullD(const LBVH &b, const float *__restrict__ px,
-                                             const float *__restrict__ py, const float *__restrict__ pz, int64_t g0,
-                                             int N, mp::Vec3 org, mp::Vec3 d, int target, float t_c,
-                                             uint16_t *occ = nullptr)
+template <class CapsuleFn>
+__device__ __forceinline__ bool visibleFullD(const LBVH &b, CapsuleFn capsule, int N, mp::Vec3 org, mp::Vec3 d,
+                                             int target, float t_c, uint16_t *occ = nullptr)
 {
     using namespace mp;
     float min_t = kFltMax;
@@ -906,7 +905,7 @@ __device__ __forceinline__ bool visibleFullD(const LBVH &b, const float *__restr
         if (j == target) {
             t = t_c;
         } else {
-            Vec3 co = v3(px[g0 + j], py[g0 + j], pz[g0 + j]);
+            Vec3 co = capsule(j);
             co.z += kCapsuleRadius;
             const Vec3 tr = org - co;
             // the conservative culls of traceWorldD (skip only exact misses)
@@ -932,8 +931,9 @@ __device__ __forceinline__ bool visibleRayD(const LBVH &b, const float *__restri
                                             uint16_t *occ = nullptr, uint32_t numTris = 0)
 {
     float t_c;
-    if (visibleQuickD(b, px, py, pz, g0, org, d, target, occ, numTris, t_c)) return false;
-    return visibleFullD(b, px, py, pz, g0, N, org, d, target, t_c, occ);
+    auto capsule = [&](int j) { return mp::v3(px[g0 + j], py[g0 + j], pz[g0 + j]); };
+    if (visibleQuickD(b, capsule, org, d, target, occ, numTris, t_c)) return false;
+    return visibleFullD(b, capsule, N, org, d, target, t_c, occ);
 }
 
 } // namespace mpenv

@@ -2495,6 +2495,14 @@ __device__ __forceinline__ bool inFrustumD(const SceneDev &sc, Vec3 vp)
 // loop that ran at roughly a third of the wave's lanes.
 constexpr int kVisMaxRays = kBlock * 4;
 
+// k_vis stages its block's agents with their worlds' whole rosters (the
+// opponents the block's lanes test and every capsule a ray may meet) in LDS
+// after the BVH image: 4 waves x floor(64/T) agents plus up to N-1 agents of
+// the partial first and last worlds.  Columns: px, py, pz, view height,
+// aim quaternion (w, x, y, z), alive.
+constexpr int kVisStageCols = 9;
+__host__ __device__ __forceinline__ int visStageAgents(int T, int N) { return (kBlock / 64) * (64 / T) + 2 * (N - 1); }
+
 __device__ __forceinline__ Vec3 visSamplePointD(const DevState &S, int64_t gt, Vec3 delta_right, int p)
 {
     Vec3 pt = ldPos(S, gt);
@@ -2582,12 +2590,49 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
         nrays2 = 0;
     }
     masks[threadIdx.x] = 0;
-    const LBVH bvh = stageBVH(smem, sc); // barrier
     const int T = S.T, N = S.N;
     const int apw = 64 / T;
     const int wl = threadIdx.x & 63;
     const int64_t wave = ((int64_t)xcdBlockId() * blockDim.x + threadIdx.x) >> 6;
     const int64_t agent0 = (((int64_t)xcdBlockId() * blockDim.x) >> 6) * apw; // first agent of the block
+    const int nsMax = visStageAgents(T, N);
+    float *st = (float *)(smem + (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16);
+    const int64_t s0 = (agent0 / N) * N;
+    {
+        const int64_t a_hi = min(S.A, agent0 + (int64_t)(kBlock / 64) * apw);
+        const int ns = agent0 < a_hi ? (int)(((a_hi - 1) / N + 1) * N - s0) : 0;
+        for (int k = threadIdx.x; k < ns; k += kBlock) {
+            const int64_t g = s0 + k;
+            st[0 * nsMax + k] = S.px[g];
+            st[1 * nsMax + k] = S.py[g];
+            st[2 * nsMax + k] = S.pz[g];
+            st[3 * nsMax + k] = viewHeightD(S.curPose[g]);
+            st[4 * nsMax + k] = S.aw[g];
+            st[5 * nsMax + k] = S.ax[g];
+            st[6 * nsMax + k] = S.ay[g];
+            st[7 * nsMax + k] = S.az[g];
+            st[8 * nsMax + k] = S.alive[g];
+        }
+    }
+    const LBVH bvh = stageBVH(smem, sc); // barrier
+    auto sPos = [&](int64_t g) {
+        const int l = (int)(g - s0);
+        return v3(st[0 * nsMax + l], st[1 * nsMax + l], st[2 * nsMax + l]);
+    };
+    auto sAim = [&](int64_t g) {
+        const int l = (int)(g - s0);
+        return quat(st[4 * nsMax + l], st[5 * nsMax + l], st[6 * nsMax + l], st[7 * nsMax + l]);
+    };
+    auto sView = [&](int64_t g) { return st[3 * nsMax + (int)(g - s0)]; };
+    auto sAlive = [&](int64_t g) { return st[8 * nsMax + (int)(g - s0)]; };
+    // visSamplePointD from the stage
+    auto sSample = [&](int64_t gt, Vec3 delta_right, int p) {
+        Vec3 pt = sPos(gt);
+        pt.z += p == 0 ? c::kAgentRadius : sView(gt);
+        if (p == 2) pt = pt - delta_right;
+        if (p == 3) pt = pt + delta_right;
+        return pt;
+    };
 
     // ---- phase A: view tests, reserve ray slots
     {
@@ -2599,15 +2644,15 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
             const int w = (int)(g / N);
             const int i = (int)(g - (int64_t)w * N);
             const int64_t gt = (int64_t)w * N + ((i / T) ^ 1) * T + k;
-            if (S.alive[g] != 0.f && S.alive[gt] != 0.f) {
-                Vec3 org = ldPos(S, g);
-                org.z += viewHeightD(S.curPose[g]);
-                const Quat aim_rot = ldAimRot(S, g);
+            if (sAlive(g) != 0.f && sAlive(gt) != 0.f) {
+                Vec3 org = sPos(g);
+                org.z += sView(g);
+                const Quat aim_rot = sAim(g);
                 const Quat inv_rot = qinv(aim_rot);
                 const Vec3 delta_right = rotateVec(aim_rot, kRight) * 0.9f * c::kAgentRadius;
 #pragma unroll
                 for (int p = 0; p < 4; p++) {
-                    Vec3 to_test = visSamplePointD(S, gt, delta_right, p) - org;
+                    Vec3 to_test = sSample(gt, delta_right, p) - org;
                     Vec3 view = rotateVec(inv_rot, to_test);
                     if (view.y <= 0.f) continue;
                     if (!inFrustumD(sc, view)) continue;
@@ -2619,9 +2664,9 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
         const int nc = __popc(cand);
         if (S.stats) {
             uint32_t pair = 0;
-            if (valid && S.alive[g] != 0.f) {
+            if (valid && sAlive(g) != 0.f) {
                 const int64_t gt2 = (g / N) * N + (((int)(g % N) / T) ^ 1) * T + k;
-                pair = S.alive[gt2] != 0.f ? 1u : 0u;
+                pair = sAlive(gt2) != 0.f ? 1u : 0u;
             }
             statAdd(S.stats + kStatLosPairs, pair);
             statAdd(S.stats + kStatLosRays, (uint32_t)nc);
@@ -2668,11 +2713,11 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
         const int i = (int)(g - (int64_t)w * N);
         g0 = (int64_t)w * N;
         target = ((i / T) ^ 1) * T + k;
-        org = ldPos(S, g);
-        org.z += viewHeightD(S.curPose[g]);
-        const Quat aim_rot = ldAimRot(S, g);
+        org = sPos(g);
+        org.z += sView(g);
+        const Quat aim_rot = sAim(g);
         const Vec3 delta_right = rotateVec(aim_rot, kRight) * 0.9f * c::kAgentRadius;
-        Vec3 to_test = visSamplePointD(S, g0 + target, delta_right, p) - org;
+        Vec3 to_test = sSample(g0 + target, delta_right, p) - org;
         const float len = length(to_test);
         dir = to_test / len;
     };
@@ -2682,7 +2727,9 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
         Vec3 org, dir;
         rayOf(r, g, k, p, g0, target, org, dir);
         float t_c;
-        if (!visibleQuickD(bvh, S.px, S.py, S.pz, g0, org, dir, target,
+        const int l0 = (int)(g0 - s0);
+        auto capsule = [&](int j) { return v3(st[0 * nsMax + l0 + j], st[1 * nsMax + l0 + j], st[2 * nsMax + l0 + j]); };
+        if (!visibleQuickD(bvh, capsule, org, dir, target,
                            hints ? S.visOcc + (g * T + k) * 4 + p : nullptr, numTris, t_c))
             rays2[atomicAdd(&nrays2, 1u)] = (uint16_t)r;
     }
@@ -2695,10 +2742,12 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
         Vec3 org, dir;
         rayOf(rays2[q], g, k, p, g0, target, org, dir);
         // t_c again (the same bits as in B1)
-        Vec3 ct = v3(S.px[g0 + target], S.py[g0 + target], S.pz[g0 + target]);
+        const int l0 = (int)(g0 - s0);
+        auto capsule = [&](int j) { return v3(st[0 * nsMax + l0 + j], st[1 * nsMax + l0 + j], st[2 * nsMax + l0 + j]); };
+        Vec3 ct = capsule(target);
         ct.z += kCapsuleRadius;
         const float t_c = intersectRayZOriginCapsule(org - ct, dir, kCapsuleRadius, kCapsuleSegment);
-        const bool seen = visibleFullD(bvh, S.px, S.py, S.pz, g0, N, org, dir, target, t_c,
+        const bool seen = visibleFullD(bvh, capsule, N, org, dir, target, t_c,
                                        hints ? S.visOcc + (g * T + k) * 4 + p : nullptr);
         if (seen) atomicOr(&masks[(int)(g - agent0)], 1u << k);
         if (S.stats) statAdd(S.stats + kStatLosSeen, seen ? 1u : 0u);
@@ -3748,7 +3797,8 @@ int launchVisibility(const DevState &s, const SceneDev &sc, void *stream)
 {
     const int64_t waves = (s.A + (64 / s.T) - 1) / (64 / s.T);
     const int blocks = (int)((waves * 64 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_vis, dim3(blocks), dim3(kBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
+    hipLaunchKernelGGL(k_vis, dim3(blocks), dim3(kBlock),
+                       bvhLdsBytes(sc) + (size_t)kVisStageCols * 4 * visStageAgents(s.T, s.N), (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }
 
