@@ -275,6 +275,12 @@ def stream_buffers(sim, ring, dev):
 
 def main():
     args = parse()
+    # stdout carries the one JSON line only: native libraries print to fd 1
+    # (RCCL's version banner at communicator init), so fd 1 is pointed at
+    # stderr for the run and the line goes to a copy of the original.
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -557,7 +563,7 @@ def main():
     if rank == 0 and world_size == 1 and args.cpu_baseline == "auto":
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=line_out, flush=True)
     if learner is not None:
         learner.close()
     if dist.is_initialized():
