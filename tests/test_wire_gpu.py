@@ -128,3 +128,52 @@ def test_wire_rejects_foreign_or_mismatched_messages():
     assert a.lib.mpenv_wire_unpack(a.h, buf, 0, None) == 0
     assert _error(a) == 0
     a.mem.free(buf)
+
+
+def test_learner_wire_loopback_matches_the_engine():
+    """LearnerWire at one rank (bench.py --exchange wire): the rank's own
+    message packed and unpacked into its shadow every step through the
+    Python module -- the shadow's trainInterface outputs (outputs()) equal
+    the engine's bit for bit, with combat actions driving kills and
+    last-known rows."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    import madrona_mp_env as m
+    from mpenv_dist import LearnerGather, LearnerWire
+
+    ts, W, steps = 6, 512, 60
+    A = W * 2 * ts
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        def mk():
+            return m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=0, num_worlds=W, rand_seed=5,
+                                auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                                team_size=ts, num_pbt_policies=0, policy_history_size=0, scene_path=T.SCENE)
+
+        sim = mk()
+        ctrl = sim.sim_control_tensor().to_torch()
+        ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=ctrl.device).view_as(ctrl))
+        torch.cuda.synchronize()
+        sim.init()
+        lw = LearnerWire(sim, make_shadow=lambda r: mk(), device=torch.device("cuda", 0))
+        ring = torch.from_numpy(T.mpenv_tape.tape_ring(SEED, 0, A, RING)).to("cuda")
+        sptr = torch.cuda.current_stream().cuda_stream
+        for s in range(steps):
+            sim.combat_actions(ring[s % RING].data_ptr(), 0, 1, sptr)
+            sim.step_async(sptr)
+            lw.submit(sptr)
+            if s % 20 == 19:
+                got = lw.outputs()
+                own = LearnerGather.from_sim(sim)
+                torch.cuda.synchronize()
+                for n, t in got.items():
+                    a, b = t[0].contiguous(), own[n].contiguous()
+                    assert a.shape == b.shape and torch.equal(a.view(torch.uint8), b.view(torch.uint8)), (n, s)
+        lw.close()
+    finally:
+        dist.destroy_process_group()
