@@ -107,6 +107,9 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--share-device", action="store_true",
                     help="debug: map every rank to GPU 0 (rehearse N>1 on a one-GPU box; no --gather)")
+    ap.add_argument("--wire-serial", action="store_true",
+                    help="--exchange wire: the learner unpacks on the step stream (back to back with its own "
+                         "step) instead of its own unpack stream")
     ap.add_argument("--no-profile-pass", action="store_true",
                     help="skip the second (kernel-timing + workload-counter) pass")
     ap.add_argument("--bots", choices=["none", "team1", "all"], default="none",
@@ -295,6 +298,11 @@ def main():
     exchange = "gather" if args.gather else args.exchange
     if exchange == "auto":
         exchange = "wire" if world_size > 1 and not args.share_device else "none"
+    if exchange != "none":
+        # the step, the pack / unpack and the transfers on one explicit
+        # stream (the default stream's handle, 0, means each manager's own
+        # internal stream at the C ABI)
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     xgroup = None
     if world_size > 1:
         # Control plane (barriers, max-over-ranks time) on gloo: the step has
@@ -359,7 +367,7 @@ def main():
         learner = make_exchange(exchange, sim, group=xgroup, grad_bytes=int(args.grad_mb * (1 << 20)),
                                 update_every=args.update_every)
     elif exchange == "wire":
-        learner = make_exchange(exchange, sim, group=xgroup, make_shadow=make_shadow)
+        learner = make_exchange(exchange, sim, group=xgroup, make_shadow=make_shadow, overlap=not args.wire_serial)
     else:
         learner = make_exchange(exchange, sim, group=xgroup)
 
@@ -486,6 +494,8 @@ def main():
     }
     if learner is not None:
         result["exchange_bytes_per_step"] = learner.bytes_per_step()
+        if exchange == "wire":
+            result["wire_unpack"] = "step stream" if args.wire_serial else "own stream (overlaps the step)"
         if exchange in ("wire", "gather"):
             result["exchange_bytes_per_agent"] = round(result["exchange_bytes_per_step"]["sent_per_rank"] / A, 1)
     if stream_ptrs is not None:

@@ -316,13 +316,21 @@ class LearnerWire:
     the rank packs its own message and unpacks it into its own shadow each
     step, so the line carries the per-message pack and unpack cost a learner
     pays for each peer (nothing crosses xGMI).
+
+    On a GPU the learner unpacks on a stream of its own (`overlap`, on by
+    default): the unpacks of one slot wait on GPU events for that slot's
+    receives (or, loopback, its pack), the next receive / pack into the slot
+    waits for the slot's unpacks, and nothing blocks the host -- so the
+    learner's own simulation step and its peers' unpacks share the GPU
+    instead of running back to back.  `drain()` orders the caller's stream
+    after every unpack.  submit() takes torch's current stream (the step's).
     """
 
     NOT_SHIPPED = NOT_SHIPPED
     mode = "wire"
 
     def __init__(self, sim, make_shadow=None, dst: int = 0, group=None, slots: int = 2, pack=None, unpack=None,
-                 nbytes=None, device=None):
+                 nbytes=None, device=None, overlap: bool = True):
         import torch
         import torch.distributed as dist
 
@@ -355,9 +363,30 @@ class LearnerWire:
         self.unpacked = [True] * slots
         self.keyframe = [True] * slots  # the kind of message in each slot
         self.k = 0
+        # the learner's unpack stream and, per slot, the event its unpacks end with
+        self.ustream, self.udone = None, None
+        if overlap and self.rank == dst and dev.type == "cuda":
+            self.torch = torch
+            self.ustream = torch.cuda.Stream(device=dev)
+            self.udone = [torch.cuda.Event() for _ in range(slots)]
 
     def bytes_per_step(self) -> dict:
         return {"sent_per_rank": self.nb, "learner_ingress": self.nb * (self.ws - 1), "keyframe": self.nk}
+
+    def _caller_stream(self, stream_ptr):
+        cur = self.torch.cuda.current_stream()
+        if stream_ptr and stream_ptr != cur.cuda_stream:
+            raise ValueError("LearnerWire(overlap=True): submit() on a stream other than torch's current one")
+        return cur
+
+    def _unpack_slot(self, slot, ranks, stream_ptr):
+        if self.ustream is None:
+            for r in ranks:
+                self._unpack(r, self.bufs[slot][r].data_ptr(), self.keyframe[slot], stream_ptr or 0)
+            return
+        for r in ranks:
+            self._unpack(r, self.bufs[slot][r].data_ptr(), self.keyframe[slot], self.ustream.cuda_stream)
+        self.udone[slot].record(self.ustream)
 
     def _peer(self, r):
         return self.dist.get_global_rank(self.group, r) if self.group is not None else r
@@ -365,27 +394,40 @@ class LearnerWire:
     def _finish(self, slot, stream_ptr):
         """Wait for a slot's transfers and (learner) unpack its messages."""
         if self.pending[slot] is not None:
-            for w in self.pending[slot]:
-                w.wait()
+            if self.ustream is not None:
+                # the unpack stream (not the caller's) waits for the receives
+                with self.torch.cuda.stream(self.ustream):
+                    for w in self.pending[slot]:
+                        w.wait()
+            else:
+                for w in self.pending[slot]:
+                    w.wait()
             self.pending[slot] = None
         if self.rank == self.dst and not self.unpacked[slot]:
-            for r in range(self.ws):
-                if r != self.dst:
-                    self._unpack(r, self.bufs[slot][r].data_ptr(), self.keyframe[slot], stream_ptr or 0)
+            self._unpack_slot(slot, [r for r in range(self.ws) if r != self.dst], stream_ptr)
             self.unpacked[slot] = True
 
     def submit(self, stream_ptr=None):
         dist = self.dist
+        if self.loopback and not stream_ptr:
+            # pack and unpack must share a stream: 0 would put each on its own
+            # manager's internal stream, unordered against each other
+            raise ValueError("LearnerWire loopback: submit() needs the step's stream (not 0)")
         slot = self.k % self.slots
         kf = self.k == 0
         self.k += 1
         self._finish(slot, stream_ptr)  # the slot's previous round is done before it is reused
         n = self.nk if kf else self.nb
         self.keyframe[slot] = kf
+        if self.ustream is not None:
+            # the slot's buffers are rewritten (pack / receive) only after its
+            # previous unpacks have read them
+            self._caller_stream(stream_ptr).wait_event(self.udone[slot])
         if self.loopback:
-            buf = self.bufs[slot][0].data_ptr()
-            self._pack(buf, kf, stream_ptr or 0)
-            self._unpack(0, buf, kf, stream_ptr or 0)
+            self._pack(self.bufs[slot][0].data_ptr(), kf, stream_ptr or 0)
+            if self.ustream is not None:
+                self.ustream.wait_stream(self._caller_stream(stream_ptr))
+            self._unpack_slot(slot, [0], stream_ptr)
             return slot
         if self.rank == self.dst:
             ops = [dist.P2POp(dist.irecv, self.bufs[slot][r][:n], self._peer(r), self.group)
@@ -404,6 +446,8 @@ class LearnerWire:
     def drain(self, stream_ptr=None):
         for i in range(self.slots):
             self._finish((self.k + i) % self.slots, stream_ptr)
+        if self.ustream is not None:
+            self._caller_stream(stream_ptr).wait_stream(self.ustream)
 
     def outputs(self):
         """{name: [world_size, rows, ...]} on dst (own engine + shadows)."""

@@ -130,12 +130,14 @@ def test_wire_rejects_foreign_or_mismatched_messages():
     a.mem.free(buf)
 
 
-def test_learner_wire_loopback_matches_the_engine():
+@pytest.mark.parametrize("overlap", [True, False])
+def test_learner_wire_loopback_matches_the_engine(overlap):
     """LearnerWire at one rank (bench.py --exchange wire): the rank's own
-    message packed and unpacked into its shadow every step through the
-    Python module -- the shadow's trainInterface outputs (outputs()) equal
-    the engine's bit for bit, with combat actions driving kills and
-    last-known rows."""
+    message packed on the step stream and unpacked into its shadow every
+    step through the Python module, on the learner's own unpack stream
+    ordered by GPU events (overlap) or on the step stream -- the shadow's
+    trainInterface outputs (outputs()) equal the engine's bit for bit, with
+    combat actions driving kills and last-known rows."""
     import socket
 
     import torch
@@ -160,9 +162,16 @@ def test_learner_wire_loopback_matches_the_engine():
         ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=ctrl.device).view_as(ctrl))
         torch.cuda.synchronize()
         sim.init()
-        lw = LearnerWire(sim, make_shadow=lambda r: mk(), device=torch.device("cuda", 0))
+        lw = LearnerWire(sim, make_shadow=lambda r: mk(), device=torch.device("cuda", 0), overlap=overlap)
+        assert (lw.ustream is not None) == overlap
         ring = torch.from_numpy(T.mpenv_tape.tape_ring(SEED, 0, A, RING)).to("cuda")
-        sptr = torch.cuda.current_stream().cuda_stream
+        torch.cuda.synchronize()
+        st = torch.cuda.Stream()
+        torch.cuda.set_stream(st)
+        sptr = st.cuda_stream
+        assert sptr != 0
+        with pytest.raises(ValueError):
+            lw.submit(0)  # loopback needs the step's stream
         for s in range(steps):
             sim.combat_actions(ring[s % RING].data_ptr(), 0, 1, sptr)
             sim.step_async(sptr)
@@ -176,4 +185,5 @@ def test_learner_wire_loopback_matches_the_engine():
                     assert a.shape == b.shape and torch.equal(a.view(torch.uint8), b.view(torch.uint8)), (n, s)
         lw.close()
     finally:
+        torch.cuda.set_stream(torch.cuda.default_stream())
         dist.destroy_process_group()
