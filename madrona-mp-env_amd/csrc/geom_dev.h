@@ -718,6 +718,90 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
     return h;
 }
 
+// Two sphere casts along the same direction from origins that differ in z
+// only (applyVelocity's low and high forward casts), in one traversal.  Each
+// cast keeps its own hit_t, and each stack entry carries which casts entered
+// that node, so a cast tests exactly the children of the nodes it entered,
+// in the same depth-first order as bvhSphereCastD (fixed child order; a node
+// only the other cast entered changes nothing for it) -- every result is
+// bit-identical to two bvhSphereCastD calls.  The x / y slab values are
+// shared (same origin xy and direction); z and the running bounds are per
+// cast.  act1 = false: cast 1 is not run (h1 untouched).
+__device__ __noinline__ void bvhSphereCast2D(const LBVH b, mp::Vec3 o0, float z1, mp::Vec3 ray_d, float r,
+                                             float t_max0, bool act1, SphereHit &h0, SphereHit &h1)
+{
+    using namespace mp;
+    Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
+    Vec3 closest0 = v3(0.f, 0.f, 0.f), closest1 = v3(0.f, 0.f, 0.f);
+    float hit0 = t_max0, hit1 = t_max0;
+    const bool negX = __builtin_signbit(inv_d.x), negY = __builtin_signbit(inv_d.y),
+               negZ = __builtin_signbit(inv_d.z);
+    const int nX = negX ? 12 : 0, fX = negX ? 0 : 12;
+    const int nY = negY ? 16 : 4, fY = negY ? 4 : 16;
+    const int nZ = negZ ? 20 : 8, fZ = negZ ? 8 : 20;
+    const Vec3 o1 = v3(o0.x, o0.y, z1);
+    ByteStack st;
+    st.lo = 0; st.hi = 0; st.n = 0;
+    uint32_t ms = 0; // 2 bits per stack entry: the casts that entered the node
+    bsPush(st, 0);
+    ms = act1 ? 3u : 1u;
+    while (st.n > 0) {
+        const uint32_t node_idx = bsPop(st);
+        const uint32_t m = ms & 3u;
+        ms >>= 2;
+        const MP_LDS float *nd = b.snodes + node_idx * kSNodeFloats;
+#pragma unroll 1
+        for (int i = 0; i < 4; i++) {
+            const int32_t child = __float_as_int(nd[24 + i]);
+            if (child == -1) continue;
+            const float i_min_x = (nd[nX + i] - o0.x) * inv_d.x, i_max_x = (nd[fX + i] - o0.x) * inv_d.x;
+            const float i_min_y = (nd[nY + i] - o0.y) * inv_d.y, i_max_y = (nd[fY + i] - o0.y) * inv_d.y;
+            const float zn = nd[nZ + i], zf = nd[fZ + i];
+            const float i_min_z0 = (zn - o0.z) * inv_d.z, i_max_z0 = (zf - o0.z) * inv_d.z;
+            const float i_min_z1 = (zn - z1) * inv_d.z, i_max_z1 = (zf - z1) * inv_d.z;
+            const float lo_xy = fmax_(fmax_(0.f, i_min_x), i_min_y);
+            const float t_lo0 = fmax_(lo_xy, i_min_z0), t_lo1 = fmax_(lo_xy, i_min_z1);
+            const float t_hi0 = fmin_(fmin_(fmin_(hit0, i_max_x), i_max_y), i_max_z0);
+            const float t_hi1 = fmin_(fmin_(fmin_(hit1, i_max_x), i_max_y), i_max_z1);
+            const uint32_t pass = ((m & 1u) && t_lo0 < t_hi0 ? 1u : 0u) | ((m & 2u) && t_lo1 < t_hi1 ? 2u : 0u);
+            if (pass == 0u) continue;
+            if (child & 0x80000000) {
+                const int leaf = child & 0x7fffffff;
+                const int ntri = (int)__float_as_uint(nd[28 + i]);
+                Vec3 n0 = v3(0.f, 0.f, 0.f), n1 = v3(0.f, 0.f, 0.f);
+                float t0 = hit0, t1 = hit1;
+                for (int k = 0; k < ntri; k++) {
+                    Vec3 a, bb, c;
+                    loadTri(b, leaf + k, a, bb, c);
+                    const MP_LDS lf4 *pp = reinterpret_cast<const MP_LDS lf4 *>(b.pre) + 2 * (leaf + k);
+                    const lf4 p0 = pp[0], p1 = pp[1];
+                    const float4 q0 = make_float4(p0.x, p0.y, p0.z, p0.w), q1 = make_float4(p1.x, p1.y, p1.z, p1.w);
+                    if (pass & 1u) t0 = sphereTriD(a, bb, c, q0, q1, o0, ray_d, t0, r, n0);
+                    if (pass & 2u) t1 = sphereTriD(a, bb, c, q0, q1, o1, ray_d, t1, r, n1);
+                }
+                if ((pass & 1u) && t0 < hit0) {
+                    hit0 = t0;
+                    closest0 = n0;
+                }
+                if ((pass & 2u) && t1 < hit1) {
+                    hit1 = t1;
+                    closest1 = n1;
+                }
+            } else {
+                bsPush(st, (uint32_t)child);
+                ms = (ms << 2) | pass;
+            }
+        }
+    }
+    if (b.stats) statAdd(b.stats + kStatSphereCasts, act1 ? 2u : 1u);
+    h0.t = hit0;
+    h0.n = closest0;
+    if (act1) {
+        h1.t = hit1;
+        h1.n = closest1;
+    }
+}
+
 constexpr float kCapsuleRadius = 15.f;         // consts::agentRadius
 constexpr float kCapsuleSegment = 65.f - 30.f; // standHeight - 2 * agentRadius
 

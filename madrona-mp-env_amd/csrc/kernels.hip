@@ -471,6 +471,22 @@ __device__ __forceinline__ SphereHit castNearD(const LBVH &bvh, const SceneDev &
     return h;
 }
 
+// castNearD for the low cast from o and, when act1, the high cast from
+// (o.x, o.y, z1): one traversal (bvhSphereCast2D), the same results.  The
+// path guard depends on o.xy, d and near_b only, so both casts take the
+// same branch.
+__device__ __forceinline__ void castNear2D(const LBVH &bvh, const SceneDev &sc, Vec3 o, float z1, Vec3 d,
+                                           float near_b, bool act1, SphereHit &h0, SphereHit &h1)
+{
+    if (!castPathQuirkFreeD(sc, o, d, near_b)) {
+        bvhSphereCast2D(bvh, o, z1, d, kSphereR, kFltMax, act1, h0, h1);
+        return;
+    }
+    bvhSphereCast2D(bvh, o, z1, d, kSphereR, near_b, act1, h0, h1);
+    if (!(h0.t < near_b)) h0.t = kFltMax;
+    if (act1 && !(h1.t < near_b)) h1.t = kFltMax;
+}
+
 // The full cast's t, searched within near_b first.  Vertical d only (the
 // path guard is the cell of 2o).
 __device__ __forceinline__ float castFirstNearD(const LBVH &bvh, const SceneDev &sc, Vec3 o, Vec3 d, float near_b)
@@ -601,21 +617,20 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
         const float fwd_b = (move_dist + buffer) + kCastSlack;
         ray_o = x + v_norm * buffer * 0.5f;
         ray_o.z += low_check;
-        float low_dist;
-        {
-            SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
-            low_dist = h.t;
-            if (h.t < kFltMax) normal = h.n;
-        }
+        // the low cast and (standing / crouching) the high cast from
+        // (ray_o.xy, x.z + top), traversed together
+        SphereHit hl, hh;
+        hh.t = kFltMax;
+        castNear2D(bvh, sc, ray_o, x.z + top, v_norm, fwd_b, pose != kProne, hl, hh);
+        float low_dist = hl.t;
+        if (hl.t < kFltMax) normal = hl.n;
         float high_dist = low_dist;
         bool high_hit = false;
         if (pose != kProne) {
-            ray_o.z = x.z + top;
-            SphereHit h = castNearD(bvh, sc, ray_o, v_norm, fwd_b);
-            high_dist = h.t;
+            high_dist = hh.t;
             if (high_dist < low_dist) {
                 low_dist = high_dist;
-                normal = h.n;
+                normal = hh.n;
                 high_hit = true;
             }
         }
