@@ -726,8 +726,10 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
 // only the other cast entered changes nothing for it) -- every result is
 // bit-identical to two bvhSphereCastD calls.  The x / y slab values are
 // shared (same origin xy and direction); z and the running bounds are per
-// cast.  act1 = false: cast 1 is not run (h1 untouched).
-__device__ __noinline__ void bvhSphereCast2D(const LBVH b, mp::Vec3 o0, float z1, mp::Vec3 ray_d, float r,
+// cast.  act1 = false: cast 1 is not run (h1 untouched).  Inlined into its
+// one caller: 164 VGPRs and no scratch, against 168 + 48 B of spills as a
+// call (k_move -1.3%, `profiles/r04ap_lab_cast2_inline.jsonl`).
+__device__ __forceinline__ void bvhSphereCast2D(const LBVH b, mp::Vec3 o0, float z1, mp::Vec3 ray_d, float r,
                                              float t_max0, bool act1, SphereHit &h0, SphereHit &h1)
 {
     using namespace mp;
