@@ -346,6 +346,29 @@ int mpenv_step_async(mpenv_manager *mgr, void *hip_stream);
 int mpenv_gpu_stream_init(mpenv_manager *mgr, void *hip_stream, void **buffers);
 int mpenv_gpu_stream_step(mpenv_manager *mgr, void *hip_stream, void **buffers);
 
+/* The XLA GPU custom-call targets behind SimManager.jax() (reference:
+ * madrona::py::JAXInterface::buildEntry over gpuStreamInit / gpuStreamStep,
+ * src/bindings.cpp:149-158, src/mgr.cpp:507-645).  XLA's GPU custom-call
+ * signature, API version 1 ("original"): buffers = the call's operands then
+ * its results -- the flat trainInterface array of mpenv_gpu_stream_* (inputs
+ * then outputs, mpenv_train_interface order); opaque = the bytes of an
+ * mpenv_xla_opaque naming the manager (mpenv_xla_opaque_make).  That ABI has
+ * no error return: a bad opaque or a failed launch sets mpenv_last_error on
+ * the calling thread and counts in mpenv_xla_errors(). */
+typedef struct mpenv_xla_opaque {
+    uint32_t magic;   /* MPENV_XLA_MAGIC */
+    uint32_t version; /* MPENV_XLA_VERSION */
+    uint64_t manager; /* mpenv_manager * */
+    int32_t num_buffers; /* trainInterface inputs + outputs */
+    int32_t reserved;
+} mpenv_xla_opaque;
+#define MPENV_XLA_MAGIC 0x4a4c4d58u /* "XMLJ" */
+#define MPENV_XLA_VERSION 1u
+int mpenv_xla_opaque_make(mpenv_manager *mgr, mpenv_xla_opaque *out);
+void mpenv_xla_gpu_stream_init(void *hip_stream, void **buffers, const char *opaque, size_t opaque_len);
+void mpenv_xla_gpu_stream_step(void *hip_stream, void **buffers, const char *opaque, size_t opaque_len);
+int64_t mpenv_xla_errors(void);
+
 /* Manager::*Tensor() getters (mgr.cpp:1965-2381): zero-copy view of an
  * engine-owned buffer.  dims must hold 8 entries. gpu_id = -1 for host. */
 int mpenv_export_tensor(mpenv_manager *mgr, int32_t export_id, void **ptr,
@@ -390,9 +413,15 @@ int mpenv_debug_trace_rays(mpenv_manager *mgr, const float *o_device, const floa
  * sender's shadow): the message's state, lidar and rewards, then the
  * observation system over them, so every trainInterface output of the
  * shadow equals the sender's bit for bit.  A message for another
- * configuration, of the other kind, or one whose values did not fit the
- * packed fields is not unpacked and raises the error word that
- * mpenv_wire_error returns (and clears; it synchronises the device). */
+ * configuration or shard (header world offset != the shadow's
+ * world_id_offset), of the other kind, or one whose values did not fit the
+ * packed fields is not unpacked; it raises MPENV_WIRE_ERR_REFUSED and
+ * MPENV_WIRE_ERR_DESYNC in the error word mpenv_wire_error returns (it
+ * synchronises the device).  The read clears REFUSED; DESYNC stays set --
+ * later plain messages are refused too (REFUSED again) and the shadow's
+ * observation rows are not rebuilt -- until a keyframe is unpacked. */
+#define MPENV_WIRE_ERR_REFUSED 1u
+#define MPENV_WIRE_ERR_DESYNC 2u
 int mpenv_wire_bytes(mpenv_manager *mgr, int32_t keyframe, int64_t *bytes);
 int mpenv_wire_pack(mpenv_manager *mgr, void *dst_device, int32_t keyframe, void *hip_stream);
 int mpenv_wire_unpack(mpenv_manager *mgr, const void *src_device, int32_t keyframe, void *hip_stream);

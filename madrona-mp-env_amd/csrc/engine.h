@@ -157,6 +157,9 @@ struct DevState {
 
     // Workload counters (mpenv_enable_stats), null when off: see StatId.
     unsigned long long *stats;
+    // k_obs does nothing while (*obsGate & MPENV_WIRE_ERR_DESYNC): a learner
+    // shadow whose wire history broke (wire.hip wireOk); null on the step path.
+    const uint32_t *obsGate;
 };
 
 // Per-step workload counters accumulated by the kernels in stats mode
@@ -313,6 +316,7 @@ int launchCopyBatch(const CopyBatch &b, void *stream);
 // Learner-exchange wire format (wire.hip)
 int64_t wireBytes(const DevState &s, bool keyframe);
 int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOffset, void *stream);
-int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, void *stream);
+int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, uint32_t worldOffset,
+                     void *stream);
 
 } // namespace mpenv

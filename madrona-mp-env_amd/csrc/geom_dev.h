@@ -545,7 +545,11 @@ __device__ __forceinline__ bool sphereNodeCheckD(mp::Vec3 o, mp::Vec3 inv_d, flo
     return t_min < t_max;
 }
 
-// mesh_bvh.inl:885-1127 (same quirks as the oracle restatement)
+// mesh_bvh.inl:885-1127 (same quirks as the oracle restatement).  The
+// reference marks this swept-sphere / triangle test as heavily based on Jolt
+// Physics' (Copyright 2021 Jorrit Rouwe, MIT licence; mesh_bvh.inl:894-915
+// carries the licence text); it is followed statement for statement here
+// for bit parity, so that credit and licence apply to this function too.
 // pre: unit normal, |normal|, squared edge lengths (SceneDev::triPre) --
 // the ray-independent subexpressions, same bits as computing them here.
 __device__ __forceinline__ float sphereTriD(mp::Vec3 ta, mp::Vec3 tb, mp::Vec3 tc, float4 pre0, float4 pre1,

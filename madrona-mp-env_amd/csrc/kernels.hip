@@ -2810,68 +2810,6 @@ __device__ __forceinline__ void relAnglesD(const SelfFrame &sf, Vec3 to, float &
     dist_out = d; yaw_out = yaw_delta; pitch_out = pitch_delta;
 }
 
-// fillCommonOb (sim.cpp:2720-2774) into a register array; returns alive.
-__device__ __forceinline__ bool fillCommonD(const DevState &S, const SceneDev &sc, const SelfFrame &sf, int64_t gj,
-                                            float *ob, float *pos_ob)
-{
-    ob[0] = 1.f;
-    if (!S.alive[gj]) return false;
-    ob[1] = 1.f;
-    Vec3 np = normalizedPosD(sc, ldPos(S, gj));
-    ob[2] = np.x; ob[3] = np.y; ob[4] = np.z;
-    pos_ob[0] = np.x; pos_ob[1] = np.y; pos_ob[2] = np.z;
-    ob[5] = 0.5f * ((S.ayaw[gj] / kPi) + 1.f);
-    ob[6] = 0.5f * (S.apitch[gj] / (0.25f * kPi) + 1.f);
-    Vec3 rv = rotateVec(sf.invRot, ldVel(S, gj));
-    ob[7] = rv.x; ob[8] = rv.y; ob[9] = rv.z;
-    ob[10] = S.dyv[gj]; ob[11] = S.dpv[gj];
-    const int cp = S.curPose[gj], tp = S.tgtPose[gj];
-    ob[12] = cp == kStand ? 1.f : 0.f;
-    ob[13] = cp == kCrouch ? 1.f : 0.f;
-    ob[14] = cp == kProne ? 1.f : 0.f;
-    ob[15] = tp == kStand ? 1.f : 0.f;
-    ob[16] = tp == kCrouch ? 1.f : 0.f;
-    ob[17] = tp == kProne ? 1.f : 0.f;
-    ob[18] = (float)S.transRem[gj] / (float)c::kPoseTransitionSpeed;
-    ob[19] = (S.flags[gj] & kFlagInZone) ? 1.f : 0.f;
-    const int wt = S.weapon[gj];
-    ob[20] = wt == 0 ? 1.f : 0.f;
-    ob[21] = wt == 1 ? 1.f : 0.f;
-    ob[22] = wt == 2 ? 1.f : 0.f;
-    return true;
-}
-
-__device__ __forceinline__ void fillCombatD(const DevState &S, int64_t gj, float *ob)
-{
-    ob[0] = (float)S.hp[gj] / 100.f;
-    ob[1] = (float)S.magazine[2 * gj];
-    ob[2] = (float)S.magazine[2 * gj + 1];
-    ob[3] = float(S.autohealSteps[gj]) / float(c::kOutOfCombatSteps);
-}
-
-__device__ __forceinline__ void fillOtherD(const DevState &S, const SelfFrame &sf, int64_t gj, float *ob)
-{
-    relAnglesD(sf, ldPos(S, gj) - sf.pos, ob[23], ob[24], ob[25]);
-    float rfy = S.ayaw[gj] - sf.yaw;
-    float rfp = S.apitch[gj] - sf.pitch;
-    if (rfy > kPi) rfy -= 2.f * kPi;
-    else if (rfy < -kPi) rfy += 2.f * kPi;
-    ob[26] = rfy;
-    ob[27] = rfp;
-}
-
-__device__ __forceinline__ void storeVec(float *dst, const float *src, int n)
-{
-    for (int k = 0; k < n; k++) dst[k] = src[k];
-}
-
-// fullTeamObservationsSystem (sim.cpp:3054-3301), the part owned by agent g
-// (team, slot off): its player slot in its own team's interface, its enemy
-// and last-known slots in the other team's interface (the common block is
-// the same in both, the one-hot id is the slot), and for slot 0 the team's
-// global observation and the zeroed slots past team_size.  Positions are
-// normalised without the clamp pvpObservations applies.  The lidar copy is
-// fused into k_lidar.
 __device__ __forceinline__ Vec3 normalizedPosUnclampedD(const SceneDev &sc, Vec3 p)
 {
     float min_x = sc.worldBounds.pMin.x, min_y = sc.worldBounds.pMin.y, min_z = sc.worldBounds.pMin.z;
@@ -2880,402 +2818,555 @@ __device__ __forceinline__ Vec3 normalizedPosUnclampedD(const SceneDev &sc, Vec3
     return v3((p.x - min_x) / xr, (p.y - min_y) / yr, (p.z - min_z) / zr);
 }
 
-// pvpOpponentMasksSystem (sim.cpp:2562-2614) + pvpObservationsSystem
-// (sim.cpp:2645-3052).  Lane = agent.
+// ---- k_obs: pvpOpponentMasksSystem (sim.cpp:2562-2614), pvpObservationsSystem
+// (sim.cpp:2645-3052) and fullTeamObservationsSystem (sim.cpp:3054-3301).
 //
-// Teammate / opponent observation rows ([A][slots][32] f32, 128 B each) leave
-// through LDS: written straight from the lane, one store instruction would
-// put a 16-byte piece into each of 64 rows (64 partial lines for the L2 to
-// merge); transposed per wave, each instruction writes 8 whole rows.
-constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats), 16-B aligned, banks spread
-constexpr int kObsSpanPad = 44;            // rowBuf floats per lane: >= kObsRowPad and the 43-float self obs
-constexpr int kPosPad = 19;                // posBuf floats per lane: 6 slots x 3, odd stride
+// Load first, then store.  gfx9's vector-memory counter retires loads and
+// stores in issue order, so a load issued after a burst of stores cannot be
+// waited for without waiting for those stores' write acknowledgements too.
+// The round-1..4 k_obs gathered each world-mate's fields from HBM/L2 inside
+// its slot loop, between the previous slot's row stores: every slot paid a
+// full store round trip (55 `s_waitcnt vmcnt(0)` in its ISA; ~95 us per wave
+// for ~141 KB of rows, 3.4 TB/s).  Now every input is read before the first
+// store: a block (256 consecutive agents) stages the columns of every agent
+// of its worlds in LDS (<= 256 + 2 (N - 1) agents, coalesced column loads),
+// each lane loads its own rotation and world fields, and from then on the
+// kernel only reads LDS and stores.
+//
+// Rows leave through a per-wave LDS transpose, half a wave (32 rows) at a
+// time so the stage fits next to the agent columns (3 blocks per CU): a
+// lane computes its row in registers, its half writes the rows to LDS, and
+// every lane of the wave stores whole row pieces (float4 where the rows are
+// 16-B aligned), so a store instruction writes a few whole 128-B lines
+// instead of one 4-16 B piece of 64 different rows.
+constexpr int kObsBlock = 256;
+constexpr int kObsStageMax = kObsBlock + 2 * (kMaxAgents - 1); // the block's agents plus a partial world at each end
+enum : int {
+    kOsPX, kOsPY, kOsPZ, kOsVX, kOsVY, kOsVZ, kOsYaw, kOsPitch, kOsDYV, kOsDPV, kOsHP, kOsFired, kOsAlive, // f32
+    kOsCurPose, kOsTgtPose, kOsWeapon, kOsVis, kOsTrans, kOsFlags, kOsShot, kOsHeal, kOsMag0, kOsMag1,      // i32
+    kObsCols
+};
+constexpr int kObsRowPad = kOtherObs + 4; // LDS row stride (floats) of the 32-float rows: 16-B aligned
+constexpr int kObsSpanPad = 44;           // floats per staged row: >= kObsRowPad and the 43-float self obs
 
-// Observation stores: plain (nontemporal stores for the ~1.2 GB per C3
-// step were measured no faster, round 2).
-template <typename V> __device__ __forceinline__ void obsStore(V *p, V v) { *p = v; }
+// The block's agent columns in LDS (index = global agent id - s0).
+struct ObsStage {
+    const float (*c)[kObsStageMax];
+    __device__ __forceinline__ float f(int col, int k) const { return c[col][k]; }
+    __device__ __forceinline__ int32_t i(int col, int k) const { return __float_as_int(c[col][k]); }
+    __device__ __forceinline__ Vec3 pos(int k) const { return v3(c[kOsPX][k], c[kOsPY][k], c[kOsPZ][k]); }
+    __device__ __forceinline__ Vec3 vel(int k) const { return v3(c[kOsVX][k], c[kOsVY][k], c[kOsVZ][k]); }
+    __device__ __forceinline__ bool alive(int k) const { return c[kOsAlive][k] != 0.f; }
+};
 
-
-// Flushes the wave's staged 32-float rows (lane l's row at buf + l *
-// kObsRowPad, written there by the lane) to arr[(gw0 + r) * slots + k].
-__device__ __forceinline__ void flushRowsWave(float *arr, int slots, int k, int64_t gw0, int64_t A, const float *buf,
-                                              int lane)
+// fillCommonOb (sim.cpp:2720-2774) of stage agent j into a register array;
+// returns alive.
+__device__ __forceinline__ bool fillCommonS(const ObsStage &st, const SceneDev &sc, const SelfFrame &sf, int j,
+                                            float *ob, float *pos_ob)
 {
-    // Cross-lane exchange through LDS inside one wave: the wave's DS
-    // instructions execute in issue order, so the hardware needs no wait;
-    // what must be ordered is the compiler's view.  A wavefront-scope
-    // release/acquire fence pair around a wave barrier makes the other
-    // lanes' row writes visible to this lane's reads (and, below, the reads
-    // complete before the next rows overwrite the buffer) without a
-    // data race in the source.
-    waveSync();
-    // the wave's m live lanes (a tail wave's lanes past A have returned)
-    // share its m rows x 8 chunks
-    const int m = (int)(A - gw0 < 64 ? A - gw0 : 64);
-    // wave-uniform base + 32-bit per-lane offsets (64-bit per-lane row
-    // addresses were hoisted out of the slot loops and held ~60 VGPRs)
-    float *base = arr + (gw0 * slots + k) * kOtherObs;
-#pragma unroll
-    for (int j = 0; j < kOtherObs / 4; j++) {
-        const int c = lane + j * m, r = c >> 3, col = c & 7;
-        obsStore(reinterpret_cast<float4 *>(base + r * slots * kOtherObs) + col,
-                 reinterpret_cast<const float4 *>(buf + r * kObsRowPad)[col]);
-    }
-    waveSync(); // reads done before the next rows land
+    ob[0] = 1.f;
+    if (!st.alive(j)) return false;
+    ob[1] = 1.f;
+    Vec3 np = normalizedPosD(sc, st.pos(j));
+    ob[2] = np.x; ob[3] = np.y; ob[4] = np.z;
+    pos_ob[0] = np.x; pos_ob[1] = np.y; pos_ob[2] = np.z;
+    ob[5] = 0.5f * ((st.f(kOsYaw, j) / kPi) + 1.f);
+    ob[6] = 0.5f * (st.f(kOsPitch, j) / (0.25f * kPi) + 1.f);
+    Vec3 rv = rotateVec(sf.invRot, st.vel(j));
+    ob[7] = rv.x; ob[8] = rv.y; ob[9] = rv.z;
+    ob[10] = st.f(kOsDYV, j); ob[11] = st.f(kOsDPV, j);
+    const int cp = st.i(kOsCurPose, j), tp = st.i(kOsTgtPose, j);
+    ob[12] = cp == kStand ? 1.f : 0.f;
+    ob[13] = cp == kCrouch ? 1.f : 0.f;
+    ob[14] = cp == kProne ? 1.f : 0.f;
+    ob[15] = tp == kStand ? 1.f : 0.f;
+    ob[16] = tp == kCrouch ? 1.f : 0.f;
+    ob[17] = tp == kProne ? 1.f : 0.f;
+    ob[18] = (float)st.i(kOsTrans, j) / (float)c::kPoseTransitionSpeed;
+    ob[19] = (st.i(kOsFlags, j) & kFlagInZone) ? 1.f : 0.f;
+    const int wt = st.i(kOsWeapon, j);
+    ob[20] = wt == 0 ? 1.f : 0.f;
+    ob[21] = wt == 1 ? 1.f : 0.f;
+    ob[22] = wt == 2 ? 1.f : 0.f;
+    return true;
 }
 
-// The other per-agent rows (self obs, positions, masks, last-known rows,
-// the full-team slots) are short (3-33 floats) and laid out at a per-lane
-// row offset.  Written straight from the lane, each dword store instruction
-// touches 64 different rows; staged here, lane l's n floats go to LDS (row
-// stride P, odd: conflict-free), then each store instruction writes 64
-// consecutive staged floats -- a handful of whole rows, a few cache lines.
-// `off` is the lane's row offset in floats within dst, < 0 for "no row"
-// (conditional rows: the last-known slots); `zero` stores zeros instead of
-// the staged values.  Every live lane of the wave takes part (m = live
-// lanes, the wave's first m).
-struct WaveStage {
+__device__ __forceinline__ void fillCombatS(const ObsStage &st, int j, float *ob)
+{
+    ob[0] = st.f(kOsHP, j) / 100.f;
+    ob[1] = (float)st.i(kOsMag0, j);
+    ob[2] = (float)st.i(kOsMag1, j);
+    ob[3] = float(st.i(kOsHeal, j)) / float(c::kOutOfCombatSteps);
+}
+
+__device__ __forceinline__ void fillOtherS(const ObsStage &st, const SelfFrame &sf, int j, float *ob)
+{
+    relAnglesD(sf, st.pos(j) - sf.pos, ob[23], ob[24], ob[25]);
+    float rfy = st.f(kOsYaw, j) - sf.yaw;
+    float rfp = st.f(kOsPitch, j) - sf.pitch;
+    if (rfy > kPi) rfy -= 2.f * kPi;
+    else if (rfy < -kPi) rfy += 2.f * kPi;
+    ob[26] = rfy;
+    ob[27] = rfp;
+}
+
+// Half-wave row stage.  `buf` holds 32 rows (stride P <= kObsSpanPad floats)
+// and `offs` 32 row offsets.  Half h = lanes [32h, 32h + 32) of the wave's
+// m live lanes (a tail wave's lanes past A have returned).  Pattern:
+//   stage(h, ...) by the half's lanes -> waveSync -> flush*(h, ...) by every
+//   live lane -> waveSync (reads done before the next rows land).
+// The cross-lane exchange stays inside one wave: the wave's DS instructions
+// execute in issue order, so only the compiler needs ordering, which the
+// wavefront-scope fences of waveSync give.
+struct HalfStage {
     float *buf;
     int64_t *offs;
     int lane, m;
 
-    template <int P> __device__ __forceinline__ void stage(const float *vals, int n) const
+    __device__ __forceinline__ int halves() const { return m > 32 ? 2 : 1; }
+    __device__ __forceinline__ int rowsOf(int h) const { return m - 32 * h < 32 ? m - 32 * h : 32; }
+    __device__ __forceinline__ bool mine(int h) const { return (lane >> 5) == h; }
+    template <int P> __device__ __forceinline__ void stage(int h, const float *v, int n, int at = 0) const
     {
-        for (int k = 0; k < n; k++) buf[lane * P + k] = vals[k];
+        if (mine(h))
+            for (int k = 0; k < n; k++) buf[(lane & 31) * P + at + k] = v[k];
     }
-    template <int n, int P> __device__ __forceinline__ void flush(float *dst, int64_t off, bool zero = false) const
+    __device__ __forceinline__ void stageOff(int h, int64_t off) const
     {
-        // which rows exist / are zeros: wave-wide bit masks (lane r = row r)
-        const uint64_t wbits = __ballot(off >= 0), zbits = __ballot(zero);
-        offs[lane] = off;
-        waveSync();
-        // the m live lanes (a tail wave's lanes past A have returned) share
-        // the m x n staged floats
-#pragma unroll 1
-        for (int j = 0; j < n; j++) {
-            const int c = lane + m * j;
-            const int r = c / n, col = c - r * n;
-            if ((wbits >> r) & 1u) {
-                const float v = ((zbits >> r) & 1u) ? 0.f : buf[r * P + col];
-                obsStore(dst + offs[r] + col, v);
-            }
-        }
-        waveSync(); // reads done before the next rows land
+        if (mine(h)) offs[lane & 31] = off;
     }
-    // The same for rows of n4 float4 (16-B aligned rows, P a multiple of 4):
-    // one 16-B store per lane per instruction, 4 lanes per 64-B row piece.
-    template <int n4, int P> __device__ __forceinline__ void flush4(float *dst, int64_t off, bool zero = false) const
+    // Rows of half h back to back from dst (row r at dst + r * n; the
+    // caller passes dst at the half's first row).  float4 when dst is 16-B
+    // aligned (a world group starting off a 4-agent boundary is not).
+    template <int n, int P> __device__ __forceinline__ void flushSpan(int h, float *dst) const
     {
-        static_assert(P % 4 == 0, "float4 rows");
-        const uint64_t wbits = __ballot(off >= 0), zbits = __ballot(zero);
-        offs[lane] = off;
-        waveSync();
-#pragma unroll
-        for (int j = 0; j < n4; j++) {
-            const int c = lane + m * j;
-            const int r = c / n4, col = c - r * n4;
-            if ((wbits >> r) & 1u) {
-                const float4 v = ((zbits >> r) & 1u) ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                                     : reinterpret_cast<const float4 *>(buf + r * P)[col];
-                obsStore(reinterpret_cast<float4 *>(dst + offs[r]) + col, v);
-            }
-        }
-        waveSync();
-    }
-    // A contiguous span: every live lane's row of n floats, rows back to
-    // back from dst (the row of lane r at dst + r * n -- per-agent exports
-    // whose rows the wave's agents fill completely), staged at stride P.
-    // Written as float4 (a quarter of the dword flush's store instructions;
-    // each float4 gathers its 4 floats from up to two staged rows), dwords
-    // when dst is not 16-B aligned (a world group starting off a 4-agent
-    // boundary).
-    template <int n, int P> __device__ __forceinline__ void flushSpan(float *dst) const
-    {
-        waveSync();
-        const int total = m * n;
+        const int total = rowsOf(h) * n;
         auto val = [&](int f) {
             const int r = f / n;
             return buf[r * P + (f - r * n)];
         };
-        // only the m live lanes run (a tail wave's others have returned)
         if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
             const int q4 = total >> 2;
-            for (int j = lane; j < q4; j += m)
-                obsStore(reinterpret_cast<float4 *>(dst) + j,
-                         make_float4(val(4 * j), val(4 * j + 1), val(4 * j + 2), val(4 * j + 3)));
-            if (lane < (total & 3)) obsStore(dst + 4 * q4 + lane, val(4 * q4 + lane));
+            // rolled, one division per float4 (the four floats walk the
+            // staged row and wrap to the next): unrolled, the compiler hoisted
+            // per-element LDS offsets out of the loop and held ~40 VGPRs
+#pragma unroll 1
+            for (int j = lane; j < q4; j += m) {
+                int r = (4 * j) / n, c = 4 * j - r * n;
+                float v[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    v[q] = buf[r * P + c];
+                    if (++c == n) {
+                        c = 0;
+                        r++;
+                    }
+                }
+                reinterpret_cast<float4 *>(dst)[j] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+            if (lane < (total & 3)) dst[4 * q4 + lane] = val(4 * q4 + lane);
         } else {
-            for (int f = lane; f < total; f += m) obsStore(dst + f, val(f));
+#pragma unroll 1
+            for (int f = lane; f < total; f += m) dst[f] = val(f);
         }
-        waveSync(); // reads done before the next rows land
     }
+    // 32-float rows: row r of half h to arr[((gw0 + 32h + r) * slots + k) * 32]
+    // as 8 float4 pieces (each store instruction writes 8 whole rows).
+    template <int P> __device__ __forceinline__ void flushRows32(int h, float *arr, int slots, int k, int64_t gw0) const
+    {
+        static_assert(P % 4 == 0, "float4 rows");
+        const int nc = rowsOf(h) * (kOtherObs / 4);
+        float *base = arr + ((gw0 + 32 * h) * slots + k) * kOtherObs;
+        // <= 32 rows x 8 pieces over m >= rows lanes: at most 8 rounds (4 in a full wave)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int c = lane + j * m;
+            if (c < nc) {
+                const int r = c >> 3, col = c & 7;
+                const uint32_t o = (uint32_t)(r * slots * kOtherObs + col * 4); // < 32 rows x 6 slots x 32
+                *reinterpret_cast<float4 *>(base + o) = reinterpret_cast<const float4 *>(buf + r * P)[col];
+            }
+        }
+    }
+    // Rows of n floats at per-row offsets (offs, staged with stageOff) into
+    // dst; wbits / zbits: wave ballots of "row exists" / "row is zeros".
+    template <int n, int P> __device__ __forceinline__ void flushOff(int h, float *dst, uint64_t wbits, uint64_t zbits) const
+    {
+        const uint32_t wb = (uint32_t)(wbits >> (32 * h)), zb = (uint32_t)(zbits >> (32 * h));
+        const int total = rowsOf(h) * n;
+#pragma unroll 1
+        for (int c = lane; c < total; c += m) {
+            const int r = c / n, col = c - r * n;
+            if ((wb >> r) & 1u) dst[offs[r] + col] = ((zb >> r) & 1u) ? 0.f : buf[r * P + col];
+        }
+    }
+    // The same for rows of n4 float4 (16-B aligned rows, P a multiple of 4).
+    template <int n4, int P> __device__ __forceinline__ void flushOff4(int h, float *dst, uint64_t wbits, uint64_t zbits) const
+    {
+        static_assert(P % 4 == 0, "float4 rows");
+        const uint32_t wb = (uint32_t)(wbits >> (32 * h)), zb = (uint32_t)(zbits >> (32 * h));
+        const int total = rowsOf(h) * n4;
+        for (int c = lane; c < total; c += m) {
+            const int r = c / n4, col = c - r * n4;
+            if ((wb >> r) & 1u)
+                reinterpret_cast<float4 *>(dst + offs[r])[col] =
+                    ((zb >> r) & 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : reinterpret_cast<const float4 *>(buf + r * P)[col];
+        }
+    }
+    // A contiguous span export (lane r's n floats at dst + r * n).
     template <int n> __device__ __forceinline__ void putSpan(float *dst, const float *vals) const
     {
-        constexpr int P = n | 1;
-        stage<P>(vals, n);
-        flushSpan<n, P>(dst);
-    }
-    template <int n> __device__ __forceinline__ void put(float *dst, int64_t off, const float *vals) const
-    {
-        constexpr int P = n | 1;
-        static_assert(P <= kObsRowPad, "span larger than the row buffer");
-        stage<P>(vals, n);
-        flush<n, P>(dst, off);
+        constexpr int P = n | 1; // odd stride: conflict-free staging
+        static_assert(P <= kObsSpanPad, "span larger than the row stage");
+        for (int h = 0; h < halves(); h++) {
+            stage<P>(h, vals, n);
+            waveSync();
+            flushSpan<n, P>(h, dst + (int64_t)32 * h * n);
+            waveSync();
+        }
     }
 };
 
-__device__ __forceinline__ void fullTeamSlotD(const DevState &S, const SceneDev &sc, int w, int64_t g, int team,
-                                              int off, const WaveStage &ws)
+__global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(3))) k_obs(DevState S, SceneDev sc)
 {
-    const int T = S.T;
-    const int64_t mine = (int64_t)w * 2 + team, theirs = (int64_t)w * 2 + (team ^ 1);
-    const int64_t g0 = (int64_t)w * S.N;
-    const bool alive = S.alive[g] != 0.f;
+    __shared__ float ost[kObsCols][kObsStageMax];
+    __shared__ __attribute__((aligned(16))) float rowBuf[kObsBlock / 64][32 * kObsSpanPad];
+    __shared__ int64_t offBuf[kObsBlock / 64][32];
+    // a learner shadow out of wire sync keeps its rows (wire.hip wireOk);
+    // the same word for every thread of the grid
+    if (S.obsGate && (*S.obsGate & MPENV_WIRE_ERR_DESYNC)) return;
+    const int T = S.T, N = S.N;
+    const int64_t b0 = (int64_t)xcdBlockId() * kObsBlock; // < A (grid = ceil(A / kObsBlock))
+    const int64_t g = b0 + threadIdx.x;
+    const bool live = g < S.A;
 
-    // enemy-only fields first: they decide whether the last-known slot
-    // receives the common block
-    const float fired = alive && S.firedT[g] >= 0.f ? 1.f : 0.f;
-    bool knows = fired != 0.f;
-    uint32_t los = 0;
-    if (alive) {
-        const int64_t gm0 = g0 + (team ^ 1) * T;
-        for (int m = 0; m < T; m++) los |= ((S.visMask[gm0 + m] >> off) & 1u) << m;
-        knows = knows || los != 0;
+    // ---- loads: the block's worlds' agent columns, then this lane's own
+    // rotation and world fields (no store is issued before all of them)
+    const int64_t a_end = b0 + kObsBlock < S.A ? b0 + kObsBlock : S.A;
+    const int64_t s0 = (b0 / N) * N;
+    const int ns = (int)(((a_end - 1) / N + 1) * N - s0);
+    for (int k = threadIdx.x; k < ns; k += kObsBlock) {
+        const int64_t j = s0 + k;
+        ost[kOsPX][k] = S.px[j];
+        ost[kOsPY][k] = S.py[j];
+        ost[kOsPZ][k] = S.pz[j];
+        ost[kOsVX][k] = S.vx[j];
+        ost[kOsVY][k] = S.vy[j];
+        ost[kOsVZ][k] = S.vz[j];
+        ost[kOsYaw][k] = S.ayaw[j];
+        ost[kOsPitch][k] = S.apitch[j];
+        ost[kOsDYV][k] = S.dyv[j];
+        ost[kOsDPV][k] = S.dpv[j];
+        ost[kOsHP][k] = S.hp[j];
+        ost[kOsFired][k] = S.firedT[j];
+        ost[kOsAlive][k] = S.alive[j];
+        ost[kOsCurPose][k] = __int_as_float(S.curPose[j]);
+        ost[kOsTgtPose][k] = __int_as_float(S.tgtPose[j]);
+        ost[kOsWeapon][k] = __int_as_float(S.weapon[j]);
+        ost[kOsVis][k] = __int_as_float((int32_t)S.visMask[j]);
+        ost[kOsTrans][k] = __int_as_float(S.transRem[j]);
+        ost[kOsFlags][k] = __int_as_float(S.flags[j]);
+        ost[kOsShot][k] = __int_as_float(S.wasShot[j]);
+        ost[kOsHeal][k] = __int_as_float(S.autohealSteps[j]);
+        ost[kOsMag0][k] = __int_as_float(S.magazine[2 * j]);
+        ost[kOsMag1][k] = __int_as_float(S.magazine[2 * j + 1]);
     }
-
-    // the common block (same in the player, enemy and last-known slots)
-    float cm[MPENV_FT_COMMON_DIM];
-    cm[0] = 1.f;
-    for (int k = 0; k < kMaxTeamSize; k++) cm[1 + k] = k == off ? 1.f : 0.f;
-    for (int k = 7; k < MPENV_FT_COMMON_DIM; k++) cm[k] = 0.f;
-    float ext[4] = { 0.f, 0.f, 0.f, 0.f };
-    if (alive) {
-        cm[7] = 1.f;
-        const Vec3 np = normalizedPosUnclampedD(sc, ldPos(S, g));
-        cm[8] = np.x; cm[9] = np.y; cm[10] = np.z;
-        cm[11] = 0.5f * ((S.ayaw[g] / kPi) + 1.f);
-        cm[12] = 0.5f * (S.apitch[g] / (0.25f * kPi) + 1.f);
-        cm[13] = S.vx[g]; cm[14] = S.vy[g]; cm[15] = S.vz[g];
-        const int cp = S.curPose[g], tp = S.tgtPose[g];
-        cm[16] = cp == kStand ? 1.f : 0.f;
-        cm[17] = cp == kCrouch ? 1.f : 0.f;
-        cm[18] = cp == kProne ? 1.f : 0.f;
-        cm[19] = tp == kStand ? 1.f : 0.f;
-        cm[20] = tp == kCrouch ? 1.f : 0.f;
-        cm[21] = tp == kProne ? 1.f : 0.f;
-        cm[22] = (float)S.transRem[g] / (float)c::kPoseTransitionSpeed;
-        cm[23] = (S.flags[g] & kFlagInZone) ? 1.f : 0.f;
-        ext[0] = S.hp[g] / 100.f;
-        ext[1] = (float)S.magazine[2 * g] / 30;
-        ext[2] = (float)S.magazine[2 * g + 1];
-        ext[3] = float(S.autohealSteps[g]) / float(c::kOutOfCombatSteps);
-    }
-    // one staged row (stride kObsRowPad) serves all three slots: the common
-    // block, then the enemy tail; the player tail is staged over the enemy
-    // tail after the enemy row has left
-    constexpr int P = kObsRowPad;
-    static_assert(MPENV_FT_ENEMY_DIM <= P && MPENV_FT_PLAYER_DIM <= P, "ft rows");
-    ws.stage<P>(cm, MPENV_FT_COMMON_DIM);
-    {
-        float et[MPENV_FT_ENEMY_DIM - MPENV_FT_COMMON_DIM];
-        et[0] = alive ? (float)S.wasShot[g] : 0.f;
-        et[1] = fired;
-        for (int m = 0; m < kMaxTeamSize; m++) et[2 + m] = (los >> m) & 1u ? 1.f : 0.f;
-        et[8] = knows ? 1.f : 0.f;
-        for (int k = 0; k < MPENV_FT_ENEMY_DIM - MPENV_FT_COMMON_DIM; k++)
-            ws.buf[ws.lane * P + MPENV_FT_COMMON_DIM + k] = et[k];
-    }
-    static_assert(MPENV_FT_COMMON_DIM % 4 == 0 && MPENV_FT_PLAYER_DIM % 4 == 0, "16-B ft rows");
-    ws.flush<MPENV_FT_ENEMY_DIM, P>(S.ftEnemies, (theirs * 6 + off) * MPENV_FT_ENEMY_DIM);
-    ws.flush4<MPENV_FT_COMMON_DIM / 4, P>(S.ftLastKnown, (theirs * 6 + off) * MPENV_FT_COMMON_DIM, !knows);
-    for (int k = 0; k < 4; k++) ws.buf[ws.lane * P + MPENV_FT_COMMON_DIM + k] = ext[k];
-    ws.flush4<MPENV_FT_PLAYER_DIM / 4, P>(S.ftPlayers, (mine * 6 + off) * MPENV_FT_PLAYER_DIM);
-
-    if (off != 0) return;
-    for (int s = T; s < kMaxTeamSize; s++) {
-        for (int k = 0; k < MPENV_FT_PLAYER_DIM; k++) S.ftPlayers[(mine * 6 + s) * MPENV_FT_PLAYER_DIM + k] = 0.f;
-        for (int k = 0; k < MPENV_FT_ENEMY_DIM; k++) S.ftEnemies[(mine * 6 + s) * MPENV_FT_ENEMY_DIM + k] = 0.f;
-        for (int k = 0; k < MPENV_FT_COMMON_DIM; k++) S.ftLastKnown[(mine * 6 + s) * MPENV_FT_COMMON_DIM + k] = 0.f;
-    }
-    float gob[MPENV_FT_GLOBAL_DIM];
-    gob[0] = team == 0 ? 0.f : 1.f;
-    gob[1] = team == 0 ? 1.f : 0.f;
-    gob[2] = float(c::kEpisodeLen - S.curStep[w]) / c::kEpisodeLen;
+    const int64_t gs = live ? g : S.A - 1; // tail lanes load a valid agent's fields, then leave
+    const int w = (int)(gs / N);
+    const int i = (int)(gs - (int64_t)w * N);
+    const int team = i / T, off = i - team * T;
+    const Quat rot = ldRot(S, gs);
+    const int cur_step = S.curStep[w];
+    const int fm = team == 0 ? S.filtMatched0[w] : S.filtMatched1[w];
     const int cz = S.curZone[w];
-    const AABB za = sc.tab->zoneAABB[cz];
-    const Vec3 nc = normalizedPosUnclampedD(sc, (za.pMax + za.pMin) / 2.f);
-    gob[3] = nc.x; gob[4] = nc.y; gob[5] = nc.z;
     const int ctrl = S.controlling[w];
-    gob[6] = ctrl == team ? 1.f : 0.f;
-    gob[7] = (ctrl != -1 && ctrl != team) ? 1.f : 0.f;
-    gob[8] = S.contested[w] ? 1.f : 0.f;
-    gob[9] = S.captured[w] ? 1.f : 0.f;
-    gob[10] = float(S.stepsUntilPoint[w]) / float(c::kZonePointInterval);
-    gob[11] = float(S.zoneSteps[w]) / float(c::kNumStepsPerZone);
-    for (int k = 0; k < 4; k++) gob[12 + k] = cz == k ? 1.f : 0.f;
-    storeVec(&S.ftGlobal[mine * MPENV_FT_GLOBAL_DIM], gob, MPENV_FT_GLOBAL_DIM);
-}
+    const int contested = S.contested[w], captured = S.captured[w];
+    const int until_point = S.stepsUntilPoint[w], zone_steps = S.zoneSteps[w];
+    const AABB za = sc.tab->zoneAABB[cz];
+    __syncthreads();
+    if (!live) return; // the flushes count the live lanes
 
-__global__ void __launch_bounds__(kBlock) k_obs(DevState S, SceneDev sc)
-{
-    // per wave: observation rows (stride kObsRowPad) or a whole self-obs
-    // span (stride 43); position rows of the slot loops (stride kPosPad)
-    __shared__ __attribute__((aligned(16))) float rowBuf[kBlock / 64][64 * kObsSpanPad];
-    __shared__ float posBuf[kBlock / 64][64 * kPosPad];
-    __shared__ int64_t offBuf[kBlock / 64][64];
-    const int64_t g = (int64_t)xcdBlockId() * blockDim.x + threadIdx.x;
+    const ObsStage st { ost };
     const int lane = threadIdx.x & 63;
     const int64_t gw0 = g - lane; // first agent of the wave
-    float *wbuf = rowBuf[threadIdx.x >> 6];
-    if (g >= S.A) return; // the tail wave's lanes past A (the flushes count the live ones)
-    WaveStage ws;
-    ws.buf = wbuf;
-    ws.offs = offBuf[threadIdx.x >> 6];
-    ws.lane = lane;
-    ws.m = (int)(S.A - gw0 < 64 ? S.A - gw0 : 64);
-    const int T = S.T, N = S.N;
-    const int w = (int)(g / N);
-    const int i = (int)(g - (int64_t)w * N);
+    HalfStage hs;
+    hs.buf = rowBuf[threadIdx.x >> 6];
+    hs.offs = offBuf[threadIdx.x >> 6];
+    hs.lane = lane;
+    hs.m = (int)(S.A - gw0 < 64 ? S.A - gw0 : 64);
     const int64_t g0 = (int64_t)w * N;
-    const int team = i / T, off = i - team * T;
-    const uint8_t *vm = S.visMask;
-    const bool self_alive = S.alive[g] != 0.f;
+    const int me = (int)(g - s0), l0 = (int)(g0 - s0); // stage indices: this agent, its world's first
+    const bool self_alive = st.alive(me);
 
     // ---- masks
     float mask[kMaxTeamSize];
     for (int k = 0; k < kMaxTeamSize; k++) {
         mask[k] = 0.f;
         if (!self_alive || k >= T) continue;
-        const int64_t go = g0 + (team ^ 1) * T + k;
-        if (S.alive[go] == 0.f) continue;
-        bool can_see = (vm[g] >> k) & 1;
+        const int jo = l0 + (team ^ 1) * T + k;
+        if (!st.alive(jo)) continue;
+        bool can_see = (st.i(kOsVis, me) >> k) & 1;
         for (int t = 0; t < T - 1 && !can_see; t++) {
-            const int64_t gt = g0 + team * T + (t < off ? t : t + 1);
-            if ((vm[gt] >> k) & 1) can_see = true;
+            const int jt = l0 + team * T + (t < off ? t : t + 1);
+            if ((st.i(kOsVis, jt) >> k) & 1) can_see = true;
         }
         if (can_see) mask[k] = 1.f;
-        if (S.firedT[go] >= 0) mask[k] = 1.f;
+        if (st.f(kOsFired, jo) >= 0) mask[k] = 1.f;
     }
-    ws.putSpan<6>(S.masks + gw0 * 6, mask);
+    hs.putSpan<6>(S.masks + gw0 * 6, mask);
     // teamKnowsLocation (mask[k] == 1) as bits for the opponent loop.
-    // Reading the float array there instead gives wrong last-known updates
-    // on the 2v2_navmesh_curriculum golden case at init (agents 4, 6, 9
-    // and 10 see knows(1) = 0 while their stored mask[1] is 1), with the
-    // row exchange synchronised either by s_waitcnt or by the wave barrier
-    // and wavefront fences below -- so the LDS exchange is not the cause;
-    // the bits form passes under both.  Cause (ISA, DESIGN.md §4 "k_obs
-    // mask read"): hipcc keeps a second copy of mask[] as a VGPR tuple that
-    // misses the teammate loop's can_see update (register miscompile).
+    // Reading the float array there instead gave wrong last-known updates in
+    // round 2 -- a register miscompile of the float form ("k_obs
+    // mask read"); the bits form is taken right here.
     uint32_t knowsBits = 0;
     for (int k = 0; k < kMaxTeamSize; k++) knowsBits |= (mask[k] == 1.f ? 1u : 0u) << k;
 
-    // ---- observations
-    const int cur_step = S.curStep[w];
-    const int fm = team == 0 ? S.filtMatched0[w] : S.filtMatched1[w];
     S.filters[g] = (cur_step - fm < 5) ? 1.f : 0.f;
 
+    // ---- fullTeamObservationsSystem, per (world, team): the global
+    // observation and the zeroed slots past team_size (slot-0 agents)
+    const int64_t mine = (int64_t)w * 2 + team, theirs = (int64_t)w * 2 + (team ^ 1);
+    if (off == 0) {
+        for (int s = T; s < kMaxTeamSize; s++) {
+            for (int k = 0; k < MPENV_FT_PLAYER_DIM; k++) S.ftPlayers[(mine * 6 + s) * MPENV_FT_PLAYER_DIM + k] = 0.f;
+            for (int k = 0; k < MPENV_FT_ENEMY_DIM; k++) S.ftEnemies[(mine * 6 + s) * MPENV_FT_ENEMY_DIM + k] = 0.f;
+            for (int k = 0; k < MPENV_FT_COMMON_DIM; k++) S.ftLastKnown[(mine * 6 + s) * MPENV_FT_COMMON_DIM + k] = 0.f;
+        }
+        float gob[MPENV_FT_GLOBAL_DIM];
+        gob[0] = team == 0 ? 0.f : 1.f;
+        gob[1] = team == 0 ? 1.f : 0.f;
+        gob[2] = float(c::kEpisodeLen - cur_step) / c::kEpisodeLen;
+        const Vec3 nc = normalizedPosUnclampedD(sc, (za.pMax + za.pMin) / 2.f);
+        gob[3] = nc.x; gob[4] = nc.y; gob[5] = nc.z;
+        gob[6] = ctrl == team ? 1.f : 0.f;
+        gob[7] = (ctrl != -1 && ctrl != team) ? 1.f : 0.f;
+        gob[8] = contested ? 1.f : 0.f;
+        gob[9] = captured ? 1.f : 0.f;
+        gob[10] = float(until_point) / float(c::kZonePointInterval);
+        gob[11] = float(zone_steps) / float(c::kNumStepsPerZone);
+        for (int k = 0; k < 4; k++) gob[12 + k] = cz == k ? 1.f : 0.f;
+        static_assert(MPENV_FT_GLOBAL_DIM == 16, "ft global row: 4 float4");
+        float4 *gdst = reinterpret_cast<float4 *>(&S.ftGlobal[mine * MPENV_FT_GLOBAL_DIM]);
+        for (int q = 0; q < 4; q++) gdst[q] = make_float4(gob[4 * q], gob[4 * q + 1], gob[4 * q + 2], gob[4 * q + 3]);
+    }
+
+    // ---- self observation
     SelfFrame sf;
-    sf.pos = ldPos(S, g);
-    sf.invRot = qinv(ldRot(S, g));
-    sf.yaw = S.ayaw[g];
-    sf.pitch = S.apitch[g];
-
-    float ob[kSelfObs];
-    float pos3[3];
-    for (int k = 0; k < kSelfObs; k++) ob[k] = 0.f;
-    pos3[0] = pos3[1] = pos3[2] = -1000.f;
-    const bool alive_ok = fillCommonD(S, sc, sf, g, ob, pos3);
-    if (alive_ok) {
-        fillCombatD(S, g, &ob[23]);
-        float *zo = &ob[27];
-        const int cz = S.curZone[w];
-        AABB za = sc.tab->zoneAABB[cz];
-        Vec3 center = (za.pMax + za.pMin) / 2.f;
-        Vec3 nc = normalizedPosD(sc, center);
-        zo[0] = nc.x; zo[1] = nc.y; zo[2] = nc.z;
-        relAnglesD(sf, center - sf.pos, zo[3], zo[4], zo[5]);
-        const int ctrl = S.controlling[w];
-        zo[6] = (ctrl == team) ? 1.f : 0.f;
-        zo[7] = (ctrl != -1 && ctrl != team) ? 1.f : 0.f;
-        zo[8] = S.contested[w] ? 1.f : 0.f;
-        zo[9] = S.captured[w] ? 1.f : 0.f;
-        zo[10] = float(S.stepsUntilPoint[w]) / float(c::kZonePointInterval);
-        zo[11] = float(S.zoneSteps[w]) / float(c::kNumStepsPerZone);
-        zo[12] = cz == 0 ? 1.f : 0.f;
-        zo[13] = cz == 1 ? 1.f : 0.f;
-        zo[14] = cz == 2 ? 1.f : 0.f;
-        zo[15] = cz == 3 ? 1.f : 0.f;
+    sf.pos = st.pos(me);
+    sf.invRot = qinv(rot);
+    sf.yaw = st.f(kOsYaw, me);
+    sf.pitch = st.f(kOsPitch, me);
+    {
+        float ob[kSelfObs];
+        float pos3[3];
+        for (int k = 0; k < kSelfObs; k++) ob[k] = 0.f;
+        pos3[0] = pos3[1] = pos3[2] = -1000.f;
+        if (fillCommonS(st, sc, sf, me, ob, pos3)) {
+            fillCombatS(st, me, &ob[23]);
+            float *zo = &ob[27];
+            Vec3 center = (za.pMax + za.pMin) / 2.f;
+            Vec3 nc = normalizedPosD(sc, center);
+            zo[0] = nc.x; zo[1] = nc.y; zo[2] = nc.z;
+            relAnglesD(sf, center - sf.pos, zo[3], zo[4], zo[5]);
+            zo[6] = (ctrl == team) ? 1.f : 0.f;
+            zo[7] = (ctrl != -1 && ctrl != team) ? 1.f : 0.f;
+            zo[8] = contested ? 1.f : 0.f;
+            zo[9] = captured ? 1.f : 0.f;
+            zo[10] = float(until_point) / float(c::kZonePointInterval);
+            zo[11] = float(zone_steps) / float(c::kNumStepsPerZone);
+            zo[12] = cz == 0 ? 1.f : 0.f;
+            zo[13] = cz == 1 ? 1.f : 0.f;
+            zo[14] = cz == 2 ? 1.f : 0.f;
+            zo[15] = cz == 3 ? 1.f : 0.f;
+        }
+        static_assert(kSelfObs == 43 && (kSelfObs | 1) <= kObsSpanPad, "self obs span");
+        hs.putSpan<kSelfObs>(S.selfObs + gw0 * kSelfObs, ob);
+        hs.putSpan<3>(S.selfPos + gw0 * 3, pos3);
     }
-    static_assert(kSelfObs == 43 && (kSelfObs | 1) <= kObsSpanPad, "self obs span");
-    ws.putSpan<kSelfObs>(S.selfObs + gw0 * kSelfObs, ob);
-    ws.putSpan<3>(S.selfPos + gw0 * 3, pos3);
-    // slot positions are staged per slot into posBuf and leave as one span
-    // per export after the slot loop
-    float *prow = posBuf[threadIdx.x >> 6] + lane * kPosPad;
-    WaveStage wp = ws;
-    wp.buf = posBuf[threadIdx.x >> 6];
+    const bool alive_ok = self_alive; // fillCommonOb's alive test of the agent itself
 
-    // teammate / opponent rows are built in place in the lane's LDS row
-    float *row = wbuf + lane * kObsRowPad;
-    // teammates
-    for (int k = 0; k < kMaxTeamSize - 1; k++) {
-        float *tob = row;
-        float tpos[3];
-        for (int q = 0; q < kOtherObs / 4; q++) reinterpret_cast<float4 *>(tob)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        tpos[0] = tpos[1] = tpos[2] = -1000.f;
-        if (alive_ok && k < T - 1) {
-            const int64_t gj = g0 + team * T + (k < off ? k : k + 1);
-            if (fillCommonD(S, sc, sf, gj, tob, tpos)) {
-                fillOtherD(S, sf, gj, tob);
-                fillCombatD(S, gj, &tob[28]);
+    // Slot positions (teammate, opponent, last-known rows) are recomputed
+    // after each slot loop in fully unrolled form: written from inside the
+    // rolled loops, the arrays were indexed dynamically and went to scratch,
+    // whose loads would wait behind the row stores.
+    auto slotPos = [&](bool exists, int j, float *p3) {
+        if (exists && st.alive(j)) {
+            const Vec3 np = normalizedPosD(sc, st.pos(j));
+            p3[0] = np.x; p3[1] = np.y; p3[2] = np.z;
+        } else {
+            p3[0] = p3[1] = p3[2] = -1000.f;
+        }
+    };
+    auto mateIdx = [&](int k) { return l0 + team * T + (k < off ? k : k + 1); };
+    auto oppIdx = [&](int k) { return l0 + (team ^ 1) * T + k; };
+
+    // ---- teammates
+    {
+        for (int k = 0; k < kMaxTeamSize - 1; k++) {
+            float row[kOtherObs];
+            float unused[3];
+            for (int q = 0; q < kOtherObs; q++) row[q] = 0.f;
+            if (alive_ok && k < T - 1) {
+                const int jt = mateIdx(k);
+                if (fillCommonS(st, sc, sf, jt, row, unused)) {
+                    fillOtherS(st, sf, jt, row);
+                    fillCombatS(st, jt, &row[28]);
+                }
+            }
+            for (int h = 0; h < hs.halves(); h++) {
+                hs.stage<kObsRowPad>(h, row, kOtherObs);
+                waveSync();
+                hs.flushRows32<kObsRowPad>(h, S.tmObs, 5, k, gw0);
+                waveSync();
             }
         }
-        flushRowsWave(S.tmObs, 5, k, gw0, S.A, wbuf, lane);
-        for (int q = 0; q < 3; q++) prow[3 * k + q] = tpos[q];
+        float tpos[15];
+#pragma unroll
+        for (int k = 0; k < kMaxTeamSize - 1; k++) slotPos(alive_ok && k < T - 1, mateIdx(k), &tpos[3 * k]);
+        hs.putSpan<15>(S.tmPos + gw0 * 15, tpos);
     }
-    wp.flushSpan<15, kPosPad>(S.tmPos + gw0 * 15);
 
-    // opponents (+ last known)
-    for (int k = 0; k < kMaxTeamSize; k++) {
-        float *oob = row;
-        float opos[3];
-        for (int q = 0; q < kOtherObs / 4; q++) reinterpret_cast<float4 *>(oob)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        opos[0] = opos[1] = opos[2] = -1000.f;
-        // last-known slot: cleared (opponent dead / just killed), then
-        // overwritten with the observation when the team knows the location
-        bool lk_write = false, lk_keep = false;
-        if (alive_ok && k < T) {
-            const int64_t gj = g0 + (team ^ 1) * T + k;
-            if (!fillCommonD(S, sc, sf, gj, oob, opos)) {
-                lk_write = true;
-            } else {
-                fillOtherD(S, sf, gj, oob);
-                if (S.flags[gj] & kFlagWasKilled) lk_write = true;
-                oob[28] = (float)S.wasShot[gj];
-                oob[29] = S.firedT[gj] >= 0.f ? 1.f : 0.f;
-                oob[30] = ((vm[g] >> k) & 1) ? 1.f : 0.f;
-                // teamKnowsLocation (sim.cpp:2995-3003) from the bits taken
-                // where the masks are computed ("k_obs mask read")
-                const bool knows = (knowsBits >> k) & 1u;
-                oob[31] = knows ? 1.f : 0.f;
-                lk_keep = knows;
-                lk_write = lk_write || knows;
+    // ---- opponents (+ last known)
+    {
+        uint32_t lkWrite = 0, lkKeep = 0; // per slot: last-known row written / kept (else cleared)
+        for (int k = 0; k < kMaxTeamSize; k++) {
+            float row[kOtherObs];
+            float unused[3];
+            for (int q = 0; q < kOtherObs; q++) row[q] = 0.f;
+            // last-known slot: cleared (opponent dead / just killed), then
+            // overwritten with the observation when the team knows the location
+            bool lk_write = false, lk_keep = false;
+            if (alive_ok && k < T) {
+                const int jo = oppIdx(k);
+                if (!fillCommonS(st, sc, sf, jo, row, unused)) {
+                    lk_write = true;
+                } else {
+                    fillOtherS(st, sf, jo, row);
+                    if (st.i(kOsFlags, jo) & kFlagWasKilled) lk_write = true;
+                    row[28] = (float)st.i(kOsShot, jo);
+                    row[29] = st.f(kOsFired, jo) >= 0.f ? 1.f : 0.f;
+                    row[30] = ((st.i(kOsVis, me) >> k) & 1) ? 1.f : 0.f;
+                    // teamKnowsLocation (sim.cpp:2995-3003)
+                    const bool knows = (knowsBits >> k) & 1u;
+                    row[31] = knows ? 1.f : 0.f;
+                    lk_keep = knows;
+                    lk_write = lk_write || knows;
+                }
+            }
+            lkWrite |= (lk_write ? 1u : 0u) << k;
+            lkKeep |= (lk_keep ? 1u : 0u) << k;
+            if (S.stats) statAdd(S.stats + kStatLkRows, lk_write ? 1u : 0u);
+            const uint64_t wb = __ballot(lk_write), zb = __ballot(!lk_keep);
+            for (int h = 0; h < hs.halves(); h++) {
+                hs.stage<kObsRowPad>(h, row, kOtherObs);
+                hs.stageOff(h, (g * 6 + k) * kOtherObs);
+                waveSync();
+                hs.flushRows32<kObsRowPad>(h, S.oppObs, 6, k, gw0);
+                // the staged row is also the last-known copy
+                hs.flushOff4<kOtherObs / 4, kObsRowPad>(h, S.lkObs, wb, zb);
+                waveSync();
             }
         }
-        flushRowsWave(S.oppObs, 6, k, gw0, S.A, wbuf, lane);
-        // the rows are still staged (stride kObsRowPad): the last-known copy
-        ws.flush4<kOtherObs / 4, kObsRowPad>(S.lkObs, lk_write ? (g * 6 + k) * kOtherObs : -1, !lk_keep);
-        if (S.stats) statAdd(S.stats + kStatLkRows, lk_write ? 1u : 0u);
-        for (int q = 0; q < 3; q++) prow[3 * k + q] = opos[q];
+        float opos[18];
+#pragma unroll
+        for (int k = 0; k < kMaxTeamSize; k++) slotPos(alive_ok && k < T, oppIdx(k), &opos[3 * k]);
+        hs.putSpan<18>(S.oppPos + gw0 * 18, opos);
+        // last-known positions: the written slots of each row (kept: the
+        // observed position, cleared: -1000)
         {
-            float lpos[3];
-            for (int q = 0; q < 3; q++) lpos[q] = lk_keep ? opos[q] : -1000.f;
-            ws.put<3>(S.lkPos, lk_write ? (g * 6 + k) * 3 : -1, lpos);
+            float lpos[18];
+#pragma unroll
+            for (int q = 0; q < 18; q++) lpos[q] = ((lkKeep >> (q / 3)) & 1u) ? opos[q] : -1000.f;
+            constexpr int P = 19;
+            for (int h = 0; h < hs.halves(); h++) {
+                hs.stage<P>(h, lpos, 18);
+                hs.stageOff(h, (int64_t)lkWrite); // the row's slot mask (rows at g * 18)
+                waveSync();
+                const int total = hs.rowsOf(h) * 18;
+                float *dst = S.lkPos + (gw0 + 32 * h) * 18;
+#pragma unroll 1
+                for (int c = lane; c < total; c += hs.m) {
+                    const int r = c / 18, col = c - r * 18;
+                    if ((hs.offs[r] >> (col / 3)) & 1) dst[c] = hs.buf[r * P + col];
+                }
+                waveSync();
+            }
         }
     }
-    wp.flushSpan<18, kPosPad>(S.oppPos + gw0 * 18);
 
-    fullTeamSlotD(S, sc, w, g, team, off, ws);
+    // ---- fullTeamObservationsSystem, the part owned by agent g (team, slot
+    // off): its player slot in its own team's interface, its enemy and
+    // last-known slots in the other team's interface (the common block is the
+    // same in all three, the one-hot id is the slot).  Positions are
+    // normalised without the clamp pvpObservations applies.  The lidar copy is
+    // fused into k_lidar.
+    {
+        const bool alive = self_alive;
+        // enemy-only fields first: they decide whether the last-known slot
+        // receives the common block
+        const float fired = alive && st.f(kOsFired, me) >= 0.f ? 1.f : 0.f;
+        bool knows = fired != 0.f;
+        uint32_t los = 0;
+        if (alive) {
+            const int jm0 = l0 + (team ^ 1) * T;
+            for (int mm = 0; mm < T; mm++) los |= ((st.i(kOsVis, jm0 + mm) >> off) & 1u) << mm;
+            knows = knows || los != 0;
+        }
+        float cm[MPENV_FT_ENEMY_DIM]; // the common block, then the enemy tail
+        cm[0] = 1.f;
+        for (int k = 0; k < kMaxTeamSize; k++) cm[1 + k] = k == off ? 1.f : 0.f;
+        for (int k = 7; k < MPENV_FT_COMMON_DIM; k++) cm[k] = 0.f;
+        float ext[4] = { 0.f, 0.f, 0.f, 0.f };
+        if (alive) {
+            cm[7] = 1.f;
+            const Vec3 np = normalizedPosUnclampedD(sc, st.pos(me));
+            cm[8] = np.x; cm[9] = np.y; cm[10] = np.z;
+            cm[11] = 0.5f * ((st.f(kOsYaw, me) / kPi) + 1.f);
+            cm[12] = 0.5f * (st.f(kOsPitch, me) / (0.25f * kPi) + 1.f);
+            cm[13] = st.f(kOsVX, me); cm[14] = st.f(kOsVY, me); cm[15] = st.f(kOsVZ, me);
+            const int cp = st.i(kOsCurPose, me), tp = st.i(kOsTgtPose, me);
+            cm[16] = cp == kStand ? 1.f : 0.f;
+            cm[17] = cp == kCrouch ? 1.f : 0.f;
+            cm[18] = cp == kProne ? 1.f : 0.f;
+            cm[19] = tp == kStand ? 1.f : 0.f;
+            cm[20] = tp == kCrouch ? 1.f : 0.f;
+            cm[21] = tp == kProne ? 1.f : 0.f;
+            cm[22] = (float)st.i(kOsTrans, me) / (float)c::kPoseTransitionSpeed;
+            cm[23] = (st.i(kOsFlags, me) & kFlagInZone) ? 1.f : 0.f;
+            ext[0] = st.f(kOsHP, me) / 100.f;
+            ext[1] = (float)st.i(kOsMag0, me) / 30;
+            ext[2] = (float)st.i(kOsMag1, me);
+            ext[3] = float(st.i(kOsHeal, me)) / float(c::kOutOfCombatSteps);
+        }
+        cm[MPENV_FT_COMMON_DIM + 0] = alive ? (float)st.i(kOsShot, me) : 0.f;
+        cm[MPENV_FT_COMMON_DIM + 1] = fired;
+        for (int mm = 0; mm < kMaxTeamSize; mm++) cm[MPENV_FT_COMMON_DIM + 2 + mm] = (los >> mm) & 1u ? 1.f : 0.f;
+        cm[MPENV_FT_COMMON_DIM + 8] = knows ? 1.f : 0.f;
+        static_assert(MPENV_FT_ENEMY_DIM == MPENV_FT_COMMON_DIM + 9, "ft enemy tail");
+        // one staged row serves all three slots: the common block + enemy
+        // tail; the player tail is staged over the enemy tail after the
+        // enemy row has left
+        constexpr int P = kObsRowPad;
+        static_assert(MPENV_FT_ENEMY_DIM <= P && MPENV_FT_PLAYER_DIM <= P, "ft rows");
+        static_assert(MPENV_FT_COMMON_DIM % 4 == 0 && MPENV_FT_PLAYER_DIM % 4 == 0, "16-B ft rows");
+        const uint64_t all = __ballot(true), zlk = __ballot(!knows);
+        for (int h = 0; h < hs.halves(); h++) {
+            hs.stage<P>(h, cm, MPENV_FT_ENEMY_DIM);
+            hs.stageOff(h, (theirs * 6 + off) * MPENV_FT_ENEMY_DIM);
+            waveSync();
+            hs.flushOff<MPENV_FT_ENEMY_DIM, P>(h, S.ftEnemies, all, 0ull);
+            waveSync();
+            hs.stage<P>(h, ext, 4, MPENV_FT_COMMON_DIM);
+            hs.stageOff(h, (theirs * 6 + off) * MPENV_FT_COMMON_DIM);
+            waveSync();
+            hs.flushOff4<MPENV_FT_COMMON_DIM / 4, P>(h, S.ftLastKnown, all, zlk);
+            waveSync();
+            hs.stageOff(h, (mine * 6 + off) * MPENV_FT_PLAYER_DIM);
+            waveSync();
+            hs.flushOff4<MPENV_FT_PLAYER_DIM / 4, P>(h, S.ftPlayers, all, 0ull);
+            waveSync();
+        }
+    }
 }
 
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray.  Rays are dealt to
@@ -3819,8 +3910,8 @@ int launchVisibility(const DevState &s, const SceneDev &sc, void *stream)
 
 int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
 {
-    const int blocks = (int)((s.A + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, s, sc);
+    const int blocks = (int)((s.A + kObsBlock - 1) / kObsBlock);
+    hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }
 

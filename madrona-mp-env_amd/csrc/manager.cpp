@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -879,6 +880,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         HIP_CHECK(hipSetDevice(cfg->gpu_id));
         m = new mpenv_manager();
         m->S.stats = nullptr;
+        m->S.obsGate = nullptr;
         m->cfg = *cfg;
         m->scenePath = cfg->scene_path;
         m->cfg.scene_path = m->scenePath.c_str();
@@ -1075,6 +1077,46 @@ int mpenv_debug_trace_rays(mpenv_manager *m, const float *o, const float *d, int
     return MPENV_OK;
 }
 
+// XLA GPU custom-call targets (SimManager.jax(); include/mpenv.h)
+static std::atomic<int64_t> g_xlaErrors { 0 };
+
+int mpenv_xla_opaque_make(mpenv_manager *m, mpenv_xla_opaque *out)
+{
+    if (!m || !out) return fail(MPENV_ERR_INVALID, "null argument");
+    *out = mpenv_xla_opaque {};
+    out->magic = MPENV_XLA_MAGIC;
+    out->version = MPENV_XLA_VERSION;
+    out->manager = (uint64_t)(uintptr_t)m;
+    out->num_buffers = kNumTIInputs + kNumTIOutputs;
+    return MPENV_OK;
+}
+
+static mpenv_manager *xlaManager(const char *opaque, size_t len)
+{
+    mpenv_xla_opaque o;
+    if (!opaque || len != sizeof(o)) return nullptr;
+    std::memcpy(&o, opaque, sizeof(o));
+    if (o.magic != MPENV_XLA_MAGIC || o.version != MPENV_XLA_VERSION || o.num_buffers != kNumTIInputs + kNumTIOutputs)
+        return nullptr;
+    return reinterpret_cast<mpenv_manager *>((uintptr_t)o.manager);
+}
+
+void mpenv_xla_gpu_stream_init(void *stream, void **buffers, const char *opaque, size_t opaque_len)
+{
+    mpenv_manager *m = xlaManager(opaque, opaque_len);
+    const int rc = m ? mpenv_gpu_stream_init(m, stream, buffers) : fail(MPENV_ERR_INVALID, "bad XLA opaque");
+    if (rc != MPENV_OK) g_xlaErrors.fetch_add(1);
+}
+
+void mpenv_xla_gpu_stream_step(void *stream, void **buffers, const char *opaque, size_t opaque_len)
+{
+    mpenv_manager *m = xlaManager(opaque, opaque_len);
+    const int rc = m ? mpenv_gpu_stream_step(m, stream, buffers) : fail(MPENV_ERR_INVALID, "bad XLA opaque");
+    if (rc != MPENV_OK) g_xlaErrors.fetch_add(1);
+}
+
+int64_t mpenv_xla_errors(void) { return g_xlaErrors.load(); }
+
 // Learner exchange wire format (wire.hip)
 int mpenv_wire_bytes(mpenv_manager *m, int32_t keyframe, int64_t *bytes)
 {
@@ -1096,8 +1138,10 @@ int mpenv_wire_unpack(mpenv_manager *m, const void *src, int32_t keyframe, void 
 {
     if (!m || !src) return fail(MPENV_ERR_INVALID, "null argument");
     void *st = stream ? stream : (void *)m->stream;
-    if (launchWireUnpack(m->S, static_cast<const char *>(src), keyframe != 0, m->wireErr, st) ||
-        launchObservations(m->S, m->sc, st))
+    DevState gated = m->S;
+    gated.obsGate = m->wireErr;
+    if (launchWireUnpack(m->S, static_cast<const char *>(src), keyframe != 0, m->wireErr, m->sc.worldOffset, st) ||
+        launchObservations(gated, m->sc, st))
         return fail(MPENV_ERR_HIP, "wire unpack launch failed");
     return MPENV_OK;
 }
@@ -1107,8 +1151,13 @@ int mpenv_wire_error(mpenv_manager *m, uint32_t *out)
     if (!m || !out) return fail(MPENV_ERR_INVALID, "null argument");
     try {
         HIP_CHECK(hipDeviceSynchronize());
-        HIP_CHECK(hipMemcpy(out, m->wireErr, sizeof(uint32_t), hipMemcpyDeviceToHost));
-        HIP_CHECK(hipMemset(m->wireErr, 0, sizeof(uint32_t)));
+        uint32_t v = 0;
+        HIP_CHECK(hipMemcpy(&v, m->wireErr, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        *out = v;
+        // the refused bit is cleared by this read; the desync bit stays until a
+        // keyframe is unpacked (wire.hip wireOk)
+        const uint32_t keep = v & MPENV_WIRE_ERR_DESYNC;
+        HIP_CHECK(hipMemcpy(m->wireErr, &keep, sizeof(uint32_t), hipMemcpyHostToDevice));
     } catch (const std::exception &e) {
         return fail(MPENV_ERR_HIP, e.what());
     }

@@ -123,6 +123,20 @@ enum SimFlagsE : uint32_t {
     SimFlagsE_SubZones = 1u << 11,
 };
 
+// The flat buffer array of gpuStreamInit / gpuStreamStep: exactly one
+// pointer per trainInterface input and output (the C ABI reads that many).
+std::vector<void *> streamBuffers(const std::vector<uintptr_t> &bufs)
+{
+    int32_t ni = 0, no = 0;
+    mpenv_train_interface_size(&ni, &no);
+    if (bufs.size() != (size_t)(ni + no))
+        throw py::value_error("gpu_stream_*: buffers must hold " + std::to_string(ni + no) +
+                              " pointers (trainInterface inputs then outputs), got " + std::to_string(bufs.size()));
+    std::vector<void *> b(bufs.size());
+    for (size_t k = 0; k < bufs.size(); k++) b[k] = reinterpret_cast<void *>(bufs[k]);
+    return b;
+}
+
 } // namespace
 
 PYBIND11_MODULE(madrona_mp_env, m)
@@ -230,13 +244,11 @@ PYBIND11_MODULE(madrona_mp_env, m)
         // buffer array of the XLA custom call -- trainInterface inputs then
         // outputs, caller-owned device pointers (0 = skip that tensor).
         .def("gpu_stream_init", [](PySimManager &s, uintptr_t stream, const std::vector<uintptr_t> &bufs) {
-            std::vector<void *> b(bufs.size());
-            for (size_t k = 0; k < bufs.size(); k++) b[k] = reinterpret_cast<void *>(bufs[k]);
+            std::vector<void *> b = streamBuffers(bufs);
             check(mpenv_gpu_stream_init(s.h->mgr, reinterpret_cast<void *>(stream), b.data()));
         }, py::arg("stream"), py::arg("buffers"))
         .def("gpu_stream_step", [](PySimManager &s, uintptr_t stream, const std::vector<uintptr_t> &bufs) {
-            std::vector<void *> b(bufs.size());
-            for (size_t k = 0; k < bufs.size(); k++) b[k] = reinterpret_cast<void *>(bufs[k]);
+            std::vector<void *> b = streamBuffers(bufs);
             check(mpenv_gpu_stream_step(s.h->mgr, reinterpret_cast<void *>(stream), b.data()));
         }, py::arg("stream"), py::arg("buffers"))
         // the learner exchange's compact wire format (include/mpenv.h
@@ -345,10 +357,44 @@ PYBIND11_MODULE(madrona_mp_env, m)
             ti["outputs"] = outputs;
             return ti;
         })
-        .def("jax", [](PySimManager &, py::object) -> py::object {
-            throw std::runtime_error(
-                "madrona_mp_env.SimManager.jax: the XLA custom-call hook is not built in this round "
-                "(jax is not installed; SURVEY.md §8f#1). Use train_interface() tensors with "
-                "step()/step_async().");
-        }, py::arg("gpu") = true);
+        // JAXInterface::buildEntry (bindings.cpp:149-158): the XLA GPU
+        // custom-call targets over gpuStreamInit / gpuStreamStep as PyCapsules
+        // named "xla._CUSTOM_CALL_TARGET" (what jax's
+        // xla_client.register_custom_call_target takes), the opaque bytes that
+        // name this manager, and the trainInterface the call's operand
+        // (inputs) and result (outputs) shapes come from.  Registering them
+        // needs jax, absent from this image; the targets themselves are plain
+        // C functions of XLA's API-version-1 signature (include/mpenv.h).
+        .def("jax", [](PySimManager &s, bool xla_gpu) -> py::object {
+            if (!xla_gpu)
+                throw std::runtime_error("madrona_mp_env.SimManager.jax: only the XLA GPU (ROCm) target is built; "
+                                         "ExecMode.CPU is not supported by this engine");
+            mpenv_xla_opaque o;
+            check(mpenv_xla_opaque_make(s.h->mgr, &o));
+            const char *kName = "xla._CUSTOM_CALL_TARGET";
+            py::dict d;
+            d["init"] = py::capsule(reinterpret_cast<void *>(&mpenv_xla_gpu_stream_init), kName);
+            d["step"] = py::capsule(reinterpret_cast<void *>(&mpenv_xla_gpu_stream_step), kName);
+            d["opaque"] = py::bytes(reinterpret_cast<const char *>(&o), sizeof(o));
+            d["platform"] = "ROCM";
+            d["api_version"] = 1;
+            int32_t ni = 0, no = 0;
+            mpenv_train_interface_size(&ni, &no);
+            py::list in_names, out_names;
+            for (int k = 0; k < ni; k++) {
+                const char *name; int32_t id;
+                mpenv_train_interface_entry(0, k, &name, &id);
+                in_names.append(py::str(name));
+            }
+            for (int k = 0; k < no; k++) {
+                const char *name; int32_t id;
+                mpenv_train_interface_entry(1, k, &name, &id);
+                out_names.append(py::str(name));
+            }
+            d["input_names"] = in_names;
+            d["output_names"] = out_names;
+            // keeps the manager alive as long as the registration data is
+            d["sim"] = py::cast(s);
+            return d;
+        }, py::arg("xla_gpu") = true);
 }

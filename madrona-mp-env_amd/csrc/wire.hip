@@ -40,6 +40,8 @@ using namespace mp;
 constexpr uint32_t kWireMagic = 0x3157504du; // "MPW1"
 constexpr uint32_t kWireVersion = 1;
 constexpr uint32_t kWireKeyframe = 1u, kWireOverflow = 2u;
+// error word bits (mpenv_wire_error)
+constexpr uint32_t kWireErrRefused = MPENV_WIRE_ERR_REFUSED, kWireErrDesync = MPENV_WIRE_ERR_DESYNC;
 
 // agent f32 columns, agent i32 columns, world i32 columns (order = wire order)
 #define MP_WIRE_AF(X) \
@@ -198,25 +200,35 @@ __global__ void k_wire_pack_worlds(DevState S, char *dst, WireLayout L, uint32_t
 
 // ---------------------------------------------------------------- unpack
 // Every unpack kernel checks the header first: a message for another
-// configuration, of the other kind (keyframe or not), or one the pack kernels
-// flagged is not unpacked; *err is raised (mpenv_wire_error).
-__device__ __forceinline__ bool wireOk(const DevState &S, const char *src, const WireLayout &L, uint32_t *err)
+// configuration or shard (world offset), of the other kind (keyframe or not),
+// or one the pack kernels flagged is not unpacked, and raises both error
+// bits.  A refused message leaves the shadow out of sync for good (the next
+// plain messages build on history it missed: last-known rows, episode
+// counters), so the desync bit is sticky: later plain messages are refused
+// too (refused bit again), and only a keyframe, which carries that history,
+// is unpacked and clears it (the last unpack kernel, after the others have
+// read the word).  k_obs skips a shadow whose desync bit is set
+// (DevState::obsGate), so its rows are never rebuilt from stale state.
+__device__ __forceinline__ bool wireOk(const DevState &S, const char *src, const WireLayout &L, uint32_t *err,
+                                       uint32_t worldOffset)
 {
     const WireHeader *h = reinterpret_cast<const WireHeader *>(src);
-    const bool ok = h->magic == kWireMagic && h->version == kWireVersion && h->W == S.W && h->N == S.N &&
-                    h->A == S.A && h->bytes == L.total && !(h->flags & kWireOverflow) &&
-                    ((h->flags & kWireKeyframe) != 0) == (L.lkObs >= 0);
-    if (!ok && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 1u);
+    const bool keyframe = L.lkObs >= 0;
+    const bool hdr = h->magic == kWireMagic && h->version == kWireVersion && h->W == S.W && h->N == S.N &&
+                     h->A == S.A && h->bytes == L.total && h->worldOffset == worldOffset &&
+                     !(h->flags & kWireOverflow) && ((h->flags & kWireKeyframe) != 0) == keyframe;
+    const bool ok = hdr && (keyframe || !(*(volatile uint32_t *)err & kWireErrDesync));
+    if (!ok && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, hdr ? kWireErrRefused : kWireErrRefused | kWireErrDesync);
     return ok;
 }
 
 // thread = world: world columns; a world whose episode counter moved since
 // the last message had its agents' last-known rows cleared by the reset on
 // the sender (resetAgentD / resetPersistentEntitiesD): the same here.
-__global__ void k_wire_unpack_worlds(DevState S, const char *src, WireLayout L, uint32_t *err)
+__global__ void k_wire_unpack_worlds(DevState S, const char *src, WireLayout L, uint32_t *err, uint32_t worldOffset)
 {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (!wireOk(S, src, L, err) || w >= S.W) return;
+    if (!wireOk(S, src, L, err, worldOffset) || w >= S.W) return;
     const int32_t ep = reinterpret_cast<const int32_t *>(src + L.wi[kWireWI - 1])[w];
     if (ep != S.episodeCounter[w] && L.lkObs < 0) {
         for (int64_t g = w * S.N; g < (w + 1) * S.N; g++) {
@@ -232,10 +244,10 @@ __global__ void k_wire_unpack_worlds(DevState S, const char *src, WireLayout L, 
     for (int c = 0; c < 30; c++) S.matchResult[w * 30 + c] = reinterpret_cast<const int32_t *>(src + L.match)[w * 30 + c];
 }
 
-__global__ void k_wire_unpack_agents(DevState S, const char *src, WireLayout L, uint32_t *err)
+__global__ void k_wire_unpack_agents(DevState S, const char *src, WireLayout L, uint32_t *err, uint32_t worldOffset)
 {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (!wireOk(S, src, L, err) || g >= S.A) return;
+    if (!wireOk(S, src, L, err, worldOffset) || g >= S.A) return;
     int k = 0;
 #define MP_GET_F(n) S.n[g] = reinterpret_cast<const float *>(src + L.af[k++])[g];
     MP_WIRE_AF(MP_GET_F)
@@ -266,10 +278,14 @@ __global__ void k_wire_unpack_agents(DevState S, const char *src, WireLayout L, 
     }
 }
 
-__global__ void k_wire_unpack_lidar(DevState S, const char *src, WireLayout L, uint32_t *err)
+__global__ void k_wire_unpack_lidar(DevState S, const char *src, WireLayout L, uint32_t *err, uint32_t worldOffset)
 {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (!wireOk(S, src, L, err) || r >= S.A * kLidarRays) return;
+    if (!wireOk(S, src, L, err, worldOffset)) return;
+    // an accepted keyframe resynchronises the shadow (every block of this
+    // kernel has read the word: keyframes ignore the desync bit)
+    if (L.lkObs >= 0 && r == 0) atomicAnd(err, ~kWireErrDesync);
+    if (r >= S.A * kLidarRays) return;
     const float d = reinterpret_cast<const float *>(src + L.depth)[r];
     const uint32_t b0 = (reinterpret_cast<const uint32_t *>(src + L.plane[0])[r >> 5] >> (r & 31)) & 1u;
     const uint32_t b1 = (reinterpret_cast<const uint32_t *>(src + L.plane[1])[r >> 5] >> (r & 31)) & 1u;
@@ -339,13 +355,15 @@ int launchCopyBatch(const CopyBatch &b, void *stream)
     return checkW(hipGetLastError());
 }
 
-int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, void *stream)
+int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, uint32_t worldOffset,
+                     void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     const WireLayout L = wireLayout(s.A, s.W, keyframe);
-    hipLaunchKernelGGL(k_wire_unpack_worlds, dim3(grid(s.W)), dim3(256), 0, st, s, src, L, err);
-    hipLaunchKernelGGL(k_wire_unpack_agents, dim3(grid(s.A)), dim3(256), 0, st, s, src, L, err);
-    hipLaunchKernelGGL(k_wire_unpack_lidar, dim3(grid(s.A * kLidarRays)), dim3(256), 0, st, s, src, L, err);
+    hipLaunchKernelGGL(k_wire_unpack_worlds, dim3(grid(s.W)), dim3(256), 0, st, s, src, L, err, worldOffset);
+    hipLaunchKernelGGL(k_wire_unpack_agents, dim3(grid(s.A)), dim3(256), 0, st, s, src, L, err, worldOffset);
+    hipLaunchKernelGGL(k_wire_unpack_lidar, dim3(grid(s.A * kLidarRays)), dim3(256), 0, st, s, src, L, err,
+                       worldOffset);
     return checkW(hipGetLastError());
 }
 

@@ -330,7 +330,7 @@ class LearnerWire:
     mode = "wire"
 
     def __init__(self, sim, make_shadow=None, dst: int = 0, group=None, slots: int = 2, pack=None, unpack=None,
-                 nbytes=None, device=None, overlap: bool = True):
+                 nbytes=None, device=None, overlap: bool = True, check_every: int = 0, wire_error=None):
         import torch
         import torch.distributed as dist
 
@@ -353,6 +353,14 @@ class LearnerWire:
         if any(x != (self.nb, self.nk) for x in sizes):
             raise ValueError(f"LearnerWire: message sizes differ across ranks: {sizes}")
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.torch = torch
+        self.gpu = dev.type == "cuda"
+        # each shadow's wire error word (mpenv_wire_error): nonzero once a
+        # message was refused -- the shadow is then out of sync until a
+        # keyframe, so outputs() / close() (and every `check_every` submits)
+        # raise instead of handing out stale rows
+        self._wire_error = wire_error or (lambda r: self.shadows[r].wire_error())
+        self.check_every = int(check_every)
         self.slots = slots
         if self.rank == dst:
             self.bufs = [[torch.empty(self.nk, dtype=torch.uint8, device=dev) for _ in range(self.ws)]
@@ -366,7 +374,6 @@ class LearnerWire:
         # the learner's unpack stream and, per slot, the event its unpacks end with
         self.ustream, self.udone = None, None
         if overlap and self.rank == dst and dev.type == "cuda":
-            self.torch = torch
             self.ustream = torch.cuda.Stream(device=dev)
             self.udone = [torch.cuda.Event() for _ in range(slots)]
 
@@ -376,8 +383,25 @@ class LearnerWire:
     def _caller_stream(self, stream_ptr):
         cur = self.torch.cuda.current_stream()
         if stream_ptr and stream_ptr != cur.cuda_stream:
-            raise ValueError("LearnerWire(overlap=True): submit() on a stream other than torch's current one")
+            raise ValueError("LearnerWire: submit() on a stream other than torch's current one")
         return cur
+
+    def check(self):
+        """Raise if any shadow refused a message (learner; synchronises the
+        device).  A refused message -- wrong configuration or shard, wrong
+        kind, or values the pack flagged as not fitting the wire -- leaves
+        that shadow's history (last-known rows, episode counters) behind the
+        sender's until a keyframe; its outputs are not the sender's."""
+        if self.rank != self.dst:
+            return
+        bad = {}
+        for r in sorted(self.shadows):
+            e = int(self._wire_error(r))
+            if e:
+                bad[r] = e
+        if bad:
+            raise RuntimeError(f"LearnerWire: shadow(s) refused wire messages {bad} (error bits: 1 refused, "
+                               "2 out of sync until a keyframe); their outputs are stale")
 
     def _unpack_slot(self, slot, ranks, stream_ptr):
         if self.ustream is None:
@@ -413,6 +437,12 @@ class LearnerWire:
             # pack and unpack must share a stream: 0 would put each on its own
             # manager's internal stream, unordered against each other
             raise ValueError("LearnerWire loopback: submit() needs the step's stream (not 0)")
+        if self.gpu and self.rank != self.dst:
+            # a sender packs on torch's current stream, the one the RCCL send
+            # below is ordered after (0 would be the manager's own stream: the
+            # send could ship a half-written buffer, and the next pack into
+            # the slot overwrite one still in flight)
+            stream_ptr = self._caller_stream(stream_ptr).cuda_stream
         slot = self.k % self.slots
         kf = self.k == 0
         self.k += 1
@@ -428,6 +458,8 @@ class LearnerWire:
             if self.ustream is not None:
                 self.ustream.wait_stream(self._caller_stream(stream_ptr))
             self._unpack_slot(slot, [0], stream_ptr)
+            if self.check_every and self.k % self.check_every == 0:
+                self.check()
             return slot
         if self.rank == self.dst:
             ops = [dist.P2POp(dist.irecv, self.bufs[slot][r][:n], self._peer(r), self.group)
@@ -441,6 +473,8 @@ class LearnerWire:
         prev = (slot - 1) % self.slots
         if self.slots > 1 and self.k > 1:
             self._finish(prev, stream_ptr)
+        if self.check_every and self.k % self.check_every == 0:
+            self.check()
         return slot
 
     def drain(self, stream_ptr=None):
@@ -456,6 +490,7 @@ class LearnerWire:
         if self.rank != self.dst:
             return {}
         self.drain()
+        self.check()
         own = LearnerGather.from_sim(self.sim)
         if self.loopback:  # the shadow's rebuild of the rank's own outputs
             own = LearnerGather.from_sim(self.shadows[0])
@@ -464,6 +499,7 @@ class LearnerWire:
 
     def close(self):
         self.drain()
+        self.check()
 
 
 def make_exchange(mode: str, sim, group=None, **kw):

@@ -448,8 +448,10 @@ def test_python_module_zero_copy_and_stream_step():
     ti = sim.train_interface()
     assert set(ti) == {"inputs", "outputs"}
     assert "rewards" in ti["outputs"] and "discrete" in ti["inputs"]
+    reg = sim.jax(True)  # the XLA targets (test_jax_custom_call_targets_match_gpu_stream_step)
+    assert set(reg["output_names"]) == set(ti["outputs"])
     with pytest.raises(Exception):
-        sim.jax(True)
+        sim.jax(False)  # no CPU (ExecMode.CPU) targets
 
 
 def test_kernel_timing_hooks():
@@ -528,6 +530,84 @@ def test_gpu_stream_step_buffers_abi():
         for (io, nm, ename), b in zip(names, bufs):
             if io == 1:
                 T.compare(b.cpu().numpy(), o.get(ename), f"{nm} @ {s}")
+
+
+def test_jax_custom_call_targets_match_gpu_stream_step():
+    """SimManager.jax() (JAXInterface::buildEntry, bindings.cpp:149-158): the
+    XLA GPU custom-call targets as PyCapsules named xla._CUSTOM_CALL_TARGET
+    plus the opaque bytes naming the manager.  Called as XLA would -- the
+    function pointer taken out of the capsule, (stream, operands + results,
+    opaque, len) -- on one manager, and gpu_stream_step on a twin with the
+    same inputs: every output buffer equal byte for byte.  Also: a short
+    buffer list is refused (ValueError), a foreign opaque is counted in
+    mpenv_xla_errors and touches nothing."""
+    import ctypes as C
+
+    import torch
+    import madrona_mp_env as m
+
+    ts, W, steps = 3, 32, 30
+    A = W * 2 * ts
+
+    def mk():
+        return m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=0, num_worlds=W, rand_seed=5,
+                            auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                            team_size=ts, num_pbt_policies=0, policy_history_size=0, scene_path=T.SCENE)
+
+    a, b = mk(), mk()
+    reg = a.jax(True)
+    assert reg["platform"] == "ROCM" and reg["api_version"] == 1
+    get_ptr = C.pythonapi.PyCapsule_GetPointer
+    get_ptr.restype = C.c_void_p
+    get_ptr.argtypes = [C.py_object, C.c_char_p]
+    XlaFn = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_size_t)
+    init_fn = XlaFn(get_ptr(reg["init"], b"xla._CUSTOM_CALL_TARGET"))
+    step_fn = XlaFn(get_ptr(reg["step"], b"xla._CUSTOM_CALL_TARGET"))
+    opaque = reg["opaque"]
+    ti = a.train_interface()
+    names = list(reg["input_names"]) + list(reg["output_names"])
+    assert list(reg["input_names"]) == list(ti["inputs"]) and list(reg["output_names"]) == list(ti["outputs"])
+    ref = {**{k: v.to_torch() for k, v in ti["inputs"].items()}, **{k: v.to_torch() for k, v in ti["outputs"].items()}}
+    bufs_a = [torch.zeros_like(ref[n]) for n in names]
+    bufs_b = [torch.zeros_like(ref[n]) for n in names]
+    arr_a = (C.c_void_p * len(names))(*[t.data_ptr() for t in bufs_a])
+    ptrs_b = [t.data_ptr() for t in bufs_b]
+    ni = len(reg["input_names"])
+    idx = {n: i for i, n in enumerate(names)}
+    for bufs in (bufs_a, bufs_b):
+        bufs[idx["simCtrl"]].copy_(torch.tensor([0, 1, 1], dtype=torch.int32).view_as(bufs[idx["simCtrl"]]))
+    with pytest.raises(ValueError):
+        b.gpu_stream_step(0, ptrs_b[:-1])
+    lib = T.lib_mpenv()
+    lib.mpenv_xla_errors.restype = C.c_int64
+    errs0 = lib.mpenv_xla_errors()
+    bad = bytes(len(opaque))
+    stream = torch.cuda.Stream()
+    step_fn(C.c_void_p(stream.cuda_stream), arr_a, bad, len(bad))
+    assert lib.mpenv_xla_errors() == errs0 + 1
+    # the reference's ordering: gpuStreamInit's forced reset reads simCtrl
+    # from the engine, so set it there as Manager::init callers do
+    for sim in (a, b):
+        c = sim.sim_control_tensor().to_torch()
+        c.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=c.device).view_as(c))
+    torch.cuda.synchronize()
+    init_fn(C.c_void_p(stream.cuda_stream), arr_a, opaque, len(opaque))
+    b.gpu_stream_init(stream.cuda_stream, ptrs_b)
+    stream.synchronize()
+    for s in range(steps):
+        acts = torch.from_numpy(T.mpenv_tape.tape_actions(1234, s, 0, A))
+        for bufs in (bufs_a, bufs_b):
+            bufs[idx["discrete"]].copy_(acts[:, :4].contiguous().view_as(bufs[idx["discrete"]]))
+            bufs[idx["aim"]].copy_(acts[:, 4:6].contiguous().view_as(bufs[idx["aim"]]))
+        torch.cuda.synchronize()
+        step_fn(C.c_void_p(stream.cuda_stream), arr_a, opaque, len(opaque))
+        b.gpu_stream_step(stream.cuda_stream, ptrs_b)
+        stream.synchronize()
+        for k in range(ni, len(names)):
+            x, y = bufs_a[k], bufs_b[k]
+            assert torch.equal(x.view(torch.uint8), y.view(torch.uint8)), (names[k], s)
+    assert lib.mpenv_xla_errors() == errs0 + 1
+    assert int(bufs_a[idx["hp"]].ne(0).sum()) > 0
 
 
 _edge_aimed_rays = T.edge_aimed_rays

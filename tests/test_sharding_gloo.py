@@ -286,3 +286,33 @@ def test_learner_wire_transport_three_ranks(tmp_path):
         for s, (kf, b) in enumerate(msgs):
             assert kf == (s == 0)
             assert b == _wire_bytes(r, s, kf).tobytes(), (r, s)
+
+
+def test_learner_wire_check_raises_when_a_shadow_refused_a_message():
+    """a shadow that refused a message (overflow, wrong kind,
+    another configuration or shard) is out of sync until a keyframe;
+    LearnerWire raises on its next check (every `check_every` submits, and in
+    outputs() / close()) instead of serving stale rows.  Byte-level stand-ins,
+    one gloo rank (loopback)."""
+    from mpenv_dist import LearnerWire
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        err = {0: 0}
+        lw = LearnerWire(None, make_shadow=lambda r: object(), pack=lambda p, k, s: None,
+                         unpack=lambda r, p, k, s: None, nbytes=lambda kf: 64, device=torch.device("cpu"),
+                         check_every=3, wire_error=lambda r: err[r])
+        for _ in range(3):
+            lw.submit(1)  # the third submit checks: clean
+        lw.check()
+        err[0] = 3  # refused | out of sync
+        lw.submit(1)
+        lw.submit(1)
+        with pytest.raises(RuntimeError, match="refused"):
+            lw.submit(1)  # sixth submit: checked
+        with pytest.raises(RuntimeError, match="refused"):
+            lw.close()
+    finally:
+        dist.destroy_process_group()

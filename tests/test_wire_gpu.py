@@ -109,25 +109,98 @@ def test_wire_roundtrip_full_batch_combat_and_resets():
 
 
 def test_wire_rejects_foreign_or_mismatched_messages():
+    """Refused messages (another configuration, another shard's world offset,
+    the other kind) raise REFUSED | DESYNC; the shadow then refuses plain
+    messages (its history is behind) and skips its observation rows until a
+    keyframe resynchronises it (a silently drifting shadow)."""
+    REF, DES = 1, 2
     _lib()
     a = T.Engine(64, 3)
     b = T.Engine(32, 3)
-    for x in (a, b):
+    c = T.Engine(64, 3, world_id_offset=64)  # the same configuration, another shard
+    for x in (a, b, c):
         x.put_ctrl([0, 1, 1])
         x.init()
     buf = a.mem.upload(np.zeros(_bytes(a, True), np.uint8))
+    kbuf = a.mem.upload(np.zeros(_bytes(a, True), np.uint8))
     assert a.lib.mpenv_wire_pack(a.h, buf, 0, None) == 0
+    assert a.lib.mpenv_wire_pack(a.h, kbuf, 1, None) == 0
     a.mem.hip.hipDeviceSynchronize()
     # another configuration
     assert b.lib.mpenv_wire_unpack(b.h, buf, 0, None) == 0
-    assert _error(b) == 1
+    assert _error(b) == REF | DES
+    # another shard (header world offset 0, shadow offset 64)
+    assert c.lib.mpenv_wire_unpack(c.h, buf, 0, None) == 0
+    assert _error(c) == REF | DES
     # a plain message unpacked as a keyframe
     assert a.lib.mpenv_wire_unpack(a.h, buf, 1, None) == 0
-    assert _error(a) == 1
-    # the right kind is accepted again
+    assert _error(a) == REF | DES
+    # out of sync: the right kind is still refused
+    a.step()  # the engine's own step writes its rows (no gate on the step path)
+    stepped = a.get("OPPONENT_OBSERVATIONS").copy()
+    assert a.lib.mpenv_wire_pack(a.h, buf, 0, None) == 0
+    a.mem.hip.hipDeviceSynchronize()
+    assert a.lib.mpenv_wire_unpack(a.h, buf, 0, None) == 0
+    assert _error(a) == REF | DES
+    assert _error(a) == DES  # the read cleared REFUSED only
+    # a keyframe resynchronises; plain messages are accepted again
+    assert a.lib.mpenv_wire_unpack(a.h, kbuf, 1, None) == 0
+    assert _error(a) == 0
     assert a.lib.mpenv_wire_unpack(a.h, buf, 0, None) == 0
     assert _error(a) == 0
+    T.compare(a.get("OPPONENT_OBSERVATIONS"), stepped, "rows rebuilt after the resync")
     a.mem.free(buf)
+    a.mem.free(kbuf)
+
+
+def test_learner_wire_raises_on_a_refused_message():
+    """LearnerWire (loopback through the Python module) must not serve a
+    shadow that refused a message: a message whose header carries the pack
+    kernel's overflow flag is refused, and outputs() raises."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    import madrona_mp_env as m
+    from mpenv_dist import LearnerWire
+
+    ts, W = 3, 64
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        def mk():
+            return m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=0, num_worlds=W, rand_seed=5,
+                                auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                                team_size=ts, num_pbt_policies=0, policy_history_size=0, scene_path=T.SCENE)
+
+        sim = mk()
+        sim.init()
+        corrupt = [False]
+        lw = None
+
+        def pack(ptr, kf, st):
+            sim.wire_pack(ptr, kf, st)
+            if corrupt[0]:  # the header's flags word (offset 8): kWireOverflow
+                t = [b for slot in lw.bufs for b in slot if b.data_ptr() == ptr][0]
+                t[8] = t[8] | 2
+
+        st = torch.cuda.Stream()
+        torch.cuda.set_stream(st)
+        lw = LearnerWire(sim, make_shadow=lambda r: mk(), pack=pack, device=torch.device("cuda", 0))
+        for s in range(4):
+            sim.step_async(st.cuda_stream)
+            lw.submit(st.cuda_stream)
+        lw.outputs()  # in sync
+        corrupt[0] = True
+        sim.step_async(st.cuda_stream)
+        lw.submit(st.cuda_stream)
+        with pytest.raises(RuntimeError, match="refused"):
+            lw.outputs()
+    finally:
+        torch.cuda.set_stream(torch.cuda.default_stream())
+        dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("overlap", [True, False])

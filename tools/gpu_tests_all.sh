@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-TAG=${TAG:-r04m}
+TAG=${TAG:?set TAG}
 timeout -k 10 1100 python -u -m pytest tests -m gpu ${XFLAG:--x} -v -s --timeout 600 --timeout-method thread ${K:+-k "$K"} > gpurun_out/${TAG}_gpu_tests.log 2>&1
 rc=$?
 tail -15 gpurun_out/${TAG}_gpu_tests.log

@@ -15,9 +15,10 @@ there and compiles that copy, so no lab hook sits in the shipped sources.
                               _SIM_SKIP=, _PHASE_T, _WAVE_HIST=k, _WORK, _NO_TRI,
                               _NO_BVH, _NO_CAPSULE, _NO_REAR, _NO_FT_LIDAR, ...,
                               and the dropped variants (MPENV_LIDAR_PERM,
-                              MPENV_TRI_FLAT, MPENV_OBS_NT, MPENV_*_WPE, ...)
-  tools/lab/fan_phases.patch  k_lidar_fan per-phase wave cycles and work counts
-                              (read back through mpenv_lab_fan)
+                              MPENV_TRI_FLAT, MPENV_*_WPE, ...); the round-1..4
+                              k_obs switches went with that kernel (round 5)
+  (round 4's forward-fan candidate lists, fan_lists.patch / fan_phases.patch,
+  are in git history before round 5: measured and dropped)
 e.g. build phase --patch tools/lab/lab_hooks.patch -DMPENV_LAB_PHASE_T
 (tests/test_abi.py checks that every patch still applies to csrc/).
 """
