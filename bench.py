@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--worlds", type=int, default=16384, help="worlds per GPU")
     ap.add_argument("--team-size", type=int, default=6)
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "simple_map"))
-    ap.add_argument("--world-groups", type=int, default=2,
+    ap.add_argument("--world-groups", type=int, default=1,
                     help="world ranges stepped on concurrent streams in the timed pass (engine option); "
                          "the profile pass always runs one group so kernel times are exclusive")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -105,6 +105,11 @@ def parse():
                          "caller buffers, the step, every output copied into caller buffers")
     ap.add_argument("--policy-hidden", type=int, default=512, help="policy MLP width (--actions policy)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--learner-dedicated", choices=["auto", "on", "off"], default="auto",
+                    help="--exchange wire at N > 1: rank 0 is a learner that simulates nothing -- it only "
+                         "receives and unpacks ranks 1..N-1's messages into their shadows (C4 as 7 "
+                         "simulators + 1 learner); value counts the simulator ranks' agent-steps.  auto: "
+                         "from 4 ranks up (below that a learner that also simulates carries more)")
     ap.add_argument("--share-device", action="store_true",
                     help="debug: map every rank to GPU 0 (rehearse N>1 on a one-GPU box; no --gather)")
     ap.add_argument("--wire-serial", action="store_true",
@@ -298,6 +303,11 @@ def main():
     exchange = "gather" if args.gather else args.exchange
     if exchange == "auto":
         exchange = "wire" if world_size > 1 and not args.share_device else "none"
+    dedicated = exchange == "wire" and world_size > 1 and (
+        args.learner_dedicated == "on" or (args.learner_dedicated == "auto" and world_size >= 4))
+    learner_only = dedicated and rank == 0  # this rank simulates nothing
+    sims = world_size - 1 if dedicated else world_size  # simulator ranks
+    si = rank - 1 if dedicated else rank  # this rank's shard (simulator ranks)
     if exchange != "none":
         # the step, the pack / unpack and the transfers on one explicit
         # stream (the default stream's handle, 0, means each manager's own
@@ -327,18 +337,22 @@ def main():
     W, ts = args.worlds, args.team_size
     N = 2 * ts
     A = W * N
-    offset = rank * W  # weak scaling: each rank owns W global worlds
-    sim = m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=gpu, num_worlds=W, rand_seed=5,
-                       auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
-                       team_size=ts, num_pbt_policies=0, policy_history_size=0,
-                       scene_path=args.scene, world_id_offset=offset)
-    sim.set_world_groups(args.world_groups)
-    groups = sim.world_groups()
-    ctrl = sim.sim_control_tensor().to_torch()
+    offset = si * W  # weak scaling: each simulator rank owns W global worlds
+    sim = None
+    if not learner_only:
+        sim = m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=gpu, num_worlds=W, rand_seed=5,
+                           auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
+                           team_size=ts, num_pbt_policies=0, policy_history_size=0,
+                           scene_path=args.scene, world_id_offset=offset)
+        sim.set_world_groups(args.world_groups)
+    groups = sim.world_groups() if sim is not None else 0
+    ctrl = sim.sim_control_tensor().to_torch() if sim is not None else None
 
     def start_episode():
         # Manager::init -- a forced reset of every world (simCtrl [0, 1, 1]:
         # random start step and team sides, scripts/jax_train.py:377)
+        if sim is None:
+            return
         ctrl.copy_(torch.tensor([0, 1, 1], dtype=torch.int32, device=dev).view_as(ctrl))
         torch.cuda.synchronize()
         sim.init()
@@ -352,7 +366,7 @@ def main():
         torch.cuda.synchronize()
 
     start_episode()
-    ring = torch.from_numpy(mpenv_tape.tape_ring(TAPE_SEED, offset * N, A, RING)).to(dev)
+    ring = torch.from_numpy(mpenv_tape.tape_ring(TAPE_SEED, offset * N, A, RING)).to(dev) if sim is not None else None
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     def make_shadow(r):
@@ -361,24 +375,31 @@ def main():
         return m.SimManager(exec_mode=m.madrona.ExecMode.CUDA, gpu_id=gpu, num_worlds=W, rand_seed=5,
                             auto_reset=True, sim_flags=int(m.SimFlags.Default), task_type=m.Task.Zone,
                             team_size=ts, num_pbt_policies=0, policy_history_size=0,
-                            scene_path=args.scene, world_id_offset=r * W)
+                            scene_path=args.scene, world_id_offset=(r - 1 if dedicated else r) * W)
 
     if exchange == "local":
         learner = make_exchange(exchange, sim, group=xgroup, grad_bytes=int(args.grad_mb * (1 << 20)),
                                 update_every=args.update_every)
     elif exchange == "wire":
-        learner = make_exchange(exchange, sim, group=xgroup, make_shadow=make_shadow, overlap=not args.wire_serial)
+        learner = make_exchange(exchange, sim, group=xgroup, make_shadow=make_shadow, overlap=not args.wire_serial,
+                                dedicated=dedicated, unpack_streams=4 if dedicated else 1)
     else:
         learner = make_exchange(exchange, sim, group=xgroup)
 
-    policy = make_policy(sim, args.policy_hidden, dev) if args.actions == "policy" else None
+    policy = make_policy(sim, args.policy_hidden, dev) if args.actions == "policy" and sim is not None else None
     stream_ptrs = None
-    if args.path == "stream":
+    if args.path == "stream" and sim is not None:
         if args.actions != "tape":
             raise SystemExit("--path stream runs the tape actions only")
         stream_ptrs, stream_bytes, _keep = stream_buffers(sim, ring, dev)
 
-    def one_step(s):
+    def one_step(s, exchange_on=True):
+        if learner_only:
+            # the dedicated learner: receive this step's messages, unpack the
+            # previous step's into the shadows (LearnerWire.submit)
+            if exchange_on:
+                learner.submit(sptr)
+            return
         if stream_ptrs is not None:
             # gpuStreamStep: inputs from the caller's buffers (the step's
             # actions straight from the ring), the step, outputs copied out
@@ -395,7 +416,7 @@ def main():
             else:
                 sim.copy_actions(ring[s % RING].data_ptr(), sptr)
             sim.step_async(sptr)
-        if learner is not None:
+        if learner is not None and exchange_on:
             learner.submit(sptr)
 
     # ---- timed pass: W warmup steps, then K steps, no events or counters
@@ -418,7 +439,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_agent_steps = world_size * A * args.steps
+    total_agent_steps = sims * A * args.steps
     value = total_agent_steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
@@ -427,8 +448,10 @@ def main():
     # every kernel runs alone and its HIP-event duration is exclusive; then
     # once more with the kernels' workload counters on (their atomics slow
     # the kernels, so counters and timings never share a pass).
+    # The exchange is not part of these passes (their windows restart the
+    # episode; the learner's shadows are left as the timed pass left them).
     prof_pass = None
-    if not args.no_profile_pass:
+    if not args.no_profile_pass and not learner_only:
         if learner is not None:
             learner.drain()
         sim.set_world_groups(1)
@@ -436,12 +459,12 @@ def main():
         def window(timing, stats):
             start_episode()
             for s in range(args.warmup):
-                one_step(s)
+                one_step(s, exchange_on=False)
             torch.cuda.synchronize()
             sim.enable_kernel_timing(timing)
             sim.enable_stats(stats)
             for s in range(args.steps):
-                one_step(args.warmup + s)
+                one_step(args.warmup + s, exchange_on=False)
             torch.cuda.synchronize()
             out = sim.kernel_timings() if timing else sim.read_stats()
             sim.enable_kernel_timing(False)
@@ -458,7 +481,8 @@ def main():
         + ("" if args.path == "step" else " + gpuStreamStep buffer copies")
     result = {
         "metric": f"env steps/sec x agents (whole node), simple_map {ts}v{ts} @ {W} worlds"
-                  + ("" if world_size == 1 else f"/GPU x {world_size} GPUs"),
+                  + ("" if world_size == 1 else f"/GPU x {sims} GPUs")
+                  + (" + 1 dedicated learner GPU" if dedicated else ""),
         "value": round(value, 1),
         "unit": "agent-steps/s",
         "n_gpus": world_size,
@@ -478,7 +502,7 @@ def main():
             "workload": workload,
             "worlds_per_gpu": W,
             "agents_per_gpu": A,
-            "total_worlds": W * world_size,
+            "total_worlds": W * sims,
             "task": "Zone",
             "sim_flags": "Default",
             "sim_control": [0, 1, 1],
@@ -486,8 +510,9 @@ def main():
             "rand_seed": 5,
             "world_groups": groups,
             "actions": args.actions,
-            "parallelism": f"world-sharded x{world_size}" + ("" if learner is None else
-                                                             f" + RCCL learner exchange ({exchange})"),
+            "parallelism": f"world-sharded x{sims}" + ("" if learner is None else
+                                                       f" + RCCL learner exchange ({exchange}"
+                                                       + (", dedicated learner rank 0)" if dedicated else ")")),
             "exchange": exchange,
         },
         "world_steps_per_s": round(value / N, 1),
@@ -570,6 +595,14 @@ def main():
             "rays_per_s": round(rays / steps / (ms_per_step * 1e-3), 1),
             "bvh_queries_per_s": round((rays + counts["sphere_casts"]) / steps / (ms_per_step * 1e-3), 1),
         }
+    if dedicated:
+        # the learner rank simulates nothing: the first simulator rank's
+        # profile pass stands for the step kernels
+        obj = [{k: result[k] for k in ("roofline", "kernels_ms", "step_hbm", "workload") if k in result}]
+        dist.broadcast_object_list(obj, src=1)
+        if rank == 0:
+            result.update(obj[0])
+            result["profile_rank"] = 1
     if rank == 0 and world_size == 1 and args.cpu_baseline == "auto":
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

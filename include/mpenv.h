@@ -431,13 +431,23 @@ int mpenv_wire_error(mpenv_manager *mgr, uint32_t *out);
  * graph is re-captured whenever a kernel argument struct changes: world
  * groups, stats or timing buffers; every other step replays it). */
 int mpenv_graph_captures(mpenv_manager *mgr, int64_t *out);
+/* Whether steps replay the captured graph (1) or launch kernel by kernel
+ * (0), and why not: a capture that fails (capture invalidated, unjoined
+ * fork, end-capture or instantiate error) is abandoned -- the step runs its
+ * kernels directly -- and the reason is kept here (reason: a buffer of
+ * reason_len bytes, may be null). */
+int mpenv_graph_status(mpenv_manager *mgr, int32_t *graph_on, char *reason, int32_t reason_len);
 
 /* Extension: step the worlds as `groups` contiguous ranges on concurrent
  * HIP streams (fork/join on the step stream; results identical for any
- * split).  Default: 2 for >= 3072 worlds, else 1; env MPENV_WORLD_GROUPS
- * overrides at creation.  Capped at 3. */
+ * split).  Default 1 (round 5: one group measured fastest); env
+ * MPENV_WORLD_GROUPS overrides at creation.  Capped at 3. */
 int mpenv_set_world_groups(mpenv_manager *mgr, int32_t groups);
 int mpenv_world_groups(mpenv_manager *mgr, int32_t *groups);
+/* Extension: with one world group, run k_lidar on a branch stream beside
+ * k_vis -> k_obs (fork after k_sim, join at the end of the step; results
+ * identical).  Default off; env MPENV_LIDAR_BRANCH=1 at creation. */
+int mpenv_set_lidar_branch(mpenv_manager *mgr, int32_t on);
 
 /* Manager::triggerReset (mgr.cpp:2484-2500) */
 int mpenv_trigger_reset(mpenv_manager *mgr, int32_t world_idx);

@@ -119,6 +119,11 @@ struct mpenv_manager {
     std::vector<SceneDev> gsc;
     hipEvent_t forkEv = nullptr;
     std::vector<hipEvent_t> joinEv;
+    // One group only: k_lidar on a branch stream beside k_vis -> k_obs (no
+    // data dependence between them after k_sim).  MPENV_LIDAR_BRANCH=1.
+    bool lidarBranch = false;
+    hipStream_t bStream = nullptr;
+    hipEvent_t bForkEv = nullptr, bJoinEv = nullptr;
 
     // Record / replay / event logs (mgr.cpp:155-300: per-step file I/O
     // around the Step graph)
@@ -153,6 +158,7 @@ struct mpenv_manager {
     // launch may still run on a caller stream the manager does not own)
     hipEvent_t graphDoneEv = nullptr;
     int64_t graphCaptures = 0; // mpenv_graph_captures
+    std::string graphOffReason; // why the step is not replayed from a graph (mpenv_graph_status)
     uint32_t *wireErr = nullptr; // device word raised by a rejected wire message (wire.hip)
 
     ~mpenv_manager()
@@ -170,6 +176,12 @@ struct mpenv_manager {
         for (hipEvent_t e : joinEv) (void)hipEventDestroy(e);
         if (forkEv) (void)hipEventDestroy(forkEv);
         for (hipStream_t gs : gstreams) (void)hipStreamDestroy(gs);
+        if (bStream) {
+            (void)hipStreamSynchronize(bStream);
+            (void)hipStreamDestroy(bStream);
+        }
+        if (bForkEv) (void)hipEventDestroy(bForkEv);
+        if (bJoinEv) (void)hipEventDestroy(bJoinEv);
         for (FILE *f : { replayFile, recordFile, eventsFile, stepsFile })
             if (f) std::fclose(f);
         for (void *p : allocations) (void)hipFree(p);
@@ -220,6 +232,16 @@ struct mpenv_manager {
         record(st);
         if (launchSimStep(R, rsc, st)) throw std::runtime_error("k_sim launch failed");
         record(st);
+        if (lidarBranch && groups == 1 && !timing) {
+            HIP_CHECK(hipEventRecord(bForkEv, st));
+            HIP_CHECK(hipStreamWaitEvent(bStream, bForkEv, 0));
+            if (launchLidar(R, rsc, bStream)) throw std::runtime_error("k_lidar launch failed");
+            HIP_CHECK(hipEventRecord(bJoinEv, bStream));
+            if (launchVisibility(R, rsc, st)) throw std::runtime_error("k_vis launch failed");
+            if (launchObservations(R, rsc, st)) throw std::runtime_error("k_obs launch failed");
+            HIP_CHECK(hipStreamWaitEvent(st, bJoinEv, 0));
+            return;
+        }
         if (launchVisibility(R, rsc, st)) throw std::runtime_error("k_vis launch failed");
         record(st);
         if (launchObservations(R, rsc, st)) throw std::runtime_error("k_obs launch failed");
@@ -280,6 +302,7 @@ struct mpenv_manager {
             k.insert(k.end(), c, c + n);
         };
         put(&groups, sizeof(groups));
+        put(&lidarBranch, sizeof(lidarBranch));
         put(&S, sizeof(S));
         put(&sc, sizeof(sc));
         for (const DevState &G : gS) put(&G, sizeof(G));
@@ -304,23 +327,60 @@ struct mpenv_manager {
             // capture on a private stream (the caller's may be the legacy
             // default stream, which cannot be captured); the group streams
             // join the capture through the fork event
-            HIP_CHECK(hipStreamBeginCapture(capStream, hipStreamCaptureModeThreadLocal));
-            try {
-                launchStepDirect(capStream);
-            } catch (...) {
-                hipGraph_t g = nullptr;
-                (void)hipStreamEndCapture(capStream, &g);
-                if (g) (void)hipGraphDestroy(g);
-                throw;
+            if (!captureStep()) {
+                // abandoned capture: this and later steps launch directly
+                launchStepDirect(st);
+                return;
             }
-            HIP_CHECK(hipStreamEndCapture(capStream, &stepGraph));
-            HIP_CHECK(hipGraphInstantiate(&stepExec, stepGraph, nullptr, nullptr, 0));
             graphKey = std::move(key);
             graphCaptures++;
         }
         HIP_CHECK(hipGraphLaunch(stepExec, st));
         if (!graphDoneEv) HIP_CHECK(hipEventCreateWithFlags(&graphDoneEv, hipEventDisableTiming));
         HIP_CHECK(hipEventRecord(graphDoneEv, st));
+    }
+
+    // Captures the Step graph into stepGraph / stepExec.  Every capture call
+    // is checked, and so is the capture's state before it ends (an enqueue
+    // that invalidated it, a fork not joined back): on any failure the
+    // capture is ended and discarded, the graph is switched off with the
+    // reason kept (mpenv_graph_status), and false is returned -- a bad
+    // capture is never instantiated or launched.
+    bool captureStep()
+    {
+        auto abandon = [&](const std::string &why) {
+            hipGraph_t g = nullptr;
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(capStream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+                (void)hipStreamEndCapture(capStream, &g);
+            if (g) (void)hipGraphDestroy(g);
+            if (stepExec) (void)hipGraphExecDestroy(stepExec);
+            if (stepGraph) (void)hipGraphDestroy(stepGraph);
+            stepExec = nullptr;
+            stepGraph = nullptr;
+            (void)hipGetLastError(); // clear the sticky launch error of a failed capture call
+            useGraph = false;
+            graphOffReason = why;
+            std::fprintf(stderr, "mpenv: step graph off (%s); launching kernels directly\n", why.c_str());
+            return false;
+        };
+        hipError_t e = hipStreamBeginCapture(capStream, hipStreamCaptureModeThreadLocal);
+        if (e != hipSuccess) return abandon(std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+        try {
+            launchStepDirect(capStream);
+        } catch (const std::exception &ex) {
+            return abandon(std::string("enqueue during capture: ") + ex.what());
+        }
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        unsigned long long id = 0;
+        e = hipStreamGetCaptureInfo(capStream, &cs, &id);
+        if (e != hipSuccess) return abandon(std::string("hipStreamGetCaptureInfo: ") + hipGetErrorString(e));
+        if (cs != hipStreamCaptureStatusActive) return abandon("capture invalidated before its end");
+        e = hipStreamEndCapture(capStream, &stepGraph);
+        if (e != hipSuccess || !stepGraph) return abandon(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+        e = hipGraphInstantiate(&stepExec, stepGraph, nullptr, nullptr, 0);
+        if (e != hipSuccess || !stepExec) return abandon(std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+        return true;
     }
 
     void launchStepDirect(hipStream_t st)
@@ -905,13 +965,17 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m->cfg.curriculum_data_path = nullptr;
         {
             // World groups (concurrent streams).  MPENV_WORLD_GROUPS overrides.
-            // Two measured best at C3 in round 2 (1.447 ms/step against
-            // 1.468 with one and 1.497 with three).
-            int want = m->S.W >= 3072 ? 2 : 1;
+            // Two measured best at C3 in rounds 2-4 (round 2: 1.447 ms/step
+            // against 1.468 with one); since round 5's load-first k_obs one
+            // group is faster (driver window 1.23 vs 1.30 ms, steady 1.178 vs
+            // 1.215; profiles/r05e_ab.jsonl).
+            int want = 1;
             if (const char *e = std::getenv("MPENV_WORLD_GROUPS")) want = std::atoi(e);
             m->setupGroups(want);
         }
         if (const char *e = std::getenv("MPENV_STEP_GRAPH")) m->useGraph = std::atoi(e) != 0;
+        if (const char *e = std::getenv("MPENV_LIDAR_BRANCH"))
+            if (std::atoi(e) != 0 && mpenv_set_lidar_branch(m, 1) != MPENV_OK) throw std::runtime_error(g_last_error);
         // TrainControl from sim flags (mgr.cpp:1397-1413)
         int32_t tc[3] = { (cfg->sim_flags & MPENV_SIMFLAG_SIM_EVAL_MODE) ? 1 : 0,
                           (cfg->sim_flags & MPENV_SIMFLAG_STAGGER_STARTS) ? 1 : 0,
@@ -1168,6 +1232,33 @@ int mpenv_graph_captures(mpenv_manager *m, int64_t *out)
 {
     if (!m || !out) return fail(MPENV_ERR_INVALID, "null argument");
     *out = m->graphCaptures;
+    return MPENV_OK;
+}
+
+int mpenv_graph_status(mpenv_manager *m, int32_t *graph_on, char *reason, int32_t reason_len)
+{
+    if (!m || !graph_on) return fail(MPENV_ERR_INVALID, "null argument");
+    *graph_on = m->useGraph ? 1 : 0;
+    if (reason && reason_len > 0) {
+        std::snprintf(reason, (size_t)reason_len, "%s", m->graphOffReason.c_str());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_set_lidar_branch(mpenv_manager *m, int32_t on)
+{
+    if (!m) return fail(MPENV_ERR_INVALID, "null argument");
+    try {
+        HIP_CHECK(hipStreamSynchronize(m->stream));
+        if (on && !m->bStream) {
+            HIP_CHECK(hipStreamCreateWithFlags(&m->bStream, hipStreamNonBlocking));
+            HIP_CHECK(hipEventCreateWithFlags(&m->bForkEv, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&m->bJoinEv, hipEventDisableTiming));
+        }
+        m->lidarBranch = on != 0;
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
     return MPENV_OK;
 }
 

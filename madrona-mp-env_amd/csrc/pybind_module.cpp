@@ -272,6 +272,13 @@ PYBIND11_MODULE(madrona_mp_env, m)
             return e;
         })
         .def("set_world_groups", [](PySimManager &s, int32_t g) { check(mpenv_set_world_groups(s.h->mgr, g)); })
+        .def("set_lidar_branch", [](PySimManager &s, bool on) { check(mpenv_set_lidar_branch(s.h->mgr, on ? 1 : 0)); })
+        .def("graph_status", [](PySimManager &s) {
+            int32_t on = 0;
+            char why[512] = {};
+            check(mpenv_graph_status(s.h->mgr, &on, why, sizeof(why)));
+            return py::make_tuple(on != 0, std::string(why));
+        })
         .def("world_groups", [](PySimManager &s) { int32_t g = 0; check(mpenv_world_groups(s.h->mgr, &g)); return g; })
         .def("enable_kernel_timing", [](PySimManager &s, bool on) { check(mpenv_enable_kernel_timing(s.h->mgr, on)); })
         .def("enable_stats", [](PySimManager &s, bool on) { check(mpenv_enable_stats(s.h->mgr, on)); })

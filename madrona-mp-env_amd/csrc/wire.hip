@@ -222,79 +222,121 @@ __device__ __forceinline__ bool wireOk(const DevState &S, const char *src, const
     return ok;
 }
 
-// thread = world: world columns; a world whose episode counter moved since
-// the last message had its agents' last-known rows cleared by the reset on
-// the sender (resetAgentD / resetPersistentEntitiesD): the same here.
-__global__ void k_wire_unpack_worlds(DevState S, const char *src, WireLayout L, uint32_t *err, uint32_t worldOffset)
+// One launch, four block ranges (no kernel boundaries between the parts of
+// an unpack: round 4's three launches spent ~20 us in boundaries and short
+// blocks):
+//   lidar   thread = 4 consecutive rays of one agent (80 and 64 are
+//           multiples of 4, so a quad is all-forward or all-rear): one float4
+//           of depths, 4 bits of each class plane (one word), 64 contiguous
+//           bytes of f32 lidar out;
+//   agents  thread = agent: the state columns (+ a keyframe's last-known rows);
+//   worlds  thread = world: the world columns; a world whose episode counter
+//           moved since the last message had its agents' last-known rows
+//           cleared by the reset on the sender (resetAgentD /
+//           resetPersistentEntitiesD): the same here;
+//   match   thread = 16 bytes of the [W][30] episode results, copied flat.
+struct WireUnpackGrid {
+    uint32_t lidar, agents, worlds, match; // first block of each range (lidar = 0), then the total
+    uint32_t total;
+};
+
+__host__ __device__ inline WireUnpackGrid wireUnpackGrid(int64_t A, int64_t W)
 {
-    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (!wireOk(S, src, L, err, worldOffset) || w >= S.W) return;
-    const int32_t ep = reinterpret_cast<const int32_t *>(src + L.wi[kWireWI - 1])[w];
-    if (ep != S.episodeCounter[w] && L.lkObs < 0) {
-        for (int64_t g = w * S.N; g < (w + 1) * S.N; g++) {
-            float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
-            for (int q = 0; q < 6 * kOtherObs / 4; q++) lk[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int q = 0; q < 18; q++) S.lkPos[g * 18 + q] = -1000.f;
+    auto blocks = [](int64_t n) { return (uint32_t)((n + 255) / 256); };
+    WireUnpackGrid G;
+    G.lidar = 0;
+    G.agents = blocks(A * kLidarRays / 4);
+    G.worlds = G.agents + blocks(A);
+    G.match = G.worlds + blocks(W);
+    G.total = G.match + blocks((W * 120 + 15) / 16);
+    return G;
+}
+
+__global__ void __launch_bounds__(256) k_wire_unpack(DevState S, const char *src, WireLayout L, WireUnpackGrid G,
+                                                     uint32_t *err, uint32_t worldOffset)
+{
+    if (!wireOk(S, src, L, err, worldOffset)) return;
+    const uint32_t b = blockIdx.x;
+    // an accepted keyframe resynchronises the shadow (keyframes ignore the
+    // desync bit, so no block's decision depends on when this lands)
+    if (L.lkObs >= 0 && b == 0 && threadIdx.x == 0) atomicAnd(err, ~kWireErrDesync);
+    if (b < G.agents) {
+        const int64_t q = (int64_t)b * 256 + threadIdx.x; // ray quad
+        if (q >= S.A * kLidarRays / 4) return;
+        const int64_t r = 4 * q;
+        const float4 d = reinterpret_cast<const float4 *>(src + L.depth)[q];
+        const uint32_t sh = (uint32_t)(r & 31);
+        const uint32_t p0 = reinterpret_cast<const uint32_t *>(src + L.plane[0])[r >> 5] >> sh;
+        const uint32_t p1 = reinterpret_cast<const uint32_t *>(src + L.plane[1])[r >> 5] >> sh;
+        const int64_t g = r / kLidarRays;
+        const int k = (int)(r - g * kLidarRays);
+        float4 *dst = k < kFwdRays ? reinterpret_cast<float4 *>(S.fwdLidar) + g * kFwdRays + k
+                                   : reinterpret_cast<float4 *>(S.rearLidar) + g * kRearRays + (k - kFwdRays);
+        const float dv[4] = { d.x, d.y, d.z, d.w };
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t c = ((p0 >> j) & 1u) | (((p1 >> j) & 1u) << 1);
+            dst[j] = make_float4(dv[j], c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f, c == 3 ? 1.f : 0.f);
+        }
+    } else if (b < G.worlds) {
+        const int64_t g = (int64_t)(b - G.agents) * 256 + threadIdx.x;
+        if (g >= S.A) return;
+        int k = 0;
+#define MP_GET_F(n) S.n[g] = reinterpret_cast<const float *>(src + L.af[k++])[g];
+        MP_WIRE_AF(MP_GET_F)
+#undef MP_GET_F
+        k = 0;
+#define MP_GET_I(n) S.n[g] = reinterpret_cast<const int32_t *>(src + L.ai[k++])[g];
+        MP_WIRE_AI(MP_GET_I)
+#undef MP_GET_I
+        S.hp[g] = reinterpret_cast<const float *>(src + L.hp)[g];
+        S.alive[g] = reinterpret_cast<const float *>(src + L.alive)[g];
+        S.reward[g] = reinterpret_cast<const float *>(src + L.reward)[g];
+        S.done[g] = reinterpret_cast<const int32_t *>(src + L.done)[g];
+        const int2 mg = reinterpret_cast<const int2 *>(src + L.mag)[g];
+        S.magazine[2 * g] = mg.x;
+        S.magazine[2 * g + 1] = mg.y;
+        const uint32_t p = reinterpret_cast<const uint32_t *>(src + L.packed)[g];
+        S.curPose[g] = (int32_t)(p & 0xffu);
+        S.tgtPose[g] = (int32_t)((p >> 8) & 0xffu);
+        S.weapon[g] = (int32_t)((p >> 16) & 0xffu);
+        S.flags[g] = (int32_t)(p >> 24);
+        S.visMask[g] = reinterpret_cast<const uint8_t *>(src + L.vis)[g];
+        for (int c = 0; c < 9; c++) S.rewardCoefs[g * 9 + c] = reinterpret_cast<const float *>(src + L.coefs)[g * 9 + c];
+        if (L.lkObs >= 0) {
+            const float4 *s4 = reinterpret_cast<const float4 *>(src + L.lkObs) + g * 6 * kOtherObs / 4;
+            float4 *lk = reinterpret_cast<float4 *>(S.lkObs + g * 6 * kOtherObs);
+            for (int q = 0; q < 6 * kOtherObs / 4; q++) lk[q] = s4[q];
+            for (int q = 0; q < 18; q++) S.lkPos[g * 18 + q] = reinterpret_cast<const float *>(src + L.lkPos)[g * 18 + q];
+        }
+    } else if (b < G.match) {
+        const int64_t w = (int64_t)(b - G.worlds) * 256 + threadIdx.x;
+        if (w >= S.W) return;
+        const int32_t ep = reinterpret_cast<const int32_t *>(src + L.wi[kWireWI - 1])[w];
+        if (ep != S.episodeCounter[w] && L.lkObs < 0) {
+            for (int64_t g = w * S.N; g < (w + 1) * S.N; g++) {
+                float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
+                for (int q = 0; q < 6 * kOtherObs / 4; q++) lk[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int q = 0; q < 18; q++) S.lkPos[g * 18 + q] = -1000.f;
+            }
+        }
+        int k = 0;
+#define MP_GET_W(n) S.n[w] = reinterpret_cast<const int32_t *>(src + L.wi[k++])[w];
+        MP_WIRE_WI(MP_GET_W)
+#undef MP_GET_W
+    } else {
+        // [W][30] i32 episode results: 16-B pieces of the flat array (both
+        // ends 256-B aligned; the last piece may be partial)
+        const int64_t i = (int64_t)(b - G.match) * 256 + threadIdx.x;
+        const int64_t bytes = S.W * 120;
+        if (i * 16 >= bytes) return;
+        if (i * 16 + 16 <= bytes) {
+            reinterpret_cast<uint4 *>(S.matchResult)[i] = reinterpret_cast<const uint4 *>(src + L.match)[i];
+        } else {
+            for (int64_t o = i * 16; o < bytes; o += 4)
+                S.matchResult[o / 4] = reinterpret_cast<const int32_t *>(src + L.match)[o / 4];
         }
     }
-    int k = 0;
-#define MP_GET_W(n) S.n[w] = reinterpret_cast<const int32_t *>(src + L.wi[k++])[w];
-    MP_WIRE_WI(MP_GET_W)
-#undef MP_GET_W
-    for (int c = 0; c < 30; c++) S.matchResult[w * 30 + c] = reinterpret_cast<const int32_t *>(src + L.match)[w * 30 + c];
-}
-
-__global__ void k_wire_unpack_agents(DevState S, const char *src, WireLayout L, uint32_t *err, uint32_t worldOffset)
-{
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (!wireOk(S, src, L, err, worldOffset) || g >= S.A) return;
-    int k = 0;
-#define MP_GET_F(n) S.n[g] = reinterpret_cast<const float *>(src + L.af[k++])[g];
-    MP_WIRE_AF(MP_GET_F)
-#undef MP_GET_F
-    k = 0;
-#define MP_GET_I(n) S.n[g] = reinterpret_cast<const int32_t *>(src + L.ai[k++])[g];
-    MP_WIRE_AI(MP_GET_I)
-#undef MP_GET_I
-    S.hp[g] = reinterpret_cast<const float *>(src + L.hp)[g];
-    S.alive[g] = reinterpret_cast<const float *>(src + L.alive)[g];
-    S.reward[g] = reinterpret_cast<const float *>(src + L.reward)[g];
-    S.done[g] = reinterpret_cast<const int32_t *>(src + L.done)[g];
-    const int2 mg = reinterpret_cast<const int2 *>(src + L.mag)[g];
-    S.magazine[2 * g] = mg.x;
-    S.magazine[2 * g + 1] = mg.y;
-    const uint32_t p = reinterpret_cast<const uint32_t *>(src + L.packed)[g];
-    S.curPose[g] = (int32_t)(p & 0xffu);
-    S.tgtPose[g] = (int32_t)((p >> 8) & 0xffu);
-    S.weapon[g] = (int32_t)((p >> 16) & 0xffu);
-    S.flags[g] = (int32_t)(p >> 24);
-    S.visMask[g] = reinterpret_cast<const uint8_t *>(src + L.vis)[g];
-    for (int c = 0; c < 9; c++) S.rewardCoefs[g * 9 + c] = reinterpret_cast<const float *>(src + L.coefs)[g * 9 + c];
-    if (L.lkObs >= 0) {
-        const float4 *s4 = reinterpret_cast<const float4 *>(src + L.lkObs) + g * 6 * kOtherObs / 4;
-        float4 *lk = reinterpret_cast<float4 *>(S.lkObs + g * 6 * kOtherObs);
-        for (int q = 0; q < 6 * kOtherObs / 4; q++) lk[q] = s4[q];
-        for (int q = 0; q < 18; q++) S.lkPos[g * 18 + q] = reinterpret_cast<const float *>(src + L.lkPos)[g * 18 + q];
-    }
-}
-
-__global__ void k_wire_unpack_lidar(DevState S, const char *src, WireLayout L, uint32_t *err, uint32_t worldOffset)
-{
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (!wireOk(S, src, L, err, worldOffset)) return;
-    // an accepted keyframe resynchronises the shadow (every block of this
-    // kernel has read the word: keyframes ignore the desync bit)
-    if (L.lkObs >= 0 && r == 0) atomicAnd(err, ~kWireErrDesync);
-    if (r >= S.A * kLidarRays) return;
-    const float d = reinterpret_cast<const float *>(src + L.depth)[r];
-    const uint32_t b0 = (reinterpret_cast<const uint32_t *>(src + L.plane[0])[r >> 5] >> (r & 31)) & 1u;
-    const uint32_t b1 = (reinterpret_cast<const uint32_t *>(src + L.plane[1])[r >> 5] >> (r & 31)) & 1u;
-    const uint32_t c = b0 | (b1 << 1);
-    const float4 v = make_float4(d, c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f, c == 3 ? 1.f : 0.f);
-    const int64_t g = r / kLidarRays;
-    const int k = (int)(r - g * kLidarRays);
-    if (k < kFwdRays) reinterpret_cast<float4 *>(S.fwdLidar)[g * kFwdRays + k] = v;
-    else reinterpret_cast<float4 *>(S.rearLidar)[g * kRearRays + k - kFwdRays] = v;
 }
 
 // ------------------------------------------------------------ batch copy
@@ -360,10 +402,10 @@ int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t
 {
     hipStream_t st = (hipStream_t)stream;
     const WireLayout L = wireLayout(s.A, s.W, keyframe);
-    hipLaunchKernelGGL(k_wire_unpack_worlds, dim3(grid(s.W)), dim3(256), 0, st, s, src, L, err, worldOffset);
-    hipLaunchKernelGGL(k_wire_unpack_agents, dim3(grid(s.A)), dim3(256), 0, st, s, src, L, err, worldOffset);
-    hipLaunchKernelGGL(k_wire_unpack_lidar, dim3(grid(s.A * kLidarRays)), dim3(256), 0, st, s, src, L, err,
-                       worldOffset);
+    const WireUnpackGrid G = wireUnpackGrid(s.A, s.W);
+    // the lidar quads assume 16-B aligned f32 lidar rows and depth column
+    if (((uintptr_t)s.fwdLidar | (uintptr_t)s.rearLidar | (uintptr_t)s.matchResult) & 15u) return -1;
+    hipLaunchKernelGGL(k_wire_unpack, dim3(G.total), dim3(256), 0, st, s, src, L, G, err, worldOffset);
     return checkW(hipGetLastError());
 }
 

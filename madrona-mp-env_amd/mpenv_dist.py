@@ -291,46 +291,60 @@ class LearnerLocal:
 class LearnerWire:
     """Per-step learner exchange in the compact wire format (csrc/wire.hip,
     include/mpenv.h mpenv_wire_*): every rank packs one
-    message of its step's outputs (~477 B per agent + 160 B per world
-    instead of the 3,924 B per agent LearnerGather ships) into a 2-slot ring
-    on the step stream and sends it to the learner rank `dst`; the learner
-    receives each peer's message into its slot and unpacks it into that
-    peer's shadow manager (a SimManager of the same configuration), whose
-    own observation kernel rebuilds every trainInterface output bit for bit.
+    message of its step's outputs (~490 B per agent instead of the 3,924 B
+    per agent LearnerGather ships) into a 2-slot ring on the step stream and
+    sends it to the learner rank `dst`; the learner receives each peer's
+    message into its slot and unpacks it into that peer's shadow manager (a
+    SimManager of the same configuration and world range), whose own
+    observation kernel rebuilds every trainInterface output bit for bit.
     The first message of each sender is a keyframe (it also carries the
-    last-known rows).  Unpacking lags one step: `submit()` posts this
-    step's transfers and unpacks the previous slot's messages, so the
-    transfers overlap a whole step; `drain()` finishes both.
+    last-known rows).  Unpacking lags one step: `submit()` posts this step's
+    transfers and unpacks the previous slot's messages, so the transfers
+    overlap a whole step; `drain()` finishes both.
 
-    On `dst`, `outputs()` returns {name: [world_size, rows, ...]} stacked from
-    the learner's own engine (rank dst) and the shadows, in rank order
+    `dedicated=True`: the learner rank simulates nothing (sim is None there);
+    it only receives and unpacks the other ranks' messages, so the senders
+    run at their own speed as long as the learner's unpacks keep up (C4 at 8
+    GPUs: 7 simulators + one learner).  Otherwise the learner
+    also simulates a shard (its own outputs are read directly).
+
+    On `dst`, `outputs()` returns {name: [shards, rows, ...]}: the
+    learner's own engine (not dedicated) and the shadows, in rank order
     (global world order, as LearnerGather), after `drain()`.
 
     pack(dst_ptr, keyframe, stream) / unpack(r, src_ptr, keyframe, stream) /
-    nbytes(keyframe) default to the SimManager's wire_* methods and
-    make_shadow(r) builds the shadow of rank r; the CPU tests substitute
-    byte-level stand-ins.  Construction is a collective call (the message
-    sizes are checked across the group); with RCCL, set the device first.
+    nbytes(keyframe) / wire_error(r) default to the SimManager's wire_*
+    methods and make_shadow(r) builds the shadow of rank r; the CPU tests
+    substitute byte-level stand-ins.  Construction is a collective call (the
+    message sizes are checked across the group); with RCCL, set the device
+    first.
 
     One rank (world_size 1, bench.py --exchange wire at N = 1): loopback --
     the rank packs its own message and unpacks it into its own shadow each
     step, so the line carries the per-message pack and unpack cost a learner
     pays for each peer (nothing crosses xGMI).
 
-    On a GPU the learner unpacks on a stream of its own (`overlap`, on by
-    default): the unpacks of one slot wait on GPU events for that slot's
-    receives (or, loopback, its pack), the next receive / pack into the slot
-    waits for the slot's unpacks, and nothing blocks the host -- so the
-    learner's own simulation step and its peers' unpacks share the GPU
-    instead of running back to back.  `drain()` orders the caller's stream
-    after every unpack.  submit() takes torch's current stream (the step's).
+    On a GPU the learner unpacks on streams of its own (`overlap`, on by
+    default; `unpack_streams` of them, peers dealt round-robin, so
+    several peers' unpacks fill the GPU together): the unpacks of one slot
+    wait on GPU events for that slot's receives (loopback: its pack), the
+    next receive / pack into the slot waits on the events its unpacks
+    recorded, and nothing blocks the host -- the learner's own step (if any)
+    and its peers' unpacks share the GPU.  `drain()` orders the caller's
+    stream after every unpack.  submit() takes torch's current stream.
+
+    A shadow that refused a message (wrong configuration or shard, wrong
+    kind, values that did not fit the wire) is out of sync until a keyframe;
+    `check()` raises then -- every `check_every` submits, and in outputs()
+    and close().
     """
 
     NOT_SHIPPED = NOT_SHIPPED
     mode = "wire"
 
     def __init__(self, sim, make_shadow=None, dst: int = 0, group=None, slots: int = 2, pack=None, unpack=None,
-                 nbytes=None, device=None, overlap: bool = True, check_every: int = 0, wire_error=None):
+                 nbytes=None, device=None, overlap: bool = True, check_every: int = 0, wire_error=None,
+                 dedicated: bool = False, unpack_streams: int = 1):
         import torch
         import torch.distributed as dist
 
@@ -340,12 +354,18 @@ class LearnerWire:
         self.rank = dist.get_rank(group)
         self.ws = dist.get_world_size(group)
         self.sim = sim
-        self._nbytes = nbytes or (lambda kf: sim.wire_bytes(kf))
-        self._pack = pack or (lambda ptr, kf, st: sim.wire_pack(ptr, kf, st))
+        self.dedicated = bool(dedicated)
+        if self.dedicated and self.ws < 2:
+            raise ValueError("LearnerWire(dedicated=True) needs at least one sender rank")
         self.shadows = {}
         self.loopback = self.ws == 1
         if self.rank == dst and make_shadow is not None:
             self.shadows = {r: make_shadow(r) for r in range(self.ws) if r != dst or self.loopback}
+        if self.rank == dst and self.dedicated:
+            self.sim = None  # the learner simulates nothing
+        sizer = sim if sim is not None else (next(iter(self.shadows.values())) if self.shadows else None)
+        self._nbytes = nbytes or (lambda kf: sizer.wire_bytes(kf))
+        self._pack = pack or (lambda ptr, kf, st: sim.wire_pack(ptr, kf, st))
         self._unpack = unpack or (lambda r, ptr, kf, st: self.shadows[r].wire_unpack(ptr, kf, st))
         self.nb, self.nk = int(self._nbytes(False)), int(self._nbytes(True))
         sizes = [None] * self.ws
@@ -355,10 +375,6 @@ class LearnerWire:
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.torch = torch
         self.gpu = dev.type == "cuda"
-        # each shadow's wire error word (mpenv_wire_error): nonzero once a
-        # message was refused -- the shadow is then out of sync until a
-        # keyframe, so outputs() / close() (and every `check_every` submits)
-        # raise instead of handing out stale rows
         self._wire_error = wire_error or (lambda r: self.shadows[r].wire_error())
         self.check_every = int(check_every)
         self.slots = slots
@@ -371,11 +387,16 @@ class LearnerWire:
         self.unpacked = [True] * slots
         self.keyframe = [True] * slots  # the kind of message in each slot
         self.k = 0
-        # the learner's unpack stream and, per slot, the event its unpacks end with
-        self.ustream, self.udone = None, None
+        # the learner's unpack streams and, per slot, the events their unpacks end with
+        self.ustreams, self.udone = [], None
         if overlap and self.rank == dst and dev.type == "cuda":
-            self.ustream = torch.cuda.Stream(device=dev)
-            self.udone = [torch.cuda.Event() for _ in range(slots)]
+            self.ustreams = [torch.cuda.Stream(device=dev) for _ in range(max(1, int(unpack_streams)))]
+            self.udone = [[torch.cuda.Event() for _ in self.ustreams] for _ in range(slots)]
+
+    @property
+    def ustream(self):
+        """The (first) unpack stream, None when unpacking on the caller's stream."""
+        return self.ustreams[0] if self.ustreams else None
 
     def bytes_per_step(self) -> dict:
         return {"sent_per_rank": self.nb, "learner_ingress": self.nb * (self.ws - 1), "keyframe": self.nk}
@@ -404,13 +425,15 @@ class LearnerWire:
                                "2 out of sync until a keyframe); their outputs are stale")
 
     def _unpack_slot(self, slot, ranks, stream_ptr):
-        if self.ustream is None:
+        if not self.ustreams:
             for r in ranks:
                 self._unpack(r, self.bufs[slot][r].data_ptr(), self.keyframe[slot], stream_ptr or 0)
             return
-        for r in ranks:
-            self._unpack(r, self.bufs[slot][r].data_ptr(), self.keyframe[slot], self.ustream.cuda_stream)
-        self.udone[slot].record(self.ustream)
+        for j, r in enumerate(ranks):
+            us = self.ustreams[j % len(self.ustreams)]
+            self._unpack(r, self.bufs[slot][r].data_ptr(), self.keyframe[slot], us.cuda_stream)
+        for us, ev in zip(self.ustreams, self.udone[slot]):
+            ev.record(us)
 
     def _peer(self, r):
         return self.dist.get_global_rank(self.group, r) if self.group is not None else r
@@ -418,11 +441,12 @@ class LearnerWire:
     def _finish(self, slot, stream_ptr):
         """Wait for a slot's transfers and (learner) unpack its messages."""
         if self.pending[slot] is not None:
-            if self.ustream is not None:
-                # the unpack stream (not the caller's) waits for the receives
-                with self.torch.cuda.stream(self.ustream):
-                    for w in self.pending[slot]:
-                        w.wait()
+            if self.ustreams:
+                # the unpack streams (not the caller's) wait for the receives
+                for us in self.ustreams:
+                    with self.torch.cuda.stream(us):
+                        for w in self.pending[slot]:
+                            w.wait()
             else:
                 for w in self.pending[slot]:
                     w.wait()
@@ -449,14 +473,16 @@ class LearnerWire:
         self._finish(slot, stream_ptr)  # the slot's previous round is done before it is reused
         n = self.nk if kf else self.nb
         self.keyframe[slot] = kf
-        if self.ustream is not None:
+        if self.ustreams:
             # the slot's buffers are rewritten (pack / receive) only after its
             # previous unpacks have read them
-            self._caller_stream(stream_ptr).wait_event(self.udone[slot])
+            cur = self._caller_stream(stream_ptr)
+            for ev in self.udone[slot]:
+                cur.wait_event(ev)
         if self.loopback:
             self._pack(self.bufs[slot][0].data_ptr(), kf, stream_ptr or 0)
-            if self.ustream is not None:
-                self.ustream.wait_stream(self._caller_stream(stream_ptr))
+            for us in self.ustreams:
+                us.wait_stream(self._caller_stream(stream_ptr))
             self._unpack_slot(slot, [0], stream_ptr)
             if self.check_every and self.k % self.check_every == 0:
                 self.check()
@@ -480,22 +506,26 @@ class LearnerWire:
     def drain(self, stream_ptr=None):
         for i in range(self.slots):
             self._finish((self.k + i) % self.slots, stream_ptr)
-        if self.ustream is not None:
-            self._caller_stream(stream_ptr).wait_stream(self.ustream)
+        if self.ustreams:
+            cur = self._caller_stream(stream_ptr)
+            for us in self.ustreams:
+                cur.wait_stream(us)
 
     def outputs(self):
-        """{name: [world_size, rows, ...]} on dst (own engine + shadows)."""
+        """{name: [shards, rows, ...]} on dst: own engine (unless dedicated)
+        and shadows, in rank order."""
         import torch
 
         if self.rank != self.dst:
             return {}
         self.drain()
         self.check()
-        own = LearnerGather.from_sim(self.sim)
         if self.loopback:  # the shadow's rebuild of the rank's own outputs
-            own = LearnerGather.from_sim(self.shadows[0])
-        parts = {r: (own if r == self.dst else LearnerGather.from_sim(self.shadows[r])) for r in range(self.ws)}
-        return {n: torch.stack([parts[r][n] for r in range(self.ws)]) for n in own if n not in NOT_SHIPPED}
+            parts = [LearnerGather.from_sim(self.shadows[0])]
+        else:
+            parts = [LearnerGather.from_sim(self.sim) if r == self.dst else LearnerGather.from_sim(self.shadows[r])
+                     for r in range(self.ws) if not (self.dedicated and r == self.dst)]
+        return {n: torch.stack([p[n] for p in parts]) for n in parts[0] if n not in NOT_SHIPPED}
 
     def close(self):
         self.drain()

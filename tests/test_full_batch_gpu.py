@@ -44,7 +44,7 @@ def test_every_world_of_the_bench_window_matches_oracle(ts, W, warmup, steps, ev
     N = 2 * ts
     A = W * N
     e = T.Engine(W, ts)
-    e.set_world_groups(2)  # as bench.py's timed pass
+    e.set_world_groups(1)  # as bench.py's timed pass (multi-group parity: test_parity_gpu)
     o = T.Oracle(W, ts)
     for sim in (e, o):
         sim.put_ctrl([0, 1, 1])
@@ -81,6 +81,75 @@ def test_every_world_of_the_bench_window_matches_oracle(ts, W, warmup, steps, ev
     o.close()
 
 
+LIDAR_EXPORTS = ("FWD_LIDAR", "REAR_LIDAR", "FULL_TEAM_FWD_LIDAR", "FULL_TEAM_REAR_LIDAR")
+
+
+def compare_lidar_ulp(a, b, name):
+    """Lidar rows [..., 4] (depth, wall, teammate, opponent): the three class
+    channels byte-exact, the depth within one ulp (same sign, bit patterns
+    at most 1 apart).  Returns the number of rays whose depth differs."""
+    assert a.shape == b.shape and a.shape[-1] == 4, (name, a.shape, b.shape)
+    T.compare(np.ascontiguousarray(a[..., 1:]), np.ascontiguousarray(b[..., 1:]), f"{name} (class channels)")
+    da = np.ascontiguousarray(a[..., 0]).view(np.int32).astype(np.int64)
+    db = np.ascontiguousarray(b[..., 0]).view(np.int32).astype(np.int64)
+    diff = np.abs(da - db)
+    same_sign = (da < 0) == (db < 0)
+    bad = ~same_sign | (diff > 1)
+    assert not bad.any(), f"{name}: {int(bad.sum())} depths beyond 1 ulp, first at {tuple(np.argwhere(bad)[0])}"
+    return int((diff == 1).sum())
+
+
+def test_bench_window_every_world_against_the_reference_slot_order():
+    """The product's lidar walks each node's children in a per-octant order
+    (DESIGN.md §2 definition 12); the reference walks them in slot order
+    (mesh_bvh.inl:160-204).  Against an oracle built with the reference's
+    slot order, over every world of the driver's C3 window (Manager::init,
+    5 warm-up + 20 timed steps of the tape -- no bots, so lidar depth never
+    feeds back into the state): every export byte-exact except the lidar
+    depths, which may differ by one ulp where two coplanar triangles tie
+    (class channels exact).  The count of 1-ulp rays is printed; the north
+    star allows 1e-5 relative."""
+    t_start = time.time()
+    ts, W, total = 6, 16384, 25
+    N = 2 * ts
+    A = W * N
+    e = T.Engine(W, ts)
+    e.set_world_groups(1)
+    o = T.Oracle(W, ts, lidar_order="slot")
+    for sim in (e, o):
+        sim.put_ctrl([0, 1, 1])
+        sim.init()
+    ring = T.mpenv_tape.tape_ring(SEED, 0, A, RING)
+    dev_ring = e.mem.upload(ring)
+    threads = T.usable_cpus()
+    ulp_rays, checked = 0, 0
+
+    def compare_all(where):
+        nonlocal ulp_rays, checked
+        for n in ALL:
+            if n in LIDAR_EXPORTS:
+                a = e.get(n)
+                ulp_rays += compare_lidar_ulp(a, o.get(n), f"{n} @ {where}")
+                checked += a.size // 4
+            else:
+                T.compare(e.get(n), o.get(n), f"{n} @ {where}")
+
+    compare_all("init")
+    for s in range(total):
+        row = np.ascontiguousarray(ring[s % RING])
+        e.copy_actions(dev_ring + (s % RING) * A * 24)
+        e.step()
+        o.lib.oracle_run_threaded(o.h, 1, threads, row.ctypes.data, 1)
+        if (s + 1) % 5 == 0 or s == total - 1:
+            compare_all(f"step {s}")
+    e.mem.free(dev_ring)
+    print(f"\nC3 6v6 x {W}, init + {total} steps vs the reference's slot-order traversal: every export "
+          f"byte-exact but lidar depth; {ulp_rays} of {checked} lidar rays compared differ by 1 ulp "
+          f"({ulp_rays / max(checked, 1):.2e}); test {time.time() - t_start:.1f} s")
+    e.close()
+    o.close()
+
+
 COMBAT = [
     # team_size, worlds, steps, compare every, kills required (C3's teams
     # first meet near the zone: 120 steps see ~25 agents hit and no kill
@@ -105,7 +174,7 @@ def test_every_world_in_the_combat_regime_matches_oracle(ts, W, steps, every, ne
     N = 2 * ts
     A = W * N
     e = T.Engine(W, ts)
-    e.set_world_groups(2)  # as bench.py's timed pass
+    e.set_world_groups(1)  # as bench.py's timed pass (multi-group parity: test_parity_gpu)
     o = T.Oracle(W, ts)
     for sim in (e, o):
         sim.put_ctrl([0, 1, 1])

@@ -687,6 +687,55 @@ def test_world_groups_on_streams_match_oracle(monkeypatch):
                     T.compare(e.get_rows(n, r0, r1), o.get(n), f"{n} worlds {w0}.. @ {s}")
 
 
+def test_step_graph_captures_every_fork_layout(monkeypatch):
+    """Round-4 review: a capture of the lidar branch stream crashed the
+    process.  The capture is now checked (capture status before it ends,
+    every capture call's return) and a failed one is abandoned for direct
+    launches with the reason kept (mpenv_graph_status).  Here every fork
+    layout is captured -- 1-4 world groups (4 is capped at 3), and one
+    group with k_lidar on a branch stream beside k_vis -> k_obs -- and its
+    replay must equal kernel-by-kernel launches bit for bit, with the graph
+    on (no abandoned capture)."""
+    import ctypes as C
+
+    ts, W, steps = 3, 3000, 12
+    N = 2 * ts
+    monkeypatch.setenv("MPENV_STEP_GRAPH", "0")
+    monkeypatch.setenv("MPENV_WORLD_GROUPS", "1")
+    ref = T.Engine(W, ts)
+    monkeypatch.setenv("MPENV_STEP_GRAPH", "1")
+    layouts = [(1, False), (1, True), (2, False), (3, False), (4, False)]
+    engines = []
+    for groups, branch in layouts:
+        e = T.Engine(W, ts)
+        e.set_world_groups(groups)
+        e.lib.mpenv_set_lidar_branch.argtypes = [C.c_void_p, C.c_int32]
+        assert e.lib.mpenv_set_lidar_branch(e.h, int(branch)) == 0
+        engines.append(e)
+    for e in [ref] + engines:
+        e.put_ctrl([0, 1, 1])
+        e.init()
+    for s in range(steps):
+        acts = T.mpenv_tape.tape_actions(1234, s, 0, W * N)
+        for e in [ref] + engines:
+            e.set_actions(acts)
+            e.step()
+        if s % 4 == 3:
+            for (groups, branch), e in zip(layouts, engines):
+                for n in T.STEP_OUTPUTS:
+                    T.compare(e.get(n), ref.get(n), f"{n} graph ({groups} groups, branch {branch}) vs direct @ {s}")
+    for (groups, branch), e in zip(layouts, engines):
+        on, why = C.c_int32(-1), C.create_string_buffer(512)
+        e.lib.mpenv_graph_status.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_char_p, C.c_int32]
+        assert e.lib.mpenv_graph_status(e.h, C.byref(on), why, 512) == 0
+        assert on.value == 1 and why.value == b"", (groups, branch, why.value)
+        n_cap = C.c_int64(-1)
+        e.lib.mpenv_graph_captures.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+        assert e.lib.mpenv_graph_captures(e.h, C.byref(n_cap)) == 0 and n_cap.value == 1, (groups, branch, n_cap.value)
+        e.close()
+    ref.close()
+
+
 def test_step_graph_replay_equals_direct_launches(monkeypatch):
     """The Step graph replayed as a captured HIP graph (the default) equals
     kernel-by-kernel launches (MPENV_STEP_GRAPH=0) bit for bit, including

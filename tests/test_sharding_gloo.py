@@ -236,7 +236,7 @@ def _wire_bytes(rank, step, keyframe):
     return (np.arange(n, dtype=np.int64) * 7 + rank * 131 + step * 17 + (5 if keyframe else 0)).astype(np.uint8)
 
 
-def _wire_worker(rank, world_size, port, result_path):
+def _wire_worker(rank, world_size, port, result_path, dedicated=False):
     import ctypes as C
 
     from mpenv_dist import LearnerWire
@@ -256,7 +256,10 @@ def _wire_worker(rank, world_size, port, result_path):
             n = WIRE_NK if keyframe else WIRE_NB
             seen.append((r, bool(keyframe), bytes((C.c_uint8 * n).from_address(ptr))))
 
-        lw = LearnerWire(None, dst=0, pack=pack, unpack=unpack,
+        if dedicated and rank == 0:
+            def pack(ptr, keyframe, stream):  # the dedicated learner never packs
+                raise AssertionError("dedicated learner packed a message")
+        lw = LearnerWire(None, dst=0, pack=pack, unpack=unpack, dedicated=dedicated,
                          nbytes=lambda kf: WIRE_NK if kf else WIRE_NB, device=torch.device("cpu"))
         assert lw.bytes_per_step() == {"sent_per_rank": WIRE_NB, "learner_ingress": WIRE_NB * (world_size - 1),
                                        "keyframe": WIRE_NK}
@@ -273,11 +276,16 @@ def _wire_worker(rank, world_size, port, result_path):
         dist.destroy_process_group()
 
 
-def test_learner_wire_transport_three_ranks(tmp_path):
+@pytest.mark.parametrize("dedicated", [False, True], ids=["learner_simulates", "dedicated_learner"])
+def test_learner_wire_transport_three_ranks(tmp_path, dedicated):
+    """Three gloo ranks; rank 0 the learner.  dedicated: the learner
+    simulates nothing (sim None, never packs) and only receives and unpacks
+    ranks 1 and 2 -- C4's 7 simulators + 1 learner layout (DESIGN.md §6);
+    every message still arrives in order, keyframe first, bytes intact."""
     import pickle  # reads the file _wire_worker wrote above
 
     path = str(tmp_path / "wire.pkl")
-    mp.spawn(_wire_worker, args=(3, _free_port(), path), nprocs=3, join=True)
+    mp.spawn(_wire_worker, args=(3, _free_port(), path, dedicated), nprocs=3, join=True)
     with open(path, "rb") as f:
         seen = pickle.load(f)
     for r in (1, 2):

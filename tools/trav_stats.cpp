@@ -604,6 +604,187 @@ static void fanWave(const float *rays, size_t r0, int order, FanStats &fs)
     }
 }
 
+// Ray-pair traversal (TRAV_PAIR): one lane walks the two sheet rays of one
+// fan angle -- same direction, origins differing only in z -- through one
+// union traversal in the shared octant order: a node carries a 2-bit mask of
+// the rays that entered it, each child box is tested per ray against that
+// ray's own t_max, a leaf's triangles are tested for each ray that entered
+// it (A's, then B's), an internal child is pushed with the mask of the rays
+// that entered it.  Each ray sees exactly the node sequence and t_max of its
+// solo traversal, so the closest hits are the same; what changes is the
+// lockstep work.  Per node iteration: slotTris[it][i] = A's tests in slot i,
+// slotTrisB = B's.
+struct PairStats {
+    int pops = 0, boxesA = 0, boxesB = 0, trisA = 0, trisB = 0, solo = 0;
+    std::vector<std::array<int, 4>> slotA, slotB;
+};
+
+static void tracePair(const float *oA, const float *oB, const float *d, PairStats &st)
+{
+    const int oct = (d[0] < 0 ? 1 : 0) | (d[1] < 0 ? 2 : 0) | (d[2] < 0 ? 4 : 0);
+    float inv[3];
+    for (int k = 0; k < 3; k++) inv[k] = d[k] == 0 ? 1e7f : 1.f / d[k];
+    float tmax[2] = { 3.4e38f, 3.4e38f };
+    const float *o[2] = { oA, oB };
+    std::vector<std::pair<int, int>> stack = { { 0, 3 } };
+    while (!stack.empty()) {
+        auto [ni, mask] = stack.back();
+        stack.pop_back();
+        st.pops++;
+        if (mask != 3) st.solo++;
+        const Node &n = nodes[ni];
+        std::pair<int, int> kids[4];
+        int nk = 0;
+        st.slotA.push_back({ 0, 0, 0, 0 });
+        st.slotB.push_back({ 0, 0, 0, 0 });
+        for (int ii = 0; ii < 4; ii++) {
+            const int i = octOrder[ni][oct][ii];
+            if (n.children[i] == -1) continue;
+            float sx = std::ldexp(1.f, n.expX), sy = std::ldexp(1.f, n.expY), sz = std::ldexp(1.f, n.expZ);
+            float lo[3] = { n.minX + sx * n.qMinX[i], n.minY + sy * n.qMinY[i], n.minZ + sz * n.qMinZ[i] };
+            float hi[3] = { n.minX + sx * n.qMaxX[i], n.minY + sy * n.qMaxY[i], n.minZ + sz * n.qMaxZ[i] };
+            int enter = 0;
+            for (int r = 0; r < 2; r++) {
+                if (!((mask >> r) & 1)) continue;
+                (r ? st.boxesB : st.boxesA)++;
+                float tn = 0, tf = tmax[r];
+                for (int k = 0; k < 3; k++) {
+                    float a = (lo[k] - o[r][k]) * inv[k], b = (hi[k] - o[r][k]) * inv[k];
+                    tn = std::max(tn, std::min(a, b));
+                    tf = std::min(tf, std::max(a, b));
+                }
+                if (tn <= tf) enter |= 1 << r;
+            }
+            if (!enter) continue;
+            if (n.children[i] & 0x80000000) {
+                int leaf = n.children[i] & 0x7fffffff;
+                for (int r = 0; r < 2; r++) {
+                    if (!((enter >> r) & 1)) continue;
+                    for (int k = 0; k < n.triSize[i]; k++) {
+                        (r ? st.trisB : st.trisA)++;
+                        (r ? st.slotB : st.slotA).back()[i]++;
+                        float t;
+                        if (tri(&verts[(leaf + k) * 9], o[r], d, tmax[r], t)) tmax[r] = t;
+                    }
+                }
+            } else {
+                kids[nk++] = { n.children[i], enter };
+            }
+        }
+        std::reverse(kids, kids + nk); // nearest (first in order) popped first
+        for (int k = 0; k < nk; k++) stack.push_back(kids[k]);
+    }
+}
+
+// Lockstep cost of one wave of lanes: node iterations (max pops) and
+// triangle-test iterations (per iteration and slot, the max over lanes).
+struct Lockstep {
+    double nodeIters = 0, triIters = 0;
+};
+
+static void lockSolo(const std::vector<Stats> &lanes, Lockstep &ls)
+{
+    double mp = 0;
+    for (auto &L : lanes) mp = std::max(mp, L.pops);
+    ls.nodeIters += mp;
+    for (int it = 0; it < (int)mp; it++)
+        for (int i = 0; i < 4; i++) {
+            int m = 0;
+            for (auto &L : lanes)
+                if (it < (int)L.slotTris.size()) m = std::max(m, L.slotTris[it][i]);
+            ls.triIters += m;
+        }
+}
+
+static void lockPair(const std::vector<PairStats> &lanes, Lockstep &ls)
+{
+    int mp = 0;
+    for (auto &L : lanes) mp = std::max(mp, L.pops);
+    ls.nodeIters += mp;
+    for (int it = 0; it < mp; it++)
+        for (int i = 0; i < 4; i++) {
+            int ma = 0, mb = 0;
+            for (auto &L : lanes)
+                if (it < (int)L.slotA.size()) {
+                    ma = std::max(ma, L.slotA[it][i]);
+                    mb = std::max(mb, L.slotB[it][i]);
+                }
+            ls.triIters += ma + mb;
+        }
+}
+
+static int pairMain(const std::vector<float> &rays)
+{
+    // dump_lidar_rays order: per 4-agent unit, each agent's 64 forward rays
+    // (k = h * 32 + x), then the 4 agents' 16 rear rays (k = h * 8 + x)
+    const size_t n = rays.size() / 6, units = n / 320;
+    auto R = [&](size_t r) { return &rays[6 * r]; };
+    Lockstep soloF, soloR, pairF, pairR;
+    double soloFw = 0, soloRw = 0, pairFw = 0, pairRw = 0, dirMismatch = 0, pops = 0, solo = 0, lanesP = 0;
+    double trisSolo = 0, trisPair = 0;
+    std::vector<PairStats> rearLanes;
+    for (size_t u = 0; u < units; u++) {
+        const size_t base = u * 320;
+        // solo: 4 forward waves (one agent each) + 1 rear wave (4 x 16)
+        for (int a = 0; a < 4; a++) {
+            std::vector<Stats> lanes(64);
+            for (int k = 0; k < 64; k++) trace(R(base + a * 64 + k), R(base + a * 64 + k) + 3, 2, lanes[k]);
+            for (auto &L : lanes) trisSolo += L.tris;
+            lockSolo(lanes, soloF);
+            soloFw++;
+        }
+        {
+            std::vector<Stats> lanes(64);
+            for (int k = 0; k < 64; k++) trace(R(base + 256 + k), R(base + 256 + k) + 3, 2, lanes[k]);
+            for (auto &L : lanes) trisSolo += L.tris;
+            lockSolo(lanes, soloR);
+            soloRw++;
+        }
+        // pairs: forward waves of 2 agents x 32 angles
+        for (int a0 = 0; a0 < 4; a0 += 2) {
+            std::vector<PairStats> lanes(64);
+            for (int l = 0; l < 64; l++) {
+                const int a = a0 + l / 32, x = l % 32;
+                const float *ra = R(base + a * 64 + x), *rb = R(base + a * 64 + 32 + x);
+                for (int k = 0; k < 3; k++) dirMismatch += ra[3 + k] != rb[3 + k];
+                tracePair(ra, rb, ra + 3, lanes[l]);
+                pops += lanes[l].pops; solo += lanes[l].solo; lanesP++;
+                trisPair += lanes[l].trisA + lanes[l].trisB;
+            }
+            lockPair(lanes, pairF);
+            pairFw++;
+        }
+        // rear pairs: 4 agents x 8 angles per unit; a wave takes two units
+        for (int l = 0; l < 32; l++) {
+            const int a = l / 8, x = l % 8;
+            const float *ra = R(base + 256 + a * 16 + x), *rb = R(base + 256 + a * 16 + 8 + x);
+            rearLanes.emplace_back();
+            tracePair(ra, rb, ra + 3, rearLanes.back());
+            trisPair += rearLanes.back().trisA + rearLanes.back().trisB;
+        }
+        if (rearLanes.size() == 64) {
+            lockPair(rearLanes, pairR);
+            pairRw++;
+            rearLanes.clear();
+        }
+    }
+    printf("rays %zu (%zu units), direction mismatches within pairs %.0f\n", n, units, dirMismatch);
+    printf("solo  forward: %.0f waves, lockstep node iters/wave %.2f tri iters/wave %.2f | rear: %.0f waves, %.2f / %.2f\n",
+           soloFw, soloF.nodeIters / soloFw, soloF.triIters / soloFw, soloRw, soloR.nodeIters / soloRw, soloR.triIters / soloRw);
+    printf("pairs forward: %.0f waves, lockstep node iters/wave %.2f tri iters/wave %.2f | rear: %.0f waves, %.2f / %.2f\n",
+           pairFw, pairF.nodeIters / pairFw, pairF.triIters / pairFw, pairRw, pairR.nodeIters / std::max(pairRw, 1.0),
+           pairR.triIters / std::max(pairRw, 1.0));
+    printf("pair lanes: union pops/lane %.2f (single-ray nodes %.1f%%); lane tri tests solo %.0f pair %.0f\n",
+           pops / lanesP, 100.0 * solo / pops, trisSolo, trisPair);
+    // instruction model: per node iteration ~110 VALU solo, ~150 paired
+    // (shared decode and x/y slabs, two z slabs / t_near / t_far), ~45 per
+    // triangle test
+    const double cs = soloF.nodeIters * 110 + soloF.triIters * 45 + soloR.nodeIters * 110 + soloR.triIters * 45;
+    const double cp = pairF.nodeIters * 150 + pairF.triIters * 45 + (pairR.nodeIters * 150 + pairR.triIters * 45);
+    printf("model VALU per unit: solo %.0f, pairs %.0f (%.2fx)\n", cs / units, cp / units, cp / cs);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3) {
@@ -641,6 +822,7 @@ int main(int argc, char **argv)
         printf("packet (64 consecutive rays): union nodes/wave %.2f, union tris/wave %.2f\n", un / waves, ut / waves);
     }
     buildOctOrder();
+    if (getenv("TRAV_PAIR")) return pairMain(rays);
     if (getenv("TRAV_FAN")) {
         // forward waves only (dump_lidar_rays order: 4 forward waves, then 1 rear)
         // which side of a triangle does an accepted hit come from?

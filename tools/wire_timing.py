@@ -1,7 +1,10 @@
 """Times the learner exchange's wire kernels on the C3 batch (run on the GPU
 box): the sender's pack, the learner's unpack into a shadow manager (which
 includes the shadow's k_obs over the batch), each alone over 50 messages of
-a combat-regime step, wall clock around a device sync."""
+a combat-regime step, wall clock around a device sync; then C4's dedicated
+learner on one GPU: 7 peers' unpacks per step over 4 streams, against a
+sender's step + pack (the learner keeps up when its step is the shorter;
+c4_scaling_bound = 7 x min(1, sender / learner))."""
 import json
 import os
 import sys
@@ -47,6 +50,43 @@ def main():
             fn()
         hip.hipDeviceSynchronize()
         res[name] = round((time.perf_counter() - t0) / 50 * 1e3, 4)
+    # the dedicated learner of C4 (bench.py --learner-dedicated): per step it
+    # unpacks 7 peers' messages into 7 shadows, dealt over 4 unpack streams
+    # (LearnerWire(unpack_streams=4)); here the same message 7 times, timed
+    # against the simulator's own step (+ its pack), which is what a sender
+    # spends per message
+    peers = int(os.environ.get("WIRE_PEERS", 7))
+    shadows = [sh] + [T.Engine(W, ts) for _ in range(peers - 1)]
+    for x in shadows[1:]:
+        assert lib.mpenv_wire_unpack(x.h, buf, 1, None) == 0  # a keyframe first
+    hip.hipDeviceSynchronize()
+    nstreams = 4
+    streams = [C.c_void_p() for _ in range(nstreams)]
+    hip.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    for st in streams:
+        assert hip.hipStreamCreate(C.byref(st)) == 0
+
+    def learner_step():
+        for j, x in enumerate(shadows):
+            lib.mpenv_wire_unpack(x.h, buf, 0, streams[j % nstreams])
+
+    def sim_step(s):
+        e.combat_actions(ring + (s % 64) * A * 24, None, 1)
+        e.step()
+        lib.mpenv_wire_pack(e.h, buf, 0, None)
+
+    for name, fn in (("learner_step_ms", lambda s: learner_step()), ("sender_step_ms", sim_step)):
+        for s in range(5):
+            fn(150 + s)
+        hip.hipDeviceSynchronize()
+        t0 = time.perf_counter()
+        for s in range(40):
+            fn(155 + s)
+        hip.hipDeviceSynchronize()
+        res[name] = round((time.perf_counter() - t0) / 40 * 1e3, 4)
+    res["peers"] = peers
+    res["learner_keeps_up"] = res["learner_step_ms"] <= res["sender_step_ms"]
+    res["c4_scaling_bound"] = round(peers * min(1.0, res["sender_step_ms"] / res["learner_step_ms"]), 2)
     lib.mpenv_wire_bytes(e.h, 0, C.byref(n))
     res["message_bytes"] = n.value
     res["bytes_per_agent"] = round(n.value / A, 1)
