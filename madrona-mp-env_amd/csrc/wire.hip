@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdint>
 
 #include "engine.h"
@@ -109,93 +110,135 @@ __host__ __device__ inline WireLayout wireLayout(int64_t A, int64_t W, bool keyf
 }
 
 // ------------------------------------------------------------------ pack
-// thread = agent: state columns (and, for a keyframe, the last-known rows)
-__global__ void k_wire_pack_agents(DevState S, char *dst, WireLayout L)
+// One launch, four block ranges (round 4's three launches: ~40 us of the
+// ~105 us pack were the agent and world kernels' latency and the boundaries):
+//   lidar   thread = ray (agent * 80 + ray, forward rays first): the depth,
+//           and the class in two bit-planes (one ballot per plane per 64 rays);
+//   agents  thread = agent: state columns (and, for a keyframe, the
+//           last-known rows);
+//   worlds  thread = world: world columns; thread 0 the header;
+//   match   thread = 16 bytes of the [W][30] episode results, copied flat.
+// The header's flags word is zeroed before the launch (launchWirePack) and
+// every writer ORs its bits in, so no block's order matters.
+struct WirePackGrid {
+    uint32_t agents, worlds, match, total; // first block of each range (lidar = 0), then the total
+};
+
+__host__ __device__ inline WirePackGrid wirePackGrid(int64_t A, int64_t W)
 {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= S.A) return;
-    int k = 0;
-#define MP_PUT_F(n) reinterpret_cast<float *>(dst + L.af[k++])[g] = S.n[g];
-    MP_WIRE_AF(MP_PUT_F)
-#undef MP_PUT_F
-    k = 0;
-#define MP_PUT_I(n) reinterpret_cast<int32_t *>(dst + L.ai[k++])[g] = S.n[g];
-    MP_WIRE_AI(MP_PUT_I)
-#undef MP_PUT_I
-    reinterpret_cast<float *>(dst + L.hp)[g] = S.hp[g];
-    reinterpret_cast<float *>(dst + L.alive)[g] = S.alive[g];
-    reinterpret_cast<float *>(dst + L.reward)[g] = S.reward[g];
-    reinterpret_cast<int32_t *>(dst + L.done)[g] = S.done[g];
-    reinterpret_cast<int2 *>(dst + L.mag)[g] = make_int2(S.magazine[2 * g], S.magazine[2 * g + 1]);
-    const int32_t cp = S.curPose[g], tp = S.tgtPose[g], wp = S.weapon[g], fl = S.flags[g];
-    const bool fits = ((uint32_t)cp | (uint32_t)tp | (uint32_t)wp | (uint32_t)fl) < 256u;
-    reinterpret_cast<uint32_t *>(dst + L.packed)[g] =
-        (uint32_t)cp | ((uint32_t)tp << 8) | ((uint32_t)wp << 16) | ((uint32_t)fl << 24);
-    reinterpret_cast<uint8_t *>(dst + L.vis)[g] = S.visMask[g];
-    for (int c = 0; c < 9; c++) reinterpret_cast<float *>(dst + L.coefs)[g * 9 + c] = S.rewardCoefs[g * 9 + c];
-    if (L.lkObs >= 0) {
-        const float4 *src = reinterpret_cast<const float4 *>(S.lkObs + g * 6 * kOtherObs);
-        float4 *o = reinterpret_cast<float4 *>(dst + L.lkObs) + g * 6 * kOtherObs / 4;
-        for (int q = 0; q < 6 * kOtherObs / 4; q++) o[q] = src[q];
-        for (int q = 0; q < 18; q++) reinterpret_cast<float *>(dst + L.lkPos)[g * 18 + q] = S.lkPos[g * 18 + q];
-    }
-    if (!fits) atomicOr(&reinterpret_cast<WireHeader *>(dst)->flags, kWireOverflow);
+    auto blocks = [](int64_t n) { return (uint32_t)((n + 255) / 256); };
+    WirePackGrid G;
+    G.agents = blocks(A * kLidarRays);
+    G.worlds = G.agents + blocks(A);
+    G.match = G.worlds + blocks(W);
+    G.total = G.match + blocks((W * 120 + 15) / 16);
+    return G;
 }
 
-// thread = lidar ray (agent * 80 + ray, forward rays first): the depth, and
-// the class in two bit-planes (one ballot per plane per 64 rays)
-__global__ void k_wire_pack_lidar(DevState S, char *dst, WireLayout L)
+__global__ void __launch_bounds__(256) k_wire_pack(DevState S, char *dst, WireLayout L, WirePackGrid G,
+                                                   uint32_t worldOffset)
 {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nr = S.A * kLidarRays;
-    uint32_t c = 0;
-    bool ok = true;
-    if (r < nr) {
-        const int64_t g = r / kLidarRays;
-        const int k = (int)(r - g * kLidarRays);
-        const float4 v = k < kFwdRays ? reinterpret_cast<const float4 *>(S.fwdLidar)[g * kFwdRays + k]
-                                      : reinterpret_cast<const float4 *>(S.rearLidar)[g * kRearRays + k - kFwdRays];
-        reinterpret_cast<float *>(dst + L.depth)[r] = v.x;
-        const uint32_t y = __float_as_uint(v.y), z = __float_as_uint(v.z), w = __float_as_uint(v.w);
-        const uint32_t one = 0x3f800000u;
-        if (y == one && z == 0u && w == 0u) c = 1;
-        else if (y == 0u && z == one && w == 0u) c = 2;
-        else if (y == 0u && z == 0u && w == one) c = 3;
-        else ok = y == 0u && z == 0u && w == 0u && __float_as_uint(v.x) == 0xbf800000u; // (-1, 0, 0, 0)
+    const uint32_t b = blockIdx.x;
+    uint32_t *hflags = &reinterpret_cast<WireHeader *>(dst)->flags;
+    if (b < G.agents) {
+        const int64_t r = (int64_t)b * 256 + threadIdx.x;
+        const int64_t nr = S.A * kLidarRays;
+        uint32_t c = 0;
+        bool ok = true;
+        if (r < nr) {
+            const int64_t g = r / kLidarRays;
+            const int k = (int)(r - g * kLidarRays);
+            const float4 v = k < kFwdRays ? reinterpret_cast<const float4 *>(S.fwdLidar)[g * kFwdRays + k]
+                                          : reinterpret_cast<const float4 *>(S.rearLidar)[g * kRearRays + k - kFwdRays];
+            reinterpret_cast<float *>(dst + L.depth)[r] = v.x;
+            const uint32_t y = __float_as_uint(v.y), z = __float_as_uint(v.z), w = __float_as_uint(v.w);
+            const uint32_t one = 0x3f800000u;
+            if (y == one && z == 0u && w == 0u) c = 1;
+            else if (y == 0u && z == one && w == 0u) c = 2;
+            else if (y == 0u && z == 0u && w == one) c = 3;
+            else ok = y == 0u && z == 0u && w == 0u && __float_as_uint(v.x) == 0xbf800000u; // (-1, 0, 0, 0)
+        }
+        const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c >> 1);
+        const int lane = threadIdx.x & 63;
+        const int64_t word = (r - lane) / 32; // first of the wave's two words
+        const int64_t words = (nr + 31) / 32;
+        if (lane < 4) {
+            const int p = lane >> 1, h = lane & 1;
+            const uint64_t bb = p ? b1 : b0;
+            if (word + h < words) reinterpret_cast<uint32_t *>(dst + L.plane[p])[word + h] = (uint32_t)(bb >> (32 * h));
+        }
+        if (!ok) atomicOr(hflags, kWireOverflow);
+    } else if (b < G.worlds) {
+        const int64_t g = (int64_t)(b - G.agents) * 256 + threadIdx.x;
+        if (g >= S.A) return;
+        // every load first, then the stores (loads issued after stores wait
+        // for the stores' acknowledgements: gfx9 retires them in order)
+        float af[kWireAF];
+        int32_t ai[kWireAI];
+        int k = 0;
+#define MP_GET_F(n) af[k++] = S.n[g];
+        MP_WIRE_AF(MP_GET_F)
+#undef MP_GET_F
+        k = 0;
+#define MP_GET_I(n) ai[k++] = S.n[g];
+        MP_WIRE_AI(MP_GET_I)
+#undef MP_GET_I
+        const float hp = S.hp[g], alive = S.alive[g], reward = S.reward[g];
+        const int32_t done = S.done[g];
+        const int2 mag = make_int2(S.magazine[2 * g], S.magazine[2 * g + 1]);
+        const int32_t cp = S.curPose[g], tp = S.tgtPose[g], wp = S.weapon[g], fl = S.flags[g];
+        const uint8_t vis = S.visMask[g];
+        float coef[9];
+        for (int c = 0; c < 9; c++) coef[c] = S.rewardCoefs[g * 9 + c];
+        for (k = 0; k < kWireAF; k++) reinterpret_cast<float *>(dst + L.af[k])[g] = af[k];
+        for (k = 0; k < kWireAI; k++) reinterpret_cast<int32_t *>(dst + L.ai[k])[g] = ai[k];
+        reinterpret_cast<float *>(dst + L.hp)[g] = hp;
+        reinterpret_cast<float *>(dst + L.alive)[g] = alive;
+        reinterpret_cast<float *>(dst + L.reward)[g] = reward;
+        reinterpret_cast<int32_t *>(dst + L.done)[g] = done;
+        reinterpret_cast<int2 *>(dst + L.mag)[g] = mag;
+        const bool fits = ((uint32_t)cp | (uint32_t)tp | (uint32_t)wp | (uint32_t)fl) < 256u;
+        reinterpret_cast<uint32_t *>(dst + L.packed)[g] =
+            (uint32_t)cp | ((uint32_t)tp << 8) | ((uint32_t)wp << 16) | ((uint32_t)fl << 24);
+        reinterpret_cast<uint8_t *>(dst + L.vis)[g] = vis;
+        for (int c = 0; c < 9; c++) reinterpret_cast<float *>(dst + L.coefs)[g * 9 + c] = coef[c];
+        if (L.lkObs >= 0) {
+            const float4 *src = reinterpret_cast<const float4 *>(S.lkObs + g * 6 * kOtherObs);
+            float4 *o = reinterpret_cast<float4 *>(dst + L.lkObs) + g * 6 * kOtherObs / 4;
+            for (int q = 0; q < 6 * kOtherObs / 4; q++) o[q] = src[q];
+            for (int q = 0; q < 18; q++) reinterpret_cast<float *>(dst + L.lkPos)[g * 18 + q] = S.lkPos[g * 18 + q];
+        }
+        if (!fits) atomicOr(hflags, kWireOverflow);
+    } else if (b < G.match) {
+        const int64_t w = (int64_t)(b - G.worlds) * 256 + threadIdx.x;
+        if (w == 0) {
+            WireHeader *h = reinterpret_cast<WireHeader *>(dst);
+            h->magic = kWireMagic;
+            h->version = kWireVersion;
+            h->worldOffset = worldOffset;
+            h->W = S.W; h->N = S.N; h->T = S.T; h->pad = 0;
+            h->A = S.A;
+            h->bytes = L.total;
+            if (L.lkObs >= 0) atomicOr(hflags, kWireKeyframe);
+        }
+        if (w >= S.W) return;
+        int32_t wv[kWireWI];
+        int k = 0;
+#define MP_GET_W(n) wv[k++] = S.n[w];
+        MP_WIRE_WI(MP_GET_W)
+#undef MP_GET_W
+        for (k = 0; k < kWireWI; k++) reinterpret_cast<int32_t *>(dst + L.wi[k])[w] = wv[k];
+    } else {
+        const int64_t i = (int64_t)(b - G.match) * 256 + threadIdx.x;
+        const int64_t bytes = S.W * 120;
+        if (i * 16 >= bytes) return;
+        if (i * 16 + 16 <= bytes) {
+            reinterpret_cast<uint4 *>(dst + L.match)[i] = reinterpret_cast<const uint4 *>(S.matchResult)[i];
+        } else {
+            for (int64_t o = i * 16; o < bytes; o += 4)
+                reinterpret_cast<int32_t *>(dst + L.match)[o / 4] = S.matchResult[o / 4];
+        }
     }
-    const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c >> 1);
-    const int lane = threadIdx.x & 63;
-    const int64_t word = (r - lane) / 32; // first of the wave's two words
-    const int64_t words = (nr + 31) / 32;
-    if (lane < 4) {
-        const int p = lane >> 1, h = lane & 1;
-        const uint64_t b = p ? b1 : b0;
-        if (word + h < words) reinterpret_cast<uint32_t *>(dst + L.plane[p])[word + h] = (uint32_t)(b >> (32 * h));
-    }
-    if (!ok) atomicOr(&reinterpret_cast<WireHeader *>(dst)->flags, kWireOverflow);
-}
-
-// thread = world: world columns, episode results; thread 0 the header
-// (launched first: the agent and lidar kernels may then raise the overflow bit)
-__global__ void k_wire_pack_worlds(DevState S, char *dst, WireLayout L, uint32_t worldOffset)
-{
-    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w == 0) {
-        WireHeader *h = reinterpret_cast<WireHeader *>(dst);
-        h->magic = kWireMagic;
-        h->version = kWireVersion;
-        h->flags = L.lkObs >= 0 ? kWireKeyframe : 0u;
-        h->worldOffset = worldOffset;
-        h->W = S.W; h->N = S.N; h->T = S.T; h->pad = 0;
-        h->A = S.A;
-        h->bytes = L.total;
-    }
-    if (w >= S.W) return;
-    int k = 0;
-#define MP_PUT_W(n) reinterpret_cast<int32_t *>(dst + L.wi[k++])[w] = S.n[w];
-    MP_WIRE_WI(MP_PUT_W)
-#undef MP_PUT_W
-    for (int c = 0; c < 30; c++) reinterpret_cast<int32_t *>(dst + L.match)[w * 30 + c] = S.matchResult[w * 30 + c];
 }
 
 // ---------------------------------------------------------------- unpack
@@ -225,10 +268,9 @@ __device__ __forceinline__ bool wireOk(const DevState &S, const char *src, const
 // One launch, four block ranges (no kernel boundaries between the parts of
 // an unpack: round 4's three launches spent ~20 us in boundaries and short
 // blocks):
-//   lidar   thread = 4 consecutive rays of one agent (80 and 64 are
-//           multiples of 4, so a quad is all-forward or all-rear): one float4
-//           of depths, 4 bits of each class plane (one word), 64 contiguous
-//           bytes of f32 lidar out;
+//   lidar   thread = 4 rays 256 apart (1,024 consecutive rays per block):
+//           the depth and the class bits of each, a float4 of f32 lidar out
+//           per ray -- every load and store instruction unit-stride;
 //   agents  thread = agent: the state columns (+ a keyframe's last-known rows);
 //   worlds  thread = world: the world columns; a world whose episode counter
 //           moved since the last message had its agents' last-known rows
@@ -245,7 +287,7 @@ __host__ __device__ inline WireUnpackGrid wireUnpackGrid(int64_t A, int64_t W)
     auto blocks = [](int64_t n) { return (uint32_t)((n + 255) / 256); };
     WireUnpackGrid G;
     G.lidar = 0;
-    G.agents = blocks(A * kLidarRays / 4);
+    G.agents = (uint32_t)((A * kLidarRays + 1023) / 1024);
     G.worlds = G.agents + blocks(A);
     G.match = G.worlds + blocks(W);
     G.total = G.match + blocks((W * 120 + 15) / 16);
@@ -261,22 +303,35 @@ __global__ void __launch_bounds__(256) k_wire_unpack(DevState S, const char *src
     // desync bit, so no block's decision depends on when this lands)
     if (L.lkObs >= 0 && b == 0 && threadIdx.x == 0) atomicAnd(err, ~kWireErrDesync);
     if (b < G.agents) {
-        const int64_t q = (int64_t)b * 256 + threadIdx.x; // ray quad
-        if (q >= S.A * kLidarRays / 4) return;
-        const int64_t r = 4 * q;
-        const float4 d = reinterpret_cast<const float4 *>(src + L.depth)[q];
-        const uint32_t sh = (uint32_t)(r & 31);
-        const uint32_t p0 = reinterpret_cast<const uint32_t *>(src + L.plane[0])[r >> 5] >> sh;
-        const uint32_t p1 = reinterpret_cast<const uint32_t *>(src + L.plane[1])[r >> 5] >> sh;
-        const int64_t g = r / kLidarRays;
-        const int k = (int)(r - g * kLidarRays);
-        float4 *dst = k < kFwdRays ? reinterpret_cast<float4 *>(S.fwdLidar) + g * kFwdRays + k
-                                   : reinterpret_cast<float4 *>(S.rearLidar) + g * kRearRays + (k - kFwdRays);
-        const float dv[4] = { d.x, d.y, d.z, d.w };
+        // 1,024 consecutive rays per block, ray base + 256 j + thread: each
+        // load and store instruction is unit-stride (a 64-B run per lane made
+        // every store instruction 16-B pieces at a 64-B stride)
+        const int64_t nr = S.A * kLidarRays;
+        const int64_t r0 = (int64_t)b * 1024 + threadIdx.x;
+        float d[4];
+        uint32_t cl[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const uint32_t c = ((p0 >> j) & 1u) | (((p1 >> j) & 1u) << 1);
-            dst[j] = make_float4(dv[j], c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f, c == 3 ? 1.f : 0.f);
+            const int64_t r = r0 + 256 * j;
+            d[j] = 0.f;
+            cl[j] = 0;
+            if (r < nr) {
+                d[j] = reinterpret_cast<const float *>(src + L.depth)[r];
+                const uint32_t sh = (uint32_t)(r & 31);
+                cl[j] = ((reinterpret_cast<const uint32_t *>(src + L.plane[0])[r >> 5] >> sh) & 1u) |
+                        (((reinterpret_cast<const uint32_t *>(src + L.plane[1])[r >> 5] >> sh) & 1u) << 1);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t r = r0 + 256 * j;
+            if (r >= nr) break;
+            const int64_t g = r / kLidarRays;
+            const int k = (int)(r - g * kLidarRays);
+            float4 *dst = k < kFwdRays ? reinterpret_cast<float4 *>(S.fwdLidar) + g * kFwdRays + k
+                                       : reinterpret_cast<float4 *>(S.rearLidar) + g * kRearRays + (k - kFwdRays);
+            const uint32_t c = cl[j];
+            *dst = make_float4(d[j], c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f, c == 3 ? 1.f : 0.f);
         }
     } else if (b < G.worlds) {
         const int64_t g = (int64_t)(b - G.agents) * 256 + threadIdx.x;
@@ -341,34 +396,51 @@ __global__ void __launch_bounds__(256) k_wire_unpack(DevState S, const char *src
 
 // ------------------------------------------------------------ batch copy
 // gpuStreamStep's input and output copies (mgr.cpp:614-645) as one launch
-// per direction: blockIdx.y = segment, 16-B vectors grid-strided over it
-// (hipMemcpyAsync per tensor ran at ~1 TB/s for the 2.4 GB of a C3 step);
-// src == nullptr writes zeros (the agent maps, never written by the step).
+// per direction (hipMemcpyAsync per tensor ran at ~1 TB/s for the 2.4 GB of
+// a C3 step).  The segments' 16-B pieces form one index space (first[k] =
+// the first piece of segment k); a block takes kCopyPieces x 256 consecutive
+// pieces, so blocks are spread over the segments by size (round 4 gave every
+// segment the largest one's grid: most blocks of the small segments found
+// nothing to do) and each lane keeps kCopyPieces loads in flight before its
+// stores.  src == nullptr writes zeros (the agent maps, never written by the
+// step): store-only pieces.  A segment's last piece may be partial.
+constexpr int kCopyPieces = 8;
+
+__device__ __forceinline__ void copyPieceTail(const CopySeg &sg, int64_t piece)
+{
+    for (int64_t o = piece * 16; o < sg.bytes; o++)
+        static_cast<uint8_t *>(sg.dst)[o] = sg.src ? static_cast<const uint8_t *>(sg.src)[o] : 0;
+}
+
 __global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b)
 {
-    const CopySeg sg = b.seg[blockIdx.y];
-    const int64_t n16 = sg.bytes / 16;
-    const uint4 *src = static_cast<const uint4 *>(sg.src);
-    uint4 *dst = static_cast<uint4 *>(sg.dst);
-    // four 16-B loads in flight per lane before their stores (one per lane
-    // left the copy latency-bound at ~1.6 TB/s)
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (src) {
-        for (; i + 3 * stride < n16; i += 4 * stride) {
-            const uint4 a0 = src[i], a1 = src[i + stride], a2 = src[i + 2 * stride], a3 = src[i + 3 * stride];
-            dst[i] = a0;
-            dst[i + stride] = a1;
-            dst[i + 2 * stride] = a2;
-            dst[i + 3 * stride] = a3;
+    const int64_t base = (int64_t)blockIdx.x * (256 * kCopyPieces);
+    // the segment of the block's first piece (wave-uniform scan)
+    int s0 = 0;
+    while (s0 + 1 < b.n && b.first[s0 + 1] <= base) s0++;
+    uint4 v[kCopyPieces];
+    int seg[kCopyPieces];
+#pragma unroll
+    for (int j = 0; j < kCopyPieces; j++) {
+        const int64_t c = base + j * 256 + threadIdx.x;
+        int k = s0;
+        while (k + 1 < b.n && b.first[k + 1] <= c) k++;
+        seg[j] = c < b.first[b.n] ? k : -1;
+        v[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (seg[j] >= 0) {
+            const CopySeg &sg = b.seg[k];
+            const int64_t p = c - b.first[k];
+            if (sg.src && (p + 1) * 16 <= sg.bytes) v[j] = static_cast<const uint4 *>(sg.src)[p];
         }
-        for (; i < n16; i += stride) dst[i] = src[i];
-    } else {
-        for (; i < n16; i += stride) dst[i] = make_uint4(0u, 0u, 0u, 0u);
     }
-    if (blockIdx.x == 0 && threadIdx.x < (sg.bytes & 15)) {
-        const int64_t o = n16 * 16 + threadIdx.x;
-        static_cast<uint8_t *>(sg.dst)[o] = src ? static_cast<const uint8_t *>(sg.src)[o] : 0;
+#pragma unroll
+    for (int j = 0; j < kCopyPieces; j++) {
+        if (seg[j] < 0) continue;
+        const int64_t c = base + j * 256 + threadIdx.x;
+        const CopySeg &sg = b.seg[seg[j]];
+        const int64_t p = c - b.first[seg[j]];
+        if ((p + 1) * 16 <= sg.bytes) static_cast<uint4 *>(sg.dst)[p] = v[j];
+        else copyPieceTail(sg, p);
     }
 }
 
@@ -381,19 +453,22 @@ int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOf
 {
     hipStream_t st = (hipStream_t)stream;
     const WireLayout L = wireLayout(s.A, s.W, keyframe);
-    hipLaunchKernelGGL(k_wire_pack_worlds, dim3(grid(s.W)), dim3(256), 0, st, s, dst, L, worldOffset);
-    hipLaunchKernelGGL(k_wire_pack_agents, dim3(grid(s.A)), dim3(256), 0, st, s, dst, L);
-    hipLaunchKernelGGL(k_wire_pack_lidar, dim3(grid(s.A * kLidarRays)), dim3(256), 0, st, s, dst, L);
+    const WirePackGrid G = wirePackGrid(s.A, s.W);
+    if ((uintptr_t)s.matchResult & 15u) return -1;
+    if (checkW(hipMemsetAsync(dst + offsetof(WireHeader, flags), 0, sizeof(uint32_t), st))) return -1;
+    hipLaunchKernelGGL(k_wire_pack, dim3(G.total), dim3(256), 0, st, s, dst, L, G, worldOffset);
     return checkW(hipGetLastError());
 }
 
-int launchCopyBatch(const CopyBatch &b, void *stream)
+int launchCopyBatch(const CopyBatch &bIn, void *stream)
 {
-    if (b.n <= 0) return 0;
-    int64_t most = 0;
-    for (int k = 0; k < b.n; k++) most = b.seg[k].bytes > most ? b.seg[k].bytes : most;
-    const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>((most / 16 + 1023) / 1024, 1), 2048);
-    hipLaunchKernelGGL(k_copy_batch, dim3(gx, (unsigned)b.n), dim3(256), 0, (hipStream_t)stream, b);
+    if (bIn.n <= 0) return 0;
+    CopyBatch b = bIn;
+    b.first[0] = 0;
+    for (int k = 0; k < b.n; k++) b.first[k + 1] = b.first[k] + (b.seg[k].bytes + 15) / 16;
+    const int64_t blocks = (b.first[b.n] + 256 * kCopyPieces - 1) / (256 * kCopyPieces);
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(k_copy_batch, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, b);
     return checkW(hipGetLastError());
 }
 

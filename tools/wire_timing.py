@@ -57,9 +57,13 @@ def main():
     # spends per message
     peers = int(os.environ.get("WIRE_PEERS", 7))
     shadows = [sh] + [T.Engine(W, ts) for _ in range(peers - 1)]
-    for x in shadows[1:]:
-        assert lib.mpenv_wire_unpack(x.h, buf, 1, None) == 0  # a keyframe first
+    kbuf = e.mem.upload(np.zeros(n.value, np.uint8))
+    assert lib.mpenv_wire_pack(e.h, kbuf, 1, None) == 0  # a keyframe of the current step first
     hip.hipDeviceSynchronize()
+    for x in shadows[1:]:
+        assert lib.mpenv_wire_unpack(x.h, kbuf, 1, None) == 0
+    hip.hipDeviceSynchronize()
+    lib.mpenv_wire_error.argtypes = [C.c_void_p, C.POINTER(C.c_uint32)]
     nstreams = 4
     streams = [C.c_void_p() for _ in range(nstreams)]
     hip.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
@@ -84,6 +88,9 @@ def main():
             fn(155 + s)
         hip.hipDeviceSynchronize()
         res[name] = round((time.perf_counter() - t0) / 40 * 1e3, 4)
+    for x in shadows:  # every unpack above was accepted (a refused one is a no-op and times nothing)
+        err = C.c_uint32(9)
+        assert lib.mpenv_wire_error(x.h, C.byref(err)) == 0 and err.value == 0, err.value
     res["peers"] = peers
     res["learner_keeps_up"] = res["learner_step_ms"] <= res["sender_step_ms"]
     res["c4_scaling_bound"] = round(peers * min(1.0, res["sender_step_ms"] / res["learner_step_ms"]), 2)
