@@ -448,11 +448,6 @@ int mpenv_world_groups(mpenv_manager *mgr, int32_t *groups);
  * k_vis -> k_obs (fork after k_sim, join at the end of the step; results
  * identical).  Default off; env MPENV_LIDAR_BRANCH=1 at creation. */
 int mpenv_set_lidar_branch(mpenv_manager *mgr, int32_t on);
-/* Extension: the lidar kernel variant -- 0: one ray per lane (k_lidar),
- * 1: one fan angle's two sheet rays per lane through one paired BVH
- * traversal (k_lidar_pair).  Identical outputs.  Env MPENV_LIDAR_PAIRS at
- * creation. */
-int mpenv_set_lidar_pairs(mpenv_manager *mgr, int32_t on);
 
 /* Manager::triggerReset (mgr.cpp:2484-2500) */
 int mpenv_trigger_reset(mpenv_manager *mgr, int32_t world_idx);

@@ -160,9 +160,6 @@ struct DevState {
     // k_obs does nothing while (*obsGate & MPENV_WIRE_ERR_DESYNC): a learner
     // shadow whose wire history broke (wire.hip wireOk); null on the step path.
     const uint32_t *obsGate;
-    // k_lidar variant: 0 = one ray per lane (k_lidar), 1 = one fan angle's
-    // two sheet rays per lane (k_lidar_pair); identical outputs
-    int32_t lidarPairs;
 };
 
 // Per-step workload counters accumulated by the kernels in stats mode
@@ -313,7 +310,7 @@ struct CopySeg {
 struct CopyBatch {
     CopySeg seg[kMaxCopySegs];
     int n;
-    int64_t first[kMaxCopySegs + 1]; // 16-B piece prefix (filled by launchCopyBatch)
+    int64_t first[kMaxCopySegs + 1]; // first block of each segment (filled by launchCopyBatch)
 };
 int launchCopyBatch(const CopyBatch &b, void *stream);
 

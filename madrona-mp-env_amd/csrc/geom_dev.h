@@ -491,162 +491,6 @@ __device__ __forceinline__ bool bvhTraceRayT(const LBVH &b, mp::Vec3 ray_o, mp::
     return ray_hit;
 }
 
-// rayTriRot over vertices already loaded (the pair traversal loads a
-// triangle once for both rays); the same arithmetic, value for value.
-__device__ __forceinline__ bool rayTriRotV(const lf4 a, const lf4 b, const lf4 c, float o0, float o1, float oz,
-                                           bool sw, const RayTxfmD &tx, float t_max, float &out_t)
-{
-    using namespace mp;
-    const float a0 = a.x - o0, a1 = a.y - o1, Az_ = a.z - oz;
-    const float b0 = b.x - o0, b1 = b.y - o1, Bz_ = b.z - oz;
-    const float c0 = c.x - o0, c1 = c.y - o1, Cz_ = c.z - oz;
-    const float Akx = sw ? a1 : a0, Aky = sw ? a0 : a1;
-    const float Bkx = sw ? b1 : b0, Bky = sw ? b0 : b1;
-    const float Ckx = sw ? c1 : c0, Cky = sw ? c0 : c1;
-    const float Ax = fma_(-tx.Sx, Az_, Akx);
-    const float Ay = fma_(-tx.Sy, Az_, Aky);
-    const float Bx = fma_(-tx.Sx, Bz_, Bkx);
-    const float By = fma_(-tx.Sy, Bz_, Bky);
-    const float Cx = fma_(-tx.Sx, Cz_, Ckx);
-    const float Cy = fma_(-tx.Sy, Cz_, Cky);
-    float U = fma_(Cx, By, -(Cy * Bx));
-    float V = fma_(Ax, Cy, -(Ay * Cx));
-    float W = fma_(Bx, Ay, -(By * Ax));
-    if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
-    if (U == 0.0f || V == 0.0f || W == 0.0f) {
-        double CxBy = (double)Cx * (double)By;
-        double CyBx = (double)Cy * (double)Bx;
-        U = (float)(CxBy - CyBx);
-        double AxCy = (double)Ax * (double)Cy;
-        double AyCx = (double)Ay * (double)Cx;
-        V = (float)(AxCy - AyCx);
-        double BxAy = (double)Bx * (double)Ay;
-        double ByAx = (double)By * (double)Ax;
-        W = (float)(BxAy - ByAx);
-        if (U < 0.0f || V < 0.0f || W < 0.0f) return false;
-    }
-    float det = U + V + W;
-    if (det == 0.f) return false;
-    const float Az = tx.Sz * Az_;
-    const float Bz = tx.Sz * Bz_;
-    const float Cz = tx.Sz * Cz_;
-    const float T = fma_(U, Az, fma_(V, Bz, W * Cz));
-    if (T < 0.0f || T > t_max * det) return false;
-    const float rcpDet = 1.0f / det;
-    out_t = T * rcpDet;
-    return true;
-}
-
-// bvhTraceRayT<false, kOctNodeQ, true, true> (the lidar's closest hit over
-// the octant node images and the rotated vertex copies) for a PAIR of rays
-// with one direction and origins that differ only in z -- the two sheet
-// heights of one lidar fan angle (sim.cpp:3324-3506): o0 and (o0.x, o0.y,
-// z1).  One traversal serves both: each stack entry carries 2 bits (which
-// rays entered the node), each child box is tested per ray against that
-// ray's own t_max (the x / y slabs are shared -- same origin xy, same
-// direction), a leaf's triangles are loaded once and tested for each ray
-// that entered it, in order, an internal child is pushed with the rays that
-// entered it.  Each ray therefore visits exactly the nodes of its own
-// traversal, in the same order, with the same t_max at every test: the
-// results equal two bvhTraceRayT calls bit for bit (the shared slab values
-// are the same expressions of the same operands).
-__device__ __forceinline__ void bvhTracePairOct(const LBVH &b, mp::Vec3 o0, float z1, mp::Vec3 ray_d, float &t_out0,
-                                                bool &hit0, float &t_out1, bool &hit1)
-{
-    using namespace mp;
-    const float diveps = 0.0000001f;
-    Vec3 inv_d = v3(1.f / ray_d.x, 1.f / ray_d.y, 1.f / ray_d.z);
-    const RayTxfmD tx = rayTxfm(ray_d, inv_d);
-    const float rayXInv = copysign_(ray_d.x == 0 ? 1 / diveps : 1 / ray_d.x, ray_d.x);
-    const float rayYInv = copysign_(ray_d.y == 0 ? 1 / diveps : 1 / ray_d.y, ray_d.y);
-    const float rayZInv = copysign_(ray_d.z == 0 ? 1 / diveps : 1 / ray_d.z, ray_d.z);
-    const int kx0 = tx.kz == 2 ? 0 : tx.kz + 1, ky0 = kx0 == 2 ? 0 : kx0 + 1;
-    const MP_LDS lf4 *vrot = reinterpret_cast<const MP_LDS lf4 *>(b.verts) + tx.kz * b.rotStride;
-    const Vec3 o1 = v3(o0.x, o0.y, z1);
-    const float p00 = comp(o0, kx0), p01 = comp(o0, ky0), p0z = comp(o0, tx.kz);
-    const float p10 = comp(o1, kx0), p11 = comp(o1, ky0), p1z = comp(o1, tx.kz);
-    const bool rsw = tx.kx != kx0;
-
-    float t_max0 = kFltMax, t_max1 = kFltMax;
-    bool rh0 = false, rh1 = false;
-    ByteStack st;
-    st.lo = 0; st.hi = 0; st.n = 0;
-    uint32_t ms = 3u; // 2 bits per stack entry: the rays that entered the node
-    bsPush(st, 0);
-    while (st.n > 0) {
-        const uint32_t node_idx = bsPop(st);
-        const uint32_t m = ms & 3u;
-        ms >>= 2;
-        const NodeR node = loadNode<kOctNodeQ>(b, node_idx);
-        const float dirQuantX = expScaleD(node.expX) * rayXInv;
-        const float dirQuantY = expScaleD(node.expY) * rayYInv;
-        const float dirQuantZ = expScaleD(node.expZ) * rayZInv;
-        const float originQuantX = (node.minX - o0.x) * rayXInv;
-        const float originQuantY = (node.minY - o0.y) * rayYInv;
-        const float originQuantZ0 = (node.minZ - o0.z) * rayZInv;
-        const float originQuantZ1 = (node.minZ - z1) * rayZInv;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int32_t child = node.child[i];
-            if (child == -1) continue;
-            const float t_near_x = fma_(qb(node.qMinX, i), dirQuantX, originQuantX);
-            const float t_near_y = fma_(qb(node.qMinY, i), dirQuantY, originQuantY);
-            const float t_far_x = fma_(qb(node.qMaxX, i), dirQuantX, originQuantX);
-            const float t_far_y = fma_(qb(node.qMaxY, i), dirQuantY, originQuantY);
-            const float qzn = qb(node.qMinZ, i), qzf = qb(node.qMaxZ, i);
-            const float t_near_z0 = fma_(qzn, dirQuantZ, originQuantZ0);
-            const float t_far_z0 = fma_(qzf, dirQuantZ, originQuantZ0);
-            const float t_near_z1 = fma_(qzn, dirQuantZ, originQuantZ1);
-            const float t_far_z1 = fma_(qzf, dirQuantZ, originQuantZ1);
-            const float nxy = fmax_(t_near_x, t_near_y);
-            const float t_near0 = fmax_(nxy, fmax_(t_near_z0, 0.f));
-            const float t_near1 = fmax_(nxy, fmax_(t_near_z1, 0.f));
-            float t_far0, t_far1;
-            asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
-                : "=&v"(t_far0) : "v"(t_far_x), "v"(t_far_y), "v"(t_far_z0), "v"(t_max0));
-            asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
-                : "=&v"(t_far1) : "v"(t_far_x), "v"(t_far_y), "v"(t_far_z1), "v"(t_max1));
-            const uint32_t pass = ((m & 1u) && t_near0 <= t_far0 ? 1u : 0u) | ((m & 2u) && t_near1 <= t_far1 ? 2u : 0u);
-            if (pass == 0u) continue;
-            if (child & 0x80000000) {
-                const int leaf = child & 0x7fffffff;
-                const int ntri = (int)((node.triSize >> (8 * i)) & 0xffu);
-                bool ht0 = false, ht1 = false;
-                float hit_t0 = 0.f, hit_t1 = 0.f, leaf_tmax0 = t_max0, leaf_tmax1 = t_max1;
-#pragma unroll
-                for (int k = 0; k < 2; k++) {
-                    if (k >= ntri) break;
-                    const MP_LDS lf4 *p = vrot + (leaf + k) * 3;
-                    const lf4 va = p[0], vb = p[1], vc = p[2];
-                    if ((pass & 1u) && rayTriRotV(va, vb, vc, p00, p01, p0z, rsw, tx, leaf_tmax0, hit_t0)) {
-                        ht0 = true;
-                        leaf_tmax0 = hit_t0;
-                    }
-                    if ((pass & 2u) && rayTriRotV(va, vb, vc, p10, p11, p1z, rsw, tx, leaf_tmax1, hit_t1)) {
-                        ht1 = true;
-                        leaf_tmax1 = hit_t1;
-                    }
-                }
-                if (ht0) {
-                    rh0 = true;
-                    t_max0 = hit_t0;
-                }
-                if (ht1) {
-                    rh1 = true;
-                    t_max1 = hit_t1;
-                }
-            } else {
-                bsPush(st, (uint32_t)child);
-                ms = (ms << 2) | pass;
-            }
-        }
-    }
-    t_out0 = t_max0;
-    hit0 = rh0;
-    t_out1 = t_max1;
-    hit1 = rh1;
-}
-
 __device__ __forceinline__ bool bvhTraceRayD(const LBVH &b, mp::Vec3 ray_o, mp::Vec3 ray_d, float &t_out,
                                              float t_max0 = mp::kFltMax)
 {

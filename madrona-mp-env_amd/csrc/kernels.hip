@@ -3660,193 +3660,6 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
     }
 }
 
-// pvpLidarSystem (sim.cpp:3324-3506) with one lane per fan ANGLE: a lane
-// traces the angle's two sheet rays (heights h = 0, 1: the same direction,
-// origins that differ only in z) through one paired traversal
-// (geom_dev.h bvhTracePairOct), so the node fetches, the x / y slabs, the
-// loop control and each triangle's vertex loads serve two rays.  Rays are
-// dealt in units of 8 agents = 5 wave tasks: tasks 0-3 carry two agents'
-// forward fans each (lanes 0-31 agent 2s, 32-63 agent 2s + 1: 32 angles x 2
-// heights), task 4 the 8 agents' rear fans (8 lanes each: 8 angles x 2
-// heights).  Each ray's arithmetic and visit order are those of k_lidar, so
-// the outputs are identical.  Runtime choice (mpenv_set_lidar_pairs).
-constexpr int kLidarPairStageMax = 8 * ((kLidarIters * kLidarWaves) / 5 + 2) + 2 * (2 * kMaxTeamSize - 1);
-
-__device__ __host__ __forceinline__ int64_t lidarPairTasks(int64_t A) { return ((A + 7) / 8) * 5; }
-
-// max over each group of G lanes (G a power of two <= 64) of non-negative
-// float bit patterns as ints
-template <int G> __device__ __forceinline__ int groupMaxBits(int v)
-{
-#pragma unroll
-    for (int off = 1; off < G; off <<= 1) v = max(v, __shfl_xor(v, off));
-    return v;
-}
-
-__global__ void __launch_bounds__(kLidarBlock) __attribute__((amdgpu_waves_per_eu(5))) k_lidar_pair(DevState S, SceneDev sc, int iters)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float2 fan[32 + 8];
-    if (threadIdx.x < 40) {
-        const bool fwd = threadIdx.x < 32;
-        const int x = fwd ? threadIdx.x : threadIdx.x - 32;
-        const int width = fwd ? 32 : 8;
-        const float range = fwd ? 0.75f * kPi : -kPi;
-        const float offset = fwd ? 0.5f * (1.f - 0.75f) * kPi : 0.f;
-        const float theta = range * (float(x) / float(width - 1)) + offset;
-        fan[threadIdx.x] = make_float2(-cosf_(theta), sinf_(theta));
-    }
-    const uint32_t N = (uint32_t)S.N, T = (uint32_t)S.T;
-    const uint32_t A = (uint32_t)S.A;
-    const uint32_t ntasks = (uint32_t)lidarPairTasks(S.A);
-    __shared__ float agentStage[kLidarStageCols][kLidarPairStageMax];
-    const uint32_t t0 = xcdBlockId() * (uint32_t)iters * kLidarWaves;
-    const uint32_t t1 = min(ntasks, t0 + (uint32_t)iters * kLidarWaves);
-    uint32_t s0 = 0, ns = 0;
-    if (t0 < t1) {
-        const uint32_t a_lo = (t0 / 5u) * 8u, a_hi = min(A, ((t1 - 1u) / 5u) * 8u + 8u);
-        s0 = (a_lo / N) * N;
-        ns = ((a_hi - 1u) / N + 1u) * N - s0;
-        for (uint32_t k = threadIdx.x; k < ns; k += blockDim.x) {
-            const uint32_t g = s0 + k;
-            agentStage[0][k] = S.px[g];
-            agentStage[1][k] = S.py[g];
-            agentStage[2][k] = S.pz[g];
-            agentStage[3][k] = S.aw[g];
-            agentStage[4][k] = S.ax[g];
-            agentStage[5][k] = S.ay[g];
-            agentStage[6][k] = S.az[g];
-            agentStage[7][k] = S.rw[g];
-            agentStage[8][k] = S.rx[g];
-            agentStage[9][k] = S.ry[g];
-            agentStage[10][k] = S.rz[g];
-            agentStage[11][k] = viewHeightD(S.curPose[g]);
-        }
-    }
-    const LBVH bvh = stageBVHOct(smem, sc); // ends with __syncthreads
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int it = 0; it < iters; it++) {
-        const uint32_t task = (xcdBlockId() * iters + it) * kLidarWaves + wave; // wave-uniform
-        if (task >= ntasks) break;
-        const uint32_t unit = task / 5u, sub = task - unit * 5u;
-        const bool fwd = sub < 4u;
-        // lane -> (agent, angle); a tail unit's lanes past A trace a copy of
-        // the last agent's rays and store nothing
-        auto pairIndex = [&](uint32_t ln, uint32_t &g, bool &valid, uint32_t &x) {
-            const uint32_t g_raw = unit * 8u + (fwd ? 2u * sub + (ln >> 5) : (ln >> 3));
-            valid = g_raw < A;
-            g = valid ? g_raw : A - 1u;
-            x = fwd ? (ln & 31u) : (ln & 7u);
-        };
-        uint32_t lane;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-        uint32_t g, x;
-        bool valid;
-        Vec3 ray_o, dir;
-        float z1;
-        float tb0, tb1;
-        bool bh0, bh1;
-        {
-            pairIndex(lane, g, valid, x);
-            const uint32_t k = g - s0, qc = fwd ? 3u : 7u;
-            const Quat q = quat(agentStage[qc][k], agentStage[qc + 1u][k], agentStage[qc + 2u][k],
-                                agentStage[qc + 3u][k]);
-            const Vec3 dir_fwd = rotateVec(q, kFwd);
-            const Vec3 dir_right = rotateVec(q, kRight);
-            const float top = agentStage[11][k] + c::kAgentRadius;
-            ray_o = v3(agentStage[0][k], agentStage[1][k], agentStage[2][k]);
-            // height offsets as k_lidar forms them for h = 0 and h = 1
-            const float base_z = ray_o.z;
-            ray_o.z = base_z + (c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(0u) / float(2 - 1)));
-            z1 = base_z + (c::kAgentRadius + (top - 2.f * c::kAgentRadius) * (float(1u) / float(2 - 1)));
-            const float2 cs = fan[fwd ? x : 32 + x];
-            dir = normalize(cs.x * dir_right + cs.y * dir_fwd);
-            LBVH ob = bvh;
-            ob.nodes = reinterpret_cast<const MP_LDS BVHNode *>(reinterpret_cast<const MP_LDS uint4 *>(bvh.nodes) +
-                                                                 rayOctant(dir) * sc.numNodes * kOctNodeQ);
-            bvhTracePairOct(ob, ray_o, z1, dir, tb0, bh0, tb1, bh1);
-        }
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-        pairIndex(lane, g, valid, x);
-        const uint32_t w = __umulhi(g, S.nMagic); // g / N (engine.h)
-        const uint32_t i = g - w * N;
-        const int64_t g0 = (int64_t)w * N;
-        // The world's capsules (capsulesD, ascending j, the caster's own
-        // skipped), read from the LDS agent stage, culled per agent group
-        // (fwd: 32 lanes, rear: 8): a capsule whose axis lies farther in xy
-        // than the group's largest BVH hit (either height) plus 1.01 r + 1
-        // can enter no ray before its hit (k_lidar's cull, exact); the xy
-        // cull of a ray against a capsule is the same for both heights.
-        float min0 = bh0 ? tb0 : kFltMax, min1 = bh1 ? tb1 : kFltMax;
-        const int bits = max(__float_as_int(min0), __float_as_int(min1));
-        const float mx = __int_as_float(fwd ? groupMaxBits<32>(bits) : groupMaxBits<8>(bits));
-        bool hit0 = bh0, hit1 = bh1;
-        int ent0 = -1, ent1 = -1;
-        const float dxy2 = dir.x * dir.x + dir.y * dir.y;
-        const float cull_r2 = (kCapsuleRadius * 1.01f) * (kCapsuleRadius * 1.01f);
-        const uint32_t l0 = (uint32_t)(g0 - s0);
-        for (uint32_t j = 0; j < N; j++) {
-            if (j == i) continue;
-            const float cx = agentStage[0][l0 + j], cy = agentStage[1][l0 + j];
-            {
-                const float dx = cx - ray_o.x, dy = cy - ray_o.y;
-                if (sqrtf(dx * dx + dy * dy) - c::kAgentRadius * 1.01f - 1.f > mx) continue;
-            }
-            Vec3 co = v3(cx, cy, agentStage[2][l0 + j]);
-            co.z += kCapsuleRadius;
-            const Vec3 tr0 = ray_o - co;
-            const float cr = tr0.x * dir.y - tr0.y * dir.x;
-            if (cr * cr > cull_r2 * dxy2) continue;
-            const Vec3 tr1 = v3(ray_o.x, ray_o.y, z1) - co;
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const Vec3 tr = h ? tr1 : tr0;
-                float &min_t = h ? min1 : min0;
-                const float along = -(tr.x * dir.x + tr.y * dir.y + tr.z * dir.z);
-                const float ahead = along + fmaxD(0.f, kCapsuleSegment * dir.z) + kCapsuleRadius * 1.01f;
-                if (ahead < 0.f) continue;
-                if (along + fminD(0.f, kCapsuleSegment * dir.z) - kCapsuleRadius * 1.01f > min_t) continue;
-                const float t = intersectRayZOriginCapsule(tr, dir, kCapsuleRadius, kCapsuleSegment);
-                if (t != 0 && t < min_t) {
-                    min_t = t;
-                    if (h) {
-                        hit1 = true;
-                        ent1 = (int)j;
-                    } else {
-                        hit0 = true;
-                        ent0 = (int)j;
-                    }
-                }
-            }
-        }
-        if (!valid) continue;
-        const bool second = i >= T; // team of the casting agent
-        const int64_t slot = ((int64_t)w * 2 + (second ? 1 : 0)) * kMaxTeamSize + (second ? i - T : i);
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const bool hit = h ? hit1 : hit0;
-            const int ent = h ? ent1 : ent0;
-            const float tt = h ? min1 : min0;
-            float4 out;
-            if (hit) {
-                const bool wall = ent == -1;
-                const bool tm = !wall && ((uint32_t)ent >= T) == second;
-                out = make_float4(fminD(tt, sc.maxDist), wall ? 1.f : 0.f, tm ? 1.f : 0.f, (!wall && !tm) ? 1.f : 0.f);
-            } else {
-                out = make_float4(-1.f, 0.f, 0.f, 0.f);
-            }
-            const uint32_t kk = fwd ? (uint32_t)h * 32u + x : (uint32_t)h * 8u + x;
-            float4 *dst = fwd ? reinterpret_cast<float4 *>(S.fwdLidar) + (int64_t)g * kFwdRays + kk
-                              : reinterpret_cast<float4 *>(S.rearLidar) + (int64_t)g * kRearRays + kk;
-            float4 *tdst = fwd ? reinterpret_cast<float4 *>(S.ftFwdLidar) + slot * kFwdRays + kk
-                               : reinterpret_cast<float4 *>(S.ftRearLidar) + slot * kRearRays + kk;
-            // the previous value moves into the team interface (sim.cpp:5283-5310)
-            *tdst = *dst;
-            *dst = out;
-        }
-    }
-}
-
 static int check(hipError_t e) { return e == hipSuccess ? 0 : -1; }
 
 // Debug/test hook: closest-hit BVH queries for caller rays (mode 0 = the
@@ -4122,15 +3935,6 @@ int computeZoneGoalTris(const SceneDev &sc, int32_t *dev_scratch, int32_t *host_
 
 int launchLidar(const DevState &s, const SceneDev &sc, void *stream)
 {
-    if (s.lidarPairs) {
-        const int64_t tasks = lidarPairTasks(s.A);
-        const int iters = (int)std::max<int64_t>(1, std::min<int64_t>(kLidarIters, tasks / (kLidarWaves * 1024)));
-        const int64_t per_block = (int64_t)kLidarWaves * iters;
-        const int blocks = (int)((tasks + per_block - 1) / per_block);
-        hipLaunchKernelGGL(k_lidar_pair, dim3(blocks), dim3(kLidarBlock), bvhLdsBytesOct(sc), (hipStream_t)stream, s,
-                           sc, iters);
-        return check(hipGetLastError());
-    }
     // ~1024 blocks before the iterations grow past 1
     const int64_t tasks = lidarTasks(s.A);
     const int iters = (int)std::max<int64_t>(1, std::min<int64_t>(kLidarIters, tasks / (kLidarWaves * 1024)));

@@ -941,7 +941,6 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m = new mpenv_manager();
         m->S.stats = nullptr;
         m->S.obsGate = nullptr;
-        m->S.lidarPairs = 0;
         m->cfg = *cfg;
         m->scenePath = cfg->scene_path;
         m->cfg.scene_path = m->scenePath.c_str();
@@ -975,8 +974,6 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
             m->setupGroups(want);
         }
         if (const char *e = std::getenv("MPENV_STEP_GRAPH")) m->useGraph = std::atoi(e) != 0;
-        if (const char *e = std::getenv("MPENV_LIDAR_PAIRS"))
-            if (mpenv_set_lidar_pairs(m, std::atoi(e)) != MPENV_OK) throw std::runtime_error(g_last_error);
         if (const char *e = std::getenv("MPENV_LIDAR_BRANCH"))
             if (std::atoi(e) != 0 && mpenv_set_lidar_branch(m, 1) != MPENV_OK) throw std::runtime_error(g_last_error);
         // TrainControl from sim flags (mgr.cpp:1397-1413)
@@ -1244,19 +1241,6 @@ int mpenv_graph_status(mpenv_manager *m, int32_t *graph_on, char *reason, int32_
     *graph_on = m->useGraph ? 1 : 0;
     if (reason && reason_len > 0) {
         std::snprintf(reason, (size_t)reason_len, "%s", m->graphOffReason.c_str());
-    }
-    return MPENV_OK;
-}
-
-int mpenv_set_lidar_pairs(mpenv_manager *m, int32_t on)
-{
-    if (!m) return fail(MPENV_ERR_INVALID, "null argument");
-    try {
-        HIP_CHECK(hipStreamSynchronize(m->stream));
-        m->S.lidarPairs = on ? 1 : 0;
-        for (DevState &G : m->gS) G.lidarPairs = m->S.lidarPairs;
-    } catch (const std::exception &e) {
-        return fail(MPENV_ERR_HIP, e.what());
     }
     return MPENV_OK;
 }

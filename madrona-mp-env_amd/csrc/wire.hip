@@ -397,50 +397,49 @@ __global__ void __launch_bounds__(256) k_wire_unpack(DevState S, const char *src
 // ------------------------------------------------------------ batch copy
 // gpuStreamStep's input and output copies (mgr.cpp:614-645) as one launch
 // per direction (hipMemcpyAsync per tensor ran at ~1 TB/s for the 2.4 GB of
-// a C3 step).  The segments' 16-B pieces form one index space (first[k] =
-// the first piece of segment k); a block takes kCopyPieces x 256 consecutive
-// pieces, so blocks are spread over the segments by size (round 4 gave every
-// segment the largest one's grid: most blocks of the small segments found
-// nothing to do) and each lane keeps kCopyPieces loads in flight before its
-// stores.  src == nullptr writes zeros (the agent maps, never written by the
-// step): store-only pieces.  A segment's last piece may be partial.
+// a C3 step).  Every segment gets ceil(pieces / (256 x kCopyPieces)) blocks
+// of its own (first[k] = its first block), so a block's segment is one
+// wave-uniform lookup and blocks are spread over the segments by size
+// (round 4 gave every segment the largest one's grid: most blocks of the
+// small segments found nothing to do); each lane keeps kCopyPieces 16-B
+// loads in flight before its stores, every load and store instruction
+// unit-stride.  src == nullptr writes zeros (the agent maps, never written
+// by the step): store-only pieces.  A segment's last piece may be partial.
 constexpr int kCopyPieces = 8;
-
-__device__ __forceinline__ void copyPieceTail(const CopySeg &sg, int64_t piece)
-{
-    for (int64_t o = piece * 16; o < sg.bytes; o++)
-        static_cast<uint8_t *>(sg.dst)[o] = sg.src ? static_cast<const uint8_t *>(sg.src)[o] : 0;
-}
+constexpr int kCopyBlockPieces = 256 * kCopyPieces;
 
 __global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b)
 {
-    const int64_t base = (int64_t)blockIdx.x * (256 * kCopyPieces);
-    // the segment of the block's first piece (wave-uniform scan)
-    int s0 = 0;
-    while (s0 + 1 < b.n && b.first[s0 + 1] <= base) s0++;
-    uint4 v[kCopyPieces];
-    int seg[kCopyPieces];
+    int k = 0;
+    while (k + 1 < b.n && b.first[k + 1] <= (int64_t)blockIdx.x) k++; // uniform
+    const CopySeg sg = b.seg[k];
+    const int64_t n16 = sg.bytes / 16;
+    const int64_t p0 = ((int64_t)blockIdx.x - b.first[k]) * kCopyBlockPieces + threadIdx.x;
+    const uint4 *src = static_cast<const uint4 *>(sg.src);
+    uint4 *dst = static_cast<uint4 *>(sg.dst);
+    if (src) {
+        uint4 v[kCopyPieces];
 #pragma unroll
-    for (int j = 0; j < kCopyPieces; j++) {
-        const int64_t c = base + j * 256 + threadIdx.x;
-        int k = s0;
-        while (k + 1 < b.n && b.first[k + 1] <= c) k++;
-        seg[j] = c < b.first[b.n] ? k : -1;
-        v[j] = make_uint4(0u, 0u, 0u, 0u);
-        if (seg[j] >= 0) {
-            const CopySeg &sg = b.seg[k];
-            const int64_t p = c - b.first[k];
-            if (sg.src && (p + 1) * 16 <= sg.bytes) v[j] = static_cast<const uint4 *>(sg.src)[p];
+        for (int j = 0; j < kCopyPieces; j++) {
+            const int64_t p = p0 + j * 256;
+            v[j] = p < n16 ? src[p] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < kCopyPieces; j++) {
+            const int64_t p = p0 + j * 256;
+            if (p < n16) dst[p] = v[j];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kCopyPieces; j++) {
+            const int64_t p = p0 + j * 256;
+            if (p < n16) dst[p] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
-#pragma unroll
-    for (int j = 0; j < kCopyPieces; j++) {
-        if (seg[j] < 0) continue;
-        const int64_t c = base + j * 256 + threadIdx.x;
-        const CopySeg &sg = b.seg[seg[j]];
-        const int64_t p = c - b.first[seg[j]];
-        if ((p + 1) * 16 <= sg.bytes) static_cast<uint4 *>(sg.dst)[p] = v[j];
-        else copyPieceTail(sg, p);
+    // the partial last piece (bytes % 16), by the segment's first block
+    if (blockIdx.x == b.first[k] && threadIdx.x < (sg.bytes & 15)) {
+        const int64_t o = n16 * 16 + threadIdx.x;
+        static_cast<uint8_t *>(sg.dst)[o] = src ? static_cast<const uint8_t *>(sg.src)[o] : 0;
     }
 }
 
@@ -465,9 +464,9 @@ int launchCopyBatch(const CopyBatch &bIn, void *stream)
     if (bIn.n <= 0) return 0;
     CopyBatch b = bIn;
     b.first[0] = 0;
-    for (int k = 0; k < b.n; k++) b.first[k + 1] = b.first[k] + (b.seg[k].bytes + 15) / 16;
-    const int64_t blocks = (b.first[b.n] + 256 * kCopyPieces - 1) / (256 * kCopyPieces);
-    if (blocks == 0) return 0;
+    for (int k = 0; k < b.n; k++)
+        b.first[k + 1] = b.first[k] + std::max<int64_t>(1, (b.seg[k].bytes / 16 + kCopyBlockPieces - 1) / kCopyBlockPieces);
+    const int64_t blocks = b.first[b.n];
     hipLaunchKernelGGL(k_copy_batch, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, b);
     return checkW(hipGetLastError());
 }
