@@ -3380,13 +3380,13 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
 // consecutive task quads: up to kLidarIters (amortises the BVH staging) on
 // big batches, fewer on small ones so the grid still spreads over the CUs
 // (at 64 worlds 1v1 a fixed 8 put the whole lidar on 5 CUs).
-constexpr int kLidarIters = 4; // 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92, 16: 0.98 ms (k_lidar alone, C3, round 2)
+constexpr int kLidarIters = 6; // round 5, one world group: 4: 0.665, 5: 0.642, 6: 0.643 ms steady, step 1.185 / 1.168 / 1.163 ms (profiles/r05m_lab_lidar_iters.jsonl; round 2: 1: 0.98, 2: 0.91, 4: 0.89, 8: 0.92 ms)
 // 1024-thread blocks: the 8 octant node images + the three rotated vertex
 // copies (31 + 36 KB on simple_map) are staged once per 16 waves, so 2
 // blocks per CU (8 waves per SIMD) fit the 160 KB of LDS.
 constexpr int kLidarBlock = 1024;
 constexpr int kLidarWaves = kLidarBlock / 64;
-constexpr int kLidarStageMax = 96, kLidarStageCols = 12; // k_lidar's per-block agent stage
+constexpr int kLidarStageMax = 112, kLidarStageCols = 12; // k_lidar's per-block agent stage
 static_assert(4 * ((kLidarIters * kLidarWaves) / 5 + 2) + 2 * (2 * kMaxTeamSize - 1) <= kLidarStageMax,
               "k_lidar agent stage");
 
