@@ -71,7 +71,6 @@ constexpr uint32_t kFlagHardcodedSpawns = 1u << 6;
 constexpr uint32_t kFlagEnableCurriculum = 1u << 5;
 constexpr uint32_t kFlagNavmeshSpawn = 1u << 2;
 constexpr uint32_t kFlagSubZones = 1u << 11;
-constexpr int32_t kFlagCrumbRequest = 64; // transient (leave -> append)
 
 __device__ __forceinline__ float viewHeightD(int pose)
 {
@@ -815,11 +814,20 @@ __device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, con
 }
 
 // sim.cpp:1794-1836 applyDmgSystem
-__device__ void applyDmgD(const DevState &S, int64_t g)
+// What the world lane's respawn reads about an agent after applyDmgD (k_sim
+// hands it over in LDS).
+struct DmgOut {
+    bool alive;
+    int32_t flags;
+    Vec3 pos;
+};
+
+__device__ DmgOut applyDmgD(const DevState &S, int64_t g)
 {
     // every input read before the first store (the damage slots are floats
     // like the stores between them, which would serialise the loads)
     int32_t flags = S.flags[g] & ~kFlagWasKilled;
+    Vec3 pos = ldPos(S, g);
     const int rs = S.respawnSteps[g];
     float hp = S.hp[g];
     const bool was_alive = S.alive[g] == 1.f;
@@ -843,16 +851,23 @@ __device__ void applyDmgD(const DevState &S, int64_t g)
         statAdd(S.stats + kStatHits, was_shot > 0 ? 1u : 0u);
         statAdd(S.stats + kStatKills, (was_alive && hp <= 0.f) ? 1u : 0u);
     }
-    if (hp <= 0.f) {
+    const bool dead = hp <= 0.f;
+    if (dead) {
         hp = 0.f;
         S.alive[g] = 0.f;
-        stPos(S, g, v3(0, 0, 10000.f));
+        pos = v3(0, 0, 10000.f);
+        stPos(S, g, pos);
         stVel(S, g, v3(0, 0, 0));
     } else {
         S.alive[g] = 1.f;
     }
     S.hp[g] = hp;
     S.flags[g] = flags;
+    DmgOut o;
+    o.alive = !dead;
+    o.flags = flags;
+    o.pos = pos;
+    return o;
 }
 
 // sim.cpp:1875-1890 autoHealSystem
@@ -875,9 +890,35 @@ __device__ void autoHealD(const DevState &S, int64_t g)
 // does not evaluate them one after another (k_sim, resetPreD).
 constexpr int kPreDraws = 10;
 
+// What the world lane's spawn loop reads about its world's agents, kept in
+// LDS by k_sim (null members: read memory): positions [N][3] and alive
+// bytes, both updated as agents spawn (the respawn scoring sees earlier
+// spawns), and each agent's flags before the spawn (as float bits).
+// tabA / tabB / tabC: LDS copies of the scene's spawn lists (aSpawns,
+// bSpawns, commonRespawns), or null.
+struct SpawnLds {
+    float *pos;
+    uint8_t *alive;
+    const float *flags;
+    const Spawn *tabA, *tabB, *tabC;
+};
+
+// World values the spawn loop reads once (not per agent).
+struct SpawnWorld {
+    int teamA, cz, episodeCurr;
+    uint32_t curStep;
+};
+
+// Spawn indices taken so far in a world reset's loop, per team list (bits
+// 0..127).  The reset cleared both lists just before (resetPreD), so
+// "tracker[idx] == curStep" holds exactly for the indices taken here.
+struct SpawnTaken {
+    uint64_t a0, a1, b0, b1;
+};
+
 __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w, int ai, bool is_respawn,
                                     bool use_middle, RNG &rng, Vec3 &out_pt, float &out_yaw,
-                                    const RandKey *pre = nullptr)
+                                    const RandKey *pre, const SpawnWorld &sw, const SpawnLds &L, SpawnTaken &tk)
 {
     // rng's draws, from `pre` while the counter is inside it (same keys
     // splitI(rng.key, ctr) the RNG would produce)
@@ -889,7 +930,7 @@ __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const Sce
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
     const int team = ai / S.T;
-    const uint32_t cur_step = (uint32_t)S.curStep[w];
+    const uint32_t cur_step = sw.curStep;
     uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
 
     const Spawn *options;
@@ -909,13 +950,14 @@ __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const Sce
     if (!is_respawn || sc.numCommon == 0) {
         uint32_t *tracker;
         int num_default, num_extra, num_spawns;
-        if (team == S.teamA[w]) {
-            options = sc.aSpawns;
+        const bool list_a = team == sw.teamA;
+        if (list_a) {
+            options = L.tabA ? L.tabA : sc.aSpawns;
             num_default = sc.numDefaultA;
             num_extra = sc.numA - sc.numDefaultA;
             tracker = track;
         } else {
-            options = sc.bSpawns;
+            options = L.tabB ? L.tabB : sc.bSpawns;
             num_default = sc.numDefaultB;
             num_extra = sc.numB - sc.numDefaultB;
             tracker = track + sc.spawnTrackLen;
@@ -925,6 +967,41 @@ __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const Sce
             num_spawns = num_extra;
         } else {
             num_spawns = num_default;
+        }
+        if (pre && !is_respawn && rng.ctr == 0 && num_spawns <= 128) {
+            // world reset: the agent's draw keys in one round of loads, the
+            // taken indices from tk instead of the tracker
+            RandKey k[kPreDraws];
+            #pragma unroll
+            for (int c = 0; c < kPreDraws; c++) k[c] = pre[c];
+            uint64_t &t0 = list_a ? tk.a0 : tk.b0, &t1 = list_a ? tk.a1 : tk.b1;
+            auto taken = [&](int idx) { return (((idx < 64 ? t0 : t1) >> (idx & 63)) & 1ull) != 0; };
+            int init_idx = keyI32(k[5], 0, num_spawns), used = 6;
+            #pragma unroll
+            for (int t = 4; t >= 0; t--) {
+                const int idx = keyI32(k[t], 0, num_spawns);
+                if (!taken(idx)) { init_idx = idx; used = t + 1; }
+            }
+            // draws used .. used + 3 position the agent (spawnAgent)
+            RandKey kk[4];
+            #pragma unroll
+            for (int j = 0; j < 4; j++) {
+                kk[j] = k[6 + j];
+                #pragma unroll
+                for (int t = 5; t >= 1; t--)
+                    if (used == t) kk[j] = k[t + j];
+            }
+            rng.ctr = (uint32_t)(used + 4);
+            const Spawn sp = options[init_idx];
+            const float x_min = sp.region.pMin.x, x_diff = sp.region.pMax.x - x_min;
+            const float y_min = sp.region.pMin.y, y_diff = sp.region.pMax.y - y_min;
+            const float z_min = sp.region.pMin.z, z_diff = sp.region.pMax.z - z_min;
+            out_pt = v3(x_min + keyUniform(kk[0]) * x_diff, y_min + keyUniform(kk[1]) * y_diff,
+                        z_min + keyUniform(kk[2]) * z_diff);
+            out_yaw = sp.yawMin + keyUniform(kk[3]) * (sp.yawMax - sp.yawMin);
+            (init_idx < 64 ? t0 : t1) |= 1ull << (init_idx & 63);
+            tracker[init_idx] = cur_step;
+            return;
         }
         int init_idx = -1;
         for (int k = 0; k < 5; k++) {
@@ -939,15 +1016,18 @@ __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const Sce
         return;
     }
 
-    options = sc.commonRespawns;
+    options = L.tabC ? L.tabC : sc.commonRespawns;
     uint32_t *rtrack = track + 2 * sc.spawnTrackLen;
-    const int cz = S.curZone[w];
+    const int cz = sw.cz;
     AABB za = sc.tab->zoneAABB[cz];
     Vec3 zone_center = 0.5f * (za.pMin + za.pMax);
     float best_score = kFltMax;
     int best_idx = -1;
+    // the next entry's tracker load is in flight during this one's scoring
+    uint32_t next_used = sc.numCommon > 0 ? rtrack[0] : 0u;
     for (int s = 0; s < sc.numCommon; s++) {
-        uint32_t last_used = rtrack[s];
+        const uint32_t last_used = next_used;
+        if (s + 1 < sc.numCommon) next_used = rtrack[s + 1];
         if (last_used == cur_step) continue;
         float score = 0.f;
         uint32_t elapsed = (uint32_t)(c::kDeltaT * float(cur_step - last_used));
@@ -958,8 +1038,9 @@ __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const Sce
         #pragma unroll 1
         for (int j = 0; j < N; j++) {
             if (j == ai) continue;
-            if (S.alive[g0 + j] == 0.f) continue;
-            float dist = distance(spawn_pt, ldPos(S, g0 + j));
+            if (L.alive ? L.alive[j] == 0 : S.alive[g0 + j] == 0.f) continue;
+            const Vec3 pj = L.pos ? v3(L.pos[3 * j], L.pos[3 * j + 1], L.pos[3 * j + 2]) : ldPos(S, g0 + j);
+            float dist = distance(spawn_pt, pj);
             if (dist < 4.f * c::kAgentRadius) {
                 score += 100000.f;
             } else {
@@ -987,30 +1068,47 @@ __device__ __forceinline__ int subZoneIndexD(const DevState &S, int64_t g)
 }
 
 // utils.cpp:734-948 spawnAgents
+// dead: the world's dead agents as a bit mask when the caller knows them
+// (k_sim: from applyDmgD's results in LDS; a reset: all), else -1 and read
+// from alive.  L: the caller's LDS copies of the world's agents (k_sim), or
+// null members.  A reset (!is_respawn) also stores each agent's start
+// position (sx, sy, sz: resetPersistentEntities sets them from the spawn).
 __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool is_respawn,
-                                             const RandKey *pre = nullptr)
+                                             const RandKey *pre = nullptr, int64_t dead = -1,
+                                             SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
-    int num_dead = 0;
-    #pragma unroll 1
-    for (int i = 0; i < N; i++)
-        if (S.alive[g0 + i] == 0.f) num_dead++;
-    if (num_dead == 0) return;
+    // Dead set fixed before the loop (utils.cpp:767-780).
+    uint32_t dead_mask = 0;
+    if (dead >= 0) {
+        dead_mask = (uint32_t)dead;
+    } else {
+        #pragma unroll 1
+        for (int i = 0; i < N; i++)
+            if (S.alive[g0 + i] == 0.f) dead_mask |= 1u << i;
+    }
+    if (dead_mask == 0) return;
     RNG base = ldWRng(S, w);
+    SpawnWorld sw;
+    sw.teamA = S.teamA[w];
+    sw.cz = S.curZone[w];
+    sw.curStep = (uint32_t)S.curStep[w];
+    sw.episodeCurr = S.episodeCurr[w];
     // episodes[sampleI32(0, numEpisodes = 0)]: an empty range, the value is
     // 0 whatever the key -- only the counter advances
     base.ctr += 1;
     bool use_middle = false;
     if (sc.simFlags & kFlagSpawnInMiddle) use_middle = rngUniform(base) < 0.5f;
     const bool randomize_hp = (sc.simFlags & kFlagRandomizeHP) != 0;
-    const int cz = S.curZone[w];
-
-    // Dead set fixed before the loop (utils.cpp:767-780).
-    uint32_t dead_mask = 0;
-    #pragma unroll 1
-    for (int i = 0; i < N; i++)
-        if (S.alive[g0 + i] == 0.f) dead_mask |= 1u << i;
+    const int cz = sw.cz;
+    // the zone box in its own frame, once for every agent
+    AABB zbox = sc.tab->zoneAABB[cz];
+    const Vec3 zone_center = (zbox.pMax + zbox.pMin) / 2.f;
+    const Quat to_zone = qinv(angleAxis(sc.tab->zoneRot[cz], kUp));
+    zbox.pMin = rotateVec(to_zone, zbox.pMin);
+    zbox.pMax = rotateVec(to_zone, zbox.pMax);
+    SpawnTaken tk = { 0ull, 0ull, 0ull, 0ull };
 
     #pragma unroll 1
     for (int ai = 0; ai < N; ai++) {
@@ -1018,20 +1116,23 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
         const int64_t g = g0 + ai;
         Vec3 spawn_pt;
         float spawn_yaw;
+        int32_t flags = L.flags ? __float_as_int(L.flags[ai]) : S.flags[g];
         if ((sc.simFlags & kFlagHardcodedSpawns) && !is_respawn) {
             // utils.cpp:480-650 hardcodedSpawnPoint
             const int team = ai / S.T;
-            hardcodedSpawn((team == S.teamA[w] ? 0 : 3) + (ai - team * S.T), spawn_pt, spawn_yaw);
+            hardcodedSpawn((team == sw.teamA ? 0 : 3) + (ai - team * S.T), spawn_pt, spawn_yaw);
         } else if (sc.simFlags & kFlagNavmeshSpawn) {
             // utils.cpp:807-809
             spawn_pt = navSamplePoint(sc.navTris, sc.navCdf, sc.numNavTris, rngAdvance(base));
             spawn_yaw = rngUniform(base) * 2.f * kPi;
         } else {
-            RNG rng = ldRng(S, g);
+            const RandKey *apre = pre ? pre + ai * (kPreDraws + 1) : nullptr;
+            // a reset's agent RNG is the fresh key resetPreD stored (apre[0])
+            RNG rng = apre ? makeRNG(apre[0]) : ldRng(S, g);
             standardSpawnPointD(S, sc, w, ai, is_respawn, use_middle, rng, spawn_pt, spawn_yaw,
-                                pre ? pre + ai * (kPreDraws + 1) + 1 : nullptr);
+                                apre ? apre + 1 : nullptr, sw, L, tk);
             stRng(S, g, rng);
-            if ((sc.simFlags & kFlagEnableCurriculum) && S.episodeCurr[w] == 0) {
+            if ((sc.simFlags & kFlagEnableCurriculum) && sw.episodeCurr == 0) {
                 // utils.cpp:819-837 LearnShooting
                 const bool north = spawn_pt.y > 0.f;
                 const float x = -700.f + rngUniform(base) * 1400.f;
@@ -1040,6 +1141,9 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
             }
         }
         stPos(S, g, spawn_pt);
+        if (!is_respawn) { S.sx[g] = spawn_pt.x; S.sy[g] = spawn_pt.y; S.sz[g] = spawn_pt.z; }
+        if (L.pos) { L.pos[3 * ai] = spawn_pt.x; L.pos[3 * ai + 1] = spawn_pt.y; L.pos[3 * ai + 2] = spawn_pt.z; }
+        if (L.alive) L.alive[ai] = 1;
         stRot(S, g, qnormalize(angleAxis(spawn_yaw, kUp)));
         stAim(S, g, computeAimD(spawn_yaw, 0.f));
         stVel(S, g, v3(0.f, 0.f, 0.f));
@@ -1060,14 +1164,9 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
         S.respawnSteps[g] = is_respawn ? 0 : c::kRespawnInvincibleSteps;
         S.autohealSteps[g] = 0;
         {
-            AABB za = sc.tab->zoneAABB[cz];
-            Vec3 zone_center = (za.pMax + za.pMin) / 2.f;
-            Quat to_zone = qinv(angleAxis(sc.tab->zoneRot[cz], kUp));
-            za.pMin = rotateVec(to_zone, za.pMin);
-            za.pMax = rotateVec(to_zone, za.pMax);
             Vec3 pz = rotateVec(to_zone, spawn_pt);
             spawn_pt.z += c::kStandHeight / 2.f;
-            setFlag(S, g, kFlagInZone, aabbContains(za, pz));
+            flags = aabbContains(zbox, pz) ? (flags | kFlagInZone) : (flags & ~kFlagInZone);
             S.minDistZone[g] = distance(spawn_pt, zone_center);
         }
         if (sc.simFlags & kFlagSubZones) {
@@ -1075,15 +1174,16 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
             // of the zone block and receives it a second time
             const ZOBBDev &sz = sc.tab->subZones[subZoneIndexD(S, g)];
             AABB za = { sz.pMin, sz.pMax };
-            Vec3 zone_center = (za.pMax + za.pMin) / 2.f;
-            Quat to_zone = qinv(angleAxis(sz.rotation, kUp));
-            za.pMin = rotateVec(to_zone, za.pMin);
-            za.pMax = rotateVec(to_zone, za.pMax);
-            Vec3 pz = rotateVec(to_zone, spawn_pt);
+            Vec3 sub_center = (za.pMax + za.pMin) / 2.f;
+            Quat to_sub = qinv(angleAxis(sz.rotation, kUp));
+            za.pMin = rotateVec(to_sub, za.pMin);
+            za.pMax = rotateVec(to_sub, za.pMax);
+            Vec3 pz = rotateVec(to_sub, spawn_pt);
             spawn_pt.z += c::kStandHeight / 2.f;
-            setFlag(S, g, kFlagInSubZone, aabbContains(za, pz));
-            S.minDistSub[g] = distance(spawn_pt, zone_center);
+            flags = aabbContains(za, pz) ? (flags | kFlagInSubZone) : (flags & ~kFlagInSubZone);
+            S.minDistSub[g] = distance(spawn_pt, sub_center);
         }
+        S.flags[g] = flags;
         S.curPose[g] = kStand; S.tgtPose[g] = kStand; S.transRem[g] = 0;
         S.maxVel[g] = c::kMaxWalkVelocity;
         S.dyv[g] = 0.f; S.dpv[g] = 0.f;
@@ -1096,7 +1196,8 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
 // resetPersistentEntities, agent i's own part (level_gen.cpp:330-370):
 // position, combat RNG split_i(episodeKey, i + 1), combat flags, last-known
 // observations, breadcrumb state.
-__device__ __forceinline__ void resetAgentD(const DevState &S, int64_t g, RandKey agent_key)
+// Returns the agent's flags after the reset.
+__device__ __forceinline__ int32_t resetAgentD(const DevState &S, int64_t g, RandKey agent_key)
 {
     stPos(S, g, v3(kFltMax, kFltMax, kFltMax));
     stRng(S, g, makeRNG(agent_key));
@@ -1105,7 +1206,8 @@ __device__ __forceinline__ void resetAgentD(const DevState &S, int64_t g, RandKe
     S.autohealSteps[g] = 0;
     S.wasShot[g] = 0;
     S.firedT[g] = -kFltMax;
-    S.flags[g] = S.flags[g] & (kFlagInZone | kFlagInSubZone);
+    const int32_t flags = S.flags[g] & (kFlagInZone | kFlagInSubZone);
+    S.flags[g] = flags;
     S.alive[g] = 0.f;
     float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
     for (int k = 0; k < 6 * kOtherObs / 4; k++) lk[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1113,12 +1215,15 @@ __device__ __forceinline__ void resetAgentD(const DevState &S, int64_t g, RandKe
     S.bcPenalty[g] = 0.f;
     S.bcLast[g] = -1;
     S.bcSteps[g] = 0;
+    return flags;
 }
 
 // pre != nullptr: every agent's resetAgentD already ran on its own lane and
-// pre holds, per agent, its RNG key then kPreDraws draw keys (resetPreD).
+// pre holds, per agent, its RNG key then kPreDraws draw keys (resetPreD);
+// L (k_sim, LDS): the flags resetAgentD left and the spawn lists.
 __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, int w, RandKey episode_key,
-                                         const RandKey *pre = nullptr)
+                                         const RandKey *pre = nullptr,
+                                         SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1146,13 +1251,14 @@ __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, cons
         uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
         for (int k = 0; k < 3 * sc.spawnTrackLen; k++) track[k] = 0xFFFFFFFFu;
     }
-    spawnAgentsD(S, sc, w, false, pre);
+    // every agent is dead here (resetAgentD); spawnAgentsD also stores the
+    // start positions sx, sy, sz (= the spawn positions)
+    spawnAgentsD(S, sc, w, false, pre, pre ? (int64_t)((1u << N) - 1u) : -1, L);
 
     RNG base = ldWRng(S, w);
     #pragma unroll 1
     for (int i = 0; i < N; i++) {
         const int64_t g = g0 + i;
-        S.sx[g] = S.px[g]; S.sy[g] = S.py[g]; S.sz[g] = S.pz[g];
         for (int k = 0; k < 4; k++) S.discreteAction[4 * g + k] = 0;
         S.aimAction[2 * g] = 0.f; S.aimAction[2 * g + 1] = 0.f;
         S.newCells[g] = 0;
@@ -1206,7 +1312,8 @@ __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, cons
 
 // sim.cpp:732-833 initWorld
 __device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool triggered_reset, const int32_t *tc,
-                           const RandKey *pre = nullptr)
+                           const RandKey *pre = nullptr,
+                           SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
 {
     const uint32_t world_id = sc.worldOffset + (uint32_t)w;
     S.matchValid[w] = 1; // matchID = worldID << 32 | curEpisodeIdx (sim.cpp:736-738)
@@ -1242,7 +1349,7 @@ __device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc
     S.subState[w] = 0; // every sub-zone: controlling -1, not contested / captured (sim.cpp:815-820)
     if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) S.curZone[w] = 3; // sim.cpp:822-825
     stWRng(S, w, base);
-    resetPersistentEntitiesD(S, sc, w, episode_key, pre);
+    resetPersistentEntitiesD(S, sc, w, episode_key, pre, L);
     S.filtAct0[w] = 0; S.filtAct1[w] = 0;
     S.filtMatched0[w] = 0; S.filtMatched1[w] = 0;
 }
@@ -1258,7 +1365,8 @@ __device__ __forceinline__ bool resetDueD(const DevState &S, const SceneDev &sc,
 // agent's combat RNG key split_i(episodeKey, i + 1) and its first kPreDraws
 // draw keys into pre[0], pre[1..], the agent's resetPersistentEntities
 // stores, and its share of the spawn-usage tracker reset.
-__device__ __forceinline__ void resetPreD(const DevState &S, const SceneDev &sc, int w, int i, RandKey *pre)
+// Returns the agent's flags after its reset.
+__device__ __forceinline__ int32_t resetPreD(const DevState &S, const SceneDev &sc, int w, int i, RandKey *pre)
 {
     const uint32_t world_id = sc.worldOffset + (uint32_t)w;
     const uint32_t ep = (uint32_t)S.episodeCounter[w]; // the episode resetSystemD is about to start
@@ -1266,12 +1374,14 @@ __device__ __forceinline__ void resetPreD(const DevState &S, const SceneDev &sc,
     const RandKey key = splitI(episode_key, (uint32_t)(i + 1));
     pre[0] = key;
     for (int c = 0; c < kPreDraws; c++) pre[1 + c] = splitI(key, (uint32_t)c);
-    resetAgentD(S, (int64_t)w * S.N + i, key);
+    const int32_t flags = resetAgentD(S, (int64_t)w * S.N + i, key);
     uint32_t *track = &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen];
     for (int k = i; k < 3 * sc.spawnTrackLen; k += S.N) track[k] = 0xFFFFFFFFu;
+    return flags;
 }
 
-__device__ __forceinline__ void resetSystemD(const DevState &S, const SceneDev &sc, int w, const RandKey *pre = nullptr)
+__device__ __forceinline__ void resetSystemD(const DevState &S, const SceneDev &sc, int w, const RandKey *pre = nullptr,
+                                             SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
 {
     const int32_t force = S.reset[w];
     if (!resetDueD(S, sc, w)) return;
@@ -1289,7 +1399,7 @@ __device__ __forceinline__ void resetSystemD(const DevState &S, const SceneDev &
             S.worldCurr[w] = 1;
         }
     }
-    initWorldD(S, sc, w, force == 1, S.trainCtrl, pre);
+    initWorldD(S, sc, w, force == 1, S.trainCtrl, pre, L);
 }
 
 // ====================================================== per-world systems
@@ -1469,28 +1579,29 @@ __device__ void subzoneSystemD(const DevState &S, const SceneDev &sc, int w)
 __device__ __forceinline__ float4 *crumbPtr(const DevState &S, int w) { return &S.crumbs[(int64_t)w * kMaxCrumbs * 2]; }
 
 // sim.cpp:4845-4889 leaveBreadcrumbsSystem, agent part: refresh own last
-// crumb or request a new one (appended in agent order by the world lane).
-__device__ void leaveBreadcrumbAgentD(const DevState &S, int w, int64_t g)
+// crumb or request a new one (returns true; appended in agent order by the
+// world lane, the requests handed over in LDS).  The penalty's reset to 0
+// is accumulateCrumbsD's starting value (the two always run together).
+__device__ bool leaveBreadcrumbAgentD(const DevState &S, int w, int64_t g)
 {
-    S.bcPenalty[g] = 0.f;
     const Vec3 pos = ldPos(S, g);
     const int32_t last = S.bcLast[g];
     bool updated = false;
     if (last != -1) {
         float4 *cr = crumbPtr(S, w);
         const int n = S.numCrumbs[w];
-        // the first crumb with id `last`, its ids read 4 at a time (one
-        // round of loads per 4 crumbs; past the end re-reads the last)
+        // the first crumb with id `last`, its ids read 8 at a time (one
+        // round of loads per 8 crumbs; past the end re-reads the last)
+        constexpr int kIds = 8;
         int hit = -1;
         #pragma unroll 1
-        for (int k0 = 0; k0 < n && hit < 0; k0 += 4) {
-            const int k1 = min(k0 + 1, n - 1), k2 = min(k0 + 2, n - 1), k3 = min(k0 + 3, n - 1);
-            const int i0 = __float_as_int(cr[2 * k0 + 1].z), i1 = __float_as_int(cr[2 * k1 + 1].z);
-            const int i2 = __float_as_int(cr[2 * k2 + 1].z), i3 = __float_as_int(cr[2 * k3 + 1].z);
-            if (i0 == last) hit = k0;
-            else if (k0 + 1 < n && i1 == last) hit = k0 + 1;
-            else if (k0 + 2 < n && i2 == last) hit = k0 + 2;
-            else if (k0 + 3 < n && i3 == last) hit = k0 + 3;
+        for (int k0 = 0; k0 < n && hit < 0; k0 += kIds) {
+            int id[kIds];
+            #pragma unroll
+            for (int j = 0; j < kIds; j++) id[j] = __float_as_int(cr[2 * min(k0 + j, n - 1) + 1].z);
+            #pragma unroll
+            for (int j = kIds - 1; j >= 0; j--)
+                if (k0 + j < n && id[j] == last) hit = k0 + j;
         }
         if (hit >= 0) {
             const float4 p = cr[2 * hit];
@@ -1501,19 +1612,23 @@ __device__ void leaveBreadcrumbAgentD(const DevState &S, int w, int64_t g)
             }
         }
     }
+    bool request = false;
     if (!updated) {
         int steps = S.bcSteps[g] + 1;
         if (steps > 10) {
-            S.flags[g] |= kFlagCrumbRequest;
+            request = true;
             steps = 0;
         }
         S.bcSteps[g] = steps;
     }
+    return request;
 }
 
-// World part of leaveBreadcrumbsSystem: append requested crumbs in agent order.
-__device__ void appendCrumbsD(const DevState &S, int w)
+// World part of leaveBreadcrumbsSystem: append requested crumbs in agent
+// order (req: bit i = agent i asked, from leaveBreadcrumbAgentD).
+__device__ void appendCrumbsD(const DevState &S, int w, uint32_t req)
 {
+    if (req == 0) return;
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
     float4 *cr = crumbPtr(S, w);
@@ -1522,9 +1637,7 @@ __device__ void appendCrumbsD(const DevState &S, int w)
     #pragma unroll 1
     for (int i = 0; i < N; i++) {
         const int64_t g = g0 + i;
-        int32_t f = S.flags[g];
-        if (!(f & kFlagCrumbRequest)) continue;
-        S.flags[g] = f & ~kFlagCrumbRequest;
+        if (!(req & (1u << i))) continue;
         if (n < kMaxCrumbs) {
             const int team = i / S.T, off = i - team * S.T;
             cr[2 * n] = make_float4(S.px[g], S.py[g], S.pz[g], 1.f);
@@ -1550,7 +1663,7 @@ __device__ void accumulateCrumbsD(const DevState &S, int w, int i)
     const Vec3 pos = ldPos(S, g);
     const float4 *cr = crumbPtr(S, w);
     const int n = S.numCrumbs[w];
-    float total = S.bcPenalty[g];
+    float total = 0.f; // leaveBreadcrumbsSystem's reset (sim.cpp:4845-4889)
     // 4 crumbs per round of loads (past the end re-reads the last, unused);
     // the sum keeps creation order
     auto add = [&](float4 meta, float4 p) {
@@ -2028,7 +2141,7 @@ __device__ void exploreVisitedD(const DevState &S, int w, int64_t g)
 // sim.cpp:4089-4200 zoneCaptureDefendRewardSystem: goal-region progress,
 // kills and control of the zone by the agent's own team, +-20 / -5 at the
 // end of the match; no curriculum, breadcrumb or area terms.
-__device__ void zoneCaptureDefendRewardD(const DevState &S, const SceneDev &sc, int w, int i)
+__device__ float zoneCaptureDefendRewardD(const DevState &S, const SceneDev &sc, int w, int i)
 {
     const int64_t g = (int64_t)w * S.N + i;
     const int team = i / S.T;
@@ -2069,13 +2182,14 @@ __device__ void zoneCaptureDefendRewardD(const DevState &S, const SceneDev &sc, 
         S.firedT[g] = -kFltMax;
     }
     S.reward[g] = r;
+    return r;
 }
 
 // sim.cpp:3734-3847 subzoneRewardSystem (after the LearnShooting branch,
 // which zoneRewardD handles for both): kills pay 3, the agent's own
 // sub-zone drives the in-zone / approach / control terms, no earned-point
 // or area terms.
-__device__ void subzoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
+__device__ float subzoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
 {
     const int64_t g = (int64_t)w * S.N + i;
     int32_t flags = S.flags[g];
@@ -2119,10 +2233,13 @@ __device__ void subzoneRewardD(const DevState &S, const SceneDev &sc, int w, int
         S.firedT[g] = -kFltMax;
     }
     S.reward[g] = r;
+    return r;
 }
 
 // sim.cpp:3849-3996 zoneRewardSystem (+ learnShootingRewardSystem 3707-3732)
-__device__ __forceinline__ void zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
+// Every reward system returns the reward it stored (k_sim hands it to the
+// team reward through LDS).
+__device__ __forceinline__ float zoneRewardD(const DevState &S, const SceneDev &sc, int w, int i)
 {
     const int64_t g0 = (int64_t)w * S.N;
     const int64_t g = g0 + i;
@@ -2130,19 +2247,17 @@ __device__ __forceinline__ void zoneRewardD(const DevState &S, const SceneDev &s
     const int landed = S.landedOn[g];
     float r = 0.f;
     if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) {
-        zoneCaptureDefendRewardD(S, sc, w, i);
-        return;
+        return zoneCaptureDefendRewardD(S, sc, w, i);
     }
     if (S.worldCurr[w] == 0) {
         if (landed != -1) r += 0.5f;
         else if (S.firedT[g] >= 0.f) r -= 0.05f;
         if (flags & kFlagReloadedFullMag) r -= 0.5f;
         S.reward[g] = r;
-        return;
+        return r;
     }
     if (sc.simFlags & kFlagSubZones) {
-        subzoneRewardD(S, sc, w, i);
-        return;
+        return subzoneRewardD(S, sc, w, i);
     }
     const float *rc = &S.rewardCoefs[9 * g];
     const float shot = rc[1], explore = rc[2], in_zone = rc[3], ctrl_s = rc[5], zdist = rc[6], earned_s = rc[7],
@@ -2189,7 +2304,7 @@ __device__ __forceinline__ void zoneRewardD(const DevState &S, const SceneDev &s
         S.wasShot[g] = 0;
         S.firedT[g] = -kFltMax;
         S.reward[g] = r;
-        return;
+        return r;
     }
     {
         float poly = 0.f;
@@ -2209,6 +2324,7 @@ __device__ __forceinline__ void zoneRewardD(const DevState &S, const SceneDev &s
         r += frac * 1e-2f;
     }
     S.reward[g] = r;
+    return r;
 }
 
 // ====================================================== kernels
@@ -2336,8 +2452,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
 // holds floor(kSimBlock / N) whole worlds, lane = agent, phases separated
 // by workgroup barriers.
 constexpr int kSimBlock = 128;
+// k_sim's dynamic LDS: the BVH image (reused by the reset phase for its draw
+// keys, kPreDraws + 1 per lane) then the spawn lists.
+__host__ __device__ size_t simSpawnOffset(const SceneDev &sc)
+{
+    const size_t bvh = (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16;
+    const size_t keys = (size_t)kSimBlock * (kPreDraws + 1) * sizeof(RandKey);
+    return ((bvh > keys ? bvh : keys) + 15) & ~(size_t)15;
+}
 
-__device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
+__device__ __forceinline__ float flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
 
 // 4 waves/SIMD (128 VGPRs, at the price of ~420 B/lane of scratch spills):
 // k_sim alone 0.196 -> 0.139 ms -- every wave of a C3 launch resident,
@@ -2349,7 +2473,22 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
 {
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const LBVH bvh = stageBVH(smem, sc);
+    // dynamic LDS (simLdsBytes): the BVH image, which the reset phase reuses
+    // for its draw keys, then the scene's spawn lists
+    Spawn *const tabA = reinterpret_cast<Spawn *>(smem + simSpawnOffset(sc));
+    Spawn *const tabB = tabA + sc.numA, *const tabC = tabB + sc.numB;
+    {
+        const int nq = (sc.numA + sc.numB + sc.numCommon) * (int)(sizeof(Spawn) / 16);
+        const int na = sc.numA * (int)(sizeof(Spawn) / 16), nb = sc.numB * (int)(sizeof(Spawn) / 16);
+        uint4 *dst = reinterpret_cast<uint4 *>(tabA);
+        for (int k = threadIdx.x; k < nq; k += blockDim.x) {
+            const uint4 *src = k < na ? reinterpret_cast<const uint4 *>(sc.aSpawns) + k
+                             : k < na + nb ? reinterpret_cast<const uint4 *>(sc.bSpawns) + (k - na)
+                                           : reinterpret_cast<const uint4 *>(sc.commonRespawns) + (k - na - nb);
+            dst[k] = *src;
+        }
+    }
+    const LBVH bvh = stageBVH(smem, sc); // (its barrier also covers the spawn lists)
     const int N = S.N;
     const int wpb = kSimBlock / N;
     const int wl = threadIdx.x / N;
@@ -2359,6 +2498,13 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     const bool wlane = act && i == 0;
     const int64_t g = (int64_t)w * N + i;
 
+    __shared__ uint8_t agentB[kSimBlock]; // per-agent bytes for the world lane (alive, done)
+    // per-agent floats for the world lane, reused by phase: respawn
+    // (positions [3 * kSimBlock], flags), goal distances (stride 6), rewards,
+    // reset (flags)
+    __shared__ float goalDist[kSimBlock * 6];
+    float *const sposL = goalDist;
+    float *const sflagL = goalDist + 3 * kSimBlock;
     if (act && sc.eventsOn) { // ClearTmpNode<GameEventEntity> at step start (sim.cpp:5344)
         mpenv_game_event *ev = &S.events[(int64_t)w * S.evStride];
         ev[2 * i].type = 0;
@@ -2375,9 +2521,26 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     } else {
         if (act) fireD(S, sc, bvh, w, i);
         __syncthreads();
-        if (act) applyDmgD(S, g);
+        // the agents' alive states, positions and flags go to the world
+        // lane's respawn through LDS (it read them back from memory one
+        // agent at a time)
+        if (act) {
+            const DmgOut d = applyDmgD(S, g);
+            agentB[threadIdx.x] = d.alive ? 1 : 0;
+            sposL[3 * threadIdx.x] = d.pos.x;
+            sposL[3 * threadIdx.x + 1] = d.pos.y;
+            sposL[3 * threadIdx.x + 2] = d.pos.z;
+            sflagL[threadIdx.x] = __int_as_float(d.flags);
+        }
         __syncthreads();
-        if (wlane && !(sc.simFlags & kFlagNoRespawn)) spawnAgentsD(S, sc, w, true);
+        if (wlane && !(sc.simFlags & kFlagNoRespawn)) {
+            uint32_t dead = 0;
+            #pragma unroll 1
+            for (int k = 0; k < N; k++)
+                if (!agentB[wl * N + k]) dead |= 1u << k;
+            spawnAgentsD(S, sc, w, true, nullptr, dead,
+                         SpawnLds{ &sposL[3 * wl * N], &agentB[wl * N], &sflagL[wl * N], tabA, tabB, tabC });
+        }
         __syncthreads();
         if (act) autoHealD(S, g);
         __syncthreads();
@@ -2396,23 +2559,28 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             // the recorder reads neither), so they run between one pair of
             // barriers instead of three.
             if (act) {
-                zoneIn[threadIdx.x] = zoneInD(S, sc, zoneCz[wl], g) ? 1 : 0;
+                // bit 0 in the zone, bit 1 a new breadcrumb requested
+                const bool zin = zoneInD(S, sc, zoneCz[wl], g);
                 if (sc.recordOn) recordAgentD(S, w, i);
-                leaveBreadcrumbAgentD(S, w, g);
+                const bool req = leaveBreadcrumbAgentD(S, w, g);
+                zoneIn[threadIdx.x] = (zin ? 1 : 0) | (req ? 2 : 0);
             }
             if (wlane && sc.recordOn) S.recordLog[w].cur_step = S.curStep[w];
             __syncthreads();
             if (wlane) {
                 int na = 0, nb = 0;
+                uint32_t req = 0;
                 #pragma unroll 1
                 for (int k = 0; k < N; k++) {
-                    if (!zoneIn[wl * N + k]) continue;
+                    const int b = zoneIn[wl * N + k];
+                    if (b & 2) req |= 1u << k;
+                    if (!(b & 1)) continue;
                     if (k / S.T == 0) na += 1;
                     else nb += 1;
                 }
                 zonePostD(S, w, zp, na, nb);
                 if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
-                appendCrumbsD(S, w);
+                appendCrumbsD(S, w, req);
             }
         }
         __syncthreads();
@@ -2424,7 +2592,6 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     // zoneMatchInfoSystem's per-agent reads, one lane per agent (the world
     // lane would otherwise walk them serially)
     __shared__ uint8_t matchBits[kSimBlock];
-    __shared__ float goalDist[kSimBlock * 6];
     if (act) {
         matchBits[threadIdx.x] = (uint8_t)matchAgentBitsD(S, w, i);
         goalDistAgentD(S, sc, w, i, ldPos(S, g), &goalDist[threadIdx.x * 6]);
@@ -2436,10 +2603,16 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         goalRegionsD(S, sc, w, &goalDist[wl * N * 6]);
     }
     __syncthreads();
+    // rewards and done flags go to the world lane through LDS (rewL, agentB)
+    // instead of being read back from memory one agent at a time
+    // (in goalDist's LDS, whose last reader finished before the barrier above;
+    // teamL: 2 per world, at most kSimBlock / 2 worlds as N >= 2)
+    float *const rewL = goalDist;
+    float *const teamL = goalDist + kSimBlock;
     if (act) {
         exploreVisitedD(S, w, g);
-        if (sc.flank && sc.task == MPENV_TASK_ZONE) flankRewardD(S, sc, bvh, w, i);
-        else zoneRewardD(S, sc, w, i);
+        if (sc.flank && sc.task == MPENV_TASK_ZONE) rewL[threadIdx.x] = flankRewardD(S, sc, bvh, w, i);
+        else rewL[threadIdx.x] = zoneRewardD(S, sc, w, i);
     }
     __syncthreads();
     if (wlane) {
@@ -2449,27 +2622,34 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         #pragma unroll 1
         for (int j = 0; j < N; j++) {
             int t = j / S.T;
-            tr[t] += S.reward[(int64_t)w * N + j];
+            tr[t] += rewL[wl * N + j];
             ts[t] += 1;
         }
         tr[0] /= float(ts[0]);
         tr[1] /= float(ts[1]);
         S.teamRew0[w] = tr[0];
         S.teamRew1[w] = tr[1];
+        teamL[2 * wl] = tr[0];
+        teamL[2 * wl + 1] = tr[1];
     }
     __syncthreads();
     if (act) {
         // pvpFinalRewardSystem (sim.cpp:4315-4339) + doneSystem (4712-4717)
         const int team = i / S.T;
-        float my = S.reward[g];
-        float team_r = team == 0 ? S.teamRew0[w] : S.teamRew1[w];
-        float spirit = S.rewardCoefs[9 * g];
-        S.reward[g] = my * (1.f - spirit) + team_r * spirit;
-        S.done[g] = S.finished[w] ? 1 : 0;
+        const float spirit = S.rewardCoefs[9 * g];
+        const bool done = S.finished[w] != 0;
+        const float my = rewL[threadIdx.x];
+        const float team_r = teamL[2 * wl + team];
+        const float fr = my * (1.f - spirit) + team_r * spirit;
+        S.reward[g] = fr;
+        S.done[g] = done ? 1 : 0;
+        rewL[threadIdx.x] = fr;
+        agentB[threadIdx.x] = done ? 1 : 0;
     }
     // resets: the agents' own parts in parallel, then the world lane
-    RandKey *pre = S.resetKeys + ((int64_t)w * N) * (kPreDraws + 1);
-    if (act && resetDueD(S, sc, w)) resetPreD(S, sc, w, i, pre + i * (kPreDraws + 1));
+    // (the BVH image is dead from here on: the reset's draw keys go there)
+    RandKey *pre = reinterpret_cast<RandKey *>(smem) + (int64_t)wl * N * (kPreDraws + 1);
+    if (act && resetDueD(S, sc, w)) sflagL[threadIdx.x] = __int_as_float(resetPreD(S, sc, w, i, pre + i * (kPreDraws + 1)));
     __syncthreads();
     if (wlane) {
         // fullTeamDoneRewardSystem (sim.cpp:4720-4747)
@@ -2477,13 +2657,13 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             float r = 0.f;
             bool done = true;
             for (int j = t * S.T; j < (t + 1) * S.T; j++) {
-                r += S.reward[(int64_t)w * N + j];
-                if (!S.done[(int64_t)w * N + j]) done = false;
+                r += rewL[wl * N + j];
+                if (!agentB[wl * N + j]) done = false;
             }
             S.ftReward[(int64_t)w * 2 + t] = r;
             S.ftDone[(int64_t)w * 2 + t] = done ? 1 : 0;
         }
-        resetSystemD(S, sc, w, pre);
+        resetSystemD(S, sc, w, pre, SpawnLds{ nullptr, nullptr, &sflagL[wl * N], tabA, tabB, tabC });
     }
 }
 
@@ -2554,7 +2734,7 @@ __device__ __forceinline__ bool isAgentVisibleD(const DevState &S, const SceneDe
 // opponent that cannot see the agent (judged with the agent's own aim),
 // hits / kills from behind the target, exploration.  CombatState is taken
 // by value there, so nothing is cleared.
-__device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
+__device__ __forceinline__ float flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
 {
     const int T = S.T, N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -2591,6 +2771,7 @@ __device__ __forceinline__ void flankRewardD(const DevState &S, const SceneDev &
     S.newCells[g] = 0;
     if (nn > 0) r += float(nn) * S.rewardCoefs[9 * g + 2];
     S.reward[g] = r;
+    return r;
 }
 
 __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
@@ -3843,6 +4024,11 @@ const char *kernelName(int k)
 }
 
 size_t bvhLdsBytes(const SceneDev &sc) { return (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16; }
+
+size_t simLdsBytes(const SceneDev &sc)
+{
+    return simSpawnOffset(sc) + (size_t)(sc.numA + sc.numB + sc.numCommon) * sizeof(Spawn);
+}
 static_assert(c::kAgentRadius == kSphereR, "k_move sphere casts use the agent radius (stageBVHSphere)");
 
 size_t bvhLdsBytesSphere(const SceneDev &sc)
@@ -3895,7 +4081,7 @@ int launchSimStep(const DevState &s, const SceneDev &sc, void *stream)
 {
     const int wpb = kSimBlock / s.N;
     const int blocks = (s.W + wpb - 1) / wpb;
-    hipLaunchKernelGGL(k_sim, dim3(blocks), dim3(kSimBlock), bvhLdsBytes(sc), (hipStream_t)stream, s, sc);
+    hipLaunchKernelGGL(k_sim, dim3(blocks), dim3(kSimBlock), simLdsBytes(sc), (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }
 

@@ -12,13 +12,15 @@ Instrumentation and switched-off parts live in patches under tools/lab/
 there and compiles that copy, so no lab hook sits in the shipped sources.
 
   tools/lab/lab_hooks.patch   the round-1..3 switches: -DMPENV_LAB_MOVE_SKIP=,
-                              _SIM_SKIP=, _PHASE_T, _WAVE_HIST=k, _WORK, _NO_TRI,
+                              _WAVE_HIST=k, _WORK, _NO_TRI,
                               _NO_BVH, _NO_CAPSULE, _NO_REAR, _NO_FT_LIDAR, ...,
                               and the dropped variants (MPENV_LIDAR_PERM,
                               MPENV_TRI_FLAT, MPENV_*_WPE, ...); the round-1..4
                               k_obs switches went with that kernel (round 5)
   (round 4's forward-fan candidate lists, fan_lists.patch / fan_phases.patch,
   are in git history before round 5: measured and dropped)
+  k_sim's -DMPENV_LAB_PHASE_T / _SIM_SKIP= / MPENV_SIM_WPE= hooks are inserted
+  by text (ksim_hooks below), not by a patch
 e.g. build phase --patch tools/lab/lab_hooks.patch -DMPENV_LAB_PHASE_T
 (tests/test_abi.py checks that every patch still applies to csrc/).
 """
@@ -34,6 +36,57 @@ PKG = os.path.join(ROOT, "madrona-mp-env_amd")
 LAB = os.path.join(PKG, "lab")
 sys.path.insert(0, PKG)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+# k_sim's lab hooks, inserted by text into the lab copy (k_sim changes too
+# often for a patch): a phase timer after every block barrier
+# (-DMPENV_LAB_PHASE_T, k_sim per-phase block cycles in stats slots 10..),
+# -DMPENV_LAB_SIM_SKIP=bits to switch phases off (wrong results by design),
+# -DMPENV_SIM_WPE=n for the waves-per-SIMD target.
+KSIM_SKIP = [("fireD(", 1), ("spawnAgentsD(", 2), ("zoneMatchInfoD(", 8), ("goalRegionsD(", 16),
+             ("resetSystemD(", 128), ("appendCrumbsD(", 256), ("decayCrumbsD(", 256), ("accumulateCrumbsD(", 512),
+             ("exploreVisitedD(", 1024)]
+
+
+def ksim_hooks(path):
+    s = open(path).read()
+    s = s.replace("#define MP_SIM_ATTR __attribute__((amdgpu_waves_per_eu(4)))",
+                  "#ifndef MPENV_SIM_WPE\n#define MPENV_SIM_WPE 4\n#endif\n"
+                  "#define MP_SIM_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_SIM_WPE)))")
+    head = "k_sim(DevState S, SceneDev sc)\n{"
+    a = s.index(head) + len(head) - 1
+    d, k = 0, a
+    while True:
+        d += {"{": 1, "}": -1}.get(s[k], 0)
+        if d == 0:
+            break
+        k += 1
+    body = s[a + 1:k]
+    body = body.replace("__syncthreads();", "__syncthreads(); MP_PT();")
+    for name, bit in KSIM_SKIP:
+        body = body.replace(name, f"(MPENV_LAB_SIM_SKIP & {bit}) ? (void)0 : (void){name}")
+    prelude = """
+#ifndef MPENV_LAB_SIM_SKIP
+#define MPENV_LAB_SIM_SKIP 0
+#endif
+#ifdef MPENV_LAB_PHASE_T
+    uint64_t pt_prev = clock64();
+    int pt_k = 0;
+    auto PT = [&]() {
+        if (threadIdx.x == 0 && S.stats) {
+            const uint64_t t = clock64();
+            atomicAdd(&S.stats[10 + pt_k], (unsigned long long)(t - pt_prev));
+            pt_prev = t;
+        }
+        pt_k++;
+    };
+#define MP_PT() PT()
+#else
+#define MP_PT() ((void)0)
+#endif
+"""
+    s = s[:a + 1] + prelude + body + s[k:]
+    open(path, "w").write(s)
 
 
 def build(name, args):
@@ -55,6 +108,8 @@ def build(name, args):
     shutil.copytree(B.CSRC, src_dir)
     for pf in patches:
         subprocess.run(["patch", "-s", "-p1", "-d", src_dir, "-i", pf], check=True)
+    if any(d.startswith(("-DMPENV_LAB_PHASE_T", "-DMPENV_LAB_SIM_SKIP", "-DMPENV_SIM_WPE")) for d in defines):
+        ksim_hooks(os.path.join(src_dir, "kernels.hip"))
     common = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{src_dir}",
               f"-I{B.INCLUDE}"] + list(defines)
     objs = []
