@@ -1067,6 +1067,84 @@ __device__ __forceinline__ int subZoneIndexD(const DevState &S, int64_t g)
     return p < 0 ? 0 : (p > 7 ? 7 : p);
 }
 
+// The zone box of zone cz in its own frame (spawnAgents' in-zone test).
+struct ZoneBox {
+    AABB box;
+    Vec3 center;
+    Quat toZone;
+};
+
+__device__ __forceinline__ ZoneBox zoneBoxD(const SceneDev &sc, int cz)
+{
+    ZoneBox z;
+    z.box = sc.tab->zoneAABB[cz];
+    z.center = (z.box.pMax + z.box.pMin) / 2.f;
+    z.toZone = qinv(angleAxis(sc.tab->zoneRot[cz], kUp));
+    z.box.pMin = rotateVec(z.toZone, z.box.pMin);
+    z.box.pMax = rotateVec(z.toZone, z.box.pMax);
+    return z;
+}
+
+// A spawned agent's own stores once its spawn point is chosen (the rest of
+// utils.cpp:734-948's loop body).  rng_ctr >= 0: the agent's RNG counter
+// after its spawn draws (its key is unchanged); flags: the agent's flags
+// before the spawn.  Run by the world lane, or (k_sim) by the agent's own
+// lane from the world lane's record.
+__device__ __forceinline__ void spawnApplyD(const DevState &S, const SceneDev &sc, int64_t g, bool is_respawn,
+                                            Vec3 spawn_pt, float spawn_yaw, int32_t rng_ctr, float hp, int32_t mag,
+                                            int32_t flags, const ZoneBox &zb)
+{
+    stPos(S, g, spawn_pt);
+    if (!is_respawn) { S.sx[g] = spawn_pt.x; S.sy[g] = spawn_pt.y; S.sz[g] = spawn_pt.z; }
+    if (rng_ctr >= 0) S.rngCtr[g] = rng_ctr;
+    stRot(S, g, qnormalize(angleAxis(spawn_yaw, kUp)));
+    stAim(S, g, computeAimD(spawn_yaw, 0.f));
+    stVel(S, g, v3(0.f, 0.f, 0.f));
+    S.weapon[g] = 0;
+    S.hp[g] = hp;
+    S.magazine[2 * g] = mag;
+    S.magazine[2 * g + 1] = 0;
+    S.respawnSteps[g] = is_respawn ? 0 : c::kRespawnInvincibleSteps;
+    S.autohealSteps[g] = 0;
+    {
+        Vec3 pz = rotateVec(zb.toZone, spawn_pt);
+        spawn_pt.z += c::kStandHeight / 2.f;
+        flags = aabbContains(zb.box, pz) ? (flags | kFlagInZone) : (flags & ~kFlagInZone);
+        S.minDistZone[g] = distance(spawn_pt, zb.center);
+    }
+    if (sc.simFlags & kFlagSubZones) {
+        // utils.cpp:906-926: spawn_pt already carries the +standHeight/2
+        // of the zone block and receives it a second time
+        const ZOBBDev &sz = sc.tab->subZones[subZoneIndexD(S, g)];
+        AABB za = { sz.pMin, sz.pMax };
+        Vec3 sub_center = (za.pMax + za.pMin) / 2.f;
+        Quat to_sub = qinv(angleAxis(sz.rotation, kUp));
+        za.pMin = rotateVec(to_sub, za.pMin);
+        za.pMax = rotateVec(to_sub, za.pMax);
+        Vec3 pz = rotateVec(to_sub, spawn_pt);
+        spawn_pt.z += c::kStandHeight / 2.f;
+        flags = aabbContains(za, pz) ? (flags | kFlagInSubZone) : (flags & ~kFlagInSubZone);
+        S.minDistSub[g] = distance(spawn_pt, sub_center);
+    }
+    S.flags[g] = flags;
+    S.curPose[g] = kStand; S.tgtPose[g] = kStand; S.transRem[g] = 0;
+    S.maxVel[g] = c::kMaxWalkVelocity;
+    S.dyv[g] = 0.f; S.dpv[g] = 0.f;
+    S.alive[g] = 1.f;
+}
+
+// The world lane's spawn record of one agent for spawnApplyD on the agent's
+// lane (k_sim, LDS): position, yaw, hp, then magazine and RNG counter as
+// float bits.
+constexpr int kSpawnRec = 8;
+
+__device__ __forceinline__ void spawnApplyRecD(const DevState &S, const SceneDev &sc, int64_t g, bool is_respawn,
+                                               const float *rec, int32_t flags, const ZoneBox &zb)
+{
+    spawnApplyD(S, sc, g, is_respawn, v3(rec[0], rec[1], rec[2]), rec[3], __float_as_int(rec[6]), rec[4],
+                __float_as_int(rec[5]), flags, zb);
+}
+
 // utils.cpp:734-948 spawnAgents
 // dead: the world's dead agents as a bit mask when the caller knows them
 // (k_sim: from applyDmgD's results in LDS; a reset: all), else -1 and read
@@ -1075,7 +1153,8 @@ __device__ __forceinline__ int subZoneIndexD(const DevState &S, int64_t g)
 // position (sx, sy, sz: resetPersistentEntities sets them from the spawn).
 __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool is_respawn,
                                              const RandKey *pre = nullptr, int64_t dead = -1,
-                                             SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
+                                             SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr },
+                                             float *rec = nullptr, RNG *base_out = nullptr)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1088,7 +1167,10 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
         for (int i = 0; i < N; i++)
             if (S.alive[g0 + i] == 0.f) dead_mask |= 1u << i;
     }
-    if (dead_mask == 0) return;
+    if (dead_mask == 0) {
+        if (base_out) *base_out = ldWRng(S, w);
+        return;
+    }
     RNG base = ldWRng(S, w);
     SpawnWorld sw;
     sw.teamA = S.teamA[w];
@@ -1102,12 +1184,10 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
     if (sc.simFlags & kFlagSpawnInMiddle) use_middle = rngUniform(base) < 0.5f;
     const bool randomize_hp = (sc.simFlags & kFlagRandomizeHP) != 0;
     const int cz = sw.cz;
-    // the zone box in its own frame, once for every agent
-    AABB zbox = sc.tab->zoneAABB[cz];
-    const Vec3 zone_center = (zbox.pMax + zbox.pMin) / 2.f;
-    const Quat to_zone = qinv(angleAxis(sc.tab->zoneRot[cz], kUp));
-    zbox.pMin = rotateVec(to_zone, zbox.pMin);
-    zbox.pMax = rotateVec(to_zone, zbox.pMax);
+    // the zone box in its own frame, once for every agent (record mode: the
+    // agents' lanes compute it)
+    ZoneBox zb;
+    if (!rec) zb = zoneBoxD(sc, cz);
     SpawnTaken tk = { 0ull, 0ull, 0ull, 0ull };
 
     #pragma unroll 1
@@ -1116,7 +1196,7 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
         const int64_t g = g0 + ai;
         Vec3 spawn_pt;
         float spawn_yaw;
-        int32_t flags = L.flags ? __float_as_int(L.flags[ai]) : S.flags[g];
+        int32_t rng_ctr = -1;
         if ((sc.simFlags & kFlagHardcodedSpawns) && !is_respawn) {
             // utils.cpp:480-650 hardcodedSpawnPoint
             const int team = ai / S.T;
@@ -1131,7 +1211,7 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
             RNG rng = apre ? makeRNG(apre[0]) : ldRng(S, g);
             standardSpawnPointD(S, sc, w, ai, is_respawn, use_middle, rng, spawn_pt, spawn_yaw,
                                 apre ? apre + 1 : nullptr, sw, L, tk);
-            stRng(S, g, rng);
+            rng_ctr = (int32_t)rng.ctr; // (the key is unchanged)
             if ((sc.simFlags & kFlagEnableCurriculum) && sw.episodeCurr == 0) {
                 // utils.cpp:819-837 LearnShooting
                 const bool north = spawn_pt.y > 0.f;
@@ -1140,56 +1220,31 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
                 spawn_pt = v3(x, north ? y : -y, 0.f);
             }
         }
-        stPos(S, g, spawn_pt);
-        if (!is_respawn) { S.sx[g] = spawn_pt.x; S.sy[g] = spawn_pt.y; S.sz[g] = spawn_pt.z; }
         if (L.pos) { L.pos[3 * ai] = spawn_pt.x; L.pos[3 * ai + 1] = spawn_pt.y; L.pos[3 * ai + 2] = spawn_pt.z; }
         if (L.alive) L.alive[ai] = 1;
-        stRot(S, g, qnormalize(angleAxis(spawn_yaw, kUp)));
-        stAim(S, g, computeAimD(spawn_yaw, 0.f));
-        stVel(S, g, v3(0.f, 0.f, 0.f));
         // sampleI32(0, numWeaponTypes = 1) is 0 whatever the key: advance only
         static_assert(c::kNumWeaponTypes == 1, "weapon draw shortcut assumes one weapon type");
         base.ctr += 1;
-        S.weapon[g] = 0;
+        float hp = 100.f;
+        int32_t mag = c::kMagSize;
         if (randomize_hp) {
             int tenth = rngI32(base, 1, 11);
-            S.hp[g] = float(tenth * 10);
-            S.magazine[2 * g] = rngI32(base, 0, c::kMagSize);
-            S.magazine[2 * g + 1] = 0;
+            hp = float(tenth * 10);
+            mag = rngI32(base, 0, c::kMagSize);
+        }
+        if (rec) {
+            float *r = rec + ai * kSpawnRec;
+            r[0] = spawn_pt.x; r[1] = spawn_pt.y; r[2] = spawn_pt.z; r[3] = spawn_yaw;
+            r[4] = hp; r[5] = __int_as_float(mag); r[6] = __int_as_float(rng_ctr);
         } else {
-            S.hp[g] = 100.f;
-            S.magazine[2 * g] = c::kMagSize;
-            S.magazine[2 * g + 1] = 0;
+            const int32_t flags = L.flags ? __float_as_int(L.flags[ai]) : S.flags[g];
+            spawnApplyD(S, sc, g, is_respawn, spawn_pt, spawn_yaw, rng_ctr, hp, mag, flags, zb);
         }
-        S.respawnSteps[g] = is_respawn ? 0 : c::kRespawnInvincibleSteps;
-        S.autohealSteps[g] = 0;
-        {
-            Vec3 pz = rotateVec(to_zone, spawn_pt);
-            spawn_pt.z += c::kStandHeight / 2.f;
-            flags = aabbContains(zbox, pz) ? (flags | kFlagInZone) : (flags & ~kFlagInZone);
-            S.minDistZone[g] = distance(spawn_pt, zone_center);
-        }
-        if (sc.simFlags & kFlagSubZones) {
-            // utils.cpp:906-926: spawn_pt already carries the +standHeight/2
-            // of the zone block and receives it a second time
-            const ZOBBDev &sz = sc.tab->subZones[subZoneIndexD(S, g)];
-            AABB za = { sz.pMin, sz.pMax };
-            Vec3 sub_center = (za.pMax + za.pMin) / 2.f;
-            Quat to_sub = qinv(angleAxis(sz.rotation, kUp));
-            za.pMin = rotateVec(to_sub, za.pMin);
-            za.pMax = rotateVec(to_sub, za.pMax);
-            Vec3 pz = rotateVec(to_sub, spawn_pt);
-            spawn_pt.z += c::kStandHeight / 2.f;
-            flags = aabbContains(za, pz) ? (flags | kFlagInSubZone) : (flags & ~kFlagInSubZone);
-            S.minDistSub[g] = distance(spawn_pt, sub_center);
-        }
-        S.flags[g] = flags;
-        S.curPose[g] = kStand; S.tgtPose[g] = kStand; S.transRem[g] = 0;
-        S.maxVel[g] = c::kMaxWalkVelocity;
-        S.dyv[g] = 0.f; S.dpv[g] = 0.f;
-        S.alive[g] = 1.f;
     }
-    stWRng(S, w, base);
+    // (the caller that continues drawing takes the RNG back instead of
+    // reloading it behind every store above)
+    if (base_out) *base_out = base;
+    else stWRng(S, w, base);
 }
 
 // level_gen.cpp:330-582 resetPersistentEntities
@@ -1221,9 +1276,22 @@ __device__ __forceinline__ int32_t resetAgentD(const DevState &S, int64_t g, Ran
 // pre != nullptr: every agent's resetAgentD already ran on its own lane and
 // pre holds, per agent, its RNG key then kPreDraws draw keys (resetPreD);
 // L (k_sim, LDS): the flags resetAgentD left and the spawn lists.
+// rec (k_sim, LDS, only without curriculum snapshots): spawn records for
+// the agents' lanes, which also do resetAgentTailD.
+__device__ __forceinline__ void resetAgentTailD(const DevState &S, int64_t g)
+{
+    for (int k = 0; k < 4; k++) S.discreteAction[4 * g + k] = 0;
+    S.aimAction[2 * g] = 0.f; S.aimAction[2 * g + 1] = 0.f;
+    S.newCells[g] = 0;
+    float *rc = &S.rewardCoefs[9 * g];
+    rc[0] = 0.f; rc[1] = 0.5f; rc[2] = 0.005f; rc[3] = 0.05f; rc[4] = 0.01f;
+    rc[5] = 0.1f; rc[6] = 0.0005f; rc[7] = 1.f; rc[8] = 0.1f;
+}
+
 __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, int w, RandKey episode_key,
                                          const RandKey *pre = nullptr,
-                                         SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
+                                         SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr },
+                                         float *rec = nullptr)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1253,20 +1321,14 @@ __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, cons
     }
     // every agent is dead here (resetAgentD); spawnAgentsD also stores the
     // start positions sx, sy, sz (= the spawn positions)
-    spawnAgentsD(S, sc, w, false, pre, pre ? (int64_t)((1u << N) - 1u) : -1, L);
+    RNG base;
+    spawnAgentsD(S, sc, w, false, pre, pre ? (int64_t)((1u << N) - 1u) : -1, L, rec, &base);
 
-    RNG base = ldWRng(S, w);
     #pragma unroll 1
     for (int i = 0; i < N; i++) {
-        const int64_t g = g0 + i;
-        for (int k = 0; k < 4; k++) S.discreteAction[4 * g + k] = 0;
-        S.aimAction[2 * g] = 0.f; S.aimAction[2 * g + 1] = 0.f;
-        S.newCells[g] = 0;
+        if (!rec) resetAgentTailD(S, g0 + i);
         // level_gen.cpp:427-446: nine discarded coefficient draws.
         base.ctr += 9;
-        float *rc = &S.rewardCoefs[9 * g];
-        rc[0] = 0.f; rc[1] = 0.5f; rc[2] = 0.005f; rc[3] = 0.05f; rc[4] = 0.01f;
-        rc[5] = 0.1f; rc[6] = 0.0005f; rc[7] = 1.f; rc[8] = 0.1f;
     }
     // GoalRegionsState (level_gen.cpp:472-485)
     S.goalMin0[w] = kFltMax;
@@ -1313,7 +1375,8 @@ __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, cons
 // sim.cpp:732-833 initWorld
 __device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc, int w, bool triggered_reset, const int32_t *tc,
                            const RandKey *pre = nullptr,
-                           SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
+                           SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr },
+                           float *rec = nullptr)
 {
     const uint32_t world_id = sc.worldOffset + (uint32_t)w;
     S.matchValid[w] = 1; // matchID = worldID << 32 | curEpisodeIdx (sim.cpp:736-738)
@@ -1349,7 +1412,7 @@ __device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc
     S.subState[w] = 0; // every sub-zone: controlling -1, not contested / captured (sim.cpp:815-820)
     if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) S.curZone[w] = 3; // sim.cpp:822-825
     stWRng(S, w, base);
-    resetPersistentEntitiesD(S, sc, w, episode_key, pre, L);
+    resetPersistentEntitiesD(S, sc, w, episode_key, pre, L, rec);
     S.filtAct0[w] = 0; S.filtAct1[w] = 0;
     S.filtMatched0[w] = 0; S.filtMatched1[w] = 0;
 }
@@ -1381,7 +1444,8 @@ __device__ __forceinline__ int32_t resetPreD(const DevState &S, const SceneDev &
 }
 
 __device__ __forceinline__ void resetSystemD(const DevState &S, const SceneDev &sc, int w, const RandKey *pre = nullptr,
-                                             SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr })
+                                             SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr },
+                                             float *rec = nullptr)
 {
     const int32_t force = S.reset[w];
     if (!resetDueD(S, sc, w)) return;
@@ -1399,7 +1463,7 @@ __device__ __forceinline__ void resetSystemD(const DevState &S, const SceneDev &
             S.worldCurr[w] = 1;
         }
     }
-    initWorldD(S, sc, w, force == 1, S.trainCtrl, pre, L);
+    initWorldD(S, sc, w, force == 1, S.trainCtrl, pre, L, rec);
 }
 
 // ====================================================== per-world systems
@@ -1581,7 +1645,7 @@ __device__ __forceinline__ float4 *crumbPtr(const DevState &S, int w) { return &
 // sim.cpp:4845-4889 leaveBreadcrumbsSystem, agent part: refresh own last
 // crumb or request a new one (returns true; appended in agent order by the
 // world lane, the requests handed over in LDS).  The penalty's reset to 0
-// is accumulateCrumbsD's starting value (the two always run together).
+// is crumbRoundsD's starting value (the two always run together).
 __device__ bool leaveBreadcrumbAgentD(const DevState &S, int w, int64_t g)
 {
     const Vec3 pos = ldPos(S, g);
@@ -1654,68 +1718,64 @@ __device__ void appendCrumbsD(const DevState &S, int w, uint32_t req)
     S.nextCrumbId[w] = next_id;
 }
 
-// sim.cpp:4892-4926 accumulateBreadcrumbPenaltiesSystem, gathered per agent
-// (crumbs in creation order).
-__device__ void accumulateCrumbsD(const DevState &S, int w, int i)
+// sim.cpp:4892-4926 accumulateBreadcrumbPenaltiesSystem, with its decay and
+// compaction of the world's crumbs, by the world's N agent lanes together
+// (called by every thread of the block: it has block barriers).  Each round
+// the lanes load N consecutive crumbs into LDS (buf: 2 float4 per lane);
+// every agent adds the round's crumbs to its penalty in creation order, and
+// each lane decays its own crumb and, if it survives, stores it at its
+// compacted slot (the survivors before it: earlier rounds' plus this
+// round's lower lanes).  Stores only go to slots at or below the round being
+// read, whose crumbs are already in LDS.
+__device__ __forceinline__ void crumbRoundsD(const DevState &S, int w, int i, bool act, int wl, float4 *buf)
 {
-    const int64_t g = (int64_t)w * S.N + i;
+    const int N = S.N;
+    const int64_t g = (int64_t)w * N + i;
     const int team = i / S.T, off = i - team * S.T;
-    const Vec3 pos = ldPos(S, g);
-    const float4 *cr = crumbPtr(S, w);
-    const int n = S.numCrumbs[w];
+    float4 *cr = act ? crumbPtr(S, w) : nullptr;
+    const int n = act ? S.numCrumbs[w] : 0;
+    const Vec3 pos = act ? ldPos(S, g) : v3(0.f, 0.f, 0.f);
     float total = 0.f; // leaveBreadcrumbsSystem's reset (sim.cpp:4845-4889)
-    // 4 crumbs per round of loads (past the end re-reads the last, unused);
-    // the sum keeps creation order
-    auto add = [&](float4 meta, float4 p) {
-        if ((int)meta.x != team || (int)meta.y == off) return;
-        if (distance(pos, v3(p.x, p.y, p.z)) <= c::kAgentRadius * 4.f) total += p.w;
-    };
+    int kept = 0;      // survivors of the earlier rounds
+    const float4 *wb = buf + 2 * wl * N;
     #pragma unroll 1
-    for (int k0 = 0; k0 < n; k0 += 4) {
-        const int k1 = min(k0 + 1, n - 1), k2 = min(k0 + 2, n - 1), k3 = min(k0 + 3, n - 1);
-        const float4 m0 = cr[2 * k0 + 1], p0 = cr[2 * k0], m1 = cr[2 * k1 + 1], p1 = cr[2 * k1];
-        const float4 m2 = cr[2 * k2 + 1], p2 = cr[2 * k2], m3 = cr[2 * k3 + 1], p3 = cr[2 * k3];
-        add(m0, p0);
-        if (k0 + 1 < n) add(m1, p1);
-        if (k0 + 2 < n) add(m2, p2);
-        if (k0 + 3 < n) add(m3, p3);
-    }
-    S.bcPenalty[g] = total;
-}
-
-constexpr int kCrumbChunk = 4;
-// In chunks of kCrumbChunk crumbs loaded before any is written back: the world lane
-// waits for one round of loads per chunk instead of per crumb, and the
-// compaction only ever writes to slots at or below the chunk being read.
-__device__ void decayCrumbsD(const DevState &S, int w)
-{
-    float4 *cr = crumbPtr(S, w);
-    const int n = S.numCrumbs[w];
-    int m = 0;
-    auto keep = [&](float4 p, float4 meta, int k) {
-        if (k >= n) return;
-        p.w -= 0.025f;
-        if (!(p.w <= 0.f)) {
-            cr[2 * m] = p;
-            cr[2 * m + 1] = meta;
-            m += 1;
+    for (int r0 = 0; __syncthreads_or(r0 < n); r0 += N) {
+        const int k = r0 + i;
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f), meta = p;
+        if (k < n) {
+            p = cr[2 * k];
+            meta = cr[2 * k + 1];
+            buf[2 * threadIdx.x] = p;
+            buf[2 * threadIdx.x + 1] = meta;
         }
-    };
-    constexpr int CK = kCrumbChunk;
-    #pragma unroll 1
-    for (int k0 = 0; k0 < n; k0 += CK) {
-        // past the end: re-read the last crumb (unused)
-        float4 pp[CK], mm[CK];
-        #pragma unroll
-        for (int j = 0; j < CK; j++) {
-            const int kj = min(k0 + j, n - 1);
-            pp[j] = cr[2 * kj];
-            mm[j] = cr[2 * kj + 1];
+        __syncthreads();
+        if (r0 < n) {
+            const int cnt = min(N, n - r0);
+            int before = 0, round_kept = 0;
+            #pragma unroll 1
+            for (int j = 0; j < cnt; j++) {
+                const float4 pj = wb[2 * j], mj = wb[2 * j + 1];
+                if (!((int)mj.x != team || (int)mj.y == off))
+                    if (distance(pos, v3(pj.x, pj.y, pj.z)) <= c::kAgentRadius * 4.f) total += pj.w;
+                const bool keep = !(pj.w - 0.025f <= 0.f);
+                round_kept += keep ? 1 : 0;
+                if (j < i && keep) before += 1;
+            }
+            if (k < n) {
+                p.w -= 0.025f;
+                if (!(p.w <= 0.f)) {
+                    const int m = kept + before;
+                    cr[2 * m] = p;
+                    cr[2 * m + 1] = meta;
+                }
+            }
+            kept += round_kept;
         }
-        #pragma unroll
-        for (int j = 0; j < CK; j++) keep(pp[j], mm[j], k0 + j);
     }
-    S.numCrumbs[w] = m;
+    if (act) {
+        S.bcPenalty[g] = total;
+        if (i == 0) S.numCrumbs[w] = kept;
+    }
 }
 
 // Filter boxes of updateFiltersState (sim.cpp:128-291): x/y ranges of the
@@ -1770,14 +1830,30 @@ __device__ __forceinline__ MatchMasks matchMasksD(const uint8_t *mb, int N)
 }
 
 // sim.cpp:128-291 updateFiltersState from the world's agent bits.  The
-// filter state is read once and written once (act/last in registers).
-__device__ __forceinline__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const MatchMasks &mm)
+// filter state is read once (by the caller, with its other loads: last[6]
+// [team][filter], act[2]) and written once.
+struct FilterState {
+    int32_t last[6];
+    uint32_t act[2];
+};
+
+__device__ __forceinline__ FilterState loadFiltersD(const DevState &S, int w)
+{
+    FilterState f;
+    const int32_t *lastp = &S.filtLast[(int64_t)w * 6];
+    for (int k = 0; k < 6; k++) f.last[k] = lastp[k];
+    f.act[0] = (uint32_t)S.filtAct0[w];
+    f.act[1] = (uint32_t)S.filtAct1[w];
+    return f;
+}
+
+__device__ __forceinline__ void updateFiltersBitsD(const DevState &S, int w, int cur_step, const MatchMasks &mm,
+                                                   FilterState fs)
 {
     const int T = S.T;
     int32_t *lastp = &S.filtLast[(int64_t)w * 6]; // [team][filter]
-    int32_t last[6];
-    for (int k = 0; k < 6; k++) last[k] = lastp[k];
-    uint32_t act[2] = { (uint32_t)S.filtAct0[w], (uint32_t)S.filtAct1[w] };
+    int32_t *last = fs.last;
+    uint32_t *act = fs.act;
     const uint32_t team0 = (1u << T) - 1u, team1 = team0 << T;
     const int min_num[2] = { 5, 1 };
     for (int fi = 0; fi < 3; fi++) {
@@ -1838,6 +1914,7 @@ __device__ __forceinline__ void zoneMatchInfoD(const DevState &S, const SceneDev
     const int team_a = S.teamA[w];
     int32_t *zs = &zs_all[cz * 5];
     int z[5] = { zs[0], zs[1], zs[2], zs[3], zs[4] };
+    const FilterState fs = loadFiltersD(S, w); // before this function's stores
 
     bool finished = cur_step >= c::kEpisodeLen || reset_w == 1;
     if (cur_step == 1) {
@@ -1880,7 +1957,7 @@ __device__ __forceinline__ void zoneMatchInfoD(const DevState &S, const SceneDev
     S.captured[w] = captured ? 1 : 0;
     S.earned[w] = earned ? 1 : 0;
     for (int k = 0; k < 5; k++) zs[k] = z[k];
-    updateFiltersBitsD(S, w, cur_step, mm);
+    updateFiltersBitsD(S, w, cur_step, mm, fs);
     if (sc.eventsOn) writeSnapshotD(S, sc, w, new_captured);
     if (finished) {
         if (zcd) {
@@ -1890,9 +1967,14 @@ __device__ __forceinline__ void zoneMatchInfoD(const DevState &S, const SceneDev
         } else if (m[3] > m[4]) m[0] = 0;
         else if (m[4] > m[3]) m[0] = 1;
         else m[0] = 2;
-        #pragma unroll 1
-        for (int k = 0; k < 25; k++) mr[5 + k] = zs_all[k];
-        #pragma unroll 1
+        // every zone's stats in one round of loads, then the stores (one
+        // load-store pair per entry waited for each store before the next load)
+        int32_t zv[25];
+        #pragma unroll
+        for (int k = 0; k < 25; k++) zv[k] = zs_all[k];
+        #pragma unroll
+        for (int k = 0; k < 25; k++) mr[5 + k] = zv[k];
+        #pragma unroll
         for (int k = 0; k < 25; k++) zs_all[k] = 0;
     }
     for (int k = 0; k < 5; k++) mr[k] = m[k];
@@ -2452,13 +2534,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
 // holds floor(kSimBlock / N) whole worlds, lane = agent, phases separated
 // by workgroup barriers.
 constexpr int kSimBlock = 128;
-// k_sim's dynamic LDS: the BVH image (reused by the reset phase for its draw
-// keys, kPreDraws + 1 per lane) then the spawn lists.
+// k_sim's dynamic LDS: the BVH image, which the phases after the last BVH
+// use reuse (the reset's draw keys, kPreDraws + 1 per lane, then the spawn
+// records, kSpawnRec floats per lane), then the spawn lists.
+constexpr size_t kSimKeyBytes = (size_t)kSimBlock * (kPreDraws + 1) * sizeof(RandKey);
 __host__ __device__ size_t simSpawnOffset(const SceneDev &sc)
 {
     const size_t bvh = (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16;
-    const size_t keys = (size_t)kSimBlock * (kPreDraws + 1) * sizeof(RandKey);
-    return ((bvh > keys ? bvh : keys) + 15) & ~(size_t)15;
+    const size_t reuse = kSimKeyBytes + (size_t)kSimBlock * kSpawnRec * 4;
+    return ((bvh > reuse ? bvh : reuse) + 15) & ~(size_t)15;
 }
 
 __device__ __forceinline__ float flankRewardD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i);
@@ -2489,6 +2573,13 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         }
     }
     const LBVH bvh = stageBVH(smem, sc); // (its barrier also covers the spawn lists)
+    // spawn records in the BVH's LDS once nothing reads the BVH any more:
+    // the respawn (after fireD) unless the flank reward traces rays later,
+    // the reset (last phase) unless curriculum snapshots rewrite agents after
+    // the spawn (then the world lane stores everything itself)
+    float *const spawnRec = reinterpret_cast<float *>(smem + kSimKeyBytes);
+    const bool recRespawn = !sc.flank && !(sc.simFlags & kFlagNoRespawn);
+    const bool recReset = sc.numSnapshots == 0;
     const int N = S.N;
     const int wpb = kSimBlock / N;
     const int wl = threadIdx.x / N;
@@ -2500,9 +2591,9 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
 
     __shared__ uint8_t agentB[kSimBlock]; // per-agent bytes for the world lane (alive, done)
     // per-agent floats for the world lane, reused by phase: respawn
-    // (positions [3 * kSimBlock], flags), goal distances (stride 6), rewards,
-    // reset (flags)
-    __shared__ float goalDist[kSimBlock * 6];
+    // (positions [3 * kSimBlock], flags), crumb rounds (2 float4 per lane),
+    // goal distances (stride 6), rewards, reset (flags)
+    __shared__ __attribute__((aligned(16))) float goalDist[kSimBlock * 8];
     float *const sposL = goalDist;
     float *const sflagL = goalDist + 3 * kSimBlock;
     if (act && sc.eventsOn) { // ClearTmpNode<GameEventEntity> at step start (sim.cpp:5344)
@@ -2524,8 +2615,10 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         // the agents' alive states, positions and flags go to the world
         // lane's respawn through LDS (it read them back from memory one
         // agent at a time)
+        bool dead_now = false;
         if (act) {
             const DmgOut d = applyDmgD(S, g);
+            dead_now = !d.alive;
             agentB[threadIdx.x] = d.alive ? 1 : 0;
             sposL[3 * threadIdx.x] = d.pos.x;
             sposL[3 * threadIdx.x + 1] = d.pos.y;
@@ -2539,7 +2632,16 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             for (int k = 0; k < N; k++)
                 if (!agentB[wl * N + k]) dead |= 1u << k;
             spawnAgentsD(S, sc, w, true, nullptr, dead,
-                         SpawnLds{ &sposL[3 * wl * N], &agentB[wl * N], &sflagL[wl * N], tabA, tabB, tabC });
+                         SpawnLds{ &sposL[3 * wl * N], &agentB[wl * N], &sflagL[wl * N], tabA, tabB, tabC },
+                         recRespawn ? spawnRec + wl * N * kSpawnRec : nullptr);
+        }
+        if (recRespawn) {
+            // the respawned agents' own stores, from the world lane's records
+            __syncthreads();
+            if (dead_now) {
+                const ZoneBox zb = zoneBoxD(sc, S.curZone[w]);
+                spawnApplyRecD(S, sc, g, true, spawnRec + threadIdx.x * kSpawnRec, __float_as_int(sflagL[threadIdx.x]), zb);
+            }
         }
         __syncthreads();
         if (act) autoHealD(S, g);
@@ -2584,10 +2686,9 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             }
         }
         __syncthreads();
-        // accumulateBreadcrumbPenalties shares its agent phase with the
-        // match-info / goal-region reads below (each lane reads its own
-        // agent and the crumbs, which nothing in that phase writes)
-        if (act) accumulateCrumbsD(S, w, i);
+        // accumulateBreadcrumbPenalties and the crumbs' decay (the end of
+        // that system), in rounds over LDS (goalDist's, free until below)
+        crumbRoundsD(S, w, i, act, wl, reinterpret_cast<float4 *>(goalDist));
     }
     // zoneMatchInfoSystem's per-agent reads, one lane per agent (the world
     // lane would otherwise walk them serially)
@@ -2598,7 +2699,6 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     }
     __syncthreads();
     if (wlane) {
-        if (!sc.replayOn) decayCrumbsD(S, w); // end of accumulateBreadcrumbPenaltiesSystem // (lab: thread 0 is world 0's lane)
         zoneMatchInfoD(S, sc, w, &matchBits[wl * N]);
         goalRegionsD(S, sc, w, &goalDist[wl * N * 6]);
     }
@@ -2649,7 +2749,8 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
     // resets: the agents' own parts in parallel, then the world lane
     // (the BVH image is dead from here on: the reset's draw keys go there)
     RandKey *pre = reinterpret_cast<RandKey *>(smem) + (int64_t)wl * N * (kPreDraws + 1);
-    if (act && resetDueD(S, sc, w)) sflagL[threadIdx.x] = __int_as_float(resetPreD(S, sc, w, i, pre + i * (kPreDraws + 1)));
+    const bool resetting = act && resetDueD(S, sc, w);
+    if (resetting) sflagL[threadIdx.x] = __int_as_float(resetPreD(S, sc, w, i, pre + i * (kPreDraws + 1)));
     __syncthreads();
     if (wlane) {
         // fullTeamDoneRewardSystem (sim.cpp:4720-4747)
@@ -2663,7 +2764,17 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             S.ftReward[(int64_t)w * 2 + t] = r;
             S.ftDone[(int64_t)w * 2 + t] = done ? 1 : 0;
         }
-        resetSystemD(S, sc, w, pre, SpawnLds{ nullptr, nullptr, &sflagL[wl * N], tabA, tabB, tabC });
+        resetSystemD(S, sc, w, pre, SpawnLds{ nullptr, nullptr, &sflagL[wl * N], tabA, tabB, tabC },
+                     recReset ? spawnRec + wl * N * kSpawnRec : nullptr);
+    }
+    if (recReset) {
+        // the reset agents' own stores, from the world lane's records
+        __syncthreads();
+        if (resetting) {
+            const ZoneBox zb = zoneBoxD(sc, S.curZone[w]);
+            spawnApplyRecD(S, sc, g, false, spawnRec + threadIdx.x * kSpawnRec, __float_as_int(sflagL[threadIdx.x]), zb);
+            resetAgentTailD(S, g);
+        }
     }
 }
 

@@ -42,14 +42,17 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 # often for a patch): a phase timer after every block barrier
 # (-DMPENV_LAB_PHASE_T, k_sim per-phase block cycles in stats slots 10..),
 # -DMPENV_LAB_SIM_SKIP=bits to switch phases off (wrong results by design),
-# -DMPENV_SIM_WPE=n for the waves-per-SIMD target.
+# -DMPENV_SIM_WPE=n for the waves-per-SIMD target, -DMPENV_SIM_BLOCK=n for
+# the block size.
 KSIM_SKIP = [("fireD(", 1), ("spawnAgentsD(", 2), ("zoneMatchInfoD(", 8), ("goalRegionsD(", 16),
-             ("resetSystemD(", 128), ("appendCrumbsD(", 256), ("decayCrumbsD(", 256), ("accumulateCrumbsD(", 512),
+             ("resetSystemD(", 128), ("appendCrumbsD(", 256), ("crumbRoundsD(", 512),
              ("exploreVisitedD(", 1024)]
 
 
 def ksim_hooks(path):
     s = open(path).read()
+    s = s.replace("constexpr int kSimBlock = 128;",
+                  "#ifndef MPENV_SIM_BLOCK\n#define MPENV_SIM_BLOCK 128\n#endif\nconstexpr int kSimBlock = MPENV_SIM_BLOCK;")
     s = s.replace("#define MP_SIM_ATTR __attribute__((amdgpu_waves_per_eu(4)))",
                   "#ifndef MPENV_SIM_WPE\n#define MPENV_SIM_WPE 4\n#endif\n"
                   "#define MP_SIM_ATTR __attribute__((amdgpu_waves_per_eu(MPENV_SIM_WPE)))")
@@ -108,7 +111,8 @@ def build(name, args):
     shutil.copytree(B.CSRC, src_dir)
     for pf in patches:
         subprocess.run(["patch", "-s", "-p1", "-d", src_dir, "-i", pf], check=True)
-    if any(d.startswith(("-DMPENV_LAB_PHASE_T", "-DMPENV_LAB_SIM_SKIP", "-DMPENV_SIM_WPE")) for d in defines):
+    if any(d.startswith(("-DMPENV_LAB_PHASE_T", "-DMPENV_LAB_SIM_SKIP", "-DMPENV_SIM_WPE", "-DMPENV_SIM_BLOCK"))
+           for d in defines):
         ksim_hooks(os.path.join(src_dir, "kernels.hip"))
     common = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{src_dir}",
               f"-I{B.INCLUDE}"] + list(defines)
