@@ -15,7 +15,7 @@ there and compiles that copy, so no lab hook sits in the shipped sources.
                               _WAVE_HIST=k, _WORK, _NO_TRI,
                               _NO_BVH, _NO_CAPSULE, _NO_REAR, _NO_FT_LIDAR, ...,
                               and the dropped variants (MPENV_LIDAR_PERM,
-                              MPENV_TRI_FLAT, MPENV_*_WPE, ...); the round-1..4
+                              MPENV_TRI_FLAT, MPENV_*_WPE, ...; MPENV_CRUMB_CHUNK went with decayCrumbsD in round 5); the round-1..4
                               k_obs switches went with that kernel (round 5)
   (round 4's forward-fan candidate lists, fan_lists.patch / fan_phases.patch,
   are in git history before round 5: measured and dropped)
