@@ -656,6 +656,21 @@ struct SphereHit {
 // the search starts with hit_t = t_max0 and returns it when nothing is
 // nearer.
 
+// One node of the sphere-cast image (stageBVHSphere, kSNodeFloats = 32
+// floats: loR x / y / z of the 4 children, hiR x / y / z, the children,
+// their triangle counts) in one round of LDS loads: 8 x 16 B instead of ~7
+// scalar loads per child, one child after another.  The casts then compute
+// every child's slab entry (with 0) and exit without the running hit bound,
+// and test t_lo < fminNum(hit_t, t_exit) in child order: the same fminNum
+// over the same four values as the reference's running update (a NaN slab
+// is ignored either way; a -0 / +0 choice cannot change the < test).
+__device__ __forceinline__ void sNodeLoad(const LBVH &b, uint32_t node_idx, lf4 &lx, lf4 &ly, lf4 &lz, lf4 &hx, lf4 &hy,
+                                          lf4 &hz, lf4 &cq, lf4 &tq)
+{
+    const MP_LDS lf4 *q = reinterpret_cast<const MP_LDS lf4 *>(b.snodes + node_idx * kSNodeFloats);
+    lx = q[0]; ly = q[1]; lz = q[2]; hx = q[3]; hy = q[4]; hz = q[5]; cq = q[6]; tq = q[7];
+}
+
 __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r,
                                                  float t_max0 = mp::kFltMax)
 {
@@ -673,28 +688,33 @@ __device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, m
                negZ = __builtin_signbit(inv_d.z);
     // near / far ends per axis: loR or hiR of the pre-widened node image
     // (stageBVHSphere), picked once per cast from the sign of inv_d
-    const int nX = negX ? 12 : 0, fX = negX ? 0 : 12;
-    const int nY = negY ? 16 : 4, fY = negY ? 4 : 16;
-    const int nZ = negZ ? 20 : 8, fZ = negZ ? 8 : 20;
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
     bsPush(st, 0);
     while (st.n > 0) {
         const uint32_t node_idx = bsPop(st);
-        const MP_LDS float *nd = b.snodes + node_idx * kSNodeFloats;
-#pragma unroll 1
+        lf4 lx, ly, lz, hx, hy, hz, cq, tq;
+        sNodeLoad(b, node_idx, lx, ly, lz, hx, hy, hz, cq, tq);
+        float t_lo4[4], t_ex4[4];
+#pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int32_t child = __float_as_int(nd[24 + i]);
+            const float nxv = negX ? hx[i] : lx[i], fxv = negX ? lx[i] : hx[i];
+            const float nyv = negY ? hy[i] : ly[i], fyv = negY ? ly[i] : hy[i];
+            const float nzv = negZ ? hz[i] : lz[i], fzv = negZ ? lz[i] : hz[i];
+            const float i_min_x = (nxv - ray_o.x) * inv_d.x, i_max_x = (fxv - ray_o.x) * inv_d.x;
+            const float i_min_y = (nyv - ray_o.y) * inv_d.y, i_max_y = (fyv - ray_o.y) * inv_d.y;
+            const float i_min_z = (nzv - ray_o.z) * inv_d.z, i_max_z = (fzv - ray_o.z) * inv_d.z;
+            t_lo4[i] = fmax_(fmax_(fmax_(0.f, i_min_x), i_min_y), i_min_z);
+            t_ex4[i] = fmin_(fmin_(i_max_x, i_max_y), i_max_z);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int32_t child = __float_as_int(cq[i]);
             if (child == -1) continue;
-            const float i_min_x = (nd[nX + i] - ray_o.x) * inv_d.x, i_max_x = (nd[fX + i] - ray_o.x) * inv_d.x;
-            const float i_min_y = (nd[nY + i] - ray_o.y) * inv_d.y, i_max_y = (nd[fY + i] - ray_o.y) * inv_d.y;
-            const float i_min_z = (nd[nZ + i] - ray_o.z) * inv_d.z, i_max_z = (nd[fZ + i] - ray_o.z) * inv_d.z;
-            const float t_lo = fmax_(fmax_(fmax_(0.f, i_min_x), i_min_y), i_min_z);
-            const float t_hi = fmin_(fmin_(fmin_(hit_t, i_max_x), i_max_y), i_max_z);
-            if (t_lo < t_hi) {
+            if (t_lo4[i] < fmin_(hit_t, t_ex4[i])) {
                 if (child & 0x80000000) {
                     const int leaf = child & 0x7fffffff;
-                    const int ntri = (int)__float_as_uint(nd[28 + i]);
+                    const int ntri = (int)__float_as_uint(tq[i]);
                     Vec3 leaf_n = v3(0.f, 0.f, 0.f);
                     float leaf_t = hit_t;
                     for (int k = 0; k < ntri; k++) {
@@ -742,9 +762,6 @@ __device__ __forceinline__ void bvhSphereCast2D(const LBVH b, mp::Vec3 o0, float
     float hit0 = t_max0, hit1 = t_max0;
     const bool negX = __builtin_signbit(inv_d.x), negY = __builtin_signbit(inv_d.y),
                negZ = __builtin_signbit(inv_d.z);
-    const int nX = negX ? 12 : 0, fX = negX ? 0 : 12;
-    const int nY = negY ? 16 : 4, fY = negY ? 4 : 16;
-    const int nZ = negZ ? 20 : 8, fZ = negZ ? 8 : 20;
     const Vec3 o1 = v3(o0.x, o0.y, z1);
     ByteStack st;
     st.lo = 0; st.hi = 0; st.n = 0;
@@ -755,25 +772,35 @@ __device__ __forceinline__ void bvhSphereCast2D(const LBVH b, mp::Vec3 o0, float
         const uint32_t node_idx = bsPop(st);
         const uint32_t m = ms & 3u;
         ms >>= 2;
-        const MP_LDS float *nd = b.snodes + node_idx * kSNodeFloats;
-#pragma unroll 1
+        lf4 lx, ly, lz, hx, hy, hz, cq, tq;
+        sNodeLoad(b, node_idx, lx, ly, lz, hx, hy, hz, cq, tq);
+        float lo0[4], lo1[4], ex0[4], ex1[4];
+#pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int32_t child = __float_as_int(nd[24 + i]);
-            if (child == -1) continue;
-            const float i_min_x = (nd[nX + i] - o0.x) * inv_d.x, i_max_x = (nd[fX + i] - o0.x) * inv_d.x;
-            const float i_min_y = (nd[nY + i] - o0.y) * inv_d.y, i_max_y = (nd[fY + i] - o0.y) * inv_d.y;
-            const float zn = nd[nZ + i], zf = nd[fZ + i];
+            const float nxv = negX ? hx[i] : lx[i], fxv = negX ? lx[i] : hx[i];
+            const float nyv = negY ? hy[i] : ly[i], fyv = negY ? ly[i] : hy[i];
+            const float zn = negZ ? hz[i] : lz[i], zf = negZ ? lz[i] : hz[i];
+            const float i_min_x = (nxv - o0.x) * inv_d.x, i_max_x = (fxv - o0.x) * inv_d.x;
+            const float i_min_y = (nyv - o0.y) * inv_d.y, i_max_y = (fyv - o0.y) * inv_d.y;
             const float i_min_z0 = (zn - o0.z) * inv_d.z, i_max_z0 = (zf - o0.z) * inv_d.z;
             const float i_min_z1 = (zn - z1) * inv_d.z, i_max_z1 = (zf - z1) * inv_d.z;
             const float lo_xy = fmax_(fmax_(0.f, i_min_x), i_min_y);
-            const float t_lo0 = fmax_(lo_xy, i_min_z0), t_lo1 = fmax_(lo_xy, i_min_z1);
-            const float t_hi0 = fmin_(fmin_(fmin_(hit0, i_max_x), i_max_y), i_max_z0);
-            const float t_hi1 = fmin_(fmin_(fmin_(hit1, i_max_x), i_max_y), i_max_z1);
-            const uint32_t pass = ((m & 1u) && t_lo0 < t_hi0 ? 1u : 0u) | ((m & 2u) && t_lo1 < t_hi1 ? 2u : 0u);
+            const float ex_xy = fmin_(i_max_x, i_max_y);
+            lo0[i] = fmax_(lo_xy, i_min_z0);
+            lo1[i] = fmax_(lo_xy, i_min_z1);
+            ex0[i] = fmin_(ex_xy, i_max_z0);
+            ex1[i] = fmin_(ex_xy, i_max_z1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int32_t child = __float_as_int(cq[i]);
+            if (child == -1) continue;
+            const uint32_t pass = ((m & 1u) && lo0[i] < fmin_(hit0, ex0[i]) ? 1u : 0u) |
+                                  ((m & 2u) && lo1[i] < fmin_(hit1, ex1[i]) ? 2u : 0u);
             if (pass == 0u) continue;
             if (child & 0x80000000) {
                 const int leaf = child & 0x7fffffff;
-                const int ntri = (int)__float_as_uint(nd[28 + i]);
+                const int ntri = (int)__float_as_uint(tq[i]);
                 Vec3 n0 = v3(0.f, 0.f, 0.f), n1 = v3(0.f, 0.f, 0.f);
                 float t0 = hit0, t1 = hit1;
                 for (int k = 0; k < ntri; k++) {

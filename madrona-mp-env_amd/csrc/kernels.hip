@@ -238,7 +238,7 @@ __device__ Vec3 pathfindToPointD(const SceneDev &sc, Vec3 start, Vec3 pos, int g
     return navTriCenterD(sc, next);
 }
 
-__device__ void planAStarD(const DevState &S, const SceneDev &sc, int64_t g)
+__device__ __forceinline__ void planAStarD(const DevState &S, const SceneDev &sc, int64_t g)
 {
     if (S.policy[g] != -1) return; // consts::aStarPolicyID
     const int w = (int)(g / S.N);
@@ -305,7 +305,7 @@ __device__ void planAStarD(const DevState &S, const SceneDev &sc, int64_t g)
     out[6] = stand;
 }
 
-__device__ void applyBotActionsD(const DevState &S, int64_t g)
+__device__ __forceinline__ void applyBotActionsD(const DevState &S, int64_t g)
 {
     if (S.policy[g] != -1) return;
     const int32_t *hb = &S.botAction[7 * g];
@@ -319,7 +319,7 @@ __device__ void applyBotActionsD(const DevState &S, int64_t g)
 }
 
 // sim.cpp:2093-2199 pvpMovementSystem
-__device__ void pvpMovementD(const DevState &S, int64_t g)
+__device__ __forceinline__ void pvpMovementD(const DevState &S, int64_t g)
 {
     if (S.alive[g] == 0.f) return;
     const int32_t a_amount = S.discreteAction[4 * g + 0];
@@ -381,7 +381,7 @@ __device__ void pvpMovementD(const DevState &S, int64_t g)
 }
 
 // sim.cpp:2266-2370 continuous then discrete aim
-__device__ void pvpAimD(const DevState &S, int64_t g)
+__device__ __forceinline__ void pvpAimD(const DevState &S, int64_t g)
 {
     if (S.alive[g] == 0.f) return;
     float yaw = S.ayaw[g], pitch = S.apitch[g];
@@ -570,7 +570,7 @@ __device__ __forceinline__ void stuckCastsD(const LBVH &bvh, bool need, Vec3 x, 
 // sim.cpp:889-1039 applyVelocitySystem + updateMoveStateSystem.  Split at
 // the stuck fallback so the wave can share its casts (stuckCastsD): part 1
 // up to the ground check, the fallback's casts, part 2 to the end.
-__device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
+__device__ __forceinline__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
 {
     const Vec3 x = ldPos(S, g);
     Vec3 v = ldVel(S, g);
@@ -699,7 +699,7 @@ __device__ void applyVelocityD(const DevState &S, const SceneDev &sc, const LBVH
 }
 
 // sim.cpp:1041-1104 fallSystem + updateMoveStatePostFallSystem
-__device__ void fallD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
+__device__ __forceinline__ void fallD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int64_t g)
 {
     if (S.alive[g] == 0.f) return;
     const float fall_rate = 386.08858267717f;
