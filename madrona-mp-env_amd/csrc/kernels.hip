@@ -739,20 +739,52 @@ __device__ __forceinline__ void putEventD(const DevState &S, const SceneDev &sc,
 
 __device__ __forceinline__ int playerIdD(const DevState &S, int i) { return (i / S.T) * kMaxTeamSize + i % S.T; }
 
-__device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i)
+// What fireD reads about its own agent, loaded before any of its stores.
+struct FireIn {
+    int32_t flags, mag0, mag1, fire, pose, respawn;
+    float alive, hp, ayaw, apitch;
+    Vec3 pos;
+    RNG rng;
+};
+
+__device__ __forceinline__ FireIn fireLoadD(const DevState &S, int64_t g)
+{
+    FireIn f;
+    f.flags = S.flags[g];
+    f.alive = S.alive[g];
+    f.mag0 = S.magazine[2 * g];
+    f.mag1 = S.magazine[2 * g + 1];
+    f.fire = S.discreteAction[4 * g + 2];
+    f.pose = S.curPose[g];
+    f.respawn = S.respawnSteps[g];
+    f.hp = S.hp[g];
+    f.ayaw = S.ayaw[g];
+    f.apitch = S.apitch[g];
+    f.pos = ldPos(S, g);
+    f.rng = ldRng(S, g);
+    return f;
+}
+
+// sim.cpp:1443-1615 fireSystem.  in: the agent's own inputs (fireLoadD);
+// lpx / lpy / lpz, lhp, lrs: the world's agents' positions, hp and respawn
+// counters in LDS (k_sim stages them), indexed from lb (the world's first
+// lane).
+__device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, const LBVH &bvh, int w, int i, const FireIn &in,
+                                      const float *lpx, const float *lpy, const float *lpz, const float *lhp,
+                                      const float *lrs, int lb)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
     const int64_t g = g0 + i;
     S.landedOn[g] = -1;
     S.firedT[g] = -kFltMax;
-    int32_t flags = S.flags[g] & ~(kFlagSuccessfulKill | kFlagReloadedFullMag);
-    if (S.alive[g] == 0.f) {
+    int32_t flags = in.flags & ~(kFlagSuccessfulKill | kFlagReloadedFullMag);
+    if (in.alive == 0.f) {
         S.flags[g] = flags;
         return;
     }
-    int32_t mag0 = S.magazine[2 * g], mag1 = S.magazine[2 * g + 1];
-    const int fire = S.discreteAction[4 * g + 2];
+    int32_t mag0 = in.mag0, mag1 = in.mag1;
+    const int fire = in.fire;
     if (fire == 2) {
         if (sc.eventsOn) putEventD(S, sc, w, 2 * i, MPENV_EVENT_RELOAD, playerIdD(S, i), mag0, 0);
         if (mag0 == c::kMagSize) flags |= kFlagReloadedFullMag;
@@ -773,9 +805,9 @@ __device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, con
     S.magazine[2 * g] = mag0;
     S.magazine[2 * g + 1] = mag1;
 
-    Vec3 fire_from = ldPos(S, g);
-    fire_from.z += viewHeightD(S.curPose[g]);
-    RNG rng = ldRng(S, g);
+    Vec3 fire_from = in.pos;
+    fire_from.z += viewHeightD(in.pose);
+    RNG rng = in.rng;
     float u1 = rngUniform(rng);
     float u2 = rngUniform(rng);
     stRng(S, g, rng);
@@ -785,11 +817,11 @@ __device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, con
     const float bias = 1.5f;
     float up_delta = fminD(fmaxD((z1 + bias) * acc, 0.f), 4.f * acc);
     float right_delta = fminD(fmaxD(z2 * acc, -4.f * acc), 4.f * acc);
-    AimD a = computeAimD(S.ayaw[g] + right_delta, S.apitch[g] + up_delta);
+    AimD a = computeAimD(in.ayaw + right_delta, in.apitch + up_delta);
     stAim(S, g, a);
     Vec3 fire_dir = rotateVec(a.rot, kFwd);
 
-    WorldHit h = traceWorldD(bvh, S.px, S.py, S.pz, g0, N, fire_from, fire_dir, i); // from its own axis
+    WorldHit h = traceWorldD(bvh, lpx, lpy, lpz, lb, N, fire_from, fire_dir, i); // from its own axis
     if (S.stats) statAdd(S.stats + kStatShots, 1u);
     S.firedT[g] = h.hit ? h.t : kFltMax;
     bool success = h.hit;
@@ -799,12 +831,12 @@ __device__ __forceinline__ void fireD(const DevState &S, const SceneDev &sc, con
     } else {
         const int tteam = h.entity / S.T;
         if (success && tteam == team) success = false;
-        if (success && S.respawnSteps[g0 + h.entity] > 0) success = false;
+        if (success && __float_as_int(lrs[lb + h.entity]) > 0) success = false;
     }
     if (success) {
         if (sc.eventsOn) putEventD(S, sc, w, 2 * i, MPENV_EVENT_PLAYER_SHOT, playerIdD(S, i), playerIdD(S, h.entity), 0);
         S.landedOn[g] = h.entity;
-        if (S.hp[g0 + h.entity] <= c::kDmgPerBullet) {
+        if (lhp[lb + h.entity] <= c::kDmgPerBullet) {
             flags |= kFlagSuccessfulKill;
             if (sc.eventsOn) putEventD(S, sc, w, 2 * i + 1, MPENV_EVENT_KILL, playerIdD(S, i), playerIdD(S, h.entity), 0);
         }
@@ -915,6 +947,38 @@ struct SpawnWorld {
 struct SpawnTaken {
     uint64_t a0, a1, b0, b1;
 };
+
+// One common respawn point's score for agent ai (utils.cpp:410-475 inside
+// standardSpawnPoint's respawn branch): recently used points, points near
+// any live agent, near live opponents, and near the zone score higher.
+__device__ __forceinline__ float respawnScoreD(const DevState &S, const Spawn *options, int s, int ai, int team,
+                                               uint32_t last_used, uint32_t cur_step, Vec3 zone_center,
+                                               const SpawnLds &L, int64_t g0)
+{
+    const int N = S.N;
+    float score = 0.f;
+    uint32_t elapsed = (uint32_t)(c::kDeltaT * float(cur_step - last_used));
+    const float elapsed_weight = 0.1f, dist_weight = 0.01f;
+    if (elapsed < 3.f) score += elapsed_weight * (3.f - elapsed);
+    Spawn sp = options[s];
+    Vec3 spawn_pt = 0.5f * (sp.region.pMin + sp.region.pMax);
+    #pragma unroll 1
+    for (int j = 0; j < N; j++) {
+        if (j == ai) continue;
+        if (L.alive ? L.alive[j] == 0 : S.alive[g0 + j] == 0.f) continue;
+        const Vec3 pj = L.pos ? v3(L.pos[3 * j], L.pos[3 * j + 1], L.pos[3 * j + 2]) : ldPos(S, g0 + j);
+        float dist = distance(spawn_pt, pj);
+        if (dist < 4.f * c::kAgentRadius) {
+            score += 100000.f;
+        } else {
+            if (j / S.T == team) continue;
+            score += dist_weight * (1.f / dist);
+        }
+    }
+    float dz = distance(spawn_pt, zone_center);
+    if (dz < 100.f) score += 1000000.f;
+    return score;
+}
 
 __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const SceneDev &sc, int w, int ai, bool is_respawn,
                                     bool use_middle, RNG &rng, Vec3 &out_pt, float &out_yaw,
@@ -1029,27 +1093,7 @@ __device__ __forceinline__ void standardSpawnPointD(const DevState &S, const Sce
         const uint32_t last_used = next_used;
         if (s + 1 < sc.numCommon) next_used = rtrack[s + 1];
         if (last_used == cur_step) continue;
-        float score = 0.f;
-        uint32_t elapsed = (uint32_t)(c::kDeltaT * float(cur_step - last_used));
-        const float elapsed_weight = 0.1f, dist_weight = 0.01f;
-        if (elapsed < 3.f) score += elapsed_weight * (3.f - elapsed);
-        Spawn sp = options[s];
-        Vec3 spawn_pt = 0.5f * (sp.region.pMin + sp.region.pMax);
-        #pragma unroll 1
-        for (int j = 0; j < N; j++) {
-            if (j == ai) continue;
-            if (L.alive ? L.alive[j] == 0 : S.alive[g0 + j] == 0.f) continue;
-            const Vec3 pj = L.pos ? v3(L.pos[3 * j], L.pos[3 * j + 1], L.pos[3 * j + 2]) : ldPos(S, g0 + j);
-            float dist = distance(spawn_pt, pj);
-            if (dist < 4.f * c::kAgentRadius) {
-                score += 100000.f;
-            } else {
-                if (j / S.T == team) continue;
-                score += dist_weight * (1.f / dist);
-            }
-        }
-        float dz = distance(spawn_pt, zone_center);
-        if (dz < 100.f) score += 1000000.f;
+        const float score = respawnScoreD(S, options, s, ai, team, last_used, cur_step, zone_center, L, g0);
         if (score < best_score) {
             best_idx = s;
             best_score = score;
@@ -1245,6 +1289,134 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
     // reloading it behind every store above)
     if (base_out) *base_out = base;
     else stWRng(S, w, base);
+}
+
+// k_sim's respawn (spawnAgents with is_respawn, common respawn points, no
+// navmesh spawns) with each dead agent's candidate scoring spread over its
+// world's N lanes: one dead agent per world per round, in agent order; every
+// lane scores candidates i, i + N, ... exactly as respawnScoreD (same
+// summation order), the world lane takes the lowest score (lowest index on
+// ties, as the sequential strict-< scan does), draws the spawn point and
+// writes the agent's record (spawnApplyRecD on the agent's lane applies it).
+// Points taken earlier this step are tracked in LDS (usedL) next to the
+// tracker loads, so no lane reads back a tracker entry another lane stored.
+// Called by every thread of the block (block barriers).  coop: LDS scratch,
+// 4 floats per thread.
+__device__ __forceinline__ void respawnCoopD(const DevState &S, const SceneDev &sc, int w, int i, int wl, bool act,
+                                             const SpawnLds &L, float *rec, float *coop)
+{
+    const int N = S.N, T = S.T;
+    const int64_t g0 = (int64_t)w * N;
+    const int B = (int)blockDim.x;
+    float *const bestS = coop;          // per lane: best score
+    float *const bestI = coop + B;      // per lane: its index (float bits)
+    float *const curA = coop + 2 * B;   // per world: the agent this round (float bits)
+    float *const usedL = coop + 3 * B;  // per world: 2 x 32 bits of points taken this step
+    const bool wl0 = act && i == 0;
+    uint32_t rem = 0;
+    RNG base;
+    int episode_curr = 0;
+    const bool randomize_hp = (sc.simFlags & kFlagRandomizeHP) != 0;
+    if (wl0) {
+        for (int k = 0; k < N; k++)
+            if (!L.alive[k]) rem |= 1u << k;
+        if (rem) {
+            base = ldWRng(S, w);
+            episode_curr = S.episodeCurr[w];
+            base.ctr += 1; // episodes[sampleI32(0, 0)] (spawnAgentsD)
+            if (sc.simFlags & kFlagSpawnInMiddle) (void)rngUniform(base);
+        }
+        usedL[2 * wl] = 0.f;
+        usedL[2 * wl + 1] = 0.f;
+    }
+    const uint32_t *rtrack = act ? &S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen + 2 * sc.spawnTrackLen] : nullptr;
+    uint32_t cur_step = 0u;
+    const Spawn *options = L.tabC;
+    #pragma unroll 1
+    for (;;) {
+        int ai = -1;
+        if (wl0) {
+            ai = rem ? __builtin_ctz(rem) : -1;
+            curA[wl] = __int_as_float(ai);
+        }
+        if (!__syncthreads_or(ai >= 0)) break;
+        const int a = act ? __float_as_int(curA[wl]) : -1;
+        if (a >= 0) {
+            // (read only in blocks with a respawn: most launches have none)
+            cur_step = (uint32_t)S.curStep[w];
+            const AABB za = sc.tab->zoneAABB[S.curZone[w]];
+            const Vec3 zone_center = 0.5f * (za.pMin + za.pMax);
+            const uint32_t used0 = (uint32_t)__float_as_int(usedL[2 * wl]), used1 = (uint32_t)__float_as_int(usedL[2 * wl + 1]);
+            const int team = a / T;
+            float bs = kFltMax;
+            int bi = -1;
+            #pragma unroll 1
+            for (int sp = i; sp < sc.numCommon; sp += N) {
+                const bool taken = ((sp < 32 ? used0 : used1) >> (sp & 31)) & 1u;
+                const uint32_t last_used = taken ? cur_step : rtrack[sp];
+                if (last_used == cur_step) continue;
+                const float score = respawnScoreD(S, options, sp, a, team, last_used, cur_step, zone_center, L, g0);
+                if (score < bs) {
+                    bs = score;
+                    bi = sp;
+                }
+            }
+            bestS[threadIdx.x] = bs;
+            bestI[threadIdx.x] = __int_as_float(bi);
+        }
+        __syncthreads();
+        if (wl0 && ai >= 0) {
+            float best = kFltMax;
+            int best_idx = -1;
+            for (int k = 0; k < N; k++) {
+                const int s_k = __float_as_int(bestI[wl * N + k]);
+                if (s_k < 0) continue;
+                const float sc_k = bestS[wl * N + k];
+                if (sc_k < best || (sc_k == best && s_k < best_idx)) {
+                    best = sc_k;
+                    best_idx = s_k;
+                }
+            }
+            if (best_idx < 0) best_idx = 0;
+            const int64_t g = g0 + ai;
+            // standardSpawnPoint's spawnAgent(best_idx), the agent's RNG
+            RNG rng = ldRng(S, g);
+            const Spawn sp = options[best_idx];
+            const float x_rnd = rngUniform(rng), y_rnd = rngUniform(rng), z_rnd = rngUniform(rng);
+            const float yaw_rnd = rngUniform(rng);
+            const float x_min = sp.region.pMin.x, x_diff = sp.region.pMax.x - x_min;
+            const float y_min = sp.region.pMin.y, y_diff = sp.region.pMax.y - y_min;
+            const float z_min = sp.region.pMin.z, z_diff = sp.region.pMax.z - z_min;
+            Vec3 spawn_pt = v3(x_min + x_rnd * x_diff, y_min + y_rnd * y_diff, z_min + z_rnd * z_diff);
+            const float spawn_yaw = sp.yawMin + yaw_rnd * (sp.yawMax - sp.yawMin);
+            S.spawnTrack[(int64_t)w * 3 * sc.spawnTrackLen + 2 * sc.spawnTrackLen + best_idx] = cur_step;
+            if (best_idx < 32) usedL[2 * wl] = __int_as_float(__float_as_int(usedL[2 * wl]) | (int)(1u << best_idx));
+            else usedL[2 * wl + 1] = __int_as_float(__float_as_int(usedL[2 * wl + 1]) | (int)(1u << (best_idx & 31)));
+            if ((sc.simFlags & kFlagEnableCurriculum) && episode_curr == 0) {
+                // utils.cpp:819-837 LearnShooting
+                const bool north = spawn_pt.y > 0.f;
+                const float x = -700.f + rngUniform(base) * 1400.f;
+                const float y = rngUniform(base) * 350.f;
+                spawn_pt = v3(x, north ? y : -y, 0.f);
+            }
+            L.pos[3 * ai] = spawn_pt.x; L.pos[3 * ai + 1] = spawn_pt.y; L.pos[3 * ai + 2] = spawn_pt.z;
+            L.alive[ai] = 1;
+            base.ctr += 1; // the weapon draw (spawnAgentsD)
+            float hp = 100.f;
+            int32_t mag = c::kMagSize;
+            if (randomize_hp) {
+                int tenth = rngI32(base, 1, 11);
+                hp = float(tenth * 10);
+                mag = rngI32(base, 0, c::kMagSize);
+            }
+            float *r = rec + ai * kSpawnRec;
+            r[0] = spawn_pt.x; r[1] = spawn_pt.y; r[2] = spawn_pt.z; r[3] = spawn_yaw;
+            r[4] = hp; r[5] = __int_as_float(mag); r[6] = __int_as_float((int32_t)rng.ctr);
+            rem &= rem - 1u;
+            if (rem == 0) stWRng(S, w, base);
+        }
+        __syncthreads();
+    }
 }
 
 // level_gen.cpp:330-582 resetPersistentEntities
@@ -2610,7 +2782,25 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
         if (wlane) zoneSystemD(S, sc, w);
         __syncthreads();
     } else {
-        if (act) fireD(S, sc, bvh, w, i);
+        {
+            // every agent's own fire inputs in one round of loads; the
+            // world's positions, hp and respawn counters (the shots' capsule
+            // tests and targets) through LDS (goalDist's, free until the
+            // respawn below)
+            float *const fpx = goalDist, *const fpy = goalDist + kSimBlock, *const fpz = goalDist + 2 * kSimBlock;
+            float *const fhp = goalDist + 3 * kSimBlock, *const frs = goalDist + 4 * kSimBlock;
+            FireIn fin;
+            if (act) {
+                fin = fireLoadD(S, g);
+                fpx[threadIdx.x] = fin.pos.x;
+                fpy[threadIdx.x] = fin.pos.y;
+                fpz[threadIdx.x] = fin.pos.z;
+                fhp[threadIdx.x] = fin.hp;
+                frs[threadIdx.x] = __int_as_float(fin.respawn);
+            }
+            __syncthreads();
+            if (act) fireD(S, sc, bvh, w, i, fin, fpx, fpy, fpz, fhp, frs, wl * N);
+        }
         __syncthreads();
         // the agents' alive states, positions and flags go to the world
         // lane's respawn through LDS (it read them back from memory one
@@ -2626,7 +2816,13 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             sflagL[threadIdx.x] = __int_as_float(d.flags);
         }
         __syncthreads();
-        if (wlane && !(sc.simFlags & kFlagNoRespawn)) {
+        const bool coopRespawn = recRespawn && sc.numCommon > 0 && sc.numCommon <= 64 &&
+                                 !(sc.simFlags & kFlagNavmeshSpawn);
+        if (coopRespawn)
+            respawnCoopD(S, sc, w, i, wl, act,
+                         SpawnLds{ &sposL[3 * wl * N], &agentB[wl * N], &sflagL[wl * N], tabA, tabB, tabC },
+                         spawnRec + wl * N * kSpawnRec, reinterpret_cast<float *>(smem));
+        else if (wlane && !(sc.simFlags & kFlagNoRespawn)) {
             uint32_t dead = 0;
             #pragma unroll 1
             for (int k = 0; k < N; k++)
