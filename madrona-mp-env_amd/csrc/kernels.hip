@@ -863,6 +863,7 @@ __device__ DmgOut applyDmgD(const DevState &S, int64_t g)
     const int rs = S.respawnSteps[g];
     float hp = S.hp[g];
     const bool was_alive = S.alive[g] == 1.f;
+    int ah = S.autohealSteps[g];
     const int T = S.T;
     float dm[kMaxTeamSize];
     #pragma unroll
@@ -876,7 +877,7 @@ __device__ DmgOut applyDmgD(const DevState &S, int64_t g)
         hp -= dm[k];
         S.dmg[(int64_t)k * S.dmgStride + g] = 0.f;
     }
-    if (was_shot > 0) S.autohealSteps[g] = c::kOutOfCombatSteps;
+    if (was_shot > 0) ah = c::kOutOfCombatSteps;
     S.wasShot[g] = was_shot;
     if (was_alive && hp <= 0.f) flags |= kFlagWasKilled | kFlagHasDied;
     if (S.stats) {
@@ -892,7 +893,13 @@ __device__ DmgOut applyDmgD(const DevState &S, int64_t g)
         stVel(S, g, v3(0, 0, 0));
     } else {
         S.alive[g] = 1.f;
+        // sim.cpp:1875-1890 autoHealSystem for the agents alive after the
+        // damage (nothing between the two systems changes them; a
+        // respawned agent's autoheal is spawnApplyD's)
+        if (ah == 0 && hp < 100.f) hp = fminD(100.f, hp + c::kAutohealPerStep);
+        else if (ah > 0) ah -= 1;
     }
+    if (was_shot > 0 || !dead) S.autohealSteps[g] = ah;
     S.hp[g] = hp;
     S.flags[g] = flags;
     DmgOut o;
@@ -900,19 +907,6 @@ __device__ DmgOut applyDmgD(const DevState &S, int64_t g)
     o.flags = flags;
     o.pos = pos;
     return o;
-}
-
-// sim.cpp:1875-1890 autoHealSystem
-__device__ void autoHealD(const DevState &S, int64_t g)
-{
-    if (S.alive[g] == 0.f) return;
-    int ah = S.autohealSteps[g];
-    float hp = S.hp[g];
-    if (ah == 0 && hp < 100.f) {
-        S.hp[g] = fminD(100.f, hp + c::kAutohealPerStep);
-    } else if (ah > 0) {
-        S.autohealSteps[g] = ah - 1;
-    }
 }
 
 // ====================================================== spawning / reset
@@ -1145,6 +1139,9 @@ __device__ __forceinline__ void spawnApplyD(const DevState &S, const SceneDev &s
     stAim(S, g, computeAimD(spawn_yaw, 0.f));
     stVel(S, g, v3(0.f, 0.f, 0.f));
     S.weapon[g] = 0;
+    // a respawn is followed by autoHealSystem (sim.cpp:1875-1890; alive, no
+    // autoheal countdown)
+    if (is_respawn && hp < 100.f) hp = fminD(100.f, hp + c::kAutohealPerStep);
     S.hp[g] = hp;
     S.magazine[2 * g] = mag;
     S.magazine[2 * g + 1] = 0;
@@ -1198,7 +1195,8 @@ __device__ __forceinline__ void spawnApplyRecD(const DevState &S, const SceneDev
 __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &sc, int w, bool is_respawn,
                                              const RandKey *pre = nullptr, int64_t dead = -1,
                                              SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr },
-                                             float *rec = nullptr, RNG *base_out = nullptr)
+                                             float *rec = nullptr, RNG *base_out = nullptr,
+                                             const SpawnWorld *sw_in = nullptr, const RNG *base_in = nullptr)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1212,15 +1210,20 @@ __device__ __forceinline__ void spawnAgentsD(const DevState &S, const SceneDev &
             if (S.alive[g0 + i] == 0.f) dead_mask |= 1u << i;
     }
     if (dead_mask == 0) {
-        if (base_out) *base_out = ldWRng(S, w);
+        if (base_out) *base_out = base_in ? *base_in : ldWRng(S, w);
         return;
     }
-    RNG base = ldWRng(S, w);
+    // (a reset hands over the world values and RNG it has just stored)
+    RNG base = base_in ? *base_in : ldWRng(S, w);
     SpawnWorld sw;
-    sw.teamA = S.teamA[w];
-    sw.cz = S.curZone[w];
-    sw.curStep = (uint32_t)S.curStep[w];
-    sw.episodeCurr = S.episodeCurr[w];
+    if (sw_in) {
+        sw = *sw_in;
+    } else {
+        sw.teamA = S.teamA[w];
+        sw.cz = S.curZone[w];
+        sw.curStep = (uint32_t)S.curStep[w];
+        sw.episodeCurr = S.episodeCurr[w];
+    }
     // episodes[sampleI32(0, numEpisodes = 0)]: an empty range, the value is
     // 0 whatever the key -- only the counter advances
     base.ctr += 1;
@@ -1463,7 +1466,8 @@ __device__ __forceinline__ void resetAgentTailD(const DevState &S, int64_t g)
 __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, const SceneDev &sc, int w, RandKey episode_key,
                                          const RandKey *pre = nullptr,
                                          SpawnLds L = SpawnLds{ nullptr, nullptr, nullptr, nullptr, nullptr, nullptr },
-                                         float *rec = nullptr)
+                                         float *rec = nullptr, const SpawnWorld *sw_in = nullptr,
+                                         const RNG *base_in = nullptr)
 {
     const int N = S.N;
     const int64_t g0 = (int64_t)w * N;
@@ -1494,7 +1498,7 @@ __device__ __forceinline__ void resetPersistentEntitiesD(const DevState &S, cons
     // every agent is dead here (resetAgentD); spawnAgentsD also stores the
     // start positions sx, sy, sz (= the spawn positions)
     RNG base;
-    spawnAgentsD(S, sc, w, false, pre, pre ? (int64_t)((1u << N) - 1u) : -1, L, rec, &base);
+    spawnAgentsD(S, sc, w, false, pre, pre ? (int64_t)((1u << N) - 1u) : -1, L, rec, &base, sw_in, base_in);
 
     #pragma unroll 1
     for (int i = 0; i < N; i++) {
@@ -1552,15 +1556,19 @@ __device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc
 {
     const uint32_t world_id = sc.worldOffset + (uint32_t)w;
     S.matchValid[w] = 1; // matchID = worldID << 32 | curEpisodeIdx (sim.cpp:736-738)
-    S.episodeCurr[w] = S.worldCurr[w];
+    SpawnWorld sw;
+    sw.episodeCurr = S.worldCurr[w];
+    S.episodeCurr[w] = sw.episodeCurr;
     const uint32_t ep = (uint32_t)S.episode[w];
     RandKey episode_key = splitI(sc.initRandKey, ep, world_id);
     RNG base = makeRNG(splitI(episode_key, 0));
     bool flip = false;
     if (tc[2]) flip = rngUniform(base) < 0.5f;
-    S.teamA[w] = flip ? 1 : 0;
-    if (triggered_reset && tc[1]) S.curStep[w] = rngI32(base, 0, c::kEpisodeLen - 1);
-    else S.curStep[w] = 0;
+    sw.teamA = flip ? 1 : 0;
+    S.teamA[w] = sw.teamA;
+    const int32_t cur_step = (triggered_reset && tc[1]) ? rngI32(base, 0, c::kEpisodeLen - 1) : 0;
+    S.curStep[w] = cur_step;
+    sw.curStep = (uint32_t)cur_step;
     S.finished[w] = 0;
     const float use_prob = 1.0f;
     const float tier_probs[5] = { 0.f, 0.f, 0.3f, 0.3f, 0.4f };
@@ -1574,7 +1582,9 @@ __device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc
     }
     S.curSpawnIdx[w] = rngI32(base, 0, 0);
     if (sc.simFlags & kFlagHardcodedSpawns) (void)rngI32(base, 0, 4);
-    S.curZone[w] = rngI32(base, 0, sc.numZones);
+    sw.cz = rngI32(base, 0, sc.numZones);
+    if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) sw.cz = 3; // sim.cpp:822-825
+    S.curZone[w] = sw.cz;
     S.controlling[w] = -1;
     S.contested[w] = 0;
     S.captured[w] = 0;
@@ -1582,9 +1592,8 @@ __device__ __forceinline__ void initWorldD(const DevState &S, const SceneDev &sc
     S.zoneSteps[w] = c::kNumStepsPerZone;
     S.stepsUntilPoint[w] = c::kZonePointInterval;
     S.subState[w] = 0; // every sub-zone: controlling -1, not contested / captured (sim.cpp:815-820)
-    if (sc.task == MPENV_TASK_ZONE_CAPTURE_DEFEND) S.curZone[w] = 3; // sim.cpp:822-825
     stWRng(S, w, base);
-    resetPersistentEntitiesD(S, sc, w, episode_key, pre, L, rec);
+    resetPersistentEntitiesD(S, sc, w, episode_key, pre, L, rec, &sw, &base);
     S.filtAct0[w] = 0; S.filtAct1[w] = 0;
     S.filtMatched0[w] = 0; S.filtMatched1[w] = 0;
 }
@@ -1861,8 +1870,9 @@ __device__ bool leaveBreadcrumbAgentD(const DevState &S, int w, int64_t g)
 }
 
 // World part of leaveBreadcrumbsSystem: append requested crumbs in agent
-// order (req: bit i = agent i asked, from leaveBreadcrumbAgentD).
-__device__ void appendCrumbsD(const DevState &S, int w, uint32_t req)
+// order (req: bit i = agent i asked, from leaveBreadcrumbAgentD; lpos: the
+// world's agents' positions [N][3] in LDS).
+__device__ void appendCrumbsD(const DevState &S, int w, uint32_t req, const float *lpos)
 {
     if (req == 0) return;
     const int N = S.N;
@@ -1876,7 +1886,7 @@ __device__ void appendCrumbsD(const DevState &S, int w, uint32_t req)
         if (!(req & (1u << i))) continue;
         if (n < kMaxCrumbs) {
             const int team = i / S.T, off = i - team * S.T;
-            cr[2 * n] = make_float4(S.px[g], S.py[g], S.pz[g], 1.f);
+            cr[2 * n] = make_float4(lpos[3 * i], lpos[3 * i + 1], lpos[3 * i + 2], 1.f);
             cr[2 * n + 1] = make_float4((float)team, (float)off, __int_as_float(next_id), 0.f);
             S.bcLast[g] = next_id;
             next_id += 1;
@@ -2840,8 +2850,6 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
             }
         }
         __syncthreads();
-        if (act) autoHealD(S, g);
-        __syncthreads();
         {
             __shared__ int zoneCz[kSimBlock];
             __shared__ uint8_t zoneIn[kSimBlock];
@@ -2862,6 +2870,11 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
                 if (sc.recordOn) recordAgentD(S, w, i);
                 const bool req = leaveBreadcrumbAgentD(S, w, g);
                 zoneIn[threadIdx.x] = (zin ? 1 : 0) | (req ? 2 : 0);
+                // the position a requested crumb takes (sposL's LDS, free here)
+                const Vec3 p = ldPos(S, g);
+                sposL[3 * threadIdx.x] = p.x;
+                sposL[3 * threadIdx.x + 1] = p.y;
+                sposL[3 * threadIdx.x + 2] = p.z;
             }
             if (wlane && sc.recordOn) S.recordLog[w].cur_step = S.curStep[w];
             __syncthreads();
@@ -2878,7 +2891,7 @@ __global__ void __launch_bounds__(kSimBlock) MP_SIM_ATTR __attribute__((flatten)
                 }
                 zonePostD(S, w, zp, na, nb);
                 if (sc.simFlags & kFlagSubZones) subzoneSystemD(S, sc, w);
-                appendCrumbsD(S, w, req);
+                appendCrumbsD(S, w, req, &sposL[3 * wl * N]);
             }
         }
         __syncthreads();
