@@ -671,7 +671,7 @@ __device__ __forceinline__ void sNodeLoad(const LBVH &b, uint32_t node_idx, lf4 
     lx = q[0]; ly = q[1]; lz = q[2]; hx = q[3]; hy = q[4]; hz = q[5]; cq = q[6]; tq = q[7];
 }
 
-__device__ __noinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r,
+__device__ __forceinline__ SphereHit bvhSphereCastD(const LBVH b, mp::Vec3 ray_o, mp::Vec3 ray_d, float r,
                                                  float t_max0 = mp::kFltMax)
 {
     using namespace mp;
