@@ -124,6 +124,11 @@ struct mpenv_manager {
     bool lidarBranch = false;
     hipStream_t bStream = nullptr;
     hipEvent_t bForkEv = nullptr, bJoinEv = nullptr;
+    // gpuStreamStep: the agent maps' zero fills (no dependence on the step)
+    // on a side stream of their own, overlapping the step's kernels; joined
+    // back into the caller's stream before the call returns.
+    hipStream_t zStream = nullptr;
+    hipEvent_t zForkEv = nullptr, zJoinEv = nullptr;
 
     // Record / replay / event logs (mgr.cpp:155-300: per-step file I/O
     // around the Step graph)
@@ -182,6 +187,12 @@ struct mpenv_manager {
         }
         if (bForkEv) (void)hipEventDestroy(bForkEv);
         if (bJoinEv) (void)hipEventDestroy(bJoinEv);
+        if (zStream) {
+            (void)hipStreamSynchronize(zStream);
+            (void)hipStreamDestroy(zStream);
+        }
+        if (zForkEv) (void)hipEventDestroy(zForkEv);
+        if (zJoinEv) (void)hipEventDestroy(zJoinEv);
         for (FILE *f : { replayFile, recordFile, eventsFile, stepsFile })
             if (f) std::fclose(f);
         for (void *p : allocations) (void)hipFree(p);
@@ -1070,7 +1081,9 @@ int mpenv_train_interface_entry(int32_t is_output, int32_t idx, const char **nam
 // them, as one batched copy launch (the agent maps are never written by the
 // step and stay all zeros, so their copies are zero fills); a segment whose
 // pointers are not 16-B aligned falls back to hipMemcpyAsync.
-static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs, bool outputs)
+// zeros: 1 = only the agent maps' zero fills, 0 = the other outputs only,
+// -1 = every output.
+static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs, bool outputs, int zeros = -1)
 {
     CopyBatch b {};
     auto add = [&](const void *src, void *dst, size_t bytes) {
@@ -1094,11 +1107,13 @@ static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs,
     }
     for (int i = 0; i < kNumTIOutputs; i++, k++) {
         if (!outputs || !buffers[k]) continue;
+        const bool zero = kTIOutputs[i].id == MPENV_EXPORT_AGENT_MAP;
+        if ((zeros == 1 && !zero) || (zeros == 0 && zero)) continue;
         TensorDesc d;
         m->exportDesc(kTIOutputs[i].id, d);
-        add(kTIOutputs[i].id == MPENV_EXPORT_AGENT_MAP ? nullptr : d.ptr, buffers[k], d.bytes());
+        add(zero ? nullptr : d.ptr, buffers[k], d.bytes());
     }
-    if (launchCopyBatch(b, st)) throw std::runtime_error("copy launch failed");
+    if (b.n > 0 && launchCopyBatch(b, st)) throw std::runtime_error("copy launch failed");
     return 0;
 }
 
@@ -1122,9 +1137,21 @@ int mpenv_gpu_stream_step(mpenv_manager *m, void *stream, void **buffers)
     if (!m || !buffers) return fail(MPENV_ERR_INVALID, "null argument");
     try {
         hipStream_t st = stream ? (hipStream_t)stream : m->stream;
+        if (!m->zStream) {
+            HIP_CHECK(hipStreamCreateWithFlags(&m->zStream, hipStreamNonBlocking));
+            HIP_CHECK(hipEventCreateWithFlags(&m->zForkEv, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&m->zJoinEv, hipEventDisableTiming));
+        }
+        // the zero fills (1.6 GB of stores at C3) beside the step, ordered
+        // after whatever the caller queued before this call
+        HIP_CHECK(hipEventRecord(m->zForkEv, st));
+        HIP_CHECK(hipStreamWaitEvent(m->zStream, m->zForkEv, 0));
+        copyTI(m, m->zStream, buffers, false, true, 1);
+        HIP_CHECK(hipEventRecord(m->zJoinEv, m->zStream));
         copyTI(m, st, buffers, true, false);
         m->runStep(st);
-        copyTI(m, st, buffers, false, true);
+        copyTI(m, st, buffers, false, true, 0);
+        HIP_CHECK(hipStreamWaitEvent(st, m->zJoinEv, 0));
     } catch (const std::exception &e) {
         return fail(MPENV_ERR_HIP, e.what());
     }
