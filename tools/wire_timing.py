@@ -64,7 +64,7 @@ def main():
         assert lib.mpenv_wire_unpack(x.h, kbuf, 1, None) == 0
     hip.hipDeviceSynchronize()
     lib.mpenv_wire_error.argtypes = [C.c_void_p, C.POINTER(C.c_uint32)]
-    nstreams = 4
+    nstreams = int(os.environ.get("WIRE_STREAMS", 4))
     streams = [C.c_void_p() for _ in range(nstreams)]
     hip.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
     for st in streams:
