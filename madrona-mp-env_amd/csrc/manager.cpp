@@ -1117,11 +1117,22 @@ static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs,
     return 0;
 }
 
+// gpuStreamStep's side stream for the zero fills and its fork / join events,
+// made by gpuStreamInit (outside any graph capture of the steps that follow)
+static void ensureZStream(mpenv_manager *m)
+{
+    if (m->zStream) return;
+    HIP_CHECK(hipStreamCreateWithFlags(&m->zStream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&m->zForkEv, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&m->zJoinEv, hipEventDisableTiming));
+}
+
 // mgr.cpp:507-612
 int mpenv_gpu_stream_init(mpenv_manager *m, void *stream, void **buffers)
 {
     if (!m || !buffers) return fail(MPENV_ERR_INVALID, "null argument");
     try {
+        ensureZStream(m);
         hipStream_t st = stream ? (hipStream_t)stream : m->stream;
         m->runInitGraph(st);
         copyTI(m, st, buffers, false, true);
@@ -1137,11 +1148,7 @@ int mpenv_gpu_stream_step(mpenv_manager *m, void *stream, void **buffers)
     if (!m || !buffers) return fail(MPENV_ERR_INVALID, "null argument");
     try {
         hipStream_t st = stream ? (hipStream_t)stream : m->stream;
-        if (!m->zStream) {
-            HIP_CHECK(hipStreamCreateWithFlags(&m->zStream, hipStreamNonBlocking));
-            HIP_CHECK(hipEventCreateWithFlags(&m->zForkEv, hipEventDisableTiming));
-            HIP_CHECK(hipEventCreateWithFlags(&m->zJoinEv, hipEventDisableTiming));
-        }
+        ensureZStream(m);
         // the zero fills (1.6 GB of stores at C3) beside the step, ordered
         // after whatever the caller queued before this call
         HIP_CHECK(hipEventRecord(m->zForkEv, st));
