@@ -352,9 +352,16 @@ int mpenv_gpu_stream_step(mpenv_manager *mgr, void *hip_stream, void **buffers);
  * signature, API version 1 ("original"): buffers = the call's operands then
  * its results -- the flat trainInterface array of mpenv_gpu_stream_* (inputs
  * then outputs, mpenv_train_interface order); opaque = the bytes of an
- * mpenv_xla_opaque naming the manager (mpenv_xla_opaque_make).  That ABI has
- * no error return: a bad opaque or a failed launch sets mpenv_last_error on
- * the calling thread and counts in mpenv_xla_errors(). */
+ * mpenv_xla_opaque naming the manager (mpenv_xla_opaque_make).  The opaque
+ * is checked against the live managers before use (a destroyed manager is
+ * an error, not a read of freed memory).  API version 1 has no error return:
+ * like the reference's REQ_CUDA / FATAL (mgr.cpp:514-531, 620-638) a bad
+ * opaque or a failed launch prints "mpenv: XLA custom call ... failed: <why>"
+ * on stderr and aborts.  The *_status variants take XLA's
+ * API_VERSION_STATUS_RETURNING signature (a trailing XlaCustomCallStatus *)
+ * and report the failure through XlaCustomCallStatusSetFailure, resolved at
+ * run time from the XLA runtime loaded in the process (counted in
+ * mpenv_xla_errors()); when that symbol is absent they abort as above. */
 typedef struct mpenv_xla_opaque {
     uint32_t magic;   /* MPENV_XLA_MAGIC */
     uint32_t version; /* MPENV_XLA_VERSION */
@@ -367,6 +374,10 @@ typedef struct mpenv_xla_opaque {
 int mpenv_xla_opaque_make(mpenv_manager *mgr, mpenv_xla_opaque *out);
 void mpenv_xla_gpu_stream_init(void *hip_stream, void **buffers, const char *opaque, size_t opaque_len);
 void mpenv_xla_gpu_stream_step(void *hip_stream, void **buffers, const char *opaque, size_t opaque_len);
+void mpenv_xla_gpu_stream_init_status(void *hip_stream, void **buffers, const char *opaque, size_t opaque_len,
+                                      void *xla_status);
+void mpenv_xla_gpu_stream_step_status(void *hip_stream, void **buffers, const char *opaque, size_t opaque_len,
+                                      void *xla_status);
 int64_t mpenv_xla_errors(void);
 
 /* Manager::*Tensor() getters (mgr.cpp:1965-2381): zero-copy view of an

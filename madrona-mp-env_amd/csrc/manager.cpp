@@ -16,6 +16,9 @@
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
+#include <unordered_set>
+
+#include <dlfcn.h>
 #include <string>
 #include <vector>
 
@@ -920,6 +923,31 @@ void mpenv_manager::setupGroups(int want)
     }
 }
 
+// Live managers: the XLA targets receive a manager pointer inside opaque
+// bytes XLA keeps, so they check it against this set before using it (a
+// dropped SimManager, or foreign bytes, is then an error, not a read of freed
+// memory).
+static std::mutex g_liveMu;
+static std::unordered_set<const mpenv_manager *> g_live;
+
+static void liveAdd(const mpenv_manager *m)
+{
+    std::lock_guard<std::mutex> lk(g_liveMu);
+    g_live.insert(m);
+}
+
+static void liveRemove(const mpenv_manager *m)
+{
+    std::lock_guard<std::mutex> lk(g_liveMu);
+    g_live.erase(m);
+}
+
+static bool liveHas(const mpenv_manager *m)
+{
+    std::lock_guard<std::mutex> lk(g_liveMu);
+    return g_live.count(m) != 0;
+}
+
 extern "C" {
 
 int32_t mpenv_abi_version(void) { return MPENV_ABI_VERSION; }
@@ -979,7 +1007,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
             // Two measured best at C3 in rounds 2-4 (round 2: 1.447 ms/step
             // against 1.468 with one); since round 5's load-first k_obs one
             // group is faster (driver window 1.23 vs 1.30 ms, steady 1.178 vs
-            // 1.215; profiles/r05e_ab.jsonl).
+            // 1.215; profiles/r05e_ab_world_groups.jsonl).
             int want = 1;
             if (const char *e = std::getenv("MPENV_WORLD_GROUPS")) want = std::atoi(e);
             m->setupGroups(want);
@@ -994,6 +1022,7 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         HIP_CHECK(hipMemcpyAsync(m->S.trainCtrl, tc, sizeof(tc), hipMemcpyHostToDevice, m->stream));
         if (launchConstruct(m->S, m->sc, tc, m->stream)) throw std::runtime_error("construct launch failed");
         HIP_CHECK(hipStreamSynchronize(m->stream));
+        liveAdd(m);
         *out = m;
         return MPENV_OK;
     } catch (const std::exception &e) {
@@ -1004,7 +1033,11 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
     }
 }
 
-void mpenv_destroy(mpenv_manager *m) { delete m; }
+void mpenv_destroy(mpenv_manager *m)
+{
+    if (m) liveRemove(m);
+    delete m;
+}
 
 int mpenv_init(mpenv_manager *m)
 {
@@ -1189,28 +1222,83 @@ int mpenv_xla_opaque_make(mpenv_manager *m, mpenv_xla_opaque *out)
     return MPENV_OK;
 }
 
+// The manager an opaque names, or null (with mpenv_last_error set) when the
+// bytes are not an opaque of this build or name no live manager.
 static mpenv_manager *xlaManager(const char *opaque, size_t len)
 {
     mpenv_xla_opaque o;
-    if (!opaque || len != sizeof(o)) return nullptr;
-    std::memcpy(&o, opaque, sizeof(o));
-    if (o.magic != MPENV_XLA_MAGIC || o.version != MPENV_XLA_VERSION || o.num_buffers != kNumTIInputs + kNumTIOutputs)
+    if (!opaque || len != sizeof(o)) {
+        fail(MPENV_ERR_INVALID, "bad XLA opaque: " + std::to_string(len) + " bytes, expected " +
+                                    std::to_string(sizeof(o)));
         return nullptr;
-    return reinterpret_cast<mpenv_manager *>((uintptr_t)o.manager);
+    }
+    std::memcpy(&o, opaque, sizeof(o));
+    if (o.magic != MPENV_XLA_MAGIC || o.version != MPENV_XLA_VERSION || o.num_buffers != kNumTIInputs + kNumTIOutputs) {
+        fail(MPENV_ERR_INVALID, "bad XLA opaque: not made by mpenv_xla_opaque_make of this build");
+        return nullptr;
+    }
+    mpenv_manager *m = reinterpret_cast<mpenv_manager *>((uintptr_t)o.manager);
+    if (!liveHas(m)) {
+        fail(MPENV_ERR_INVALID, "bad XLA opaque: its manager was destroyed (keep the SimManager alive while the "
+                                "registered custom call is in use)");
+        return nullptr;
+    }
+    return m;
+}
+
+static int xlaRun(bool step, void *stream, void **buffers, const char *opaque, size_t opaque_len)
+{
+    mpenv_manager *m = xlaManager(opaque, opaque_len);
+    if (!m) return MPENV_ERR_INVALID;
+    return step ? mpenv_gpu_stream_step(m, stream, buffers) : mpenv_gpu_stream_init(m, stream, buffers);
+}
+
+// API version 1 has no error channel: like the reference's REQ_CUDA / FATAL
+// (mgr.cpp:514-531, 620-638) a failure is reported on stderr and aborts the
+// process rather than leaving XLA with result buffers that were never written.
+[[noreturn]] static void xlaFatal(const char *what)
+{
+    std::fprintf(stderr, "mpenv: XLA custom call %s failed: %s\n", what, g_last_error.c_str());
+    std::fflush(stderr);
+    std::abort();
 }
 
 void mpenv_xla_gpu_stream_init(void *stream, void **buffers, const char *opaque, size_t opaque_len)
 {
-    mpenv_manager *m = xlaManager(opaque, opaque_len);
-    const int rc = m ? mpenv_gpu_stream_init(m, stream, buffers) : fail(MPENV_ERR_INVALID, "bad XLA opaque");
-    if (rc != MPENV_OK) g_xlaErrors.fetch_add(1);
+    if (xlaRun(false, stream, buffers, opaque, opaque_len) != MPENV_OK) xlaFatal("gpuStreamInit");
 }
 
 void mpenv_xla_gpu_stream_step(void *stream, void **buffers, const char *opaque, size_t opaque_len)
 {
-    mpenv_manager *m = xlaManager(opaque, opaque_len);
-    const int rc = m ? mpenv_gpu_stream_step(m, stream, buffers) : fail(MPENV_ERR_INVALID, "bad XLA opaque");
-    if (rc != MPENV_OK) g_xlaErrors.fetch_add(1);
+    if (xlaRun(true, stream, buffers, opaque, opaque_len) != MPENV_OK) xlaFatal("gpuStreamStep");
+}
+
+// API_VERSION_STATUS_RETURNING: the failure goes to XLA through
+// XlaCustomCallStatusSetFailure, exported by the XLA runtime that calls the
+// target (jaxlib); it is looked up at run time so this library links without
+// XLA.  Without it there is no one to hand the status to: abort as above.
+typedef void (*XlaStatusSetFailureFn)(void *status, const char *message, size_t message_len);
+
+static void xlaStatusFail(const char *what, void *status)
+{
+    static XlaStatusSetFailureFn fn =
+        reinterpret_cast<XlaStatusSetFailureFn>(dlsym(RTLD_DEFAULT, "XlaCustomCallStatusSetFailure"));
+    if (!fn || !status) xlaFatal(what);
+    g_xlaErrors.fetch_add(1);
+    const std::string msg = std::string("mpenv: ") + what + ": " + g_last_error;
+    fn(status, msg.data(), msg.size());
+}
+
+void mpenv_xla_gpu_stream_init_status(void *stream, void **buffers, const char *opaque, size_t opaque_len,
+                                      void *status)
+{
+    if (xlaRun(false, stream, buffers, opaque, opaque_len) != MPENV_OK) xlaStatusFail("gpuStreamInit", status);
+}
+
+void mpenv_xla_gpu_stream_step_status(void *stream, void **buffers, const char *opaque, size_t opaque_len,
+                                      void *status)
+{
+    if (xlaRun(true, stream, buffers, opaque, opaque_len) != MPENV_OK) xlaStatusFail("gpuStreamStep", status);
 }
 
 int64_t mpenv_xla_errors(void) { return g_xlaErrors.load(); }

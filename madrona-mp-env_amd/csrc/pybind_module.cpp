@@ -371,7 +371,8 @@ PYBIND11_MODULE(madrona_mp_env, m)
         // name this manager, and the trainInterface the call's operand
         // (inputs) and result (outputs) shapes come from.  Registering them
         // needs jax, absent from this image; the targets themselves are plain
-        // C functions of XLA's API-version-1 signature (include/mpenv.h).
+        // C functions of XLA's API-version-1 signature, plus status-returning
+        // twins (include/mpenv.h).
         .def("jax", [](PySimManager &s, bool xla_gpu) -> py::object {
             if (!xla_gpu)
                 throw std::runtime_error("madrona_mp_env.SimManager.jax: only the XLA GPU (ROCm) target is built; "
@@ -383,8 +384,14 @@ PYBIND11_MODULE(madrona_mp_env, m)
             d["init"] = py::capsule(reinterpret_cast<void *>(&mpenv_xla_gpu_stream_init), kName);
             d["step"] = py::capsule(reinterpret_cast<void *>(&mpenv_xla_gpu_stream_step), kName);
             d["opaque"] = py::bytes(reinterpret_cast<const char *>(&o), sizeof(o));
+            // the same targets in XLA's status-returning form (API version 2,
+            // API_VERSION_STATUS_RETURNING): failures reach XLA instead of
+            // aborting the process
+            d["init_status"] = py::capsule(reinterpret_cast<void *>(&mpenv_xla_gpu_stream_init_status), kName);
+            d["step_status"] = py::capsule(reinterpret_cast<void *>(&mpenv_xla_gpu_stream_step_status), kName);
             d["platform"] = "ROCM";
             d["api_version"] = 1;
+            d["status_api_version"] = 2;
             int32_t ni = 0, no = 0;
             mpenv_train_interface_size(&ni, &no);
             py::list in_names, out_names;

@@ -169,3 +169,59 @@ def test_product_kernels_carry_no_lab_switches_and_lab_patches_apply(tmp_path):
             r = subprocess.run(["patch", "-p1", "-d", str(work), "-i", os.path.join(lab, q)],
                                capture_output=True, text=True)
             assert r.returncode == 0 and "fuzz" not in r.stdout, (p, q, r.stdout, r.stderr)
+
+
+_XLA_CALL = r"""
+import ctypes as C, sys
+fake = sys.argv[2]
+if fake:
+    C.CDLL(fake, mode=C.RTLD_GLOBAL)
+lib = C.CDLL(sys.argv[1])
+Fn = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_size_t)
+FnS = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_size_t, C.c_void_p)
+bad = bytes(24)
+if fake:
+    f = FnS(C.cast(lib.mpenv_xla_gpu_stream_step_status, C.c_void_p).value)
+    status = C.create_string_buffer(8)
+    f(None, None, bad, len(bad), C.cast(status, C.c_void_p))
+    lib.mpenv_xla_errors.restype = C.c_int64
+    got = C.CDLL(fake).fake_status_message
+    got.restype = C.c_char_p
+    print("status:", got().decode(), "errors:", lib.mpenv_xla_errors())
+else:
+    f = Fn(C.cast(lib.mpenv_xla_gpu_stream_step, C.c_void_p).value)
+    f(None, None, bad, len(bad))
+    print("returned")
+"""
+
+
+def test_xla_v1_target_aborts_on_a_foreign_opaque():
+    """The API-v1 custom call has no error channel: like the reference's
+    REQ_CUDA / FATAL (src/mgr.cpp:514-531, 620-638) a bad opaque prints why
+    and aborts instead of leaving XLA with unwritten result buffers.  Run in a
+    subprocess that never touches a GPU (the opaque check fails first)."""
+    import sys
+
+    r = subprocess.run([sys.executable, "-c", _XLA_CALL, T.build_native.LIB, ""], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0 and "returned" not in r.stdout
+    assert "mpenv: XLA custom call gpuStreamStep failed: bad XLA opaque" in r.stderr, r.stderr
+
+
+def test_xla_status_target_reports_failure_through_xla(tmp_path):
+    """The status-returning twin hands the failure to XLA's
+    XlaCustomCallStatusSetFailure (resolved at run time; here a stand-in
+    library exports it) and returns; the failure is counted."""
+    import sys
+
+    src = tmp_path / "fake_xla.c"
+    src.write_text('#include <string.h>\n#include <stddef.h>\nstatic char msg[512];\n'
+                   'void XlaCustomCallStatusSetFailure(void *s, const char *m, size_t n)\n'
+                   '{ (void)s; if (n > 511) n = 511; memcpy(msg, m, n); msg[n] = 0; }\n'
+                   'const char *fake_status_message(void) { return msg; }\n')
+    so = tmp_path / "libfake_xla.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    r = subprocess.run([sys.executable, "-c", _XLA_CALL, T.build_native.LIB, str(so)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "status: mpenv: gpuStreamStep: bad XLA opaque" in r.stdout and "errors: 1" in r.stdout, r.stdout
