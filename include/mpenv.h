@@ -421,9 +421,13 @@ int mpenv_debug_trace_rays(mpenv_manager *mgr, const float *o_device, const floa
  * mpenv_wire_bytes bytes), asynchronous on hip_stream; keyframe != 0 also
  * carries the last-known rows (the first message of an exchange).
  * unpack: on the learner, into a manager of the same configuration (the
- * sender's shadow): the message's state, lidar and rewards, then the
- * observation system over them, so every trainInterface output of the
- * shadow equals the sender's bit for bit.  A message for another
+ * sender's shadow): the lidar, rewards and other per-agent outputs, then the
+ * observation system reading the message's state columns in place, so every
+ * trainInterface output of the shadow equals the sender's bit for bit (the
+ * shadow's internal state columns and full-team rows are not rebuilt: they
+ * are not trainInterface outputs).  Message buffers must be 16-B aligned;
+ * the buffer must stay unmodified until the unpack has run on hip_stream.
+ * A message for another
  * configuration or shard (header world offset != the shadow's
  * world_id_offset), of the other kind, or one whose values did not fit the
  * packed fields is not unpacked; it raises MPENV_WIRE_ERR_REFUSED and
@@ -437,6 +441,12 @@ int mpenv_wire_bytes(mpenv_manager *mgr, int32_t keyframe, int64_t *bytes);
 int mpenv_wire_pack(mpenv_manager *mgr, void *dst_device, int32_t keyframe, void *hip_stream);
 int mpenv_wire_unpack(mpenv_manager *mgr, const void *src_device, int32_t keyframe, void *hip_stream);
 int mpenv_wire_error(mpenv_manager *mgr, uint32_t *out);
+/* The same read without a device synchronisation: ordered on hip_stream
+ * (the stream the shadow's unpacks run on); with `out` in pinned host memory
+ * the call returns at once and *out holds the word once the stream has
+ * reached the read (record an event after it).  Clears REFUSED like
+ * mpenv_wire_error. */
+int mpenv_wire_error_async(mpenv_manager *mgr, uint32_t *out, void *hip_stream);
 
 /* Measurement hook: how many times the Step graph has been captured (the
  * graph is re-captured whenever a kernel argument struct changes: world

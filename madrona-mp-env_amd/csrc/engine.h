@@ -160,7 +160,28 @@ struct DevState {
     // k_obs does nothing while (*obsGate & MPENV_WIRE_ERR_DESYNC): a learner
     // shadow whose wire history broke (wire.hip wireOk); null on the step path.
     const uint32_t *obsGate;
+    // gpuStreamStep's caller buffers (OutTab): while outTab->on, k_obs writes
+    // its pure outputs there instead of into the engine's exports, and
+    // k_lidar writes the lidar rows there too; outBase = this state's first
+    // agent in those buffers (world groups).  Null on a wire view.
+    const struct OutTab *outTab;
+    int64_t outBase;
 };
+
+// The caller's trainInterface output buffers k_obs / k_lidar write directly
+// during a gpuStreamStep (mgr.cpp:614-645 copies them from the engine's
+// exports instead).  A device table, so the captured step graph's kernel
+// arguments never change: gpuStreamStep sets it (on = 1, the call's
+// pointers) in front of the step and clears it behind it.
+struct OutTab {
+    int32_t on, pad;
+    float *masks, *filters, *selfObs, *selfPos, *tmObs, *tmPos, *oppObs, *oppPos, *fwdLidar, *rearLidar;
+    // the two agent-map outputs (constant zeros, as the reference copies
+    // them): zero-filled by k_lidar's forward waves, 8 KB per agent of
+    // stores that need no loads, issued beside its VALU-bound traversals
+    float *agentMap0, *agentMap1;
+};
+int launchSetOutTab(OutTab *dev, const OutTab &v, void *stream);
 
 // Per-step workload counters accumulated by the kernels in stats mode
 // (bench.py's workload window; never on in the timed region).
@@ -288,6 +309,14 @@ int launchMove(const DevState &s, const SceneDev &sc, void *stream);
 int launchSimStep(const DevState &s, const SceneDev &sc, void *stream);
 int launchVisibility(const DevState &s, const SceneDev &sc, void *stream);
 int launchObservations(const DevState &s, const SceneDev &sc, void *stream);
+// k_obs over a wire message (wire.hip launchWireUnpack): `view` is the
+// shadow's DevState with its input columns pointing into the message.
+struct WireObs {
+    const uint32_t *packed;  // [A] curPose | tgtPose << 8 | weapon << 16 | flags << 24
+    const int32_t *epPrev;   // [W] the previous message's episode counters (the shadow's copy)
+    int32_t keyframe;        // a keyframe carries the last-known rows: nothing is cleared
+};
+int launchObservationsWire(const DevState &view, const SceneDev &sc, const WireObs &wo, void *stream);
 int launchLidar(const DevState &s, const SceneDev &sc, void *stream);
 // synchronous on `stream`, at scene upload; dev_scratch holds kMaxZones ints
 int computeZoneGoalTris(const SceneDev &sc, int32_t *dev_scratch, int32_t *host_out, void *stream);
@@ -317,7 +346,10 @@ int launchCopyBatch(const CopyBatch &b, void *stream);
 // Learner-exchange wire format (wire.hip)
 int64_t wireBytes(const DevState &s, bool keyframe);
 int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOffset, void *stream);
-int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, uint32_t worldOffset,
-                     void *stream);
+// epPrev / epNext: the shadow's double-buffered copies of the previous and
+// this message's episode counters ([W] each, swapped by the caller per unpack)
+int launchWireErrClear(uint32_t *err, void *stream); // keeps only the desync bit
+int launchWireUnpack(const DevState &s, const SceneDev &sc, const char *src, bool keyframe, uint32_t *err,
+                     uint32_t worldOffset, const int32_t *epPrev, int32_t *epNext, void *stream);
 
 } // namespace mpenv

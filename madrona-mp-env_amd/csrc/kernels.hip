@@ -3528,7 +3528,16 @@ struct HalfStage {
     }
 };
 
-__global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(3))) k_obs(DevState S, SceneDev sc)
+// kWire: the learner's rebuild of a shadow's rows from a wire message
+// (wire.hip launchWireUnpack): S is a view whose input columns point into
+// the message (the same SoA columns the sender's engine holds), the packed
+// pose / weapon / flags word is split here, the full-team rows (not
+// trainInterface outputs) are skipped, and a world whose episode counter
+// moved since the previous message has every last-known row written -- the
+// reset's clear on the sender (resetAgentD / resetPersistentEntitiesD),
+// then this step's updates -- exactly the rows the sender's k_obs leaves.
+template <bool kWire>
+__device__ __forceinline__ void obsBody(const DevState &S, const SceneDev &sc, const WireObs &wo)
 {
     __shared__ float ost[kObsCols][kObsStageMax];
     __shared__ __attribute__((aligned(16))) float rowBuf[kObsBlock / 64][32 * kObsSpanPad];
@@ -3561,12 +3570,22 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
         ost[kOsHP][k] = S.hp[j];
         ost[kOsFired][k] = S.firedT[j];
         ost[kOsAlive][k] = S.alive[j];
-        ost[kOsCurPose][k] = __int_as_float(S.curPose[j]);
-        ost[kOsTgtPose][k] = __int_as_float(S.tgtPose[j]);
-        ost[kOsWeapon][k] = __int_as_float(S.weapon[j]);
-        ost[kOsVis][k] = __int_as_float((int32_t)S.visMask[j]);
-        ost[kOsTrans][k] = __int_as_float(S.transRem[j]);
-        ost[kOsFlags][k] = __int_as_float(S.flags[j]);
+        if constexpr (kWire) {
+            const uint32_t p = wo.packed[j]; // curPose | tgtPose << 8 | weapon << 16 | flags << 24
+            ost[kOsCurPose][k] = __int_as_float((int32_t)(p & 0xffu));
+            ost[kOsTgtPose][k] = __int_as_float((int32_t)((p >> 8) & 0xffu));
+            ost[kOsWeapon][k] = __int_as_float((int32_t)((p >> 16) & 0xffu));
+            ost[kOsVis][k] = __int_as_float((int32_t)S.visMask[j]);
+            ost[kOsTrans][k] = __int_as_float(S.transRem[j]);
+            ost[kOsFlags][k] = __int_as_float((int32_t)(p >> 24));
+        } else {
+            ost[kOsCurPose][k] = __int_as_float(S.curPose[j]);
+            ost[kOsTgtPose][k] = __int_as_float(S.tgtPose[j]);
+            ost[kOsWeapon][k] = __int_as_float(S.weapon[j]);
+            ost[kOsVis][k] = __int_as_float((int32_t)S.visMask[j]);
+            ost[kOsTrans][k] = __int_as_float(S.transRem[j]);
+            ost[kOsFlags][k] = __int_as_float(S.flags[j]);
+        }
         ost[kOsShot][k] = __int_as_float(S.wasShot[j]);
         ost[kOsHeal][k] = __int_as_float(S.autohealSteps[j]);
         ost[kOsMag0][k] = __int_as_float(S.magazine[2 * j]);
@@ -3584,6 +3603,25 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
     const int contested = S.contested[w], captured = S.captured[w];
     const int until_point = S.stepsUntilPoint[w], zone_steps = S.zoneSteps[w];
     const AABB za = sc.tab->zoneAABB[cz];
+    // the pure outputs' destinations: the engine's exports, or during a
+    // gpuStreamStep the caller's buffers (OutTab; uniform loads, issued with
+    // the other loads before the barrier)
+    float *oMasks = S.masks, *oFilters = S.filters, *oSelf = S.selfObs, *oSelfPos = S.selfPos;
+    float *oTm = S.tmObs, *oTmPos = S.tmPos, *oOpp = S.oppObs, *oOppPos = S.oppPos;
+    if (!kWire && S.outTab && S.outTab->on) {
+        const OutTab *t = S.outTab;
+        const int64_t b = S.outBase;
+        oMasks = t->masks + b * 6;
+        oFilters = t->filters + b;
+        oSelf = t->selfObs + b * kSelfObs;
+        oSelfPos = t->selfPos + b * 3;
+        oTm = t->tmObs + b * 5 * kOtherObs;
+        oTmPos = t->tmPos + b * 15;
+        oOpp = t->oppObs + b * 6 * kOtherObs;
+        oOppPos = t->oppPos + b * 18;
+    }
+    bool wreset = false; // kWire: the world's episode counter moved since the previous message
+    if constexpr (kWire) wreset = !wo.keyframe && wo.epPrev[w] != S.episodeCounter[w];
     __syncthreads();
     if (!live) return; // the flushes count the live lanes
 
@@ -3614,7 +3652,7 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
         if (can_see) mask[k] = 1.f;
         if (st.f(kOsFired, jo) >= 0) mask[k] = 1.f;
     }
-    hs.putSpan<6>(S.masks + gw0 * 6, mask);
+    hs.putSpan<6>(oMasks + gw0 * 6, mask);
     // teamKnowsLocation (mask[k] == 1) as bits for the opponent loop.
     // Reading the float array there instead gave wrong last-known updates in
     // round 2 -- a register miscompile of the float form ("k_obs
@@ -3622,12 +3660,12 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
     uint32_t knowsBits = 0;
     for (int k = 0; k < kMaxTeamSize; k++) knowsBits |= (mask[k] == 1.f ? 1u : 0u) << k;
 
-    S.filters[g] = (cur_step - fm < 5) ? 1.f : 0.f;
+    oFilters[g] = (cur_step - fm < 5) ? 1.f : 0.f;
 
     // ---- fullTeamObservationsSystem, per (world, team): the global
     // observation and the zeroed slots past team_size (slot-0 agents)
     const int64_t mine = (int64_t)w * 2 + team, theirs = (int64_t)w * 2 + (team ^ 1);
-    if (off == 0) {
+    if (!kWire && off == 0) {
         for (int s = T; s < kMaxTeamSize; s++) {
             for (int k = 0; k < MPENV_FT_PLAYER_DIM; k++) S.ftPlayers[(mine * 6 + s) * MPENV_FT_PLAYER_DIM + k] = 0.f;
             for (int k = 0; k < MPENV_FT_ENEMY_DIM; k++) S.ftEnemies[(mine * 6 + s) * MPENV_FT_ENEMY_DIM + k] = 0.f;
@@ -3681,8 +3719,8 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
             zo[15] = cz == 3 ? 1.f : 0.f;
         }
         static_assert(kSelfObs == 43 && (kSelfObs | 1) <= kObsSpanPad, "self obs span");
-        hs.putSpan<kSelfObs>(S.selfObs + gw0 * kSelfObs, ob);
-        hs.putSpan<3>(S.selfPos + gw0 * 3, pos3);
+        hs.putSpan<kSelfObs>(oSelf + gw0 * kSelfObs, ob);
+        hs.putSpan<3>(oSelfPos + gw0 * 3, pos3);
     }
     const bool alive_ok = self_alive; // fillCommonOb's alive test of the agent itself
 
@@ -3717,14 +3755,14 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
             for (int h = 0; h < hs.halves(); h++) {
                 hs.stage<kObsRowPad>(h, row, kOtherObs);
                 waveSync();
-                hs.flushRows32<kObsRowPad>(h, S.tmObs, 5, k, gw0);
+                hs.flushRows32<kObsRowPad>(h, oTm, 5, k, gw0);
                 waveSync();
             }
         }
         float tpos[15];
 #pragma unroll
         for (int k = 0; k < kMaxTeamSize - 1; k++) slotPos(alive_ok && k < T - 1, mateIdx(k), &tpos[3 * k]);
-        hs.putSpan<15>(S.tmPos + gw0 * 15, tpos);
+        hs.putSpan<15>(oTmPos + gw0 * 15, tpos);
     }
 
     // ---- opponents (+ last known)
@@ -3754,6 +3792,7 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
                     lk_write = lk_write || knows;
                 }
             }
+            lk_write = lk_write || wreset;
             lkWrite |= (lk_write ? 1u : 0u) << k;
             lkKeep |= (lk_keep ? 1u : 0u) << k;
             if (S.stats) statAdd(S.stats + kStatLkRows, lk_write ? 1u : 0u);
@@ -3762,7 +3801,7 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
                 hs.stage<kObsRowPad>(h, row, kOtherObs);
                 hs.stageOff(h, (g * 6 + k) * kOtherObs);
                 waveSync();
-                hs.flushRows32<kObsRowPad>(h, S.oppObs, 6, k, gw0);
+                hs.flushRows32<kObsRowPad>(h, oOpp, 6, k, gw0);
                 // the staged row is also the last-known copy
                 hs.flushOff4<kOtherObs / 4, kObsRowPad>(h, S.lkObs, wb, zb);
                 waveSync();
@@ -3771,7 +3810,7 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
         float opos[18];
 #pragma unroll
         for (int k = 0; k < kMaxTeamSize; k++) slotPos(alive_ok && k < T, oppIdx(k), &opos[3 * k]);
-        hs.putSpan<18>(S.oppPos + gw0 * 18, opos);
+        hs.putSpan<18>(oOppPos + gw0 * 18, opos);
         // last-known positions: the written slots of each row (kept: the
         // observed position, cleared: -1000)
         {
@@ -3801,7 +3840,7 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
     // same in all three, the one-hot id is the slot).  Positions are
     // normalised without the clamp pvpObservations applies.  The lidar copy is
     // fused into k_lidar.
-    {
+    if constexpr (!kWire) {
         const bool alive = self_alive;
         // enemy-only fields first: they decide whether the last-known slot
         // receives the common block
@@ -3868,6 +3907,17 @@ __global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(
             waveSync();
         }
     }
+}
+
+__global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(3))) k_obs(DevState S, SceneDev sc)
+{
+    obsBody<false>(S, sc, WireObs {});
+}
+
+__global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(3)))
+k_obs_wire(DevState S, SceneDev sc, WireObs wo)
+{
+    obsBody<true>(S, sc, wo);
 }
 
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray.  Rays are dealt to
@@ -3956,6 +4006,8 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             agentStage[11][k] = viewHeightD(S.curPose[g]);
         }
     }
+    // gpuStreamStep's caller buffers (engine.h OutTab), read once with the staging
+    const OutTab *ot = (S.outTab && S.outTab->on) ? S.outTab : nullptr;
     const LBVH bvh = stageBVHOct(smem, sc); // ends with __syncthreads
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int it = 0; it < iters; it++) {
@@ -4158,6 +4210,27 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
         // the team interface's slot.
         *tdst = *dst;
         *dst = out;
+        // gpuStreamStep: the caller's lidar buffer too (the engine's copy is
+        // state: the bots and the next full-team copy read it), and the
+        // agent's two agent maps zero-filled by its forward wave (4 KB each:
+        // 4 store instructions of 64 x 16 B per map, no loads; the stores
+        // drain while the wave's next traversal runs)
+        if (ot) {
+            const int64_t gb = S.outBase + (int64_t)g;
+            float4 *cdst = fwd ? reinterpret_cast<float4 *>(ot->fwdLidar) + gb * kFwdRays + kk
+                               : reinterpret_cast<float4 *>(ot->rearLidar) + gb * kRearRays + kk;
+            *cdst = out;
+            if (fwd) {
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 *m0 = reinterpret_cast<float4 *>(ot->agentMap0) + gb * 256 + kk;
+                float4 *m1 = reinterpret_cast<float4 *>(ot->agentMap1) + gb * 256 + kk;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    m0[64 * q] = z;
+                    m1[64 * q] = z;
+                }
+            }
+        }
     }
 }
 
@@ -4418,6 +4491,21 @@ int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
 {
     const int blocks = (int)((s.A + kObsBlock - 1) / kObsBlock);
     hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, s, sc);
+    return check(hipGetLastError());
+}
+
+__global__ void k_set_outtab(OutTab *dev, OutTab v) { *dev = v; }
+
+int launchSetOutTab(OutTab *dev, const OutTab &v, void *stream)
+{
+    hipLaunchKernelGGL(k_set_outtab, dim3(1), dim3(1), 0, (hipStream_t)stream, dev, v);
+    return check(hipGetLastError());
+}
+
+int launchObservationsWire(const DevState &view, const SceneDev &sc, const WireObs &wo, void *stream)
+{
+    const int blocks = (int)((view.A + kObsBlock - 1) / kObsBlock);
+    hipLaunchKernelGGL(k_obs_wire, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, view, sc, wo);
     return check(hipGetLastError());
 }
 

@@ -168,6 +168,9 @@ struct mpenv_manager {
     int64_t graphCaptures = 0; // mpenv_graph_captures
     std::string graphOffReason; // why the step is not replayed from a graph (mpenv_graph_status)
     uint32_t *wireErr = nullptr; // device word raised by a rejected wire message (wire.hip)
+    int32_t *wireEp = nullptr;   // [2][W] a shadow's episode counters of the last two messages
+    int wireParity = 0;          // which half of wireEp holds the previous message's
+    OutTab *outTabDev = nullptr; // gpuStreamStep's caller output buffers (engine.h OutTab)
 
     ~mpenv_manager()
     {
@@ -732,6 +735,10 @@ static void allocState(mpenv_manager &m)
     S.visMask = m.alloc<uint8_t>(A);
     m.wireErr = m.alloc<uint32_t>(1);
     HIP_CHECK(hipMemsetAsync(m.wireErr, 0, sizeof(uint32_t), m.stream));
+    m.outTabDev = m.alloc<OutTab>(1); // zeros: off
+    S.outTab = m.outTabDev;
+    m.wireEp = m.alloc<int32_t>(2 * W);
+    HIP_CHECK(hipMemsetAsync(m.wireEp, 0, sizeof(int32_t) * 2 * W, m.stream));
     S.visOcc = m.alloc<uint16_t>((size_t)A * S.T * 4);
     HIP_CHECK(hipMemsetAsync(S.visOcc, 0xff, sizeof(uint16_t) * (size_t)A * S.T * 4, m.stream));
     S.exploreBits = m.alloc<uint64_t>(A * kExploreTiles);
@@ -835,6 +842,7 @@ static void sliceState(const DevState &S, const SceneDev &sc, int64_t w0, int64_
     MP_WORLD_F32(MP_SL_W)
 #undef MP_SL_A
 #undef MP_SL_W
+    G.outBase = S.outBase + g0;
     G.dmg = S.dmg + g0; // stride stays S.dmgStride
     G.visMask = S.visMask + g0;
     G.visOcc = S.visOcc + g0 * S.T * 4;
@@ -980,6 +988,8 @@ int mpenv_create(const mpenv_config *cfg, mpenv_manager **out)
         m = new mpenv_manager();
         m->S.stats = nullptr;
         m->S.obsGate = nullptr;
+        m->S.outTab = nullptr;
+        m->S.outBase = 0;
         m->cfg = *cfg;
         m->scenePath = cfg->scene_path;
         m->cfg.scene_path = m->scenePath.c_str();
@@ -1114,9 +1124,59 @@ int mpenv_train_interface_entry(int32_t is_output, int32_t idx, const char **nam
 // them, as one batched copy launch (the agent maps are never written by the
 // step and stay all zeros, so their copies are zero fills); a segment whose
 // pointers are not 16-B aligned falls back to hipMemcpyAsync.
-// zeros: 1 = only the agent maps' zero fills, 0 = the other outputs only,
-// -1 = every output.
-static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs, bool outputs, int zeros = -1)
+// zeros: 1 = only the agent maps' zero fills, 0 or -2 = the other outputs
+// only, -1 = every output.
+// The outputs gpuStreamStep has k_obs / k_lidar write straight into the
+// caller's buffers (engine.h OutTab) instead of copying them afterwards.
+static bool directOutput(int32_t id)
+{
+    switch (id) {
+    case MPENV_EXPORT_OPPONENT_MASKS: case MPENV_EXPORT_FILTERS_STATE: case MPENV_EXPORT_SELF_OBSERVATION:
+    case MPENV_EXPORT_SELF_POSITION: case MPENV_EXPORT_TEAMMATE_OBSERVATIONS:
+    case MPENV_EXPORT_TEAMMATE_POSITIONS: case MPENV_EXPORT_OPPONENT_OBSERVATIONS:
+    case MPENV_EXPORT_OPPONENT_POSITIONS: case MPENV_EXPORT_FWD_LIDAR: case MPENV_EXPORT_REAR_LIDAR:
+        return true;
+    default:
+        return false;
+    }
+}
+
+// The call's OutTab, or false when some direct output's buffer is missing
+// or not 16-B aligned (the kernels store float4 rows): then every output is
+// copied as before.
+static bool directTable(void **buffers, OutTab &t)
+{
+    t = OutTab {};
+    t.on = 1;
+    int maps = 0;
+    for (int i = 0; i < kNumTIOutputs; i++) {
+        const int32_t id = kTIOutputs[i].id;
+        if (!directOutput(id) && id != MPENV_EXPORT_AGENT_MAP) continue;
+        float *p = static_cast<float *>(buffers[kNumTIInputs + i]);
+        if (!p || ((uintptr_t)p & 15u)) return false;
+        if (id == MPENV_EXPORT_AGENT_MAP) {
+            (maps++ == 0 ? t.agentMap0 : t.agentMap1) = p;
+            continue;
+        }
+        switch (id) {
+        case MPENV_EXPORT_OPPONENT_MASKS: t.masks = p; break;
+        case MPENV_EXPORT_FILTERS_STATE: t.filters = p; break;
+        case MPENV_EXPORT_SELF_OBSERVATION: t.selfObs = p; break;
+        case MPENV_EXPORT_SELF_POSITION: t.selfPos = p; break;
+        case MPENV_EXPORT_TEAMMATE_OBSERVATIONS: t.tmObs = p; break;
+        case MPENV_EXPORT_TEAMMATE_POSITIONS: t.tmPos = p; break;
+        case MPENV_EXPORT_OPPONENT_OBSERVATIONS: t.oppObs = p; break;
+        case MPENV_EXPORT_OPPONENT_POSITIONS: t.oppPos = p; break;
+        case MPENV_EXPORT_FWD_LIDAR: t.fwdLidar = p; break;
+        case MPENV_EXPORT_REAR_LIDAR: t.rearLidar = p; break;
+        default: break;
+        }
+    }
+    return maps == 2;
+}
+
+static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs, bool outputs, int zeros = -1,
+                  bool skip_direct = false)
 {
     CopyBatch b {};
     auto add = [&](const void *src, void *dst, size_t bytes) {
@@ -1141,7 +1201,8 @@ static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs,
     for (int i = 0; i < kNumTIOutputs; i++, k++) {
         if (!outputs || !buffers[k]) continue;
         const bool zero = kTIOutputs[i].id == MPENV_EXPORT_AGENT_MAP;
-        if ((zeros == 1 && !zero) || (zeros == 0 && zero)) continue;
+        if ((zeros == 1 && !zero) || ((zeros == 0 || zeros == -2) && zero)) continue;
+        if (skip_direct && directOutput(kTIOutputs[i].id)) continue;
         TensorDesc d;
         m->exportDesc(kTIOutputs[i].id, d);
         add(zero ? nullptr : d.ptr, buffers[k], d.bytes());
@@ -1182,16 +1243,28 @@ int mpenv_gpu_stream_step(mpenv_manager *m, void *stream, void **buffers)
     try {
         hipStream_t st = stream ? (hipStream_t)stream : m->stream;
         ensureZStream(m);
-        // the zero fills (1.6 GB of stores at C3) beside the step, ordered
-        // after whatever the caller queued before this call
-        HIP_CHECK(hipEventRecord(m->zForkEv, st));
-        HIP_CHECK(hipStreamWaitEvent(m->zStream, m->zForkEv, 0));
-        copyTI(m, m->zStream, buffers, false, true, 1);
-        HIP_CHECK(hipEventRecord(m->zJoinEv, m->zStream));
+        // The observation rows, the lidar and the agent maps' zeros go
+        // straight into the caller's buffers (OutTab, set in front of the
+        // step and cleared behind it, so the captured step graph is the same
+        // for every call); the rest -- the state-backed outputs (hp,
+        // magazine, alive, last-known rows, rewards, dones, episode results)
+        // -- is copied after the step.
+        OutTab tab;
+        const bool direct = directTable(buffers, tab);
+        if (!direct) {
+            // every output copied: the zero fills (1.6 GB of stores at C3)
+            // beside the step, ordered after whatever the caller queued
+            HIP_CHECK(hipEventRecord(m->zForkEv, st));
+            HIP_CHECK(hipStreamWaitEvent(m->zStream, m->zForkEv, 0));
+            copyTI(m, m->zStream, buffers, false, true, 1);
+            HIP_CHECK(hipEventRecord(m->zJoinEv, m->zStream));
+        }
         copyTI(m, st, buffers, true, false);
+        if (direct && launchSetOutTab(m->outTabDev, tab, st)) throw std::runtime_error("out-table launch failed");
         m->runStep(st);
-        copyTI(m, st, buffers, false, true, 0);
-        HIP_CHECK(hipStreamWaitEvent(st, m->zJoinEv, 0));
+        copyTI(m, st, buffers, false, true, direct ? -2 : 0, direct);
+        if (direct && launchSetOutTab(m->outTabDev, OutTab {}, st)) throw std::runtime_error("out-table launch failed");
+        if (!direct) HIP_CHECK(hipStreamWaitEvent(st, m->zJoinEv, 0));
     } catch (const std::exception &e) {
         return fail(MPENV_ERR_HIP, e.what());
     }
@@ -1314,6 +1387,7 @@ int mpenv_wire_bytes(mpenv_manager *m, int32_t keyframe, int64_t *bytes)
 int mpenv_wire_pack(mpenv_manager *m, void *dst, int32_t keyframe, void *stream)
 {
     if (!m || !dst) return fail(MPENV_ERR_INVALID, "null argument");
+    if ((uintptr_t)dst & 15u) return fail(MPENV_ERR_INVALID, "wire message buffer must be 16-B aligned");
     if (launchWirePack(m->S, static_cast<char *>(dst), keyframe != 0, m->sc.worldOffset,
                        stream ? stream : (void *)m->stream))
         return fail(MPENV_ERR_HIP, "wire pack launch failed");
@@ -1323,12 +1397,35 @@ int mpenv_wire_pack(mpenv_manager *m, void *dst, int32_t keyframe, void *stream)
 int mpenv_wire_unpack(mpenv_manager *m, const void *src, int32_t keyframe, void *stream)
 {
     if (!m || !src) return fail(MPENV_ERR_INVALID, "null argument");
+    if ((uintptr_t)src & 15u) return fail(MPENV_ERR_INVALID, "wire message buffer must be 16-B aligned");
     void *st = stream ? stream : (void *)m->stream;
-    DevState gated = m->S;
-    gated.obsGate = m->wireErr;
-    if (launchWireUnpack(m->S, static_cast<const char *>(src), keyframe != 0, m->wireErr, m->sc.worldOffset, st) ||
-        launchObservations(gated, m->sc, st))
+    const int W = m->S.W;
+    int32_t *prev = m->wireEp + (size_t)m->wireParity * W, *next = m->wireEp + (size_t)(m->wireParity ^ 1) * W;
+    if (launchWireUnpack(m->S, m->sc, static_cast<const char *>(src), keyframe != 0, m->wireErr, m->sc.worldOffset,
+                         prev, next, st))
         return fail(MPENV_ERR_HIP, "wire unpack launch failed");
+    m->wireParity ^= 1;
+    return MPENV_OK;
+}
+
+// The error word's bits now; the refused bit is cleared by this read, the
+// desync bit stays until a keyframe is unpacked (wire.hip wireOk).  `stream`
+// null: the whole device is synchronised first (every unpack queued so far
+// has run); otherwise the read is ordered on that stream only, and with a
+// pinned `out` (hipHostMalloc / torch pin_memory) the call does not block:
+// the value lands when the stream reaches it (record an event after the
+// call and wait on it before reading *out).
+int mpenv_wire_error_async(mpenv_manager *m, uint32_t *out, void *stream)
+{
+    if (!m || !out) return fail(MPENV_ERR_INVALID, "null argument");
+    try {
+        hipStream_t st = (hipStream_t)stream;
+        HIP_CHECK(hipMemcpyAsync(out, m->wireErr, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        // clear REFUSED, keep DESYNC: one atomic AND on the device word
+        if (launchWireErrClear(m->wireErr, st)) throw std::runtime_error("wire error clear launch failed");
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_HIP, e.what());
+    }
     return MPENV_OK;
 }
 

@@ -271,6 +271,9 @@ PYBIND11_MODULE(madrona_mp_env, m)
             check(mpenv_wire_error(s.h->mgr, &e));
             return e;
         })
+        .def("wire_error_async", [](PySimManager &s, uintptr_t out, uintptr_t stream) {
+            check(mpenv_wire_error_async(s.h->mgr, reinterpret_cast<uint32_t *>(out), reinterpret_cast<void *>(stream)));
+        }, py::arg("out"), py::arg("stream"))
         .def("set_world_groups", [](PySimManager &s, int32_t g) { check(mpenv_set_world_groups(s.h->mgr, g)); })
         .def("set_lidar_branch", [](PySimManager &s, bool on) { check(mpenv_set_lidar_branch(s.h->mgr, on ? 1 : 0)); })
         .def("graph_status", [](PySimManager &s) {

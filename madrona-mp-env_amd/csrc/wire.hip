@@ -245,13 +245,14 @@ __global__ void __launch_bounds__(256) k_wire_pack(DevState S, char *dst, WireLa
 // Every unpack kernel checks the header first: a message for another
 // configuration or shard (world offset), of the other kind (keyframe or not),
 // or one the pack kernels flagged is not unpacked, and raises both error
-// bits.  A refused message leaves the shadow out of sync for good (the next
-// plain messages build on history it missed: last-known rows, episode
-// counters), so the desync bit is sticky: later plain messages are refused
-// too (refused bit again), and only a keyframe, which carries that history,
-// is unpacked and clears it (the last unpack kernel, after the others have
-// read the word).  k_obs skips a shadow whose desync bit is set
-// (DevState::obsGate), so its rows are never rebuilt from stale state.
+// bits.  A refused message leaves the shadow out of sync (the next plain
+// messages build on history it missed: last-known rows, episode counters),
+// so the desync bit is sticky: later plain messages are refused too (refused
+// bit again), and only a keyframe, which carries that history, is unpacked
+// and clears it.  k_obs_wire, launched after k_wire_unpack on the same
+// stream, skips a shadow whose desync bit is set (DevState::obsGate), so its
+// rows are never rebuilt from stale state.  Senders send a keyframe every
+// `keyframe_every` messages (mpenv_dist.LearnerWire), so a shadow recovers.
 __device__ __forceinline__ bool wireOk(const DevState &S, const char *src, const WireLayout &L, uint32_t *err,
                                        uint32_t worldOffset)
 {
@@ -265,18 +266,21 @@ __device__ __forceinline__ bool wireOk(const DevState &S, const char *src, const
     return ok;
 }
 
-// One launch, four block ranges (no kernel boundaries between the parts of
-// an unpack: round 4's three launches spent ~20 us in boundaries and short
-// blocks):
-//   lidar   thread = 4 rays 256 apart (1,024 consecutive rays per block):
-//           the depth and the class bits of each, a float4 of f32 lidar out
-//           per ray -- every load and store instruction unit-stride;
-//   agents  thread = agent: the state columns (+ a keyframe's last-known rows);
-//   worlds  thread = world: the world columns; a world whose episode counter
-//           moved since the last message had its agents' last-known rows
-//           cleared by the reset on the sender (resetAgentD /
-//           resetPersistentEntitiesD): the same here;
-//   match   thread = 16 bytes of the [W][30] episode results, copied flat.
+// The learner's rebuild of one message (launchWireUnpack), two launches:
+//   k_wire_unpack, one launch in four block ranges --
+//     lidar   thread = 4 rays 256 apart (1,024 consecutive rays per block):
+//             the depth and the class bits of each, a float4 of f32 lidar out
+//             per ray -- every load and store instruction unit-stride;
+//     agents  thread = agent: the per-agent outputs that are state columns
+//             (hp, alive, reward, done, magazine, reward coefficients) and,
+//             for a keyframe, the last-known rows;
+//     worlds  thread = world: the message's episode counters, kept for the
+//             next message's reset test (double-buffered: next != prev);
+//     match   thread = 16 bytes of the [W][30] episode results, copied flat;
+//   k_obs_wire (kernels.hip) -- the observation rows, read straight from the
+//     message's state columns (the shadow's own state columns are not
+//     written: round 5 stored ~90 B per agent there and k_obs read them
+//     back), with the last-known clear of a reset world folded in.
 struct WireUnpackGrid {
     uint32_t lidar, agents, worlds, match; // first block of each range (lidar = 0), then the total
     uint32_t total;
@@ -295,7 +299,7 @@ __host__ __device__ inline WireUnpackGrid wireUnpackGrid(int64_t A, int64_t W)
 }
 
 __global__ void __launch_bounds__(256) k_wire_unpack(DevState S, const char *src, WireLayout L, WireUnpackGrid G,
-                                                     uint32_t *err, uint32_t worldOffset)
+                                                     uint32_t *err, uint32_t worldOffset, int32_t *epNext)
 {
     if (!wireOk(S, src, L, err, worldOffset)) return;
     const uint32_t b = blockIdx.x;
@@ -336,28 +340,19 @@ __global__ void __launch_bounds__(256) k_wire_unpack(DevState S, const char *src
     } else if (b < G.worlds) {
         const int64_t g = (int64_t)(b - G.agents) * 256 + threadIdx.x;
         if (g >= S.A) return;
-        int k = 0;
-#define MP_GET_F(n) S.n[g] = reinterpret_cast<const float *>(src + L.af[k++])[g];
-        MP_WIRE_AF(MP_GET_F)
-#undef MP_GET_F
-        k = 0;
-#define MP_GET_I(n) S.n[g] = reinterpret_cast<const int32_t *>(src + L.ai[k++])[g];
-        MP_WIRE_AI(MP_GET_I)
-#undef MP_GET_I
-        S.hp[g] = reinterpret_cast<const float *>(src + L.hp)[g];
-        S.alive[g] = reinterpret_cast<const float *>(src + L.alive)[g];
-        S.reward[g] = reinterpret_cast<const float *>(src + L.reward)[g];
-        S.done[g] = reinterpret_cast<const int32_t *>(src + L.done)[g];
+        const float hp = reinterpret_cast<const float *>(src + L.hp)[g];
+        const float alive = reinterpret_cast<const float *>(src + L.alive)[g];
+        const float reward = reinterpret_cast<const float *>(src + L.reward)[g];
+        const int32_t done = reinterpret_cast<const int32_t *>(src + L.done)[g];
         const int2 mg = reinterpret_cast<const int2 *>(src + L.mag)[g];
-        S.magazine[2 * g] = mg.x;
-        S.magazine[2 * g + 1] = mg.y;
-        const uint32_t p = reinterpret_cast<const uint32_t *>(src + L.packed)[g];
-        S.curPose[g] = (int32_t)(p & 0xffu);
-        S.tgtPose[g] = (int32_t)((p >> 8) & 0xffu);
-        S.weapon[g] = (int32_t)((p >> 16) & 0xffu);
-        S.flags[g] = (int32_t)(p >> 24);
-        S.visMask[g] = reinterpret_cast<const uint8_t *>(src + L.vis)[g];
-        for (int c = 0; c < 9; c++) S.rewardCoefs[g * 9 + c] = reinterpret_cast<const float *>(src + L.coefs)[g * 9 + c];
+        float coef[9];
+        for (int c = 0; c < 9; c++) coef[c] = reinterpret_cast<const float *>(src + L.coefs)[g * 9 + c];
+        S.hp[g] = hp;
+        S.alive[g] = alive;
+        S.reward[g] = reward;
+        S.done[g] = done;
+        reinterpret_cast<int2 *>(S.magazine)[g] = mg;
+        for (int c = 0; c < 9; c++) S.rewardCoefs[g * 9 + c] = coef[c];
         if (L.lkObs >= 0) {
             const float4 *s4 = reinterpret_cast<const float4 *>(src + L.lkObs) + g * 6 * kOtherObs / 4;
             float4 *lk = reinterpret_cast<float4 *>(S.lkObs + g * 6 * kOtherObs);
@@ -367,18 +362,7 @@ __global__ void __launch_bounds__(256) k_wire_unpack(DevState S, const char *src
     } else if (b < G.match) {
         const int64_t w = (int64_t)(b - G.worlds) * 256 + threadIdx.x;
         if (w >= S.W) return;
-        const int32_t ep = reinterpret_cast<const int32_t *>(src + L.wi[kWireWI - 1])[w];
-        if (ep != S.episodeCounter[w] && L.lkObs < 0) {
-            for (int64_t g = w * S.N; g < (w + 1) * S.N; g++) {
-                float4 *lk = reinterpret_cast<float4 *>(&S.lkObs[g * 6 * kOtherObs]);
-                for (int q = 0; q < 6 * kOtherObs / 4; q++) lk[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                for (int q = 0; q < 18; q++) S.lkPos[g * 18 + q] = -1000.f;
-            }
-        }
-        int k = 0;
-#define MP_GET_W(n) S.n[w] = reinterpret_cast<const int32_t *>(src + L.wi[k++])[w];
-        MP_WIRE_WI(MP_GET_W)
-#undef MP_GET_W
+        epNext[w] = reinterpret_cast<const int32_t *>(src + L.wi[kWireWI - 1])[w];
     } else {
         // [W][30] i32 episode results: 16-B pieces of the flat array (both
         // ends 256-B aligned; the last piece may be partial)
@@ -444,6 +428,14 @@ __global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b)
 }
 
 static int checkW(hipError_t e) { return e == hipSuccess ? 0 : -1; }
+
+__global__ void k_wire_err_clear(uint32_t *err) { atomicAnd(err, kWireErrDesync); }
+
+int launchWireErrClear(uint32_t *err, void *stream)
+{
+    hipLaunchKernelGGL(k_wire_err_clear, dim3(1), dim3(1), 0, (hipStream_t)stream, err);
+    return checkW(hipGetLastError());
+}
 static unsigned grid(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 int64_t wireBytes(const DevState &s, bool keyframe) { return wireLayout(s.A, s.W, keyframe).total; }
@@ -471,16 +463,47 @@ int launchCopyBatch(const CopyBatch &bIn, void *stream)
     return checkW(hipGetLastError());
 }
 
-int launchWireUnpack(const DevState &s, const char *src, bool keyframe, uint32_t *err, uint32_t worldOffset,
-                     void *stream)
+int launchWireUnpack(const DevState &s, const SceneDev &sc, const char *src, bool keyframe, uint32_t *err,
+                     uint32_t worldOffset, const int32_t *epPrev, int32_t *epNext, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     const WireLayout L = wireLayout(s.A, s.W, keyframe);
     const WireUnpackGrid G = wireUnpackGrid(s.A, s.W);
-    // the lidar quads assume 16-B aligned f32 lidar rows and depth column
-    if (((uintptr_t)s.fwdLidar | (uintptr_t)s.rearLidar | (uintptr_t)s.matchResult) & 15u) return -1;
-    hipLaunchKernelGGL(k_wire_unpack, dim3(G.total), dim3(256), 0, st, s, src, L, G, err, worldOffset);
-    return checkW(hipGetLastError());
+    // the lidar quads assume 16-B aligned f32 lidar rows; the match copy
+    // 16-B pieces at both ends
+    if (((uintptr_t)s.fwdLidar | (uintptr_t)s.rearLidar | (uintptr_t)s.matchResult | (uintptr_t)src) & 15u) return -1;
+    hipLaunchKernelGGL(k_wire_unpack, dim3(G.total), dim3(256), 0, st, s, src, L, G, err, worldOffset, epNext);
+    if (checkW(hipGetLastError())) return -1;
+    // the shadow seen through the message: input columns in the message,
+    // outputs (and the last-known history) in the shadow; k_obs_wire skips
+    // everything while the shadow is out of sync (obsGate), so a refused
+    // message rebuilds nothing
+    DevState v = s;
+    char *m = const_cast<char *>(src);
+    int k = 0;
+#define MP_VIEW_F(n) v.n = reinterpret_cast<float *>(m + L.af[k++]);
+    MP_WIRE_AF(MP_VIEW_F)
+#undef MP_VIEW_F
+    k = 0;
+#define MP_VIEW_I(n) v.n = reinterpret_cast<int32_t *>(m + L.ai[k++]);
+    MP_WIRE_AI(MP_VIEW_I)
+#undef MP_VIEW_I
+    k = 0;
+#define MP_VIEW_W(n) v.n = reinterpret_cast<int32_t *>(m + L.wi[k++]);
+    MP_WIRE_WI(MP_VIEW_W)
+#undef MP_VIEW_W
+    v.hp = reinterpret_cast<float *>(m + L.hp);
+    v.alive = reinterpret_cast<float *>(m + L.alive);
+    v.magazine = reinterpret_cast<int32_t *>(m + L.mag);
+    v.visMask = reinterpret_cast<uint8_t *>(m + L.vis);
+    v.obsGate = err;
+    v.stats = nullptr;
+    v.outTab = nullptr;
+    WireObs wo;
+    wo.packed = reinterpret_cast<const uint32_t *>(src + L.packed);
+    wo.epPrev = epPrev;
+    wo.keyframe = keyframe ? 1 : 0;
+    return launchObservationsWire(v, sc, wo, stream);
 }
 
 } // namespace mpenv

@@ -335,16 +335,23 @@ class LearnerWire:
 
     A shadow that refused a message (wrong configuration or shard, wrong
     kind, values that did not fit the wire) is out of sync until a keyframe;
-    `check()` raises then -- every `check_every` submits, and in outputs()
-    and close().
+    `check()` raises then -- every `check_every` submits (default 64), and in
+    outputs() and close().  Senders send a keyframe every `keyframe_every`
+    messages (default 256; both sides derive the schedule from the message
+    count, so no back channel is needed), so a shadow that refused a message
+    recovers within that many steps instead of staying frozen.  On a GPU the
+    periodic check reads every shadow's error word asynchronously (into
+    pinned host memory, on the streams the unpacks run on, no device
+    synchronisation) and raises at the next check on what the previous one
+    fetched.
     """
 
     NOT_SHIPPED = NOT_SHIPPED
     mode = "wire"
 
     def __init__(self, sim, make_shadow=None, dst: int = 0, group=None, slots: int = 2, pack=None, unpack=None,
-                 nbytes=None, device=None, overlap: bool = True, check_every: int = 0, wire_error=None,
-                 dedicated: bool = False, unpack_streams: int = 1):
+                 nbytes=None, device=None, overlap: bool = True, check_every: int = 64, wire_error=None,
+                 dedicated: bool = False, unpack_streams: int = 1, keyframe_every: int = 256):
         import torch
         import torch.distributed as dist
 
@@ -377,6 +384,13 @@ class LearnerWire:
         self.gpu = dev.type == "cuda"
         self._wire_error = wire_error or (lambda r: self.shadows[r].wire_error())
         self.check_every = int(check_every)
+        self.keyframe_every = max(0, int(keyframe_every))
+        # asynchronous error reads (GPU shadows): pinned words + the events
+        # that mark them written
+        self._err_async = (wire_error is None and self.gpu and self.rank == dst and bool(self.shadows)
+                           and all(hasattr(x, "wire_error_async") for x in self.shadows.values()))
+        self._err_host = torch.zeros(self.ws, dtype=torch.int32, pin_memory=True) if self._err_async else None
+        self._err_events = None
         self.slots = slots
         if self.rank == dst:
             self.bufs = [[torch.empty(self.nk, dtype=torch.uint8, device=dev) for _ in range(self.ws)]
@@ -407,22 +421,71 @@ class LearnerWire:
             raise ValueError("LearnerWire: submit() on a stream other than torch's current one")
         return cur
 
-    def check(self):
-        """Raise if any shadow refused a message (learner; synchronises the
-        device).  A refused message -- wrong configuration or shard, wrong
-        kind, or values the pack flagged as not fitting the wire -- leaves
-        that shadow's history (last-known rows, episode counters) behind the
-        sender's until a keyframe; its outputs are not the sender's."""
+    def _unpack_stream(self, r):
+        """The stream rank r's unpacks run on (None: the caller's)."""
+        if not self.ustreams:
+            return None
+        ranks = [q for q in range(self.ws) if q != self.dst or self.loopback]
+        return self.ustreams[ranks.index(r) % len(self.ustreams)]
+
+    def _fetch_errors(self):
+        """Queue every shadow's error-word read into pinned memory, ordered
+        after its unpacks; events mark the words written."""
+        cur = self.torch.cuda.current_stream()
+        used = []
+        for r in sorted(self.shadows):
+            us = self._unpack_stream(r) or cur
+            self.shadows[r].wire_error_async(self._err_host.data_ptr() + 4 * r, us.cuda_stream)
+            if us not in used:
+                used.append(us)
+        self._err_events = []
+        for us in used:
+            ev = self.torch.cuda.Event()
+            ev.record(us)
+            self._err_events.append(ev)
+
+    def _raise_if_bad(self, bad):
+        if bad:
+            raise RuntimeError(f"LearnerWire: shadow(s) refused wire messages {bad} (error bits: 1 refused, "
+                               "2 out of sync until a keyframe); their outputs are stale")
+
+    def check(self, block: bool = True):
+        """Raise if any shadow refused a message (learner).  A refused message
+        -- wrong configuration or shard, wrong kind, or values the pack
+        flagged as not fitting the wire -- leaves that shadow's history
+        (last-known rows, episode counters) behind the sender's until a
+        keyframe; its outputs are not the sender's.  block=True reads the
+        words now (after every queued unpack); block=False (the periodic
+        check on a GPU) raises on the words the previous check fetched and
+        queues the next read, without synchronising."""
         if self.rank != self.dst:
+            return
+        if self._err_async:
+            if self._err_events is not None:
+                for ev in self._err_events:
+                    ev.synchronize()  # recorded a check_every ago: long done
+                self._err_events = None
+                words = self._err_host.tolist()
+                self._raise_if_bad({r: words[r] for r in sorted(self.shadows) if words[r]})
+            self._fetch_errors()
+            if block:
+                for ev in self._err_events:
+                    ev.synchronize()
+                self._err_events = None
+                words = self._err_host.tolist()
+                self._raise_if_bad({r: words[r] for r in sorted(self.shadows) if words[r]})
             return
         bad = {}
         for r in sorted(self.shadows):
             e = int(self._wire_error(r))
             if e:
                 bad[r] = e
-        if bad:
-            raise RuntimeError(f"LearnerWire: shadow(s) refused wire messages {bad} (error bits: 1 refused, "
-                               "2 out of sync until a keyframe); their outputs are stale")
+        self._raise_if_bad(bad)
+
+    def is_keyframe(self, k: int) -> bool:
+        """Whether message k (0-based, per sender) is a keyframe: the first,
+        then every keyframe_every-th."""
+        return k == 0 or (self.keyframe_every > 0 and k % self.keyframe_every == 0)
 
     def _unpack_slot(self, slot, ranks, stream_ptr):
         if not self.ustreams:
@@ -468,7 +531,7 @@ class LearnerWire:
             # the slot overwrite one still in flight)
             stream_ptr = self._caller_stream(stream_ptr).cuda_stream
         slot = self.k % self.slots
-        kf = self.k == 0
+        kf = self.is_keyframe(self.k)
         self.k += 1
         self._finish(slot, stream_ptr)  # the slot's previous round is done before it is reused
         n = self.nk if kf else self.nb
@@ -485,7 +548,7 @@ class LearnerWire:
                 us.wait_stream(self._caller_stream(stream_ptr))
             self._unpack_slot(slot, [0], stream_ptr)
             if self.check_every and self.k % self.check_every == 0:
-                self.check()
+                self.check(block=False)
             return slot
         if self.rank == self.dst:
             ops = [dist.P2POp(dist.irecv, self.bufs[slot][r][:n], self._peer(r), self.group)
@@ -500,7 +563,7 @@ class LearnerWire:
         if self.slots > 1 and self.k > 1:
             self._finish(prev, stream_ptr)
         if self.check_every and self.k % self.check_every == 0:
-            self.check()
+            self.check(block=False)
         return slot
 
     def drain(self, stream_ptr=None):

@@ -144,8 +144,10 @@ def test_caller_written_against_mgr_hpp_compiles_and_out_of_scope_parts_throw(tm
 
 def test_product_kernels_carry_no_lab_switches_and_lab_patches_apply(tmp_path):
     """Only the shipped configuration is in csrc/ (no lab hooks or dropped
-    variants behind compile-time switches); the lab overlay under tools/lab/
-    still applies to it, so kernel_lab variants keep building."""
+    variants behind compile-time switches); any lab overlay under tools/lab/
+    still applies to it, so kernel_lab variants keep building.  (Round 6
+    retired the round-1..5 lab_hooks.patch: it is in git history before
+    commit "retire lab_hooks.patch".)"""
     import shutil
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -157,8 +159,7 @@ def test_product_kernels_carry_no_lab_switches_and_lab_patches_apply(tmp_path):
             assert not switch.search(text), f"compile-time MPENV_ switch left in {f}"
             assert "MPENV_LAB" not in text and "MP_LAB_" not in text, f"lab hook left in {f}"
     lab = os.path.join(root, "tools", "lab")
-    patches = sorted(p for p in os.listdir(lab) if p.endswith(".patch"))
-    assert "lab_hooks.patch" in patches
+    patches = sorted(p for p in os.listdir(lab) if p.endswith(".patch")) if os.path.isdir(lab) else []
     for p in patches:
         work = tmp_path / p
         shutil.copytree(csrc, work)

@@ -481,10 +481,17 @@ def test_cpp_manager_headless_runs():
     assert "FPS" in r.stdout and float(r.stdout.split("FPS")[1].split()[0]) > 0
 
 
-def test_gpu_stream_step_buffers_abi():
+@pytest.mark.parametrize("groups", [1, 2])
+def test_gpu_stream_step_buffers_abi(groups):
     """Manager::gpuStreamInit/gpuStreamStep (mgr.cpp:507-645): a flat
     buffer array of TrainInterface inputs then outputs, caller-owned, on the
-    caller's stream — the XLA custom-call ABI scripts/jax_train.py uses."""
+    caller's stream — the XLA custom-call ABI scripts/jax_train.py uses.
+    The observation rows and the lidar are written by k_obs / k_lidar
+    straight into the call's buffers (engine.h OutTab): two caller buffer
+    sets alternate step by step (XLA hands out fresh result buffers), every
+    output of the set a step used equals the oracle, and the captured step
+    graph is not re-captured for them.  Afterwards a plain step() writes the
+    engine's own exports again (the table is off outside the call)."""
     import ctypes as C
     import torch
 
@@ -499,7 +506,10 @@ def test_gpu_stream_step_buffers_abi():
     o = T.Oracle(W, ts)
     ni, no = C.c_int32(), C.c_int32()
     assert lib.mpenv_train_interface_size(C.byref(ni), C.byref(no)) == 0
-    names, bufs = [], []
+    if groups > 1:
+        lib.mpenv_set_world_groups.argtypes = [C.c_void_p, C.c_int32]
+        assert lib.mpenv_set_world_groups(e.h, groups) == 0
+    names, sets = [], [[], []]
     inv = {v: k for k, v in T.EXPORT.items()}
     for io, n in ((0, ni.value), (1, no.value)):
         for k in range(n):
@@ -508,28 +518,46 @@ def test_gpu_stream_step_buffers_abi():
             _, dt, shape = e.desc(inv[eid.value])
             tdt = {np.int32: torch.int32, np.float32: torch.float32}[dt]
             names.append((io, nm.value.decode(), inv[eid.value]))
-            bufs.append(torch.zeros(shape, dtype=tdt, device="cuda"))
-    arr = (C.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+            for bs in sets:  # outputs not zeros: every byte must be written
+                bs.append(torch.full(shape, 7 if io == 1 else 0, dtype=tdt, device="cuda"))
+    arrs = [(C.c_void_p * len(bs))(*[b.data_ptr() for b in bs]) for bs in sets]
     idx = {nm: i for i, (io, nm, _) in enumerate(names)}
-    bufs[idx["simCtrl"]].copy_(torch.tensor([0, 1, 1], dtype=torch.int32).view_as(bufs[idx["simCtrl"]]))
+    for bs in sets:
+        bs[idx["simCtrl"]].copy_(torch.tensor([0, 1, 1], dtype=torch.int32).view_as(bs[idx["simCtrl"]]))
     o.put_ctrl([0, 1, 1])
     stream = torch.cuda.Stream()
     e.put_ctrl([0, 1, 1])
-    assert lib.mpenv_gpu_stream_init(e.h, C.c_void_p(stream.cuda_stream), arr) == 0
+    assert lib.mpenv_gpu_stream_init(e.h, C.c_void_p(stream.cuda_stream), arrs[0]) == 0
     o.init()
     stream.synchronize()
+    lib.mpenv_graph_captures.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+    caps = []
     for s in range(40):
+        bufs = sets[s % 2]
         acts = T.mpenv_tape.tape_actions(1234, s, 0, A)
         bufs[idx["discrete"]].copy_(torch.from_numpy(acts[:, :4].copy()).view_as(bufs[idx["discrete"]]))
         bufs[idx["aim"]].copy_(torch.from_numpy(acts[:, 4:6].copy()).view_as(bufs[idx["aim"]]))
         torch.cuda.synchronize()
-        assert lib.mpenv_gpu_stream_step(e.h, C.c_void_p(stream.cuda_stream), arr) == 0
+        assert lib.mpenv_gpu_stream_step(e.h, C.c_void_p(stream.cuda_stream), arrs[s % 2]) == 0
         o.set_actions(acts)
         o.step()
         stream.synchronize()
         for (io, nm, ename), b in zip(names, bufs):
             if io == 1:
                 T.compare(b.cpu().numpy(), o.get(ename), f"{nm} @ {s}")
+        n = C.c_int64()
+        assert lib.mpenv_graph_captures(e.h, C.byref(n)) == 0
+        caps.append(n.value)
+    assert caps[1] >= 1 and caps[-1] == caps[1], caps  # one capture serves both buffer sets
+    # a plain step afterwards: the engine's own exports are written again
+    acts = T.mpenv_tape.tape_actions(1234, 40, 0, A)
+    e.set_actions(acts)
+    e.step()
+    o.set_actions(acts)
+    o.step()
+    for (io, nm, ename) in names:
+        if io == 1 and nm != "unmasked_agent_map" and nm != "agent_map":
+            T.compare(e.get(ename), o.get(ename), f"engine export {nm} after the stream steps")
 
 
 def test_jax_custom_call_targets_match_gpu_stream_step():

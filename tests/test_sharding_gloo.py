@@ -226,9 +226,10 @@ def test_learner_gather_rejects_non_contiguous_sources():
 
 # ---- LearnerWire transport (the compact wire format's exchange): byte-level
 # stand-ins for pack / unpack, three ranks on gloo.  Every message of every
-# sender must reach the learner's unpack in order, the first as a keyframe,
-# each sized as its kind, with its bytes intact.
-WIRE_NB, WIRE_NK, WIRE_STEPS = 1000, 1600, 7
+# sender must reach the learner's unpack in order, the first and then every
+# WIRE_KF-th as a keyframe (periodic keyframes, so a shadow that
+# refused a message recovers), each sized as its kind, with its bytes intact.
+WIRE_NB, WIRE_NK, WIRE_STEPS, WIRE_KF = 1000, 1600, 7, 3
 
 
 def _wire_bytes(rank, step, keyframe):
@@ -260,7 +261,8 @@ def _wire_worker(rank, world_size, port, result_path, dedicated=False):
             def pack(ptr, keyframe, stream):  # the dedicated learner never packs
                 raise AssertionError("dedicated learner packed a message")
         lw = LearnerWire(None, dst=0, pack=pack, unpack=unpack, dedicated=dedicated,
-                         nbytes=lambda kf: WIRE_NK if kf else WIRE_NB, device=torch.device("cpu"))
+                         nbytes=lambda kf: WIRE_NK if kf else WIRE_NB, device=torch.device("cpu"),
+                         keyframe_every=WIRE_KF)
         assert lw.bytes_per_step() == {"sent_per_rank": WIRE_NB, "learner_ingress": WIRE_NB * (world_size - 1),
                                        "keyframe": WIRE_NK}
         for s in range(WIRE_STEPS):
@@ -281,7 +283,8 @@ def test_learner_wire_transport_three_ranks(tmp_path, dedicated):
     """Three gloo ranks; rank 0 the learner.  dedicated: the learner
     simulates nothing (sim None, never packs) and only receives and unpacks
     ranks 1 and 2 -- C4's 7 simulators + 1 learner layout (DESIGN.md §6);
-    every message still arrives in order, keyframe first, bytes intact."""
+    every message still arrives in order, keyframes first and every
+    WIRE_KF-th, bytes intact."""
     import pickle  # reads the file _wire_worker wrote above
 
     path = str(tmp_path / "wire.pkl")
@@ -292,7 +295,7 @@ def test_learner_wire_transport_three_ranks(tmp_path, dedicated):
         msgs = [(kf, b) for rr, kf, b in seen if rr == r]
         assert len(msgs) == WIRE_STEPS
         for s, (kf, b) in enumerate(msgs):
-            assert kf == (s == 0)
+            assert kf == (s % WIRE_KF == 0)
             assert b == _wire_bytes(r, s, kf).tobytes(), (r, s)
 
 

@@ -153,10 +153,13 @@ def test_wire_rejects_foreign_or_mismatched_messages():
     a.mem.free(kbuf)
 
 
-def test_learner_wire_raises_on_a_refused_message():
+def test_learner_wire_raises_on_a_refused_message_then_recovers_at_a_keyframe():
     """LearnerWire (loopback through the Python module) must not serve a
     shadow that refused a message: a message whose header carries the pack
-    kernel's overflow flag is refused, and outputs() raises."""
+    kernel's overflow flag is refused, and outputs() raises (the periodic
+    asynchronous check too).  The periodic keyframe (keyframe_every) then
+    resynchronises the shadow: after it the outputs equal the engine's again
+    (a refused message must not freeze a shadow for good)."""
     import socket
 
     import torch
@@ -186,18 +189,42 @@ def test_learner_wire_raises_on_a_refused_message():
                 t = [b for slot in lw.bufs for b in slot if b.data_ptr() == ptr][0]
                 t[8] = t[8] | 2
 
+        from mpenv_dist import LearnerGather
+
         st = torch.cuda.Stream()
         torch.cuda.set_stream(st)
-        lw = LearnerWire(sim, make_shadow=lambda r: mk(), pack=pack, device=torch.device("cuda", 0))
+        lw = LearnerWire(sim, make_shadow=lambda r: mk(), pack=pack, device=torch.device("cuda", 0),
+                         keyframe_every=8, check_every=2)
+        assert lw._err_async
         for s in range(4):
             sim.step_async(st.cuda_stream)
             lw.submit(st.cuda_stream)
         lw.outputs()  # in sync
         corrupt[0] = True
         sim.step_async(st.cuda_stream)
-        lw.submit(st.cuda_stream)
+        lw.submit(st.cuda_stream)  # message 4: refused
+        corrupt[0] = False
         with pytest.raises(RuntimeError, match="refused"):
             lw.outputs()
+        def step():
+            sim.step_async(st.cuda_stream)
+            lw.submit(st.cuda_stream)
+
+        step()  # message 5: refused (out of sync); the periodic check (k = 6) queues its read
+        step()  # message 6: refused
+        with pytest.raises(RuntimeError, match="refused"):
+            step()  # message 7: the check (k = 8) raises on what the k = 6 read fetched
+        step()  # message 8: a keyframe resynchronises
+        step()  # message 9: accepted; the check (k = 10) queues a read (messages 6-7's refusals)
+        step()  # message 10
+        with pytest.raises(RuntimeError, match="refused"):
+            lw.check()  # those refusals, reported once
+        got = lw.outputs()  # clean again
+        own = LearnerGather.from_sim(sim)
+        torch.cuda.synchronize()
+        for n, t in got.items():
+            a, b = t[0].contiguous(), own[n].contiguous()
+            assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), n
     finally:
         torch.cuda.set_stream(torch.cuda.default_stream())
         dist.destroy_process_group()

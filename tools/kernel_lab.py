@@ -11,17 +11,14 @@ Instrumentation and switched-off parts live in patches under tools/lab/
 (the overlay): a build copies csrc/ into lab/NAME/src, applies the patches
 there and compiles that copy, so no lab hook sits in the shipped sources.
 
-  tools/lab/lab_hooks.patch   the round-1..3 switches: -DMPENV_LAB_MOVE_SKIP=,
-                              _WAVE_HIST=k, _WORK, _NO_TRI,
-                              _NO_BVH, _NO_CAPSULE, _NO_REAR, _NO_FT_LIDAR, ...,
-                              and the dropped variants (MPENV_LIDAR_PERM,
-                              MPENV_TRI_FLAT, MPENV_*_WPE, ...; MPENV_CRUMB_CHUNK went with decayCrumbsD in round 5); the round-1..4
-                              k_obs switches went with that kernel (round 5)
-  (round 4's forward-fan candidate lists, fan_lists.patch / fan_phases.patch,
-  are in git history before round 5: measured and dropped)
+  tools/lab/lab_hooks.patch   the round-1..5 switches (-DMPENV_LAB_MOVE_SKIP=,
+                              _NO_TRI, _NO_BVH, _NO_CAPSULE, ...) and dropped
+                              variants: retired in round 6 (every kernel change
+                              had to re-merge it); it is in git history, before
+                              the commit "retire lab_hooks.patch"
   k_sim's -DMPENV_LAB_PHASE_T / _SIM_SKIP= / MPENV_SIM_WPE= hooks are inserted
   by text (ksim_hooks below), not by a patch
-e.g. build phase --patch tools/lab/lab_hooks.patch -DMPENV_LAB_PHASE_T
+e.g. build phase -DMPENV_LAB_PHASE_T
 (tests/test_abi.py checks that every patch still applies to csrc/).
 """
 import ctypes as C
