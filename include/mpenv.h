@@ -513,6 +513,18 @@ int mpenv_read_stats(mpenv_manager *mgr, uint64_t *out, int32_t n);
  * outputs to query sizes.  Used by the parity oracle and tests. */
 int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes,
                     float *verts_out, int32_t *num_verts, int32_t *max_stack);
+/* k_lidar's own tree of the scene's triangles (scene.h lidarBVHOpts), same
+ * format: closest hits are tree-independent up to coplanar ties, so the
+ * lidar walks a tree built for its near-horizontal fans. */
+int mpenv_scene_lidar_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes,
+                          float *verts_out, int32_t *num_verts, int32_t *max_stack);
+/* The same for another build of the scene's triangles (scene.h
+ * BVHBuildOpts): opts[0] max leaf size (1-2), [1] SAH bins (0 = full sweep),
+ * [2] measure (0 surface area, 1 lidar-weighted), [3] traversal cost x 100,
+ * [4] the lidar measure's floor weight x 100; missing entries keep the
+ * defaults.  For tools/trav_stats.cpp (tree models). */
+int mpenv_scene_bvh_variant(const char *scene_path, const int32_t *opts, int32_t num_opts, void *nodes_out,
+                            int32_t *num_nodes, float *verts_out, int32_t *num_verts, int32_t *max_stack);
 
 /* The sphere-cast quirk guard k_move uses (scene.h quirkGrid, radius 15,
  * margin 2, 16-unit cells): header[0..2] = minX, minY, cell (float bits),

@@ -238,7 +238,9 @@ struct SceneTables {
 struct SceneDev {
     const SceneTables *tab; // device copy of the arrays below (set after scene upload)
     const BVHNode *nodes;
-    const BVHNode *octNodes; // [8][numNodes] octant node images (scene.h octantNodeImages)
+    const BVHNode *octNodes; // [8][numLidarNodes] octant node images of the lidar tree (scene.h octantNodeImages)
+    const float *lidarVerts; // the lidar tree's triangles, 3 floats per vertex (scene.h Scene::lidarVerts)
+    int32_t numLidarNodes, numLidarVerts;
     const float *verts;     // 3 floats per vertex, 3 vertices per triangle
     // Per triangle, ray-independent terms of sphereCastTriangle
     // (mesh_bvh.inl:885-1127): unit normal xyz, |normal|, |e01|^2, |e02|^2,

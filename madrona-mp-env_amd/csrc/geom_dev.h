@@ -154,8 +154,9 @@ __device__ __forceinline__ LBVH stageBVHSphere(char *smem, const SceneDev &sc)
     return b;
 }
 
-// k_lidar's LDS image: the 8 octant node images (scene.h octantNodeImages,
-// 8 x numNodes nodes) then the vertices as float4 (three rotated copies).
+// k_lidar's LDS image: the 8 octant node images of the lidar tree (scene.h
+// octantNodeImages, 8 x numLidarNodes nodes) then its vertices as float4
+// (three rotated copies).
 // The traversal of a ray reads image (d.x < 0) | (d.y < 0) << 1 | (d.z < 0) << 2.  Each node takes
 // kOctNodeQ = 4 16-B slots (packed 64-B nodes; a fifth pad slot, which moves
 // nodes k != k' (mod 16) to different LDS bank groups, measured no faster in
@@ -166,15 +167,15 @@ constexpr int kOctNodeQ = 4;
 
 __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
 {
-    const int node_q = sc.numNodes * kOctNodeQ * 8;
+    const int node_q = sc.numLidarNodes * kOctNodeQ * 8;
     const uint4 *src_n = reinterpret_cast<const uint4 *>(sc.octNodes);
     uint4 *dst_n = reinterpret_cast<uint4 *>(smem);
-    for (int k = threadIdx.x; k < sc.numNodes * 4 * 8; k += blockDim.x)
+    for (int k = threadIdx.x; k < sc.numLidarNodes * 4 * 8; k += blockDim.x)
         dst_n[(k >> 2) * kOctNodeQ + (k & 3)] = src_n[k];
-    const float *src_v = sc.verts;
+    const float *src_v = sc.lidarVerts;
     float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
-    for (int k = threadIdx.x; k < sc.numVerts * 3; k += blockDim.x) {
-        const int r = k / sc.numVerts, v = k - r * sc.numVerts;
+    for (int k = threadIdx.x; k < sc.numLidarVerts * 3; k += blockDim.x) {
+        const int r = k / sc.numLidarVerts, v = k - r * sc.numLidarVerts;
         const int r1 = r == 2 ? 0 : r + 1, r2 = r1 == 2 ? 0 : r1 + 1;
         dst_v[k] = make_float4(src_v[3 * v + r1], src_v[3 * v + r2], src_v[3 * v + r], 0.f);
     }
@@ -185,7 +186,7 @@ __device__ __forceinline__ LBVH stageBVHOct(char *smem, const SceneDev &sc)
     b.pre = nullptr;
     b.snodes = nullptr;
     b.stats = nullptr;
-    b.rotStride = sc.numVerts;
+    b.rotStride = sc.numLidarVerts;
     return b;
 }
 

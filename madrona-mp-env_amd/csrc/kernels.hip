@@ -3536,8 +3536,12 @@ struct HalfStage {
 // moved since the previous message has every last-known row written -- the
 // reset's clear on the sender (resetAgentD / resetPersistentEntitiesD),
 // then this step's updates -- exactly the rows the sender's k_obs leaves.
+// (One templated kernel, k_obs<false> on the step path and k_obs<true> =
+// "k_obs_wire" on the learner: the same body as a __device__ function under
+// two kernels compiled ~45% more instructions and ran 6% slower.)
 template <bool kWire>
-__device__ __forceinline__ void obsBody(const DevState &S, const SceneDev &sc, const WireObs &wo)
+__global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(3)))
+k_obs(DevState S, SceneDev sc, WireObs wo)
 {
     __shared__ float ost[kObsCols][kObsStageMax];
     __shared__ __attribute__((aligned(16))) float rowBuf[kObsBlock / 64][32 * kObsSpanPad];
@@ -3909,17 +3913,6 @@ __device__ __forceinline__ void obsBody(const DevState &S, const SceneDev &sc, c
     }
 }
 
-__global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(3))) k_obs(DevState S, SceneDev sc)
-{
-    obsBody<false>(S, sc, WireObs {});
-}
-
-__global__ void __launch_bounds__(kObsBlock) __attribute__((amdgpu_waves_per_eu(3)))
-k_obs_wire(DevState S, SceneDev sc, WireObs wo)
-{
-    obsBody<true>(S, sc, wo);
-}
-
 // pvpLidarSystem (sim.cpp:3324-3506).  Lane = ray.  Rays are dealt to
 // waves in units of 4 agents = 5 wave tasks: tasks 0-3 carry one agent's 64
 // forward rays each (32 angles x 2 heights, one origin and a narrow fan, so
@@ -4057,7 +4050,7 @@ __global__ void __launch_bounds__(kLidarBlock) MP_LIDAR_ATTR k_lidar(DevState S,
             // order (scene.h octantNodeImages)
             LBVH ob = bvh;
             ob.nodes = reinterpret_cast<const MP_LDS BVHNode *>(reinterpret_cast<const MP_LDS uint4 *>(bvh.nodes) +
-                                                                 rayOctant(dir) * sc.numNodes * kOctNodeQ);
+                                                                 rayOctant(dir) * sc.numLidarNodes * kOctNodeQ);
             bhit = bvhTraceRayT<false, kOctNodeQ, true, true>(ob, ray_o, dir, tb, kFltMax, 0.f);
         }
         // The lane id again (volatile) and the ray's indices from it: integer
@@ -4432,7 +4425,7 @@ size_t bvhLdsBytesSphere(const SceneDev &sc)
 
 size_t bvhLdsBytesOct(const SceneDev &sc)
 {
-    return (size_t)sc.numNodes * 16 * kOctNodeQ * 8 + (size_t)sc.numVerts * 16 * 3;
+    return (size_t)sc.numLidarNodes * 16 * kOctNodeQ * 8 + (size_t)sc.numLidarVerts * 16 * 3;
 }
 
 int launchConstruct(const DevState &s, const SceneDev &sc, const int32_t tc[3], void *stream)
@@ -4490,7 +4483,7 @@ int launchVisibility(const DevState &s, const SceneDev &sc, void *stream)
 int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
 {
     const int blocks = (int)((s.A + kObsBlock - 1) / kObsBlock);
-    hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, s, sc);
+    hipLaunchKernelGGL(k_obs<false>, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, s, sc, WireObs {});
     return check(hipGetLastError());
 }
 
@@ -4505,7 +4498,7 @@ int launchSetOutTab(OutTab *dev, const OutTab &v, void *stream)
 int launchObservationsWire(const DevState &view, const SceneDev &sc, const WireObs &wo, void *stream)
 {
     const int blocks = (int)((view.A + kObsBlock - 1) / kObsBlock);
-    hipLaunchKernelGGL(k_obs_wire, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, view, sc, wo);
+    hipLaunchKernelGGL(k_obs<true>, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, view, sc, wo);
     return check(hipGetLastError());
 }
 

@@ -536,6 +536,8 @@ static void buildSceneDev(mpenv_manager &m)
     if (s.nodes.size() > 256) throw std::runtime_error("BVH has more than 256 nodes (byte-stack limit)");
     if (s.maxStack > kMaxBVHStack || s.maxStackAnyOrder > kMaxBVHStack)
         throw std::runtime_error("BVH too deep for the 16-entry register stack");
+    if (s.lidarNodes.size() > 256) throw std::runtime_error("lidar BVH has more than 256 nodes (byte-stack limit)");
+    if (s.lidarMaxStack > kMaxBVHStack) throw std::runtime_error("lidar BVH too deep for the 16-entry register stack");
     if (s.zoneAABBs.empty() || s.zoneAABBs.size() > (size_t)kMaxZones) throw std::runtime_error("bad zone count");
     if (s.numDefaultASpawns == 0 || s.numDefaultBSpawns == 0) throw std::runtime_error("scene needs A and B spawns");
     if ((m.cfg.sim_flags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) &&
@@ -546,10 +548,16 @@ static void buildSceneDev(mpenv_manager &m)
     BVHNode *d_nodes = m.alloc<BVHNode>(s.nodes.size());
     m.upload(d_nodes, s.nodes.data(), sizeof(BVHNode) * s.nodes.size());
     {
-        const std::vector<BVHNode> oct = octantNodeImages(s.nodes);
+        // k_lidar: octant images of the lidar tree and its triangles
+        const std::vector<BVHNode> oct = octantNodeImages(s.lidarNodes);
         BVHNode *d_oct = m.alloc<BVHNode>(oct.size());
         m.upload(d_oct, oct.data(), sizeof(BVHNode) * oct.size());
         sc.octNodes = d_oct;
+        float *d_lv = m.alloc<float>(s.lidarVerts.size() * 3);
+        m.upload(d_lv, s.lidarVerts.data(), sizeof(float) * 3 * s.lidarVerts.size());
+        sc.lidarVerts = d_lv;
+        sc.numLidarNodes = (int32_t)s.lidarNodes.size();
+        sc.numLidarVerts = (int32_t)s.lidarVerts.size();
     }
     float *d_verts = m.alloc<float>(s.bvhVerts.size() * 3);
     m.upload(d_verts, s.bvhVerts.data(), sizeof(float) * 3 * s.bvhVerts.size());
@@ -1727,6 +1735,58 @@ int mpenv_scene_quirk_grid(const char *scene_path, int32_t *header_out, uint32_t
 }
 
 // Host-side access to the scene BVH (for the parity oracle and tests).
+int mpenv_scene_bvh_variant(const char *scene_path, const int32_t *opts, int32_t num_opts, void *nodes_out,
+                            int32_t *num_nodes, float *verts_out, int32_t *num_verts, int32_t *max_stack)
+{
+    try {
+        Scene s = loadScene(scene_path);
+        BVHBuildOpts o;
+        if (opts && num_opts > 0) o.maxLeaf = opts[0];
+        if (opts && num_opts > 1) o.bins = opts[1];
+        if (opts && num_opts > 2) o.measure = opts[2];
+        if (opts && num_opts > 3) o.travCost = (float)opts[3] / 100.f;
+        if (opts && num_opts > 4) o.floorWeight = (float)opts[4] / 100.f;
+        Scene t;
+        buildBVH(s.triVerts, t, o);
+        if (num_nodes) {
+            if (nodes_out && *num_nodes >= (int32_t)t.nodes.size())
+                std::memcpy(nodes_out, t.nodes.data(), t.nodes.size() * sizeof(BVHNode));
+            *num_nodes = (int32_t)t.nodes.size();
+        }
+        if (num_verts) {
+            if (verts_out && *num_verts >= (int32_t)t.bvhVerts.size())
+                std::memcpy(verts_out, t.bvhVerts.data(), t.bvhVerts.size() * 12);
+            *num_verts = (int32_t)t.bvhVerts.size();
+        }
+        if (max_stack) *max_stack = std::max(t.maxStack, t.maxStackAnyOrder);
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_IO, e.what());
+    }
+    return MPENV_OK;
+}
+
+int mpenv_scene_lidar_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes, float *verts_out,
+                          int32_t *num_verts, int32_t *max_stack)
+{
+    try {
+        Scene s = loadScene(scene_path);
+        if (num_nodes) {
+            if (nodes_out && *num_nodes >= (int32_t)s.lidarNodes.size())
+                std::memcpy(nodes_out, s.lidarNodes.data(), s.lidarNodes.size() * sizeof(BVHNode));
+            *num_nodes = (int32_t)s.lidarNodes.size();
+        }
+        if (num_verts) {
+            if (verts_out && *num_verts >= (int32_t)s.lidarVerts.size())
+                std::memcpy(verts_out, s.lidarVerts.data(), s.lidarVerts.size() * 12);
+            *num_verts = (int32_t)s.lidarVerts.size();
+        }
+        if (max_stack) *max_stack = s.lidarMaxStack;
+    } catch (const std::exception &e) {
+        return fail(MPENV_ERR_IO, e.what());
+    }
+    return MPENV_OK;
+}
+
 int mpenv_scene_bvh(const char *scene_path, void *nodes_out, int32_t *num_nodes, float *verts_out,
                     int32_t *num_verts, int32_t *max_stack)
 {

@@ -49,6 +49,14 @@ struct Box {
         for (int i = 0; i < 3; i++) d[i] = std::max(0.0, hi[i] - lo[i]);
         return 2.0 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
     }
+    // BVHBuildOpts::measure
+    double measure(int m, double floor_w) const
+    {
+        if (m == 0) return area();
+        double d[3];
+        for (int i = 0; i < 3; i++) d[i] = std::max(0.0, hi[i] - lo[i]);
+        return (d[0] + d[1]) * d[2] + floor_w * d[0] * d[1];
+    }
 };
 
 struct BNode {            // binary build node
@@ -62,12 +70,16 @@ struct Builder {
     std::vector<Box> triBox;
     std::vector<Vec3> centroid;
     std::vector<BNode> bnodes;
+    BVHBuildOpts o;
     int maxLeaf = 2;
 
-    explicit Builder(const std::vector<Vec3> &verts) : v(verts)
+    Builder(const std::vector<Vec3> &verts, const BVHBuildOpts &opts) : v(verts), o(opts)
     {
-        if (const char *e = std::getenv("MPENV_BVH_LEAF")) maxLeaf = std::max(1, std::min(2, std::atoi(e)));
+        maxLeaf = std::max(1, std::min(2, o.maxLeaf));
     }
+
+    double meas(const Box &b) const { return b.measure(o.measure, o.floorWeight); }
+    static double cen(const Vec3 &c, int ax) { return ax == 0 ? c.x : (ax == 1 ? c.y : c.z); }
 
     int build(std::vector<int> tris)
     {
@@ -82,20 +94,44 @@ struct Builder {
             return id;
         }
 
-        // Binned SAH over centroids (16 bins per axis), traversal cost 4,
-        // intersection cost 1 (mesh_bvh_builder.cpp:347-348).
+        // SAH over centroids, intersection cost 1, traversal cost
+        // o.travCost (4: mesh_bvh_builder.cpp:347-348), under o.measure:
+        // binned (o.bins per axis) or a full sweep over sorted centroids.
         Box cbox; cbox.reset();
         for (int t : tris) {
             Box b; b.lo[0] = b.hi[0] = centroid[t].x; b.lo[1] = b.hi[1] = centroid[t].y;
             b.lo[2] = b.hi[2] = centroid[t].z; cbox.grow(b);
         }
-        const int kBins = 16;
         double best_cost = 1e300;
         int best_axis = -1, best_split = -1;
+        std::vector<int> lt, rt;
+        if (o.bins <= 0) {
+            // full sweep: split after position s of the centroid order
+            std::vector<int> order;
+            const int n = (int)tris.size();
+            std::vector<double> right(n + 1);
+            for (int ax = 0; ax < 3; ax++) {
+                std::vector<int> ord = tris;
+                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cen(centroid[a], ax) < cen(centroid[b], ax); });
+                Box acc; acc.reset();
+                for (int i = n - 1; i >= 1; i--) { acc.grow(triBox[ord[i]]); right[i] = meas(acc); }
+                acc.reset();
+                for (int i = 0; i + 1 < n; i++) {
+                    acc.grow(triBox[ord[i]]);
+                    const double cost = o.travCost * meas(node.box) + meas(acc) * (i + 1) + right[i + 1] * (n - i - 1);
+                    if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = i + 1; order = ord; }
+                }
+            }
+            if (best_axis >= 0) {
+                lt.assign(order.begin(), order.begin() + best_split);
+                rt.assign(order.begin() + best_split, order.end());
+            }
+        } else {
+        const int kBins = std::min(64, o.bins);
         for (int ax = 0; ax < 3; ax++) {
             double ext = cbox.hi[ax] - cbox.lo[ax];
             if (ext <= 0.0) continue;
-            Box bins[kBins]; int cnt[kBins];
+            Box bins[64]; int cnt[64];
             for (int b = 0; b < kBins; b++) { bins[b].reset(); cnt[b] = 0; }
             for (int t : tris) {
                 double c = ax == 0 ? centroid[t].x : (ax == 1 ? centroid[t].y : centroid[t].z);
@@ -107,13 +143,20 @@ struct Builder {
                 for (int b = 0; b < s; b++) { if (cnt[b]) { l.grow(bins[b]); nl += cnt[b]; } }
                 for (int b = s; b < kBins; b++) { if (cnt[b]) { r.grow(bins[b]); nr += cnt[b]; } }
                 if (nl == 0 || nr == 0) continue;
-                double cost = 4.0 * node.box.area() + l.area() * nl + r.area() * nr;
+                double cost = o.travCost * meas(node.box) + meas(l) * nl + meas(r) * nr;
                 if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = s; }
             }
         }
+        }
 
-        std::vector<int> lt, rt;
-        if (best_axis >= 0) {
+        if (o.bins <= 0) {
+            if (best_axis < 0) { // degenerate centroids: median split by index
+                size_t h = tris.size() / 2;
+                lt.assign(tris.begin(), tris.begin() + h);
+                rt.assign(tris.begin() + h, tris.end());
+            }
+        } else if (best_axis >= 0) {
+            const int kBins = std::min(64, o.bins);
             double ext = cbox.hi[best_axis] - cbox.lo[best_axis];
             for (int t : tris) {
                 double c = best_axis == 0 ? centroid[t].x : (best_axis == 1 ? centroid[t].y : centroid[t].z);
@@ -140,7 +183,7 @@ struct WNode { // 4-wide node before quantisation
 
 } // namespace
 
-void buildBVH(const std::vector<Vec3> &tri_verts, Scene &out)
+void buildBVH(const std::vector<Vec3> &tri_verts, Scene &out, const BVHBuildOpts &opts)
 {
     const int num_tris = (int)(tri_verts.size() / 3);
     out.nodes.clear();
@@ -149,7 +192,7 @@ void buildBVH(const std::vector<Vec3> &tri_verts, Scene &out)
         throw std::runtime_error("mpenv: scene has no collision triangles");
     }
 
-    Builder b(tri_verts);
+    Builder b(tri_verts, opts);
     b.triBox.resize(num_tris);
     b.centroid.resize(num_tris);
     for (int t = 0; t < num_tris; t++) {
@@ -188,7 +231,7 @@ void buildBVH(const std::vector<Vec3> &tri_verts, Scene &out)
             int best = -1; double best_area = -1;
             for (int i = 0; i < (int)kids.size(); i++) {
                 if (isLeaf(kids[i])) continue;
-                double a = b.bnodes[kids[i]].box.area();
+                double a = b.meas(b.bnodes[kids[i]].box);
                 if (a > best_area) { best_area = a; best = i; }
             }
             if (best < 0) break;
@@ -495,6 +538,13 @@ Scene loadScene(const std::string &dir, bool spawn_in_middle)
     }
 
     buildBVH(s.triVerts, s);
+    {
+        Scene t;
+        buildBVH(s.triVerts, t, lidarBVHOpts());
+        s.lidarNodes = std::move(t.nodes);
+        s.lidarVerts = std::move(t.bvhVerts);
+        s.lidarMaxStack = std::max(t.maxStack, t.maxStackAnyOrder);
+    }
 
     // ---- navmesh.bin (map_importer.cpp:421-506)
     {

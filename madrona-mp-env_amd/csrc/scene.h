@@ -80,6 +80,15 @@ struct Scene {
     int32_t maxStack = 0;      // bound on traversal stack occupancy (reference order)
     int32_t maxStackAnyOrder = 0; // bound for any child push order
 
+    // k_lidar's own tree over the same triangles (kLidarBVHOpts): closest
+    // hits do not depend on the tree (up to ties between coplanar
+    // overlapping triangles, DESIGN.md §2 definition 12), so pvpLidar walks
+    // the tree that suits its near-horizontal fans while every other query
+    // (sphere casts, line of sight, shots) keeps the collision tree above.
+    std::vector<BVHNode> lidarNodes;
+    std::vector<mp::Vec3> lidarVerts;
+    int32_t lidarMaxStack = 0; // any push order
+
     std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
     uint32_t numDefaultASpawns = 0, numDefaultBSpawns = 0;
 
@@ -103,8 +112,38 @@ Scene loadScene(const std::string &scene_dir, bool spawn_in_middle = false);
 // Dedups, triangulates and links the navmesh and builds/reads its A* table.
 void buildNavMesh(Scene &s, const std::string &navmesh_path);
 
+// Builder options.  The defaults are the collision tree every query but
+// the lidar uses: 16-bin SAH over centroids (surface area, traversal cost 4,
+// mesh_bvh_builder.cpp:347-348), leaves of <= 2 triangles, the binary tree
+// collapsed to 4-wide by opening the largest child.
+struct BVHBuildOpts {
+    int maxLeaf = 2;        // 1 or 2 (the traversals unroll a 2-triangle leaf)
+    int bins = 16;          // 0: full sweep (every centroid split on every axis)
+    int measure = 0;        // 0: surface area; 1: lidar-weighted (below)
+    float travCost = 4.f;   // SAH cost of an inner node relative to one triangle test
+    float floorWeight = 0.f; // measure 1: weight of the horizontal (xy) face
+};
+// measure 1: the mean area a box shows to near-horizontal rays, (2/pi)
+// (dx + dy) dz for uniformly distributed horizontal directions (the constant
+// drops out of the SAH comparison), plus floorWeight * dx dy for the rays
+// the aim pitch tilts -- what pvpLidar's fans (sim.cpp:3324-3506) see.
+
+// The lidar tree's build (round 6, tools/trav_stats.cpp TRAV_TREES: the
+// lockstep model of k_lidar's waves over recorded lidar fans):
+// 12-bin SAH under the lidar measure with a 0.1 floor weight.
+inline BVHBuildOpts lidarBVHOpts()
+{
+    BVHBuildOpts o;
+    o.maxLeaf = 2;
+    o.bins = 12;
+    o.measure = 1;
+    o.travCost = 4.f;
+    o.floorWeight = 0.1f;
+    return o;
+}
+
 // Builds the compressed 4-wide BVH over de-indexed triangles.
-void buildBVH(const std::vector<mp::Vec3> &tri_verts, Scene &out);
+void buildBVH(const std::vector<mp::Vec3> &tri_verts, Scene &out, const BVHBuildOpts &opts = BVHBuildOpts {});
 
 // Octant node images for closest-hit rays (k_lidar): 8 copies of the node
 // array, copy o for rays whose direction sign bits are o (bit 0 x, bit 1 y,

@@ -246,6 +246,10 @@ struct Oracle {
     // visited k-th (octantOrder()).
     int lidarOrder = 0;
     std::vector<int8_t> octOrder; // [8][numNodes][4]
+    // pvpLidar's tree (cfg.lidar_bvh_*): the octant and lex rules walk it
+    std::vector<Node> lidarNodes;
+    std::vector<Vec3> lidarVerts;
+    std::vector<int8_t> lidarOctOrder;
     int numNavTris = 0;
     std::vector<Vec3> verts;
     std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
@@ -388,8 +392,13 @@ constexpr float kBoxSlackRel = 1.52587890625e-5f, kBoxSlackAbs = 0.00390625f;
 inline bool lexLess(float a, float b) { return (int32_t)f2u(a) < (int32_t)f2u(b); }
 
 bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_max = kFltMax, bool octant = false,
-                 bool lex = false)
+                 bool lex = false, bool lidar_tree = false)
 {
+    // lidar_tree: pvpLidar's own tree (Oracle::lidarNodes), else the
+    // collision tree every other query walks
+    const std::vector<Node> &nodes = lidar_tree ? o.lidarNodes : o.nodes;
+    const std::vector<Vec3> &verts = lidar_tree ? o.lidarVerts : o.verts;
+    const std::vector<int8_t> &octOrder = lidar_tree ? o.lidarOctOrder : o.octOrder;
     // octant: visit each node's child slots in the order octantOrder()
     // defines for the ray's direction signs (the lidar's documented child
     // order); otherwise slot order, as mesh_bvh.inl:160-204.
@@ -406,7 +415,7 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
     if (lex) t_max = t_best * kLexRelax;
     while (sp > 0) {
         int32_t node_idx = stack[--sp];
-        const Node &node = o.nodes[node_idx];
+        const Node &node = nodes[node_idx];
         float rayXInv = copysign_(ray_d.x == 0 ? 1 / diveps : 1 / ray_d.x, ray_d.x);
         float rayYInv = copysign_(ray_d.y == 0 ? 1 / diveps : 1 / ray_d.y, ray_d.y);
         float rayZInv = copysign_(ray_d.z == 0 ? 1 / diveps : 1 / ray_d.z, ray_d.z);
@@ -417,7 +426,7 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
         float originQuantY = (node.minY - ray_o.y) * rayYInv;
         float originQuantZ = (node.minZ - ray_o.z) * rayZInv;
         for (int slot = 0; slot < 4; slot++) {
-            const int i = octant ? o.octOrder[((size_t)oct * o.nodes.size() + node_idx) * 4 + slot] : slot;
+            const int i = octant ? octOrder[((size_t)oct * nodes.size() + node_idx) * 4 + slot] : slot;
             if (node.children[i] == -1) continue;
             // q * dirQuant + originQuant, fused: the reference's GPU build is
             // compiled with NVRTC's default --fmad=true, which contracts it
@@ -438,8 +447,8 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
                         for (int k = 0; k < node.triSize[i]; k++) {
                             const int tri = leaf_idx + k;
                             float t = 0.f;
-                            if (rayTriangleIntersection(o.verts[tri * 3 + 0], o.verts[tri * 3 + 1],
-                                                        o.verts[tri * 3 + 2], tx, ray_o, t_max, &t) &&
+                            if (rayTriangleIntersection(verts[tri * 3 + 0], verts[tri * 3 + 1],
+                                                        verts[tri * 3 + 2], tx, ray_o, t_max, &t) &&
                                 lexLess(t, t_best)) {
                                 t_best = t;
                                 ray_hit = true;
@@ -453,9 +462,9 @@ bool bvhTraceRay(const Oracle &o, Vec3 ray_o, Vec3 ray_d, float *t_hit, float t_
                     float hit_t = 0.f;
                     float leaf_tmax = t_max;
                     for (int k = 0; k < node.triSize[i]; k++) {
-                        Vec3 a = o.verts[(leaf_idx + k) * 3 + 0];
-                        Vec3 b = o.verts[(leaf_idx + k) * 3 + 1];
-                        Vec3 c = o.verts[(leaf_idx + k) * 3 + 2];
+                        Vec3 a = verts[(leaf_idx + k) * 3 + 0];
+                        Vec3 b = verts[(leaf_idx + k) * 3 + 1];
+                        Vec3 c = verts[(leaf_idx + k) * 3 + 2];
                         if (rayTriangleIntersection(a, b, c, tx, ray_o, leaf_tmax, &hit_t)) {
                             hit_tri = true;
                             leaf_tmax = hit_t;
@@ -663,7 +672,10 @@ HitResult traceRayAgainstWorld(const Oracle &o, int w, Vec3 org, Vec3 d, int ord
 {
     float min_hit_t = kFltMax;
     float t_bvh;
-    bool hit = bvhTraceRay(o, org, d, &t_bvh, kFltMax, order == kLidarOctant, order == kLidarLex);
+    // the octant and lex rules are pvpLidar's: they walk its tree (the
+    // product's k_lidar does); the slot rule, the reference's order, walks
+    // the collision tree (the reference has one tree)
+    bool hit = bvhTraceRay(o, org, d, &t_bvh, kFltMax, order == kLidarOctant, order == kLidarLex, order != kLidarSlot);
     if (hit) min_hit_t = t_bvh;
     int hit_entity = -1;
     for (int j = 0; j < o.N; j++) {
@@ -3277,6 +3289,19 @@ void *oracle_create(const oracle_config *cfg)
         if (o->simFlags & MPENV_SIMFLAG_SPAWN_IN_MIDDLE) addMiddleSpawnCells(*o);
         o->lidarOrder = cfg->lidar_octant_order;
         o->octOrder = octantOrder(o->nodes);
+        if (cfg->lidar_bvh_nodes && cfg->num_lidar_nodes > 0) {
+            o->lidarNodes.resize(cfg->num_lidar_nodes);
+            std::memcpy(o->lidarNodes.data(), cfg->lidar_bvh_nodes, sizeof(Node) * cfg->num_lidar_nodes);
+            o->lidarVerts.resize(cfg->num_lidar_bvh_verts);
+            for (int i = 0; i < cfg->num_lidar_bvh_verts; i++)
+                o->lidarVerts[i] = v3(cfg->lidar_bvh_verts[3 * i], cfg->lidar_bvh_verts[3 * i + 1],
+                                      cfg->lidar_bvh_verts[3 * i + 2]);
+            o->lidarOctOrder = octantOrder(o->lidarNodes);
+        } else {
+            o->lidarNodes = o->nodes;
+            o->lidarVerts = o->verts;
+            o->lidarOctOrder = o->octOrder;
+        }
         {
             // bots' navmesh and A* table, built here from navmesh.bin
             NavBuild nb = navFromFile(o->scenePath + "/navmesh.bin");
@@ -3602,7 +3627,8 @@ void oracle_trace_ray_batch(void *h, int32_t n, const float *org, const float *d
             t_out[k] = tb;
             continue;
         }
-        hit_out[k] = bvhTraceRay(o, ro, rd, &t, kFltMax, order == kLidarOctant, order == kLidarLex) ? 1 : 0;
+        hit_out[k] = bvhTraceRay(o, ro, rd, &t, kFltMax, order == kLidarOctant, order == kLidarLex,
+                                 order != kLidarSlot) ? 1 : 0;
         t_out[k] = t;
     }
 }

@@ -39,6 +39,14 @@ typedef struct oracle_config {
      * rule the product's k_lidar follows (DESIGN.md §2 definition 12);
      * closest hits differ only between near-coplanar overlapping triangles. */
     int32_t lidar_octant_order;
+    /* pvpLidar's tree (the product's mpenv_scene_lidar_bvh, same format),
+     * walked by the octant and lex rules; null = the collision tree above.
+     * The slot rule (the reference's order) keeps the collision tree, the
+     * reference's only tree. */
+    const void *lidar_bvh_nodes;
+    int32_t num_lidar_nodes;
+    const float *lidar_bvh_verts;
+    int32_t num_lidar_bvh_verts;
 } oracle_config;
 
 void *oracle_create(const oracle_config *cfg);

@@ -83,6 +83,8 @@ class OracleConfig(C.Structure):
         ("scene_path", C.c_char_p), ("bvh_nodes", C.c_void_p), ("num_nodes", C.c_int32),
         ("bvh_verts", C.c_void_p), ("num_bvh_verts", C.c_int32),
         ("task_type", C.c_int32), ("train_flank", C.c_int32), ("lidar_octant_order", C.c_int32),
+        ("lidar_bvh_nodes", C.c_void_p), ("num_lidar_nodes", C.c_int32),
+        ("lidar_bvh_verts", C.c_void_p), ("num_lidar_bvh_verts", C.c_int32),
     ]
 
 
@@ -206,15 +208,18 @@ def scene_navmesh(scene=SCENE):
     return tv, adj, astar
 
 
-def scene_bvh(scene=SCENE):
+def scene_bvh(scene=SCENE, lidar=False):
+    """The collision tree, or (lidar=True) k_lidar's own tree."""
     lib = lib_mpenv()
+    fn = lib.mpenv_scene_lidar_bvh if lidar else lib.mpenv_scene_bvh
+    fn.argtypes = [C.c_char_p, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p, C.POINTER(C.c_int32),
+                   C.POINTER(C.c_int32)]
     nn, nv, ms = C.c_int32(0), C.c_int32(0), C.c_int32(0)
-    rc = lib.mpenv_scene_bvh(scene.encode(), None, C.byref(nn), None, C.byref(nv), C.byref(ms))
+    rc = fn(scene.encode(), None, C.byref(nn), None, C.byref(nv), C.byref(ms))
     assert rc == 0, lib.mpenv_last_error()
     nodes = np.zeros(nn.value * 64, dtype=np.uint8)
     verts = np.zeros(nv.value * 3, dtype=np.float32)
-    rc = lib.mpenv_scene_bvh(scene.encode(), nodes.ctypes.data, C.byref(nn), verts.ctypes.data,
-                             C.byref(nv), C.byref(ms))
+    rc = fn(scene.encode(), nodes.ctypes.data, C.byref(nn), verts.ctypes.data, C.byref(nv), C.byref(ms))
     assert rc == 0, lib.mpenv_last_error()
     return nodes, verts, ms.value
 
@@ -295,10 +300,13 @@ class Oracle:
                  lidar_order="octant"):
         self.lib = lib_oracle()
         self.nodes, self.verts, _ = scene_bvh(scene)
+        self.lnodes, self.lverts, _ = scene_bvh(scene, lidar=True)  # k_lidar's own tree
         cfg = OracleConfig(num_worlds, rand_seed, int(auto_reset), sim_flags, team_size,
                            world_id_offset, scene.encode(), self.nodes.ctypes.data,
                            len(self.nodes) // 64, self.verts.ctypes.data, len(self.verts) // 3, task,
-                           int(flank), {"slot": 0, "octant": 1, "lex": 2}[lidar_order])
+                           int(flank), {"slot": 0, "octant": 1, "lex": 2}[lidar_order],
+                           self.lnodes.ctypes.data, len(self.lnodes) // 64, self.lverts.ctypes.data,
+                           len(self.lverts) // 3)
         self.h = self.lib.oracle_create(C.byref(cfg))
         assert self.h, "oracle_create failed"
         if curriculum:

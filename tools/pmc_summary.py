@@ -36,7 +36,9 @@ VALU_PEAK = 256 * 4 * 0.5 * 2.4e9  # wave-instructions per second
 
 
 def short(name):
-    return name.split("(")[0].replace("mpenv::", "")
+    n = name.split("(")[0].replace("mpenv::", "").replace("void ", "").strip()
+    # the templated observation kernel: the step's and the learner's
+    return {"k_obs<false>": "k_obs", "k_obs<true>": "k_obs_wire"}.get(n, n)
 
 
 def counters(path):

@@ -1,7 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-T=${TAG:-r06b}
+T=${TAG:-r06c}
 timeout -k 10 900 python -u -m pytest tests/test_wire_gpu.py tests/test_exchange_gpu.py "tests/test_parity_gpu.py::test_gpu_stream_step_buffers_abi" "tests/test_parity_gpu.py::test_jax_custom_call_targets_match_gpu_stream_step" -x -v --timeout 500 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1
 rc=$?
 tail -15 gpurun_out/${T}_tests.log

@@ -3,6 +3,8 @@
 // ray for the reference child order and for front-to-back order.
 //
 //   trav_stats SCENE_DIR RAYS.f32   (RAYS: n x 6 floats, origin + direction)
+//   TRAV_TREES=1 trav_stats SCENE_DIR RAYS.f32
+//       k_lidar's lockstep cost on candidate trees (treesMain)
 //   TRAV_HINT=PREV.f32 trav_stats SCENE_DIR RAYS.f32
 //       temporal-hint model: PREV holds the same ray slots one step earlier
 //       (tools/dump_lidar_rays.py at step s - 1); each ray first tests the
@@ -14,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "mpenv.h"
@@ -785,6 +788,190 @@ static int pairMain(const std::vector<float> &rays)
     return 0;
 }
 
+// ---- TRAV_TREES: k_lidar's traversal, modelled exactly, over candidate
+// trees (mpenv_scene_bvh_variant).  Per node and ray octant the slot order
+// of scene.h octantNodeImages (leaves by ascending key, then internal
+// children by descending key -- the nearest popped first -- then empty
+// slots); a popped node tests its slots in that order against the lane's
+// t_max, a passing leaf runs its triangle tests (slot k's unrolled pair), a
+// passing internal child is pushed.  Lockstep per 64-lane wave (k_lidar's
+// waves: one agent's 64 forward rays, or 4 agents' 16 rear rays): node
+// iterations = the longest lane's pops; triangle iterations = per iteration
+// and slot, the most tests any lane runs there.  Weighted cost = 110 VALU
+// per node iteration + 45 per triangle iteration (DESIGN.md §4 model).
+struct KM {
+    double waves = 0, nodeIters = 0, triIters = 0, pops = 0, tris = 0, wrong = 0;
+};
+
+static void kernelModel(const std::vector<Node> &nd, const std::vector<float> &vt, const std::vector<float> &rays,
+                        bool fwd_waves, KM &km, const std::vector<float> *ref_t = nullptr, std::vector<float> *out_t = nullptr)
+{
+    const size_t n = rays.size() / 6;
+    // octant slot orders
+    std::vector<std::array<std::array<int, 4>, 8>> ord(nd.size());
+    for (size_t ni = 0; ni < nd.size(); ni++) {
+        const Node &x = nd[ni];
+        for (int oct = 0; oct < 8; oct++) {
+            const double sgn[3] = { (oct & 1) ? -1.0 : 1.0, (oct & 2) ? -1.0 : 1.0, (oct & 4) ? -1.0 : 1.0 };
+            double key[4];
+            const int8_t ex[3] = { x.expX, x.expY, x.expZ };
+            const float mn[3] = { x.minX, x.minY, x.minZ };
+            const uint8_t *qlo[3] = { x.qMinX, x.qMinY, x.qMinZ }, *qhi[3] = { x.qMaxX, x.qMaxY, x.qMaxZ };
+            for (int i = 0; i < 4; i++) {
+                key[i] = 0;
+                for (int a = 0; a < 3; a++)
+                    key[i] += sgn[a] * ((double)mn[a] + std::ldexp(0.5 * ((double)qlo[a][i] + (double)qhi[a][i]), ex[a]));
+            }
+            std::vector<int> lv, in, em;
+            for (int i = 0; i < 4; i++) {
+                if (x.children[i] == -1) em.push_back(i);
+                else if (x.children[i] & 0x80000000) lv.push_back(i);
+                else in.push_back(i);
+            }
+            std::stable_sort(lv.begin(), lv.end(), [&](int a, int b) { return key[a] < key[b]; });
+            std::stable_sort(in.begin(), in.end(), [&](int a, int b) { return key[a] > key[b]; });
+            std::vector<int> o = lv;
+            o.insert(o.end(), in.begin(), in.end());
+            o.insert(o.end(), em.begin(), em.end());
+            for (int k = 0; k < 4; k++) ord[ni][oct][k] = o[k];
+        }
+    }
+    for (size_t w0 = 0; w0 + 64 <= n; w0 += 64) {
+        const bool fwd = ((w0 / 64) % 5) != 4;
+        if (fwd != fwd_waves) continue;
+        km.waves++;
+        std::vector<std::vector<std::array<int, 4>>> lanes(64);
+        size_t mp = 0;
+        for (int l = 0; l < 64; l++) {
+            const float *o = &rays[6 * (w0 + l)], *d = o + 3;
+            const int oct = (d[0] < 0 ? 1 : 0) | (d[1] < 0 ? 2 : 0) | (d[2] < 0 ? 4 : 0);
+            float inv[3];
+            for (int k = 0; k < 3; k++) inv[k] = d[k] == 0 ? 1e7f : 1.f / d[k];
+            float tmax = 3.4e38f;
+            std::vector<int> st = { 0 };
+            while (!st.empty()) {
+                const int ni = st.back();
+                st.pop_back();
+                km.pops++;
+                lanes[l].push_back({ 0, 0, 0, 0 });
+                const Node &x = nd[ni];
+                const float sx = std::ldexp(1.f, x.expX), sy = std::ldexp(1.f, x.expY), sz = std::ldexp(1.f, x.expZ);
+                for (int k = 0; k < 4; k++) {
+                    const int i = ord[ni][oct][k];
+                    if (x.children[i] == -1) continue;
+                    const float lo[3] = { x.minX + sx * x.qMinX[i], x.minY + sy * x.qMinY[i], x.minZ + sz * x.qMinZ[i] };
+                    const float hi[3] = { x.minX + sx * x.qMaxX[i], x.minY + sy * x.qMaxY[i], x.minZ + sz * x.qMaxZ[i] };
+                    float tn = 0, tf = tmax;
+                    for (int a = 0; a < 3; a++) {
+                        const float p = (lo[a] - o[a]) * inv[a], q = (hi[a] - o[a]) * inv[a];
+                        tn = std::max(tn, std::min(p, q));
+                        tf = std::min(tf, std::max(p, q));
+                    }
+                    if (tn > tf) continue;
+                    if (x.children[i] & 0x80000000) {
+                        const int leaf = x.children[i] & 0x7fffffff;
+                        for (int q = 0; q < x.triSize[i]; q++) {
+                            lanes[l].back()[k]++;
+                            km.tris++;
+                            float th;
+                            if (tri(&vt[(leaf + q) * 9], o, d, tmax, th)) tmax = th;
+                        }
+                    } else {
+                        st.push_back(x.children[i]);
+                    }
+                }
+            }
+            mp = std::max(mp, lanes[l].size());
+            if (out_t) (*out_t)[w0 + l] = tmax;
+            if (ref_t && (*ref_t)[w0 + l] != tmax) {
+                const float a = (*ref_t)[w0 + l];
+                if (std::fabs(a - tmax) > 1e-4f * std::max(1.f, std::fabs(a))) km.wrong++;
+            }
+        }
+        km.nodeIters += mp;
+        for (size_t it = 0; it < mp; it++)
+            for (int k = 0; k < 4; k++) {
+                int m = 0;
+                for (auto &L : lanes)
+                    if (it < L.size()) m = std::max(m, L[it][k]);
+                km.triIters += m;
+            }
+    }
+}
+
+static int treesMain(const char *scene, const std::vector<float> &rays)
+{
+    struct V { const char *name; std::vector<int32_t> o; };
+    const std::vector<V> vs = {
+        { "product: SAH 16 bins, leaf 2", { 2, 16, 0, 400, 0 } },
+        { "SAH 16 bins, leaf 1", { 1, 16, 0, 400, 0 } },
+        { "SAH full sweep, leaf 2", { 2, 0, 0, 400, 0 } },
+        { "SAH full sweep, leaf 1", { 1, 0, 0, 400, 0 } },
+        { "SAH full sweep, leaf 2, trav 1", { 2, 0, 0, 100, 0 } },
+        { "SAH full sweep, leaf 2, trav 2", { 2, 0, 0, 200, 0 } },
+        { "SAH full sweep, leaf 2, trav 8", { 2, 0, 0, 800, 0 } },
+        { "lidar measure, 16 bins, leaf 2", { 2, 16, 1, 400, 0 } },
+        { "lidar measure, full sweep, leaf 2", { 2, 0, 1, 400, 0 } },
+        { "lidar measure, full sweep, leaf 1", { 1, 0, 1, 400, 0 } },
+        { "lidar measure + 0.05 floor, full sweep, leaf 2", { 2, 0, 1, 400, 5 } },
+        { "lidar measure + 0.2 floor, full sweep, leaf 2", { 2, 0, 1, 400, 20 } },
+        { "lidar measure + 0.2 floor, full sweep, leaf 1", { 1, 0, 1, 400, 20 } },
+        { "lidar measure, full sweep, leaf 2, trav 2", { 2, 0, 1, 200, 0 } },
+        { "lidar measure, full sweep, leaf 2, trav 8", { 2, 0, 1, 800, 0 } },
+    };
+    std::vector<V> custom;
+    if (const char *e = getenv("TRAV_OPTS")) { // "a,b,c,d,e|a,b,..." (mpenv_scene_bvh_variant opts)
+        static std::vector<std::string> names;
+        std::string all = e;
+        size_t p = 0;
+        custom.push_back(vs[0]);
+        while (p <= all.size()) {
+            size_t q = all.find('|', p);
+            if (q == std::string::npos) q = all.size();
+            std::string one = all.substr(p, q - p);
+            if (!one.empty()) {
+                V v;
+                names.push_back(one);
+                size_t a = 0;
+                while (a <= one.size()) {
+                    size_t b = one.find(',', a);
+                    if (b == std::string::npos) b = one.size();
+                    v.o.push_back(std::atoi(one.substr(a, b - a).c_str()));
+                    a = b + 1;
+                }
+                custom.push_back(v);
+            }
+            p = q + 1;
+        }
+        for (size_t i = 1; i < custom.size(); i++) custom[i].name = names[i - 1].c_str();
+    }
+    const std::vector<V> &list = custom.empty() ? vs : custom;
+    std::vector<float> ref_t(rays.size() / 6);
+    double base = 0;
+    for (size_t vi = 0; vi < list.size(); vi++) {
+        const V &cv = list[vi];
+        int32_t nn = 0, nv = 0, ms = 0;
+        if (mpenv_scene_bvh_variant(scene, cv.o.data(), (int32_t)cv.o.size(), nullptr, &nn, nullptr, &nv, &ms))
+            return 1;
+        std::vector<Node> nd(nn);
+        std::vector<float> vt((size_t)nv * 3);
+        mpenv_scene_bvh_variant(scene, cv.o.data(), (int32_t)cv.o.size(), nd.data(), &nn, vt.data(), &nv, &ms);
+        KM f, r;
+        kernelModel(nd, vt, rays, true, f, vi ? &ref_t : nullptr, vi ? nullptr : &ref_t);
+        kernelModel(nd, vt, rays, false, r, vi ? &ref_t : nullptr, vi ? nullptr : &ref_t);
+        const double units = f.waves / 4;
+        const double cost = (110 * (f.nodeIters + r.nodeIters) + 45 * (f.triIters + r.triIters)) / units;
+        if (vi == 0) base = cost;
+        printf("%-48s nodes %3d stack %2d | fwd wave: node it %5.2f tri it %5.2f | rear wave: %5.2f / %5.2f | "
+               "lane pops/ray %.2f tris/ray %.2f | cost/unit %6.0f (%+.1f%%)%s\n",
+               cv.name, nn, ms, f.nodeIters / f.waves, f.triIters / f.waves, r.nodeIters / r.waves,
+               r.triIters / r.waves, (f.pops + r.pops) / (rays.size() / 6), (f.tris + r.tris) / (rays.size() / 6), cost,
+               100.0 * (cost / base - 1), (f.wrong + r.wrong) ? " hits differ" : "");
+        if (f.wrong + r.wrong) printf("    rays whose closest hit differs from the product tree: %.0f of %zu\n", f.wrong + r.wrong, rays.size() / 6);
+    }
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3) {
@@ -802,6 +989,7 @@ int main(int argc, char **argv)
     while (fread(buf, 4, 6, f) == 6) rays.insert(rays.end(), buf, buf + 6);
     fclose(f);
     size_t n = rays.size() / 6;
+    if (getenv("TRAV_TREES")) return treesMain(argv[1], rays);
     {
         double un = 0, ut = 0;
         for (size_t w0 = 0; w0 < n; w0 += 64) {
