@@ -3,7 +3,7 @@ their step kernels on the C3 workload (development tool; variants that
 switch parts of a kernel off give wrong results by design and are never
 used outside this tool).
 
-  python tools/kernel_lab.py build NAME [--patch tools/lab/X.patch ...] [-DFOO=1 ...]
+  python tools/kernel_lab.py build NAME [--patch tools/lab/X.patch ...] [--sub 'FILE:OLD|||NEW' ...] [-DFOO=1 ...]
                                                         (here, cross-compiles)
   python tools/kernel_lab.py run NAME [NAME ...]        (on the GPU box)
 
@@ -96,11 +96,13 @@ def build(name, args):
 
     out = os.path.join(LAB, name)
     os.makedirs(out, exist_ok=True)
-    patches, defines = [], []
+    patches, defines, subs = [], [], []
     it = iter(args)
     for a in it:
         if a == "--patch":
             patches.append(os.path.abspath(next(it)))
+        elif a == "--sub":  # "FILE:OLD|||NEW", a literal text substitution in the lab copy
+            subs.append(next(it))
         else:
             defines.append(a)
     src_dir = os.path.join(out, "src")
@@ -108,6 +110,13 @@ def build(name, args):
     shutil.copytree(B.CSRC, src_dir)
     for pf in patches:
         subprocess.run(["patch", "-s", "-p1", "-d", src_dir, "-i", pf], check=True)
+    for sub in subs:
+        fname, rest = sub.split(":", 1)
+        old, new = rest.split("|||", 1)
+        fp = os.path.join(src_dir, fname)
+        text = open(fp).read()
+        assert old in text, f"--sub: {old!r} not in {fname}"
+        open(fp, "w").write(text.replace(old, new))
     if any(d.startswith(("-DMPENV_LAB_PHASE_T", "-DMPENV_LAB_SIM_SKIP", "-DMPENV_SIM_WPE", "-DMPENV_SIM_BLOCK"))
            for d in defines):
         ksim_hooks(os.path.join(src_dir, "kernels.hip"))
@@ -126,7 +135,7 @@ def build(name, args):
         objs.append(o)
     subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o",
                     os.path.join(out, "libmpenv.so")] + objs, check=True)
-    json.dump({"defines": defines, "patches": [os.path.relpath(p, ROOT) for p in patches]},
+    json.dump({"defines": defines, "patches": [os.path.relpath(p, ROOT) for p in patches], "subs": subs},
               open(os.path.join(out, "variant.json"), "w"))
     print("built", name, defines)
 

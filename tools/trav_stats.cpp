@@ -903,7 +903,8 @@ static int treesMain(const char *scene, const std::vector<float> &rays)
 {
     struct V { const char *name; std::vector<int32_t> o; };
     const std::vector<V> vs = {
-        { "product: SAH 16 bins, leaf 2", { 2, 16, 0, 400, 0 } },
+        { "collision tree: SAH 16 bins, leaf 2", { 2, 16, 0, 400, 0 } },
+        { "product lidar tree (scene.h lidarBVHOpts)", { 2, 12, 1, 400, 10 } },
         { "SAH 16 bins, leaf 1", { 1, 16, 0, 400, 0 } },
         { "SAH full sweep, leaf 2", { 2, 0, 0, 400, 0 } },
         { "SAH full sweep, leaf 1", { 1, 0, 0, 400, 0 } },
