@@ -65,7 +65,7 @@ def main(tag, src):
                 disp[k].append((int(row["Dispatch_Id"]), int(row["Grid_Size_X"]),
                                 int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
     pmc = {}
-    for sub in ("fetch", "write", "sq"):
+    for sub in ("fetch", "write", "sq", "lanes"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if os.path.exists(p):
             pmc.update(counters(p))
@@ -93,6 +93,14 @@ def main(tag, src):
                 r[c.lower()] = int(pmc[c][k])
         if valu:
             r["valu_issue_frac"] = round(valu / (avg * 1e-9) / VALU_PEAK, 4)
+        # active lanes per VALU instruction over the wave size (the
+        # "VALU thread utilisation" of the gfx9 SQ counters)
+        tcv = pmc.get("SQ_THREAD_CYCLES_VALU", {}).get(k)
+        aiv = pmc.get("SQ_ACTIVE_INST_VALU", {}).get(k)
+        if tcv is not None and aiv:
+            r["sq_thread_cycles_valu"] = int(tcv)
+            r["sq_active_inst_valu"] = int(aiv)
+            r["valu_lane_efficiency"] = round(tcv / (aiv * 64), 4)
         out["kernels"][k] = r
     # k_lidar runs as k_lidar_fan (forward fans) + k_lidar_rear (rear fans)
     # on scenes of <= 255 triangles; bench.py times the pair as "k_lidar"
@@ -114,6 +122,8 @@ def main(tag, src):
     traffic = {"tag": tag, "workload": out["workload"], "bench_window": [warm, steps],
                "per_kernel": {k: v.get("hbm_bytes_per_launch") for k, v in ks.items()},
                "valu_insts_per_launch": {k: v.get("sq_insts_valu") for k, v in ks.items()},
+               "lane_efficiency": {k: v.get("valu_lane_efficiency") for k, v in ks.items()
+                                   if v.get("valu_lane_efficiency") is not None},
                "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per whole-batch launch, separate --pmc passes"}
     # one entry per workload (bench.py picks the one it runs)
     path = os.path.join(prof, "pmc_traffic.json")

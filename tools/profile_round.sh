@@ -24,5 +24,12 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv 
     python3 bench.py $PMC_ARGS > $OUT/write_bench.json && \
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d $OUT/sq -o run -- \
-    python3 bench.py $PMC_ARGS > $OUT/sq_bench.json && \
+    python3 bench.py $PMC_ARGS > $OUT/sq_bench.json || exit $?
+# VALU lane utilisation, when gfx950's counter list has the thread-cycle
+# counters (rocprofv3 --list-avail): active lanes per VALU instruction
+timeout -k 10 120 rocprofv3 --list-avail > $OUT/list_avail.txt 2>&1
+if grep -q SQ_THREAD_CYCLES_VALU $OUT/list_avail.txt; then
+    timeout -k 10 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU --kernel-trace --output-format csv \
+        -d $OUT/lanes -o run -- python3 bench.py $PMC_ARGS > $OUT/lanes_bench.json || exit $?
+fi
 find $OUT -name "*.csv"
