@@ -517,13 +517,15 @@ __device__ __forceinline__ int nthSetBitD(uint64_t m, int n)
 }
 
 // The "stuck" fallback's four horizontal casts (sim.cpp:962-984), for the
-// lanes of the wave with `need` set: their 4·k casts are dealt one per lane
-// across the whole wave (rounds of 64) instead of four in a row on the
-// owning lane -- a wave holding one stuck agent runs one cast's time, not
-// four.  Each cast is the same function of the same owner inputs (x,
-// v_norm, low_check shuffled from the owner), so hd4 is bit-identical to
-// the serial loop's.  Called by every lane of a full wave; a partial wave
-// (batch tail) runs the serial loop.
+// lanes of the wave with `need` set: their 4·k casts are dealt one per
+// active lane across the wave (rounds of as many casts as the wave has
+// active lanes) instead of four in a row on the owning lane -- a wave holding
+// one stuck agent runs one cast's time, not four.  Each cast is the same
+// function of the same owner inputs (x, v_norm, low_check shuffled from the
+// owner), so hd4 is bit-identical to the serial loop's.  Called by every
+// active lane of the wave; on small batches k_move runs 8-32 agents per
+// wave (launchMove), and round 6 deals over those lanes too (rounds 4-5 fell
+// back to the serial loop on any partial wave, i.e. always below C3).
 __device__ __forceinline__ void stuckCastsD(const LBVH &bvh, bool need, Vec3 x, Vec3 v_norm, float low_check,
                                             float hd4[4])
 {
@@ -531,22 +533,13 @@ __device__ __forceinline__ void stuckCastsD(const LBVH &bvh, bool need, Vec3 x, 
     const uint64_t act = __ballot(1);
     const uint64_t m = __ballot(need);
     if (m == 0ull) return;
-    if (act != ~0ull) {
-        if (need) {
-            for (int dir = 0; dir < 4; dir++) {
-                const Vec3 dv = rotate2DD(v_norm, (float)dir * 3.14159f * 0.5f);
-                Vec3 ray_o = x - dv * r * 2.0f;
-                ray_o.z += low_check;
-                hd4[dir] = bvhSphereCastD(bvh, ray_o, dv, r).t;
-            }
-        }
-        return;
-    }
+    const int na = __popcll(act);
     const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const int rank = __popcll(m & ((1ull << lane) - 1ull)); // owner's index among the stuck lanes
+    const int arank = __popcll(act & ((1ull << lane) - 1ull)); // this lane's index among the active lanes
+    const int rank = __popcll(m & ((1ull << lane) - 1ull));    // owner's index among the stuck lanes
     const int tasks = 4 * __popcll(m);
-    for (int base = 0; base < tasks; base += 64) {
-        const int t = base + lane;
+    for (int base = 0; base < tasks; base += na) {
+        const int t = base + arank;
         const int owner = nthSetBitD(m, min(t, tasks - 1) >> 2);
         const float ox = __shfl(x.x, owner), oy = __shfl(x.y, owner), oz = __shfl(x.z, owner);
         const float vx = __shfl(v_norm.x, owner), vy = __shfl(v_norm.y, owner), vz = __shfl(v_norm.z, owner);
@@ -561,8 +554,10 @@ __device__ __forceinline__ void stuckCastsD(const LBVH &bvh, bool need, Vec3 x, 
 #pragma unroll
         for (int dir = 0; dir < 4; dir++) {
             const int tt = 4 * rank + dir;
-            const float got = __shfl(hd, tt & 63);
-            if (need && tt >= base && tt < base + 64) hd4[dir] = got;
+            // the active lane that ran task tt this round (any lane when none did)
+            const int src = nthSetBitD(act, min(max(tt - base, 0), na - 1));
+            const float got = __shfl(hd, src);
+            if (need && tt >= base && tt < base + na) hd4[dir] = got;
         }
     }
 }
