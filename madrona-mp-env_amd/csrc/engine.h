@@ -172,7 +172,8 @@ struct DevState {
 // during a gpuStreamStep (mgr.cpp:614-645 copies them from the engine's
 // exports instead).  A device table, so the captured step graph's kernel
 // arguments never change: gpuStreamStep sets it (on = 1, the call's
-// pointers) in front of the step and clears it behind it.
+// pointers) in front of the step and clears it behind it, both from inside
+// its input / output copy launches (CopyBatch::tabDst).
 struct OutTab {
     int32_t on, pad;
     float *masks, *filters, *selfObs, *selfPos, *tmObs, *tmPos, *oppObs, *oppPos, *fwdLidar, *rearLidar;
@@ -181,7 +182,6 @@ struct OutTab {
     // stores that need no loads, issued beside its VALU-bound traversals
     float *agentMap0, *agentMap1;
 };
-int launchSetOutTab(OutTab *dev, const OutTab &v, void *stream);
 
 // Per-step workload counters accumulated by the kernels in stats mode
 // (bench.py's workload window; never on in the timed region).
@@ -239,6 +239,7 @@ struct SceneDev {
     const SceneTables *tab; // device copy of the arrays below (set after scene upload)
     const BVHNode *nodes;
     const BVHNode *octNodes; // [8][numLidarNodes] octant node images of the lidar tree (scene.h octantNodeImages)
+    const BVHNode *lidarNodes; // the lidar tree in slot order (k_vis)
     const float *lidarVerts; // the lidar tree's triangles, 3 floats per vertex (scene.h Scene::lidarVerts)
     int32_t numLidarNodes, numLidarVerts;
     const float *verts;     // 3 floats per vertex, 3 vertices per triangle
@@ -342,6 +343,11 @@ struct CopyBatch {
     CopySeg seg[kMaxCopySegs];
     int n;
     int64_t first[kMaxCopySegs + 1]; // first block of each segment (filled by launchCopyBatch)
+    // gpuStreamStep's out table rides the copy launches: block 0 stores
+    // `tab` to *tabDst (null: nothing), so setting it before the step and
+    // clearing it after costs no launch of its own
+    OutTab *tabDst;
+    OutTab tab;
 };
 int launchCopyBatch(const CopyBatch &b, void *stream);
 

@@ -81,15 +81,20 @@ __device__ __forceinline__ uint32_t bsPop(ByteStack &s)
 // Stage nodes + vertices into dynamic LDS (all threads participate).
 // LDS image: nodes verbatim (64 B each), then every triangle vertex padded
 // to a float4 so a triangle is three ds_read_b128.
-__device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc)
+// lidar = true: the lidar tree (Scene::lidarNodes, slot order), which k_vis
+// walks too (its line-of-sight rays are near-horizontal like the fans; the
+// answer does not depend on the tree, geom_dev.h visibleFullD)
+__device__ __forceinline__ LBVH stageBVH(char *smem, const SceneDev &sc, bool lidar = false)
 {
-    const int node_q = sc.numNodes * 4; // uint4 per node
-    const uint4 *src_n = reinterpret_cast<const uint4 *>(sc.nodes);
+    const int numNodes = lidar ? sc.numLidarNodes : sc.numNodes;
+    const int numVerts = lidar ? sc.numLidarVerts : sc.numVerts;
+    const int node_q = numNodes * 4; // uint4 per node
+    const uint4 *src_n = reinterpret_cast<const uint4 *>(lidar ? sc.lidarNodes : sc.nodes);
     uint4 *dst_n = reinterpret_cast<uint4 *>(smem);
     for (int k = threadIdx.x; k < node_q; k += blockDim.x) dst_n[k] = src_n[k];
-    const float *src_v = sc.verts;
+    const float *src_v = lidar ? sc.lidarVerts : sc.verts;
     float4 *dst_v = reinterpret_cast<float4 *>(smem + (size_t)node_q * 16);
-    for (int k = threadIdx.x; k < sc.numVerts; k += blockDim.x)
+    for (int k = threadIdx.x; k < numVerts; k += blockDim.x)
         dst_v[k] = make_float4(src_v[3 * k], src_v[3 * k + 1], src_v[3 * k + 2], 0.f);
     __syncthreads();
     LBVH b;

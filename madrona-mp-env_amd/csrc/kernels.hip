@@ -3107,7 +3107,7 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
     const int64_t wave = ((int64_t)xcdBlockId() * blockDim.x + threadIdx.x) >> 6;
     const int64_t agent0 = (((int64_t)xcdBlockId() * blockDim.x) >> 6) * apw; // first agent of the block
     const int nsMax = visStageAgents(T, N);
-    float *st = (float *)(smem + (size_t)sc.numNodes * 64 + (size_t)sc.numVerts * 16);
+    float *st = (float *)(smem + (size_t)sc.numLidarNodes * 64 + (size_t)sc.numLidarVerts * 16);
     const int64_t s0 = (agent0 / N) * N;
     {
         const int64_t a_hi = min(S.A, agent0 + (int64_t)(kBlock / 64) * apw);
@@ -3125,7 +3125,7 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
             st[8 * nsMax + k] = S.alive[g];
         }
     }
-    const LBVH bvh = stageBVH(smem, sc); // barrier
+    const LBVH bvh = stageBVH(smem, sc, true); // the lidar tree; barrier
     auto sPos = [&](int64_t g) {
         const int l = (int)(g - s0);
         return v3(st[0 * nsMax + l], st[1 * nsMax + l], st[2 * nsMax + l]);
@@ -3209,7 +3209,7 @@ __global__ void __launch_bounds__(kBlock) k_vis(DevState S, SceneDev sc)
     // again so B2's traversals run in dense waves (a wave of mixed rays
     // otherwise idles all but its few traversing lanes).
     const uint32_t total = nrays;
-    const uint32_t numTris = (uint32_t)(sc.numVerts / 3);
+    const uint32_t numTris = (uint32_t)(sc.numLidarVerts / 3);
     // the occluder hint stores triangle ids as u16 with 0xffff = none: off
     // for scenes of 65,535 triangles or more
     const bool hints = numTris < 0xffffu;
@@ -4471,7 +4471,8 @@ int launchVisibility(const DevState &s, const SceneDev &sc, void *stream)
     const int64_t waves = (s.A + (64 / s.T) - 1) / (64 / s.T);
     const int blocks = (int)((waves * 64 + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_vis, dim3(blocks), dim3(kBlock),
-                       bvhLdsBytes(sc) + (size_t)kVisStageCols * 4 * visStageAgents(s.T, s.N), (hipStream_t)stream, s, sc);
+                       (size_t)sc.numLidarNodes * 64 + (size_t)sc.numLidarVerts * 16 +
+                           (size_t)kVisStageCols * 4 * visStageAgents(s.T, s.N), (hipStream_t)stream, s, sc);
     return check(hipGetLastError());
 }
 
@@ -4479,14 +4480,6 @@ int launchObservations(const DevState &s, const SceneDev &sc, void *stream)
 {
     const int blocks = (int)((s.A + kObsBlock - 1) / kObsBlock);
     hipLaunchKernelGGL(k_obs<false>, dim3(blocks), dim3(kObsBlock), 0, (hipStream_t)stream, s, sc, WireObs {});
-    return check(hipGetLastError());
-}
-
-__global__ void k_set_outtab(OutTab *dev, OutTab v) { *dev = v; }
-
-int launchSetOutTab(OutTab *dev, const OutTab &v, void *stream)
-{
-    hipLaunchKernelGGL(k_set_outtab, dim3(1), dim3(1), 0, (hipStream_t)stream, dev, v);
     return check(hipGetLastError());
 }
 

@@ -553,6 +553,9 @@ static void buildSceneDev(mpenv_manager &m)
         BVHNode *d_oct = m.alloc<BVHNode>(oct.size());
         m.upload(d_oct, oct.data(), sizeof(BVHNode) * oct.size());
         sc.octNodes = d_oct;
+        BVHNode *d_ln = m.alloc<BVHNode>(s.lidarNodes.size());
+        m.upload(d_ln, s.lidarNodes.data(), sizeof(BVHNode) * s.lidarNodes.size());
+        sc.lidarNodes = d_ln;
         float *d_lv = m.alloc<float>(s.lidarVerts.size() * 3);
         m.upload(d_lv, s.lidarVerts.data(), sizeof(float) * 3 * s.lidarVerts.size());
         sc.lidarVerts = d_lv;
@@ -1184,9 +1187,13 @@ static bool directTable(void **buffers, OutTab &t)
 }
 
 static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs, bool outputs, int zeros = -1,
-                  bool skip_direct = false)
+                  bool skip_direct = false, const OutTab *tab = nullptr)
 {
     CopyBatch b {};
+    if (tab) { // the out table rides the first copy launch (engine.h CopyBatch)
+        b.tabDst = m->outTabDev;
+        b.tab = *tab;
+    }
     auto add = [&](const void *src, void *dst, size_t bytes) {
         if (((uintptr_t)src | (uintptr_t)dst) & 15u) {
             if (src) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
@@ -1196,6 +1203,7 @@ static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs,
         if (b.n == kMaxCopySegs) {
             if (launchCopyBatch(b, st)) throw std::runtime_error("copy launch failed");
             b.n = 0;
+            b.tabDst = nullptr;
         }
         b.seg[b.n++] = CopySeg { src, dst, (int64_t)bytes };
     };
@@ -1215,7 +1223,7 @@ static int copyTI(mpenv_manager *m, hipStream_t st, void **buffers, bool inputs,
         m->exportDesc(kTIOutputs[i].id, d);
         add(zero ? nullptr : d.ptr, buffers[k], d.bytes());
     }
-    if (b.n > 0 && launchCopyBatch(b, st)) throw std::runtime_error("copy launch failed");
+    if ((b.n > 0 || b.tabDst) && launchCopyBatch(b, st)) throw std::runtime_error("copy launch failed");
     return 0;
 }
 
@@ -1267,11 +1275,10 @@ int mpenv_gpu_stream_step(mpenv_manager *m, void *stream, void **buffers)
             copyTI(m, m->zStream, buffers, false, true, 1);
             HIP_CHECK(hipEventRecord(m->zJoinEv, m->zStream));
         }
-        copyTI(m, st, buffers, true, false);
-        if (direct && launchSetOutTab(m->outTabDev, tab, st)) throw std::runtime_error("out-table launch failed");
+        const OutTab off {};
+        copyTI(m, st, buffers, true, false, -1, false, direct ? &tab : nullptr); // sets the table
         m->runStep(st);
-        copyTI(m, st, buffers, false, true, direct ? -2 : 0, direct);
-        if (direct && launchSetOutTab(m->outTabDev, OutTab {}, st)) throw std::runtime_error("out-table launch failed");
+        copyTI(m, st, buffers, false, true, 0, direct, direct ? &off : nullptr); // clears it
         if (!direct) HIP_CHECK(hipStreamWaitEvent(st, m->zJoinEv, 0));
     } catch (const std::exception &e) {
         return fail(MPENV_ERR_HIP, e.what());

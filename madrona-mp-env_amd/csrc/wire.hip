@@ -394,6 +394,8 @@ constexpr int kCopyBlockPieces = 256 * kCopyPieces;
 
 __global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b)
 {
+    if (b.tabDst && blockIdx.x == 0 && threadIdx.x == 0) *b.tabDst = b.tab;
+    if (b.n == 0) return;
     int k = 0;
     while (k + 1 < b.n && b.first[k + 1] <= (int64_t)blockIdx.x) k++; // uniform
     const CopySeg sg = b.seg[k];
@@ -453,12 +455,12 @@ int launchWirePack(const DevState &s, char *dst, bool keyframe, uint32_t worldOf
 
 int launchCopyBatch(const CopyBatch &bIn, void *stream)
 {
-    if (bIn.n <= 0) return 0;
+    if (bIn.n <= 0 && !bIn.tabDst) return 0;
     CopyBatch b = bIn;
     b.first[0] = 0;
     for (int k = 0; k < b.n; k++)
         b.first[k + 1] = b.first[k] + std::max<int64_t>(1, (b.seg[k].bytes / 16 + kCopyBlockPieces - 1) / kCopyBlockPieces);
-    const int64_t blocks = b.first[b.n];
+    const int64_t blocks = std::max<int64_t>(1, b.first[b.n]);
     hipLaunchKernelGGL(k_copy_batch, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, b);
     return checkW(hipGetLastError());
 }

@@ -801,7 +801,10 @@ static int pairMain(const std::vector<float> &rays)
 // per node iteration + 45 per triangle iteration (DESIGN.md §4 model).
 struct KM {
     double waves = 0, nodeIters = 0, triIters = 0, pops = 0, tris = 0, wrong = 0;
+    double triItersMerged = 0; // per iteration: the most triangle tests any lane runs over all its slots
 };
+
+static bool g_deferTris = false; // TRAV_DEFER: every slot's box test at the node's entry t_max, then the triangles
 
 static void kernelModel(const std::vector<Node> &nd, const std::vector<float> &vt, const std::vector<float> &rays,
                         bool fwd_waves, KM &km, const std::vector<float> *ref_t = nullptr, std::vector<float> *out_t = nullptr)
@@ -856,12 +859,15 @@ static void kernelModel(const std::vector<Node> &nd, const std::vector<float> &v
                 lanes[l].push_back({ 0, 0, 0, 0 });
                 const Node &x = nd[ni];
                 const float sx = std::ldexp(1.f, x.expX), sy = std::ldexp(1.f, x.expY), sz = std::ldexp(1.f, x.expZ);
+                const float tmax_entry = tmax;
+                std::vector<std::pair<int, int>> deferred; // (leaf, ntri, slot) of passing leaves
+                std::vector<int> dslot;
                 for (int k = 0; k < 4; k++) {
                     const int i = ord[ni][oct][k];
                     if (x.children[i] == -1) continue;
                     const float lo[3] = { x.minX + sx * x.qMinX[i], x.minY + sy * x.qMinY[i], x.minZ + sz * x.qMinZ[i] };
                     const float hi[3] = { x.minX + sx * x.qMaxX[i], x.minY + sy * x.qMaxY[i], x.minZ + sz * x.qMaxZ[i] };
-                    float tn = 0, tf = tmax;
+                    float tn = 0, tf = g_deferTris ? tmax_entry : tmax;
                     for (int a = 0; a < 3; a++) {
                         const float p = (lo[a] - o[a]) * inv[a], q = (hi[a] - o[a]) * inv[a];
                         tn = std::max(tn, std::min(p, q));
@@ -870,6 +876,11 @@ static void kernelModel(const std::vector<Node> &nd, const std::vector<float> &v
                     if (tn > tf) continue;
                     if (x.children[i] & 0x80000000) {
                         const int leaf = x.children[i] & 0x7fffffff;
+                        if (g_deferTris) {
+                            deferred.push_back({ leaf, x.triSize[i] });
+                            dslot.push_back(k);
+                            continue;
+                        }
                         for (int q = 0; q < x.triSize[i]; q++) {
                             lanes[l].back()[k]++;
                             km.tris++;
@@ -880,6 +891,13 @@ static void kernelModel(const std::vector<Node> &nd, const std::vector<float> &v
                         st.push_back(x.children[i]);
                     }
                 }
+                for (size_t e = 0; e < deferred.size(); e++)
+                    for (int q = 0; q < deferred[e].second; q++) {
+                        lanes[l].back()[dslot[e]]++;
+                        km.tris++;
+                        float th;
+                        if (tri(&vt[(deferred[e].first + q) * 9], o, d, tmax, th)) tmax = th;
+                    }
             }
             mp = std::max(mp, lanes[l].size());
             if (out_t) (*out_t)[w0 + l] = tmax;
@@ -889,13 +907,18 @@ static void kernelModel(const std::vector<Node> &nd, const std::vector<float> &v
             }
         }
         km.nodeIters += mp;
-        for (size_t it = 0; it < mp; it++)
+        for (size_t it = 0; it < mp; it++) {
             for (int k = 0; k < 4; k++) {
                 int m = 0;
                 for (auto &L : lanes)
                     if (it < L.size()) m = std::max(m, L[it][k]);
                 km.triIters += m;
             }
+            int mm = 0;
+            for (auto &L : lanes)
+                if (it < L.size()) mm = std::max(mm, L[it][0] + L[it][1] + L[it][2] + L[it][3]);
+            km.triItersMerged += mm;
+        }
     }
 }
 
@@ -963,6 +986,11 @@ static int treesMain(const char *scene, const std::vector<float> &rays)
         const double units = f.waves / 4;
         const double cost = (110 * (f.nodeIters + r.nodeIters) + 45 * (f.triIters + r.triIters)) / units;
         if (vi == 0) base = cost;
+        if (getenv("TRAV_MERGED")) {
+            const double cm = (110 * (f.nodeIters + r.nodeIters) + 45 * (f.triItersMerged + r.triItersMerged)) / units;
+            printf("   merged triangle loop: fwd tri it %5.2f rear %5.2f, cost/unit %6.0f (%+.1f%% vs this tree per-slot)\n",
+                   f.triItersMerged / f.waves, r.triItersMerged / r.waves, cm, 100.0 * (cm / cost - 1));
+        }
         printf("%-48s nodes %3d stack %2d | fwd wave: node it %5.2f tri it %5.2f | rear wave: %5.2f / %5.2f | "
                "lane pops/ray %.2f tris/ray %.2f | cost/unit %6.0f (%+.1f%%)%s\n",
                cv.name, nn, ms, f.nodeIters / f.waves, f.triIters / f.waves, r.nodeIters / r.waves,
@@ -990,6 +1018,7 @@ int main(int argc, char **argv)
     while (fread(buf, 4, 6, f) == 6) rays.insert(rays.end(), buf, buf + 6);
     fclose(f);
     size_t n = rays.size() / 6;
+    g_deferTris = getenv("TRAV_DEFER") != nullptr;
     if (getenv("TRAV_TREES")) return treesMain(argv[1], rays);
     {
         double un = 0, ut = 0;
