@@ -57,9 +57,13 @@ def scene():
     return parse_collisions(os.path.join(SCENE, "collisions.bin"))
 
 
-@pytest.fixture(scope="module")
-def bvh():
-    return T.scene_bvh()
+@pytest.fixture(scope="module", params=["collision", "lidar"])
+def bvh(request):
+    """Both trees the engine builds over the same triangles: the collision
+    tree (every query but the lidar) and k_lidar's own (scene.h
+    lidarBVHOpts); the oracle's octant / lex lidar rules walk the latter
+    (tests/test_lidar_order.py pins them against brute force)."""
+    return T.scene_bvh(lidar=request.param == "lidar")
 
 
 @pytest.fixture(scope="module")
