@@ -521,8 +521,10 @@ int mpenv_scene_lidar_bvh(const char *scene_path, void *nodes_out, int32_t *num_
 /* The same for another build of the scene's triangles (scene.h
  * BVHBuildOpts): opts[0] max leaf size (1-2), [1] SAH bins (0 = full sweep),
  * [2] measure (0 surface area, 1 lidar-weighted), [3] traversal cost x 100,
- * [4] the lidar measure's floor weight x 100; missing entries keep the
- * defaults.  For tools/trav_stats.cpp (tree models). */
+ * [4] the lidar measure's floor weight x 100, then pairs (heap index of a
+ * binary build node, root 1; rank of the SAH candidate split to take there,
+ * BVHBuildOpts::splitRank); missing entries keep the defaults.  For
+ * tools/trav_stats.cpp (tree models and the TRAV_TUNE search). */
 int mpenv_scene_bvh_variant(const char *scene_path, const int32_t *opts, int32_t num_opts, void *nodes_out,
                             int32_t *num_nodes, float *verts_out, int32_t *num_verts, int32_t *max_stack);
 

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <stdexcept>
 
 namespace mpenv {
@@ -81,7 +82,13 @@ struct Builder {
     double meas(const Box &b) const { return b.measure(o.measure, o.floorWeight); }
     static double cen(const Vec3 &c, int ax) { return ax == 0 ? c.x : (ax == 1 ? c.y : c.z); }
 
-    int build(std::vector<int> tris)
+    struct Cand {
+        double cost;
+        int axis, split;
+    };
+
+    // hid: heap index of this binary node (root 1), for o.splitRank
+    int build(std::vector<int> tris, uint64_t hid = 1)
     {
         BNode node;
         node.box.reset();
@@ -97,79 +104,101 @@ struct Builder {
         // SAH over centroids, intersection cost 1, traversal cost
         // o.travCost (4: mesh_bvh_builder.cpp:347-348), under o.measure:
         // binned (o.bins per axis) or a full sweep over sorted centroids.
+        // Every candidate split is kept; the cheapest is taken unless
+        // o.splitRank asks for another rank at this node.
         Box cbox; cbox.reset();
         for (int t : tris) {
             Box b; b.lo[0] = b.hi[0] = centroid[t].x; b.lo[1] = b.hi[1] = centroid[t].y;
             b.lo[2] = b.hi[2] = centroid[t].z; cbox.grow(b);
         }
-        double best_cost = 1e300;
-        int best_axis = -1, best_split = -1;
-        std::vector<int> lt, rt;
+        std::vector<Cand> cands;
+        const int n = (int)tris.size();
+        auto axisOrder = [&](int ax) {
+            std::vector<int> ord = tris;
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cen(centroid[a], ax) < cen(centroid[b], ax); });
+            return ord;
+        };
+        const int kBins = std::min(64, std::max(1, o.bins));
         if (o.bins <= 0) {
             // full sweep: split after position s of the centroid order
-            std::vector<int> order;
-            const int n = (int)tris.size();
             std::vector<double> right(n + 1);
             for (int ax = 0; ax < 3; ax++) {
-                std::vector<int> ord = tris;
-                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cen(centroid[a], ax) < cen(centroid[b], ax); });
+                const std::vector<int> ord = axisOrder(ax);
                 Box acc; acc.reset();
                 for (int i = n - 1; i >= 1; i--) { acc.grow(triBox[ord[i]]); right[i] = meas(acc); }
                 acc.reset();
                 for (int i = 0; i + 1 < n; i++) {
                     acc.grow(triBox[ord[i]]);
-                    const double cost = o.travCost * meas(node.box) + meas(acc) * (i + 1) + right[i + 1] * (n - i - 1);
-                    if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = i + 1; order = ord; }
+                    cands.push_back({ o.travCost * meas(node.box) + meas(acc) * (i + 1) + right[i + 1] * (n - i - 1), ax, i + 1 });
                 }
             }
-            if (best_axis >= 0) {
-                lt.assign(order.begin(), order.begin() + best_split);
-                rt.assign(order.begin() + best_split, order.end());
-            }
         } else {
-        const int kBins = std::min(64, o.bins);
-        for (int ax = 0; ax < 3; ax++) {
-            double ext = cbox.hi[ax] - cbox.lo[ax];
-            if (ext <= 0.0) continue;
-            Box bins[64]; int cnt[64];
-            for (int b = 0; b < kBins; b++) { bins[b].reset(); cnt[b] = 0; }
-            for (int t : tris) {
-                double c = ax == 0 ? centroid[t].x : (ax == 1 ? centroid[t].y : centroid[t].z);
-                int b = std::min(kBins - 1, (int)((c - cbox.lo[ax]) / ext * kBins));
-                bins[b].grow(triBox[t]); cnt[b]++;
-            }
-            for (int s = 1; s < kBins; s++) {
-                Box l, r; l.reset(); r.reset(); int nl = 0, nr = 0;
-                for (int b = 0; b < s; b++) { if (cnt[b]) { l.grow(bins[b]); nl += cnt[b]; } }
-                for (int b = s; b < kBins; b++) { if (cnt[b]) { r.grow(bins[b]); nr += cnt[b]; } }
-                if (nl == 0 || nr == 0) continue;
-                double cost = o.travCost * meas(node.box) + meas(l) * nl + meas(r) * nr;
-                if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = s; }
+            for (int ax = 0; ax < 3; ax++) {
+                double ext = cbox.hi[ax] - cbox.lo[ax];
+                if (ext <= 0.0) continue;
+                Box bins[64]; int cnt[64];
+                for (int b = 0; b < kBins; b++) { bins[b].reset(); cnt[b] = 0; }
+                for (int t : tris) {
+                    double c = cen(centroid[t], ax);
+                    int b = std::min(kBins - 1, (int)((c - cbox.lo[ax]) / ext * kBins));
+                    bins[b].grow(triBox[t]); cnt[b]++;
+                }
+                for (int s = 1; s < kBins; s++) {
+                    Box l, r; l.reset(); r.reset(); int nl = 0, nr = 0;
+                    for (int b = 0; b < s; b++) { if (cnt[b]) { l.grow(bins[b]); nl += cnt[b]; } }
+                    for (int b = s; b < kBins; b++) { if (cnt[b]) { r.grow(bins[b]); nr += cnt[b]; } }
+                    if (nl == 0 || nr == 0) continue;
+                    cands.push_back({ o.travCost * meas(node.box) + meas(l) * nl + meas(r) * nr, ax, s });
+                }
             }
         }
-        }
+        // cheapest first; ties keep generation order (axis, then split), so
+        // rank 0 is the first strict minimum
+        std::stable_sort(cands.begin(), cands.end(), [](const Cand &a, const Cand &b) { return a.cost < b.cost; });
 
-        if (o.bins <= 0) {
-            if (best_axis < 0) { // degenerate centroids: median split by index
-                size_t h = tris.size() / 2;
-                lt.assign(tris.begin(), tris.begin() + h);
-                rt.assign(tris.begin() + h, tris.end());
-            }
-        } else if (best_axis >= 0) {
-            const int kBins = std::min(64, o.bins);
-            double ext = cbox.hi[best_axis] - cbox.lo[best_axis];
-            for (int t : tris) {
-                double c = best_axis == 0 ? centroid[t].x : (best_axis == 1 ? centroid[t].y : centroid[t].z);
-                int b = std::min(kBins - 1, (int)((c - cbox.lo[best_axis]) / ext * kBins));
-                (b < best_split ? lt : rt).push_back(t);
-            }
-        } else { // degenerate centroids: median split by index
+        std::vector<int> lt, rt;
+        if (cands.empty()) { // degenerate centroids: median split by index
             size_t h = tris.size() / 2;
             lt.assign(tris.begin(), tris.begin() + h);
             rt.assign(tris.begin() + h, tris.end());
+        } else {
+            auto partition = [&](const Cand &c, std::vector<int> &l, std::vector<int> &r) {
+                l.clear();
+                r.clear();
+                if (o.bins <= 0) {
+                    const std::vector<int> ord = axisOrder(c.axis);
+                    l.assign(ord.begin(), ord.begin() + c.split);
+                    r.assign(ord.begin() + c.split, ord.end());
+                } else {
+                    const double ext = cbox.hi[c.axis] - cbox.lo[c.axis];
+                    for (int t : tris) {
+                        int b = std::min(kBins - 1, (int)((cen(centroid[t], c.axis) - cbox.lo[c.axis]) / ext * kBins));
+                        (b < c.split ? l : r).push_back(t);
+                    }
+                }
+            };
+            int rank = 0;
+            const auto it = o.splitRank.find(hid);
+            if (it != o.splitRank.end()) rank = std::max(0, it->second);
+            // rank among the DISTINCT partitions (bins with nothing between
+            // them give the same one), the last one when there are fewer
+            std::vector<std::vector<int>> seen;
+            for (const Cand &c : cands) {
+                std::vector<int> l, r;
+                partition(c, l, r);
+                std::vector<int> key = l;
+                std::sort(key.begin(), key.end());
+                if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
+                seen.push_back(key);
+                lt = l;
+                rt = r;
+                if ((int)seen.size() > rank) break;
+            }
         }
-        int l = build(lt);
-        int r = build(rt);
+        // heap index of the children (saturates below depth 62; no overrides there)
+        const uint64_t hl = hid < (1ull << 62) ? 2 * hid : 0, hr = hid < (1ull << 62) ? 2 * hid + 1 : 0;
+        int l = build(lt, hl);
+        int r = build(rt, hr);
         bnodes[id].left = l;
         bnodes[id].right = r;
         return id;
@@ -476,6 +505,53 @@ QuirkGrid quirkGrid(const std::vector<Vec3> &verts, float r, float margin, float
     return q;
 }
 
+// lidar_tree.txt (optional, next to the .bin files): k_lidar's tree tuned
+// for this scene -- BVHBuildOpts::splitRank entries ("split HID RANK") that
+// tools/trav_stats.cpp TRAV_TUNE found against recorded lidar fans
+// (tools/write_lidar_tree.py writes the file).  Any ranks give a valid BVH
+// (only the traversal cost changes), but they were tuned for one triangle
+// set: the file names the FNV-1a 64 of its collisions.bin and is ignored
+// for any other.
+static uint64_t fnv1a64File(const std::string &path)
+{
+    std::ifstream f(path, std::ios::binary);
+    uint64_t h = 1469598103934665603ull;
+    char buf[4096];
+    while (f) {
+        f.read(buf, sizeof(buf));
+        for (std::streamsize i = 0; i < f.gcount(); i++) {
+            h ^= (uint8_t)buf[i];
+            h *= 1099511628211ull;
+        }
+    }
+    return h;
+}
+
+static void readLidarTuning(const std::string &dir, BVHBuildOpts &o)
+{
+    std::ifstream f(dir + "/lidar_tree.txt");
+    if (!f) return;
+    std::map<uint64_t, int> ranks;
+    uint64_t want = 0;
+    bool have_hash = false;
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.empty() || line[0] == '#') continue;
+        char key[32] = {};
+        unsigned long long a = 0;
+        int r = 0;
+        if (std::sscanf(line.c_str(), "%31s %llx", key, &a) == 2 && std::strcmp(key, "collisions_fnv1a64") == 0) {
+            want = a;
+            have_hash = true;
+        } else if (std::sscanf(line.c_str(), "%31s %llu %d", key, &a, &r) == 3 && std::strcmp(key, "split") == 0) {
+            ranks[a] = r;
+        } else {
+            throw std::runtime_error(dir + "/lidar_tree.txt: malformed line: " + line);
+        }
+    }
+    if (have_hash && want == fnv1a64File(dir + "/collisions.bin")) o.splitRank = ranks;
+}
+
 Scene loadScene(const std::string &dir, bool spawn_in_middle)
 {
     Scene s;
@@ -540,7 +616,10 @@ Scene loadScene(const std::string &dir, bool spawn_in_middle)
     buildBVH(s.triVerts, s);
     {
         Scene t;
-        buildBVH(s.triVerts, t, lidarBVHOpts());
+        BVHBuildOpts lo = lidarBVHOpts();
+        readLidarTuning(dir, lo);
+        s.lidarTuned = !lo.splitRank.empty();
+        buildBVH(s.triVerts, t, lo);
         s.lidarNodes = std::move(t.nodes);
         s.lidarVerts = std::move(t.bvhVerts);
         s.lidarMaxStack = std::max(t.maxStack, t.maxStackAnyOrder);

@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "mpenv_core.h"
@@ -88,6 +89,7 @@ struct Scene {
     std::vector<BVHNode> lidarNodes;
     std::vector<mp::Vec3> lidarVerts;
     int32_t lidarMaxStack = 0; // any push order
+    bool lidarTuned = false;   // built with the scene's lidar_tree.txt split ranks
 
     std::vector<Spawn> aSpawns, bSpawns, commonRespawns;
     uint32_t numDefaultASpawns = 0, numDefaultBSpawns = 0;
@@ -122,6 +124,11 @@ struct BVHBuildOpts {
     int measure = 0;        // 0: surface area; 1: lidar-weighted (below)
     float travCost = 4.f;   // SAH cost of an inner node relative to one triangle test
     float floorWeight = 0.f; // measure 1: weight of the horizontal (xy) face
+    // Per binary build node, addressed by its heap index (root 1, children
+    // 2i / 2i + 1): take the split of this rank in SAH-cost order instead of
+    // the cheapest (rank 0).  A ray-driven tuning of the tree
+    // (tools/trav_stats.cpp TRAV_TUNE) writes these.
+    std::map<uint64_t, int> splitRank;
 };
 // measure 1: the mean area a box shows to near-horizontal rays, (2/pi)
 // (dx + dy) dz for uniformly distributed horizontal directions (the constant

@@ -299,3 +299,58 @@ def test_node_bytes_follow_the_documented_quantisation(bvh):
                 assert c > oid and n["triSize"][i] == 0  # DFS pre-order ids
                 internal += 1
         assert n["internal"] == internal
+
+
+def _variant(scene, opts):
+    lib = T.lib_mpenv()
+    fn = lib.mpenv_scene_bvh_variant
+    fn.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
+                   C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    o = np.asarray(opts, np.int32)
+    nn, nv, ms = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+    assert fn(scene.encode(), o.ctypes.data, len(o), None, C.byref(nn), None, C.byref(nv), C.byref(ms)) == 0
+    nodes = np.zeros(nn.value * 64, np.uint8)
+    verts = np.zeros(nv.value * 3, np.float32)
+    assert fn(scene.encode(), o.ctypes.data, len(o), nodes.ctypes.data, C.byref(nn), verts.ctypes.data,
+              C.byref(nv), C.byref(ms)) == 0
+    return nodes, verts
+
+
+def test_lidar_tree_tuning_file(tmp_path):
+    """scene.cpp readLidarTuning: k_lidar's tree is lidarBVHOpts() plus the
+    split ranks of the scene's lidar_tree.txt (tools/trav_stats.cpp
+    TRAV_TUNE), applied only to the collisions.bin whose FNV-1a 64 it names;
+    without the file, or for another collisions.bin, the untuned tree."""
+    import shutil
+    base = [2, 12, 1, 400, 10]  # scene.h lidarBVHOpts
+    path = os.path.join(SCENE, "lidar_tree.txt")
+    assert os.path.exists(path), "the shipped scene carries its tuned lidar tree"
+    pairs, want = [], None
+    for line in open(path):
+        f = line.split()
+        if not f or f[0].startswith("#"):
+            continue
+        if f[0] == "collisions_fnv1a64":
+            want = int(f[1], 16)
+        else:
+            assert f[0] == "split" and len(f) == 3
+            pairs += [int(f[1]), int(f[2])]
+    h = 1469598103934665603
+    for b in open(os.path.join(SCENE, "collisions.bin"), "rb").read():
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    assert want == h
+    tuned_nodes, tuned_verts, _ = T.scene_bvh(lidar=True)
+    n, v = _variant(SCENE, base + pairs)
+    assert np.array_equal(n, tuned_nodes) and np.array_equal(v, tuned_verts)
+    un, uv = _variant(SCENE, base)
+    assert not np.array_equal(un, tuned_nodes) or un.size != tuned_nodes.size
+    # a copy without the file, and one whose file names another hash
+    for name, text in (("none", None), ("stale", open(path).read().replace(f"{want:016x}", f"{want ^ 1:016x}"))):
+        d = tmp_path / name
+        d.mkdir()
+        for f in ("collisions.bin", "navmesh.bin", "spawns.bin", "zones.bin"):
+            shutil.copy(os.path.join(SCENE, f), d)
+        if text is not None:
+            (d / "lidar_tree.txt").write_text(text)
+        ln, lv, _ = T.scene_bvh(str(d), lidar=True)
+        assert np.array_equal(ln, un) and np.array_equal(lv, uv), name

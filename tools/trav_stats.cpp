@@ -11,6 +11,9 @@
 //       triangle its slot hit then and starts with t_max = that hit's t
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <map>
+#include <thread>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -1001,8 +1004,175 @@ static int treesMain(const char *scene, const std::vector<float> &rays)
     return 0;
 }
 
+// ---- TRAV_TUNE: ray-driven tuning of the lidar tree.  Coordinate descent
+// over BVHBuildOpts::splitRank (per binary build node down to depth
+// TRAV_TUNE_DEPTH, the rank among its distinct SAH candidate splits, up to
+// TRAV_TUNE_RANKS): each move is scored by kernelModel's lockstep cost
+// summed over the TRAIN ray sets (each relative to the untuned tree), kept
+// if it lowers it; trees over TRAV_TUNE_NODES nodes or a stack over 14 are
+// rejected.  The VAL sets are reported, never optimised.
+//   TRAV_TUNE=1 trav_stats SCENE TRAIN1.f32,TRAIN2.f32 VAL1.f32,VAL2.f32
+static std::vector<float> readRays(const std::string &path)
+{
+    std::vector<float> r;
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return r;
+    float buf[6];
+    while (fread(buf, 4, 6, f) == 6) r.insert(r.end(), buf, buf + 6);
+    fclose(f);
+    return r;
+}
+
+static std::vector<std::string> splitList(const std::string &s)
+{
+    std::vector<std::string> v;
+    size_t p = 0;
+    while (p <= s.size()) {
+        size_t q = s.find(',', p);
+        if (q == std::string::npos) q = s.size();
+        if (q > p) v.push_back(s.substr(p, q - p));
+        p = q + 1;
+    }
+    return v;
+}
+
+struct TuneEval {
+    std::vector<double> cost; // per ray set
+    int nodes = 0, stack = 0;
+    bool ok = false, same = false; // same: the tree of `skip_if` (not evaluated)
+    std::string bytes;             // node + vertex bytes
+};
+
+static TuneEval tuneEval(const char *scene, const std::vector<int32_t> &opts, const std::vector<std::vector<float>> &sets,
+                         const std::string *skip_if = nullptr)
+{
+    TuneEval e;
+    int32_t nn = 0, nv = 0, ms = 0;
+    if (mpenv_scene_bvh_variant(scene, opts.data(), (int32_t)opts.size(), nullptr, &nn, nullptr, &nv, &ms)) return e;
+    std::vector<Node> nd(nn);
+    std::vector<float> vt((size_t)nv * 3);
+    mpenv_scene_bvh_variant(scene, opts.data(), (int32_t)opts.size(), nd.data(), &nn, vt.data(), &nv, &ms);
+    e.nodes = nn;
+    e.stack = ms;
+    e.bytes.assign(reinterpret_cast<const char *>(nd.data()), nd.size() * sizeof(Node));
+    e.bytes.append(reinterpret_cast<const char *>(vt.data()), vt.size() * 4);
+    if (skip_if && *skip_if == e.bytes) {
+        e.same = true;
+        return e;
+    }
+    for (const auto &rays : sets) {
+        KM f, r;
+        kernelModel(nd, vt, rays, true, f);
+        kernelModel(nd, vt, rays, false, r);
+        e.cost.push_back((110 * (f.nodeIters + r.nodeIters) + 45 * (f.triIters + r.triIters)) / (f.waves / 4));
+    }
+    e.ok = true;
+    return e;
+}
+
+static int tuneMain(const char *scene, const char *train_list, const char *val_list)
+{
+    std::vector<std::vector<float>> train, val;
+    for (const auto &p : splitList(train_list)) train.push_back(readRays(p));
+    for (const auto &p : splitList(val_list)) val.push_back(readRays(p));
+    const int depth = getenv("TRAV_TUNE_DEPTH") ? atoi(getenv("TRAV_TUNE_DEPTH")) : 7;
+    const int ranks = getenv("TRAV_TUNE_RANKS") ? atoi(getenv("TRAV_TUNE_RANKS")) : 6;
+    const int maxNodes = getenv("TRAV_TUNE_NODES") ? atoi(getenv("TRAV_TUNE_NODES")) : 64;
+    const int passes = getenv("TRAV_TUNE_PASSES") ? atoi(getenv("TRAV_TUNE_PASSES")) : 3;
+    const std::vector<int32_t> base = { 2, 12, 1, 400, 10 };
+    std::map<uint32_t, int> cur;
+    if (const char *init = getenv("TRAV_TUNE_INIT")) { // "hid:rank hid:rank ..." (a previous run's splitRank line)
+        std::string t = init;
+        size_t p = 0;
+        while (p < t.size()) {
+            size_t q = t.find(' ', p);
+            if (q == std::string::npos) q = t.size();
+            const std::string one = t.substr(p, q - p);
+            const size_t c = one.find(':');
+            if (c != std::string::npos) cur[(uint32_t)std::stoul(one.substr(0, c))] = std::stoi(one.substr(c + 1));
+            p = q + 1;
+        }
+    }
+    auto optsOf = [&](const std::map<uint32_t, int> &m) {
+        std::vector<int32_t> o = base;
+        for (auto &kv : m) {
+            if (kv.second == 0) continue;
+            o.push_back((int32_t)kv.first);
+            o.push_back(kv.second);
+        }
+        return o;
+    };
+    const TuneEval b0 = tuneEval(scene, base, train), v0 = tuneEval(scene, base, val);
+    auto score = [&](const TuneEval &e) {
+        double s = 0;
+        for (size_t i = 0; i < e.cost.size(); i++) s += e.cost[i] / b0.cost[i];
+        return s / (double)e.cost.size();
+    };
+    const TuneEval s0 = tuneEval(scene, optsOf(cur), train);
+    double best = score(s0);
+    std::string bestBytes = s0.bytes;
+    printf("start %.4f; untuned: train", best);
+    for (double c : b0.cost) printf(" %.0f", c);
+    printf(" | val");
+    for (double c : v0.cost) printf(" %.0f", c);
+    printf(" | nodes %d stack %d\n", b0.nodes, b0.stack);
+    fflush(stdout);
+    const unsigned nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (int pass = 0; pass < passes; pass++) {
+        bool improved = false;
+        for (uint32_t hid = 1; hid < (1u << depth); hid++) {
+            std::vector<std::map<uint32_t, int>> cands;
+            const int have = cur.count(hid) ? cur[hid] : 0;
+            for (int r = 0; r < ranks; r++) {
+                if (r == have) continue;
+                auto m = cur;
+                m[hid] = r;
+                cands.push_back(m);
+            }
+            std::vector<TuneEval> res(cands.size());
+            std::vector<std::thread> th;
+            std::atomic<size_t> next { 0 };
+            for (unsigned t = 0; t < nth; t++)
+                th.emplace_back([&] {
+                    for (size_t i; (i = next++) < cands.size();)
+                        res[i] = tuneEval(scene, optsOf(cands[i]), train, &bestBytes);
+                });
+            for (auto &t : th) t.join();
+            int pick = -1;
+            for (size_t i = 0; i < cands.size(); i++) {
+                if (!res[i].ok || res[i].same || res[i].nodes > maxNodes || res[i].stack > 14) continue;
+                const double sc = score(res[i]);
+                if (sc < best - 1e-4) {
+                    best = sc;
+                    pick = (int)i;
+                }
+            }
+            if (pick >= 0) {
+                cur = cands[pick];
+                bestBytes = res[pick].bytes;
+                improved = true;
+                printf("pass %d hid %u -> rank %d: train %.4f (nodes %d stack %d)\n", pass, hid, cur[hid], best,
+                       res[pick].nodes, res[pick].stack);
+                fflush(stdout);
+            }
+        }
+        if (!improved) break;
+    }
+    const TuneEval ft = tuneEval(scene, optsOf(cur), train), fv = tuneEval(scene, optsOf(cur), val);
+    printf("tuned: train");
+    for (size_t i = 0; i < ft.cost.size(); i++) printf(" %.0f (%+.1f%%)", ft.cost[i], 100.0 * (ft.cost[i] / b0.cost[i] - 1));
+    printf(" | val");
+    for (size_t i = 0; i < fv.cost.size(); i++) printf(" %.0f (%+.1f%%)", fv.cost[i], 100.0 * (fv.cost[i] / v0.cost[i] - 1));
+    printf(" | nodes %d stack %d\nsplitRank:", ft.nodes, ft.stack);
+    for (auto &kv : cur)
+        if (kv.second) printf(" %u:%d", kv.first, kv.second);
+    printf("\n");
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (getenv("TRAV_TUNE") && argc >= 4) return tuneMain(argv[1], argv[2], argv[3]);
     if (argc < 3) {
         fprintf(stderr, "%s SCENE RAYS.f32\n", argv[0]);
         return 1;
