@@ -1073,7 +1073,15 @@ static TuneEval tuneEval(const char *scene, const std::vector<int32_t> &opts, co
 static int tuneMain(const char *scene, const char *train_list, const char *val_list)
 {
     std::vector<std::vector<float>> train, val;
-    for (const auto &p : splitList(train_list)) train.push_back(readRays(p));
+    // TRAV_TUNE_SUB=k: train on every k-th 4-agent unit (320 rays: 4 forward
+    // waves + 1 rear wave) of each set, for speed
+    const int sub = getenv("TRAV_TUNE_SUB") ? std::max(1, atoi(getenv("TRAV_TUNE_SUB"))) : 1;
+    for (const auto &p : splitList(train_list)) {
+        std::vector<float> r = readRays(p), t;
+        for (size_t u = 0; (u + 1) * 320 * 6 <= r.size(); u += sub)
+            t.insert(t.end(), r.begin() + u * 320 * 6, r.begin() + (u + 1) * 320 * 6);
+        train.push_back(t);
+    }
     for (const auto &p : splitList(val_list)) val.push_back(readRays(p));
     const int depth = getenv("TRAV_TUNE_DEPTH") ? atoi(getenv("TRAV_TUNE_DEPTH")) : 7;
     const int ranks = getenv("TRAV_TUNE_RANKS") ? atoi(getenv("TRAV_TUNE_RANKS")) : 6;
@@ -1157,6 +1165,61 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
             }
         }
         if (!improved) break;
+    }
+    // TRAV_TUNE_KICKS=n: iterated local search -- n times, re-rank 3 random
+    // nodes of the best tree (depth <= TRAV_TUNE_DEPTH), descend one pass
+    // from there, keep the result if it beats the best
+    const int kicks = getenv("TRAV_TUNE_KICKS") ? atoi(getenv("TRAV_TUNE_KICKS")) : 0;
+    uint64_t rng = 0x9e3779b97f4a7c15ull;
+    auto rnd = [&](uint32_t n) {
+        rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+        return (uint32_t)(rng % n);
+    };
+    for (int kk = 0; kk < kicks; kk++) {
+        auto m = cur;
+        for (int j = 0; j < 3; j++) m[1 + rnd((1u << std::min(depth, 7)) - 1)] = (int)rnd((uint32_t)ranks);
+        TuneEval e = tuneEval(scene, optsOf(m), train);
+        if (!e.ok || e.nodes > maxNodes || e.stack > 14) continue;
+        double sc = score(e);
+        std::string bytes = e.bytes;
+        for (uint32_t hid = 1; hid < (1u << depth); hid++) {
+            std::vector<std::map<uint32_t, int>> cands;
+            const int have = m.count(hid) ? m[hid] : 0;
+            for (int r = 0; r < ranks; r++) {
+                if (r == have) continue;
+                auto c = m;
+                c[hid] = r;
+                cands.push_back(c);
+            }
+            std::vector<TuneEval> res(cands.size());
+            std::vector<std::thread> th;
+            std::atomic<size_t> next { 0 };
+            for (unsigned t = 0; t < nth; t++)
+                th.emplace_back([&] {
+                    for (size_t i; (i = next++) < cands.size();) res[i] = tuneEval(scene, optsOf(cands[i]), train, &bytes);
+                });
+            for (auto &t : th) t.join();
+            for (size_t i = 0; i < cands.size(); i++) {
+                if (!res[i].ok || res[i].same || res[i].nodes > maxNodes || res[i].stack > 14) continue;
+                const double c = score(res[i]);
+                if (c < sc - 1e-4) {
+                    sc = c;
+                    m = cands[i];
+                    bytes = res[i].bytes;
+                }
+            }
+        }
+        printf("kick %d: %.4f (best %.4f)\n", kk, sc, best);
+        fflush(stdout);
+        if (sc < best - 1e-4) {
+            best = sc;
+            cur = m;
+            bestBytes = bytes;
+            printf("  kept:");
+            for (auto &kv : cur)
+                if (kv.second) printf(" %u:%d", kv.first, kv.second);
+            printf("\n");
+        }
     }
     const TuneEval ft = tuneEval(scene, optsOf(cur), train), fv = tuneEval(scene, optsOf(cur), val);
     printf("tuned: train");
