@@ -354,3 +354,19 @@ def test_lidar_tree_tuning_file(tmp_path):
             (d / "lidar_tree.txt").write_text(text)
         ln, lv, _ = T.scene_bvh(str(d), lidar=True)
         assert np.array_equal(ln, un) and np.array_equal(lv, uv), name
+
+
+def test_split_rank_overrides():
+    """BVHBuildOpts::splitRank (scene.cpp Builder::build): rank 0 is the SAH
+    choice itself, a heap index the tree does not have changes nothing, and
+    a real override changes the tree while keeping every triangle once."""
+    base = [2, 12, 1, 400, 10]
+    n0, v0 = _variant(SCENE, base)
+    n1, v1 = _variant(SCENE, base + [1, 0, 3, 0])
+    assert np.array_equal(n0, n1) and np.array_equal(v0, v1)
+    n2, v2 = _variant(SCENE, base + [(1 << 30) + 5, 3])
+    assert np.array_equal(n0, n2) and np.array_equal(v0, v2)
+    n3, v3 = _variant(SCENE, base + [3, 1])
+    assert not (n3.size == n0.size and np.array_equal(n3, n0))
+    # the same multiset of triangles (simple_map repeats some)
+    assert sorted(map(tuple, v3.reshape(-1, 9).tolist())) == sorted(map(tuple, v0.reshape(-1, 9).tolist()))
