@@ -1753,7 +1753,10 @@ int mpenv_scene_bvh_variant(const char *scene_path, const int32_t *opts, int32_t
         if (opts && num_opts > 2) o.measure = opts[2];
         if (opts && num_opts > 3) o.travCost = (float)opts[3] / 100.f;
         if (opts && num_opts > 4) o.floorWeight = (float)opts[4] / 100.f;
-        for (int32_t k = 5; opts && k + 1 < num_opts; k += 2) o.splitRank[(uint64_t)(uint32_t)opts[k]] = opts[k + 1];
+        for (int32_t k = 5; opts && k + 1 < num_opts; k += 2) {
+            if (opts[k] >= 0) o.splitRank[(uint64_t)opts[k]] = opts[k + 1];
+            else o.collapseChoice[(uint64_t)(-(int64_t)opts[k])] = opts[k + 1];
+        }
         Scene t;
         buildBVH(s.triVerts, t, o);
         if (num_nodes) {

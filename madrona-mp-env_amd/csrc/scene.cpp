@@ -63,6 +63,7 @@ struct Box {
 struct BNode {            // binary build node
     Box box;
     int left = -1, right = -1;
+    uint64_t hid = 0;      // heap index (root 1; 0 below depth 62)
     std::vector<int> tris; // leaf only
 };
 
@@ -94,6 +95,7 @@ struct Builder {
         node.box.reset();
         for (int t : tris) node.box.grow(triBox[t]);
         int id = (int)bnodes.size();
+        node.hid = hid;
         bnodes.push_back(node);
 
         if ((int)tris.size() <= maxLeaf) { // maxLeafSize = numTrisPerLeaf (mesh_bvh_builder.cpp:345-346)
@@ -251,19 +253,25 @@ void buildBVH(const std::vector<Vec3> &tri_verts, Scene &out, const BVHBuildOpts
     std::vector<int> order;   // binary roots of output inner nodes, DFS order
     std::vector<int> depth_of;
 
+    // opts.collapseChoice[hid of broot] bit k: at the k-th opening, open the
+    // inner child of second-largest measure instead of the largest
     auto collapse = [&](int broot) {
         std::vector<int> kids;
         if (isLeaf(broot)) { kids.push_back(broot); return kids; }
         kids.push_back(b.bnodes[broot].left);
         kids.push_back(b.bnodes[broot].right);
-        while (kids.size() < 4) {
-            int best = -1; double best_area = -1;
+        const auto cit = opts.collapseChoice.find(b.bnodes[broot].hid);
+        const int choice = cit == opts.collapseChoice.end() || b.bnodes[broot].hid == 0 ? 0 : cit->second;
+        for (int step = 0; kids.size() < 4; step++) {
+            int best = -1, second = -1; double best_area = -1, second_area = -1;
             for (int i = 0; i < (int)kids.size(); i++) {
                 if (isLeaf(kids[i])) continue;
                 double a = b.meas(b.bnodes[kids[i]].box);
-                if (a > best_area) { best_area = a; best = i; }
+                if (a > best_area) { second = best; second_area = best_area; best_area = a; best = i; }
+                else if (a > second_area) { second_area = a; second = i; }
             }
             if (best < 0) break;
+            if (((choice >> step) & 1) && second >= 0) best = second;
             int n = kids[best];
             kids.erase(kids.begin() + best);
             kids.insert(kids.begin() + best, b.bnodes[n].right);
@@ -507,7 +515,8 @@ QuirkGrid quirkGrid(const std::vector<Vec3> &verts, float r, float margin, float
 
 // lidar_tree.txt (optional, next to the .bin files): k_lidar's tree tuned
 // for this scene -- BVHBuildOpts::splitRank entries ("split HID RANK") that
-// tools/trav_stats.cpp TRAV_TUNE found against recorded lidar fans
+// tools/trav_stats.cpp TRAV_TUNE found against recorded lidar fans, and
+// BVHBuildOpts::collapseChoice entries ("collapse HID CHOICE")
 // (tools/write_lidar_tree.py writes the file).  Any ranks give a valid BVH
 // (only the traversal cost changes), but they were tuned for one triangle
 // set: the file names the FNV-1a 64 of its collisions.bin and is ignored
@@ -531,7 +540,7 @@ static void readLidarTuning(const std::string &dir, BVHBuildOpts &o)
 {
     std::ifstream f(dir + "/lidar_tree.txt");
     if (!f) return;
-    std::map<uint64_t, int> ranks;
+    std::map<uint64_t, int> ranks, collapses;
     uint64_t want = 0;
     bool have_hash = false;
     std::string line;
@@ -545,11 +554,16 @@ static void readLidarTuning(const std::string &dir, BVHBuildOpts &o)
             have_hash = true;
         } else if (std::sscanf(line.c_str(), "%31s %llu %d", key, &a, &r) == 3 && std::strcmp(key, "split") == 0) {
             ranks[a] = r;
+        } else if (std::sscanf(line.c_str(), "%31s %llu %d", key, &a, &r) == 3 && std::strcmp(key, "collapse") == 0) {
+            collapses[a] = r;
         } else {
             throw std::runtime_error(dir + "/lidar_tree.txt: malformed line: " + line);
         }
     }
-    if (have_hash && want == fnv1a64File(dir + "/collisions.bin")) o.splitRank = ranks;
+    if (have_hash && want == fnv1a64File(dir + "/collisions.bin")) {
+        o.splitRank = ranks;
+        o.collapseChoice = collapses;
+    }
 }
 
 Scene loadScene(const std::string &dir, bool spawn_in_middle)
@@ -618,7 +632,7 @@ Scene loadScene(const std::string &dir, bool spawn_in_middle)
         Scene t;
         BVHBuildOpts lo = lidarBVHOpts();
         readLidarTuning(dir, lo);
-        s.lidarTuned = !lo.splitRank.empty();
+        s.lidarTuned = !lo.splitRank.empty() || !lo.collapseChoice.empty();
         buildBVH(s.triVerts, t, lo);
         s.lidarNodes = std::move(t.nodes);
         s.lidarVerts = std::move(t.bvhVerts);

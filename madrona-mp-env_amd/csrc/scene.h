@@ -129,6 +129,10 @@ struct BVHBuildOpts {
     // the cheapest (rank 0).  A ray-driven tuning of the tree
     // (tools/trav_stats.cpp TRAV_TUNE) writes these.
     std::map<uint64_t, int> splitRank;
+    // Per 4-wide node, by the heap index of its binary root: bit k set = at
+    // the k-th child opening of the collapse take the inner child of
+    // second-largest measure instead of the largest.
+    std::map<uint64_t, int> collapseChoice;
 };
 // measure 1: the mean area a box shows to near-horizontal rays, (2/pi)
 // (dx + dy) dz for uniformly distributed horizontal directions (the constant

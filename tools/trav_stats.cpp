@@ -1088,7 +1088,7 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
     const int maxNodes = getenv("TRAV_TUNE_NODES") ? atoi(getenv("TRAV_TUNE_NODES")) : 64;
     const int passes = getenv("TRAV_TUNE_PASSES") ? atoi(getenv("TRAV_TUNE_PASSES")) : 3;
     const std::vector<int32_t> base = { 2, 12, 1, 400, 10 };
-    std::map<uint32_t, int> cur;
+    std::map<int64_t, int> cur;
     if (const char *init = getenv("TRAV_TUNE_INIT")) { // "hid:rank hid:rank ..." (a previous run's splitRank line)
         std::string t = init;
         size_t p = 0;
@@ -1097,11 +1097,11 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
             if (q == std::string::npos) q = t.size();
             const std::string one = t.substr(p, q - p);
             const size_t c = one.find(':');
-            if (c != std::string::npos) cur[(uint32_t)std::stoul(one.substr(0, c))] = std::stoi(one.substr(c + 1));
+            if (c != std::string::npos) cur[(int64_t)std::stoll(one.substr(0, c))] = std::stoi(one.substr(c + 1));
             p = q + 1;
         }
     }
-    auto optsOf = [&](const std::map<uint32_t, int> &m) {
+    auto optsOf = [&](const std::map<int64_t, int> &m) {
         std::vector<int32_t> o = base;
         for (auto &kv : m) {
             if (kv.second == 0) continue;
@@ -1129,13 +1129,17 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
     for (int pass = 0; pass < passes; pass++) {
         bool improved = false;
         for (uint32_t hid = 1; hid < (1u << depth); hid++) {
-            std::vector<std::map<uint32_t, int>> cands;
-            const int have = cur.count(hid) ? cur[hid] : 0;
-            for (int r = 0; r < ranks; r++) {
-                if (r == have) continue;
-                auto m = cur;
-                m[hid] = r;
-                cands.push_back(m);
+            std::vector<std::map<int64_t, int>> cands;
+            // split ranks at hid, then (key -hid) the collapse choices of the
+            // 4-wide node whose binary root is hid
+            for (const int64_t key : { (int64_t)hid, -(int64_t)hid }) {
+                const int have = cur.count(key) ? cur[key] : 0;
+                for (int r = 0; r < (key > 0 ? ranks : 4); r++) {
+                    if (r == have) continue;
+                    auto m = cur;
+                    m[key] = r;
+                    cands.push_back(m);
+                }
             }
             std::vector<TuneEval> res(cands.size());
             std::vector<std::thread> th;
@@ -1159,7 +1163,7 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
                 cur = cands[pick];
                 bestBytes = res[pick].bytes;
                 improved = true;
-                printf("pass %d hid %u -> rank %d: train %.4f (nodes %d stack %d)\n", pass, hid, cur[hid], best,
+                printf("pass %d hid %u: split %d collapse %d: train %.4f (nodes %d stack %d)\n", pass, hid, cur[(int64_t)hid], cur[-(int64_t)hid], best,
                        res[pick].nodes, res[pick].stack);
                 fflush(stdout);
             }
@@ -1183,13 +1187,15 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
         double sc = score(e);
         std::string bytes = e.bytes;
         for (uint32_t hid = 1; hid < (1u << depth); hid++) {
-            std::vector<std::map<uint32_t, int>> cands;
-            const int have = m.count(hid) ? m[hid] : 0;
-            for (int r = 0; r < ranks; r++) {
-                if (r == have) continue;
-                auto c = m;
-                c[hid] = r;
-                cands.push_back(c);
+            std::vector<std::map<int64_t, int>> cands;
+            for (const int64_t key : { (int64_t)hid, -(int64_t)hid }) {
+                const int have = m.count(key) ? m[key] : 0;
+                for (int r = 0; r < (key > 0 ? ranks : 4); r++) {
+                    if (r == have) continue;
+                    auto c = m;
+                    c[key] = r;
+                    cands.push_back(c);
+                }
             }
             std::vector<TuneEval> res(cands.size());
             std::vector<std::thread> th;
@@ -1217,7 +1223,7 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
             bestBytes = bytes;
             printf("  kept:");
             for (auto &kv : cur)
-                if (kv.second) printf(" %u:%d", kv.first, kv.second);
+                if (kv.second) printf(" %lld:%d", (long long)kv.first, kv.second);
             printf("\n");
         }
     }
@@ -1228,7 +1234,7 @@ static int tuneMain(const char *scene, const char *train_list, const char *val_l
     for (size_t i = 0; i < fv.cost.size(); i++) printf(" %.0f (%+.1f%%)", fv.cost[i], 100.0 * (fv.cost[i] / v0.cost[i] - 1));
     printf(" | nodes %d stack %d\nsplitRank:", ft.nodes, ft.stack);
     for (auto &kv : cur)
-        if (kv.second) printf(" %u:%d", kv.first, kv.second);
+        if (kv.second) printf(" %lld:%d", (long long)kv.first, kv.second);
     printf("\n");
     return 0;
 }

@@ -26,14 +26,17 @@ def main():
     lines = [
         "# k_lidar's tree for this scene: BVHBuildOpts::splitRank over scene.h",
         "# lidarBVHOpts() (heap index of a binary build node, root 1; rank of the",
-        "# distinct SAH candidate split taken there).  Tuned by tools/trav_stats.cpp",
+        "# distinct SAH candidate split taken there) and collapseChoice (per 4-wide",
+        "# node: which inner children its collapse opens).  Tuned by tools/trav_stats.cpp",
         "# TRAV_TUNE (k_lidar's lockstep model over recorded lidar fans), written",
         "# by tools/write_lidar_tree.py; ignored for any other collisions.bin.",
     ]
     if note:
         lines.append("# " + note)
     lines.append(f"collisions_fnv1a64 {fnv1a64(os.path.join(scene, 'collisions.bin')):016x}")
-    lines += [f"split {h} {r}" for h, r in sorted(pairs)]
+    # negative heap index: a collapse choice (BVHBuildOpts::collapseChoice)
+    lines += [f"split {h} {r}" for h, r in sorted(pairs) if h > 0]
+    lines += [f"collapse {-h} {r}" for h, r in sorted(pairs, key=lambda p: -p[0]) if h < 0]
     with open(os.path.join(scene, "lidar_tree.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
 
