@@ -1007,7 +1007,8 @@ static int treesMain(const char *scene, const std::vector<float> &rays)
 // ---- TRAV_TUNE: ray-driven tuning of the lidar tree.  Coordinate descent
 // over BVHBuildOpts::splitRank (per binary build node down to depth
 // TRAV_TUNE_DEPTH, the rank among its distinct SAH candidate splits, up to
-// TRAV_TUNE_RANKS): each move is scored by kernelModel's lockstep cost
+// TRAV_TUNE_RANKS) and collapseChoice (key -hid: which inner children the
+// 4-wide node rooted there opens): each move is scored by kernelModel's lockstep cost
 // summed over the TRAIN ray sets (each relative to the untuned tree), kept
 // if it lowers it; trees over TRAV_TUNE_NODES nodes or a stack over 14 are
 // rejected.  The VAL sets are reported, never optimised.
