@@ -1915,15 +1915,26 @@ __device__ __forceinline__ void crumbRoundsD(const DevState &S, int w, int i, bo
     float total = 0.f; // leaveBreadcrumbsSystem's reset (sim.cpp:4845-4889)
     int kept = 0;      // survivors of the earlier rounds
     const float4 *wb = buf + 2 * wl * N;
+    // the next round's crumb is loaded while this round runs: it sits at a
+    // slot >= r0 + N, which no store of this round (slots < r0 + N) touches
+    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f), mn = pn;
+    if (i < n) {
+        pn = cr[2 * i];
+        mn = cr[2 * i + 1];
+    }
     #pragma unroll 1
     for (int r0 = 0; __syncthreads_or(r0 < n); r0 += N) {
         const int k = r0 + i;
         float4 p = make_float4(0.f, 0.f, 0.f, 0.f), meta = p;
         if (k < n) {
-            p = cr[2 * k];
-            meta = cr[2 * k + 1];
+            p = pn;
+            meta = mn;
             buf[2 * threadIdx.x] = p;
             buf[2 * threadIdx.x + 1] = meta;
+        }
+        if (k + N < n) {
+            pn = cr[2 * (k + N)];
+            mn = cr[2 * (k + N) + 1];
         }
         __syncthreads();
         if (r0 < n) {
